@@ -1,0 +1,198 @@
+"""Benchmark: DOF solved/s of one full FEA load step on MI355X.
+
+A "step" = one pass of the hot path over the synthetic mesh: device assembly
+(all elements active) → Dirichlet elimination/RHS → Jacobi-PCG to ‖r‖ ≤ 1e-8‖b‖
+(x0 = 0) → reaction + stress/failure update.  Inputs are resident in HBM before
+the timed region; no CSV IO.  Workload (BASELINE.json configs[1]): the 100k-DOF
+synthetic network = 1×5 tiles of results/sim_20251117_181147 (110,625 DOF).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2_100k]
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mycelium-fea-project_amd"))
+
+import numpy as np  # noqa: E402
+
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2_100k", choices=["C2_100k", "C3_1M", "C5_10M_dense"])
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--precond", default="jacobi", choices=["jacobi", "bjacobi"])
+    ap.add_argument("--load-step", type=int, default=20, help="load step index of 40 (dy)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from mfea import Engine, make_opts, PC_BLOCK_JACOBI, PC_JACOBI, synth
+    from mfea.synth import CONFIGS
+
+    nx, ny = CONFIGS[a.config]
+    xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
+    top, bot = synth.grips(xyz)
+    n_dof = 3 * len(xyz)
+
+    import fea_solver as fs
+    eng = Engine(local)
+    eng.set_material(fs.E_mod, fs.A, fs.I)
+    eng.set_mesh(xyz, e2n)
+    eng.set_bc(top, bot)
+    eng.set_active(None)
+    info = eng.info()
+    dy = fs.DISPLACEMENT_MAX * a.load_step / (fs.N_STEPS - 1)
+    opts = make_opts(rtol=a.rtol, max_it=200000,
+                     precond=PC_BLOCK_JACOBI if a.precond == "bjacobi" else PC_JACOBI)
+
+    def one_step():
+        eng.set_active(None)                       # every step starts from the intact mesh
+        return eng.step(dy, -dy, opts, fs.MAX_STRAIN)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        one_step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(a.steps):
+        stats.append(one_step())
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    force, n_active, st = stats[-1]
+    iters = st.iters
+    # ---- roofline of the dominant kernel (SpMV), live HIP events on its stream
+    spmv_ms = eng.profile_spmv(reps=100)
+    nf = info["n_free_nodes"]
+    inc = info["free_incidences"]
+    # algorithmic bytes per SpMV launch: per free row
+    # diag block 48 B + row_len 4 B + p_i 24 B + q_i 24 B; per valid slot
+    # column 4 B + value block 48 B (neighbour p_j gathers are re-reads of p).
+    spmv_bytes = nf * (48 + 4 + 24 + 24) + inc * (4 + 48)
+    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(a.traffic):
+        try:
+            tj = json.load(open(a.traffic))
+            if tj.get("config") == a.config:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "DOF solved/sec (full load step, Jacobi-PCG to rtol 1e-8)",
+        "value": n_dof * a.steps * world / dt,
+        "unit": "DOF/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * dt / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (tiled copies of results/sim_20251117_181147; no RNG)",
+        "config": {
+            "workload": f"{a.config}: {nx}x{ny} tiles, {n_dof} DOF, {info['n_free_nodes'] * 3} free DOF, "
+                        f"{info['n_elems']} elements, load step {a.load_step}/40",
+            "n_dof": n_dof, "n_free_dof": 3 * nf, "n_elems": info["n_elems"],
+            "precond": a.precond, "rtol": a.rtol, "parallelism": f"replicas{world}" if world > 1 else "1gpu",
+        },
+        "cg_iters": iters,
+        "relres": st.relres,
+        "step_breakdown_ms": {"assemble": st.t_assemble_ms, "rhs": st.t_rhs_ms,
+                              "pcg": st.t_solve_ms, "post": st.t_post_ms},
+        "roofline": {
+            "kernel": "k_spmv_sell",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBPS,
+            "traffic": traffic,
+            "alg_bytes_per_launch": spmv_bytes,
+            "avg_launch_us": spmv_ms * 1e3,
+        },
+    }
+
+    if rank == 0 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import cpu_fea  # baseline leg only
+        cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        c = cpu_fea.CpuFea(xyz, e2n, top, bot, fs.E_mod, fs.A, fs.I)
+        t = time.perf_counter()
+        its = []
+        for _ in range(a.cpu_steps):
+            c.active[:] = 1
+            r = c.step(dy, -dy, rtol=a.rtol, max_it=200000, threads=cores)
+            its.append(r["iters"])
+        tc = time.perf_counter() - t
+        c.close()
+        out["cpu_baseline"] = {
+            "value": n_dof * a.cpu_steps / tc, "unit": "DOF/s", "cores": cores, "kind": "port",
+            "sample": f"{a.cpu_steps} full load step(s) of the same {a.config} mesh, C/OpenMP "
+                      f"restatement of fea_petsc.cpp assembly + PETSc KSPCG/PCJACOBI to rtol {a.rtol} "
+                      f"({its[-1]} iters), {tc:.2f} s on {cpu_model()}",
+        }
+        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,173 @@
+/*
+ * mfea.h — C ABI of the MI355X-native mycelium FEA engine (libmfea.so).
+ *
+ * The reference has no FFI: its hot path is Python calling NumPy/SciPy
+ * (src/fea_solver.py) or a C++ main() calling PETSc (src/fea_petsc.cpp).
+ * Each entry point below replaces one piece of that path; the reference
+ * interface it stands in for is cited beside it.  Plain pointers and sizes
+ * only (no torch types).  All functions return 0 on success and a negative
+ * MFEA_E* code on failure; mfea_last_error() returns the message of the most
+ * recent failure on the calling thread.
+ *
+ * Ownership: host arrays passed in are caller-owned and copied (or written)
+ * synchronously before the call returns.  Device buffers belong to the handle.
+ * Threading: one host thread per handle; a handle is not re-entrant.
+ * Node/element indices are 0-based rows of nodes.csv / elements.csv
+ * (src/fea_petsc.cpp:39-40 — node index = row order).
+ */
+#ifndef MFEA_H
+#define MFEA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFEA_ABI_VERSION 1
+
+/* error / status codes */
+#define MFEA_OK 0
+#define MFEA_EINVAL -1      /* bad argument (e.g. node id out of range)                */
+#define MFEA_EDEVICE -2     /* HIP runtime error                                       */
+#define MFEA_ESTATE -3      /* call out of order (no mesh, no BCs, ...)                */
+#define MFEA_EMAXIT -4      /* PCG hit max_it (PETSc KSP_DIVERGED_ITS)                  */
+#define MFEA_EBREAKDOWN -5  /* PCG breakdown: p·Ap <= 0 or non-finite (KSP_DIVERGED_*) */
+#define MFEA_ENOMEM -6
+#define MFEA_ECOMM -7       /* RCCL failure (multi-GPU)                                */
+
+/* mesh flags (mfea_set_mesh) */
+#define MFEA_MESH_SKIP_INVALID 1u /* skip elements with out-of-range node ids, as
+                                     src/fea_petsc.cpp:241 does; default: reject,
+                                     as src/fea_solver.py:82-83 would (IndexError) */
+
+/* solver selection (mfea_solve_opts.precond) */
+#define MFEA_PC_JACOBI 0        /* PCJACOBI — diagonal of K_ff + reg·I              */
+#define MFEA_PC_BLOCK_JACOBI 1  /* 3×3 node-block Jacobi (exact inverse per block)   */
+
+/* stopping norm (mfea_solve_opts.norm) */
+#define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
+#define MFEA_NORM_PRECONDITIONED 1   /* ‖z‖₂ ≤ rtol·‖M⁻¹b‖₂ (PETSc KSPCG default)     */
+
+typedef struct mfea_handle mfea_handle;
+
+typedef struct {
+  double rtol;      /* relative tolerance; PETSc default 1e-5, metric 1e-8, parity 1e-13 */
+  double atol;      /* absolute tolerance on the chosen norm (PETSc default 1e-50)       */
+  int32_t max_it;   /* PETSc default 10000                                              */
+  int32_t precond;  /* MFEA_PC_*                                                         */
+  int32_t norm;     /* MFEA_NORM_*                                                       */
+  int32_t chunk;    /* iterations per captured hipGraph replay (0 = library default)     */
+  double reg;       /* diagonal regularisation of K_ff, src/fea_solver.py:125 (1e-12)    */
+} mfea_solve_opts;
+
+typedef struct {
+  int32_t iters;     /* PCG iterations executed                                        */
+  int32_t status;    /* 0 converged, MFEA_EMAXIT, MFEA_EBREAKDOWN                       */
+  double relres;     /* final ‖r‖/‖b‖ (recursive residual)                               */
+  double bnorm;      /* ‖b_f‖₂                                                          */
+  int64_t n_free;    /* free DOFs                                                       */
+  double t_assemble_ms, t_rhs_ms, t_solve_ms, t_post_ms; /* device time (HIP events)   */
+} mfea_stats;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int mfea_abi_version(void);
+int mfea_last_error(char* buf, size_t n);
+/* One handle drives one device.  Multi-GPU = one process (one handle) per GPU,
+ * joined by mfea_dist_init. */
+int mfea_create(int device, mfea_handle** out);
+int mfea_destroy(mfea_handle* h);
+
+/* Material constants, src/fea_solver.py:14-20 / src/fea_petsc.cpp:23-27. */
+int mfea_set_material(mfea_handle* h, double E, double A, double I);
+
+/* ---- mesh + boundary conditions (symbolic, once per mesh) ------------------ */
+/* Replaces the CSV→array hand-off of fea_solver (src/fea_solver.py:193-201) and
+ * read_nodes_csv/read_elems_csv (src/fea_petsc.cpp:42-82, 179-200).
+ * xyz: n_nodes×3 row-major f64; e2n: n_elems×2 int64.  Builds the node-block
+ * sliced-ELL pattern, the free/known permutation and uploads the mesh. */
+int mfea_set_mesh(mfea_handle* h, int64_t n_nodes, const double* xyz, int64_t n_elems,
+                  const int64_t* e2n, uint32_t flags);
+/* Grip node sets, src/fea_solver.py:207-210 / src/fea_petsc.cpp:203-213.
+ * All 3 DOFs of every grip node are prescribed (x=0, y=dy, z=0); a node in
+ * both bands takes the bottom value (src/fea_solver.py:226-242 dict order,
+ * src/fea_petsc.cpp:292-294 last INSERT wins).  Rebuilds the permutation. */
+int mfea_set_bc(mfea_handle* h, int64_t n_top, const int64_t* top, int64_t n_bot,
+                const int64_t* bot);
+/* Element activity (E bytes, nonzero = active); NULL = all active
+ * (src/fea_solver.py:201, src/fea_petsc.cpp:200). */
+int mfea_set_active(mfea_handle* h, const uint8_t* active);
+
+/* ---- the hot path ---------------------------------------------------------- */
+/* Element stiffness + global assembly on device for the current active set.
+ * Replaces bar_stiffness_bulk + assemble_global_stiffness
+ * (src/fea_solver.py:30-106) and element_stiffness_6x6 + the MatSetValue loop
+ * (src/fea_petsc.cpp:88-140, 229-263). */
+int mfea_assemble(mfea_handle* h);
+/* Dirichlet elimination, RHS and preconditioned CG on device.
+ * Replaces solve_system (src/fea_solver.py:112-135) and MatZeroRowsColumnsIS +
+ * diag regularisation + KSPSolve (src/fea_petsc.cpp:286-357).
+ * Returns MFEA_EMAXIT / MFEA_EBREAKDOWN on solver failure (stats still filled);
+ * the Python shim maps them to np.linalg.LinAlgError (src/fea_solver.py:247-249). */
+int mfea_solve(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
+               mfea_stats* st);
+/* Reaction + stress/failure on device.  Replaces src/fea_solver.py:252-274 and
+ * src/fea_petsc.cpp:360-406: total_force = Σ_{top} (K·U)[3n+1] on the
+ * unregularised K; stress = E·ε for elements active at step start (0 else);
+ * elements with |ε| > max_strain are deactivated for the next step. */
+int mfea_post(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active);
+/* One full load step = assemble + solve + post (the bench "step"). */
+int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
+              double max_strain, double* total_force, int64_t* n_active, mfea_stats* st);
+
+/* ---- results (device → host, original node/element order) ----------------- */
+int mfea_get_displacement(mfea_handle* h, double* U /* 3·n_nodes, interleaved xyz */);
+int mfea_get_stress(mfea_handle* h, double* stress /* n_elems */);
+int mfea_get_active(mfea_handle* h, uint8_t* active /* n_elems */);
+
+/* ---- reference-API helpers ------------------------------------------------- */
+/* bar_stiffness_bulk on device (src/fea_solver.py:30-68): Ke n×36 row-major, L n. */
+int mfea_element_stiffness(mfea_handle* h, int64_t n, const double* p1s, const double* p2s,
+                           double E, double A, double I, double* Ke, double* L);
+/* Export the assembled global K (active elements only) as scalar CSR over the
+ * 3·n_nodes DOFs in original order, same pattern as the reference's
+ * csr_matrix (explicit zeros kept, duplicates summed).  Call with indptr ==
+ * NULL to query *nnz. */
+int mfea_export_csr(mfea_handle* h, int64_t* nnz, int64_t* indptr, int32_t* indices,
+                    double* data);
+/* solve_system(K, known_dofs, known_vals) for an arbitrary caller-supplied
+ * scalar CSR K (src/fea_solver.py:112-135), on device. U: n out. */
+int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32_t* indices,
+                   const double* data, int64_t n_known, const int64_t* known_dofs,
+                   const double* known_vals, const mfea_solve_opts* opts, double* U,
+                   mfea_stats* st);
+
+/* ---- introspection / measurement ------------------------------------------- */
+typedef struct {
+  int64_t n_nodes, n_elems;
+  int64_t n_free_nodes;     /* free rows (3 DOF each)                               */
+  int64_t n_top, n_known;   /* grip rows                                            */
+  int64_t n_slices;         /* SELL-64 slices                                       */
+  int64_t n_slots;          /* slot rows × 64 = allocated slot entries              */
+  int64_t free_incidences;  /* Σ row_len over free rows = valid slots the SpMV reads */
+  int32_t planar;           /* all z == 0                                           */
+  int32_t pad;
+} mfea_info;
+int mfea_get_info(mfea_handle* h, mfea_info* info);
+/* Launches the PCG SpMV kernel `reps` times on the handle's stream between two
+ * HIP events (current p vector) and returns the average launch duration. */
+int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------- */
+/* Replaces the PETSC_COMM_WORLD row-block distribution of
+ * src/fea_petsc_parallel.cpp:169-171, 234-268, 330-409.  unique_id: the 128-byte
+ * ncclUniqueId made by rank 0 (mfea_dist_unique_id) and broadcast by the caller.
+ * Must precede mfea_set_mesh; each rank then owns one y-band of nodes. */
+int mfea_dist_unique_id(uint8_t* unique_id /* 128 bytes */);
+int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MFEA_H */

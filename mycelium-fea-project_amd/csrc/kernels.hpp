@@ -1,0 +1,105 @@
+// kernels.hpp — device kernels of the mfea engine (gfx950 / CDNA4, wave64).
+//
+// Data layout in HBM (all f64 unless noted), rows = nodes in the permuted
+// order of symbolic.cpp (free rows [0,nf), top grip rows, bottom rows):
+//   xyz[3N]            node coordinates, interleaved x,y,z
+//   slice_ptr[ns+1]    SELL-64 slot offsets; row_len[N] incident elements
+//   s_col/s_elem[G]    per slot (slot t, lane l at t·64+l): neighbour row, element
+//   val[6][G]          per slot K_ij = −S_e, six symmetric components (SoA)
+//   diag[6][N]         per row K_ii = Σ S_e (unregularised)
+//   x,r,p,q[3N]        PCG vectors, interleaved DOFs (x holds the full U)
+//   dinv[3N] / binv[6N] Jacobi / 3×3 block-Jacobi inverse
+// Components of a symmetric 3×3 block: 0 xx, 1 xy, 2 xz, 3 yy, 4 yz, 5 zz.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mfea {
+
+constexpr int kBlock = 256;  // 4 wavefronts
+
+// PCG per-iteration scalar slot (see DESIGN.md "PCG scalar slots").
+// v[0] = p·q, v[1] = r·z, v[2] = r·r, v[3] = z·z (v[1..3] reduced together),
+// flag: 0 RUN, 1 STOP (propagated / after done), 2 BREAKDOWN.
+struct Slot {
+  double v[4];
+  int32_t flag;
+  int32_t pad[3];
+};
+enum SlotFlag : int32_t { kRun = 0, kStop = 1, kBreakdown = 2 };
+
+struct SolveState {
+  double tol2;     // stopping threshold on the chosen norm²
+  double reg;      // diagonal regularisation
+  double bb0;      // ‖b‖²
+  double res_final;
+  int32_t base;    // absolute iteration index of slot 0
+  int32_t max_it;
+  int32_t norm;    // 0 unpreconditioned (‖r‖), 1 preconditioned (‖z‖)
+  int32_t done;
+  int32_t iters;
+  int32_t status;  // 0 converged, -4 maxit, -5 breakdown
+  int32_t pad[2];
+  double res0;     // initial value of the chosen norm² (‖b‖² or ‖M⁻¹b‖²)
+};
+
+struct Material {
+  double EA;    // E·A            (src/fea_solver.py:45 numerator)
+  double EI12;  // (12·E)·I       (src/fea_solver.py:58 numerator)
+  double E;     // for stress = E·ε (src/fea_solver.py:271)
+};
+
+// ---- launchers (defined in kernels.hip) -------------------------------------
+void launch_assemble(hipStream_t s, int64_t N, const double* xyz, const int32_t* slice_ptr,
+                     const int32_t* row_len, const int32_t* s_col, const int32_t* s_elem,
+                     const uint8_t* active, Material m, int64_t G, double* val, double* diag);
+
+void launch_rhs_init(hipStream_t s, int64_t N, int64_t nf, const int32_t* slice_ptr,
+                     const int32_t* row_len, const int32_t* s_col, const double* val,
+                     const double* diag, int64_t G, const uint8_t* code, double dy_top,
+                     double dy_bot, double reg, int precond, double* x, double* r, double* p,
+                     double* dinv, double* partials, unsigned* ticket, double* red_out);
+
+void launch_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
+                          int max_it, double reg, Slot* slots, SolveState* st);
+
+void launch_spmv_sell(hipStream_t s, int j, int64_t nf, int64_t N, const int32_t* slice_ptr,
+                      const int32_t* row_len, const int32_t* s_col, const double* val,
+                      const double* diag, int64_t G, const double* p, double* q, Slot* slots,
+                      const SolveState* st, double* partials, unsigned* ticket);
+
+void launch_update(hipStream_t s, int j, int64_t n, int precond, double* x, double* r,
+                   const double* p, const double* q, const double* dinv, Slot* slots,
+                   const SolveState* st, double* partials, unsigned* ticket);
+
+void launch_direction(hipStream_t s, int j, int64_t n, int precond, const double* r, double* p,
+                      const double* dinv, const Slot* slots, const SolveState* st);
+
+void launch_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st);
+
+void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
+                     const int32_t* slice_ptr, const int32_t* row_len, const int32_t* s_col,
+                     const double* val, const double* diag, int64_t G, const double* u,
+                     double* partials, unsigned* ticket, double* red_out);
+
+void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
+                   const double* u, Material m, double max_strain, uint8_t* active,
+                   double* stress, double* partials, unsigned* ticket, double* red_out);
+
+void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,
+                              Material m, double* Ke, double* L);
+
+// generic scalar-CSR operator (mfea_solve_csr)
+void launch_csr_rhs_init(hipStream_t s, int64_t n, const int64_t* indptr, const int32_t* indices,
+                         const double* data, const uint8_t* known, const double* kval, double reg,
+                         double* x, double* r, double* p, double* dinv, double* partials,
+                         unsigned* ticket, double* red_out);
+void launch_spmv_csr(hipStream_t s, int j, int64_t n, const int64_t* indptr,
+                     const int32_t* indices, const double* data, const uint8_t* known,
+                     double reg, const double* p, double* q, Slot* slots, const SolveState* st,
+                     double* partials, unsigned* ticket);
+
+int64_t grid_rows(int64_t rows);
+int64_t grid_elementwise(int64_t n);
+
+}  // namespace mfea

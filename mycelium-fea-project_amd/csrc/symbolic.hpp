@@ -1,0 +1,60 @@
+// symbolic.hpp — host-side symbolic phase of the mfea engine (once per mesh/BC set).
+//
+// The reference rebuilds its sparse pattern every load step: a Python COO list
+// of 36 triplets per element handed to scipy's csr_matrix (src/fea_solver.py:88-105),
+// or unpreallocated PETSc MatSetValue calls (src/fea_petsc.cpp:229-263).  Here
+// the pattern is built once, on the host, as a node-block sliced ELL
+// ("SELL-64"): one matrix row = one node (3 DOF), one slice = 64 consecutive
+// rows = one wavefront, one slot = one incident element of the row.  Only the
+// values change between steps (element deactivation zeroes a slot).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mfea {
+
+constexpr int kSlice = 64;  // rows per slice = wavefront width on CDNA4
+
+enum NodeCode : uint8_t { kFree = 0, kTop = 1, kBot = 2 };
+
+struct Pattern {
+  int64_t n_nodes = 0, n_elems = 0;
+  int64_t n_free = 0;   // free nodes occupy permuted rows [0, n_free)
+  int64_t n_top = 0;    // top grip rows [n_free, n_free + n_top) in top-list order
+  int64_t n_known = 0;  // known rows [n_free, n_nodes)
+  std::vector<int32_t> perm;   // perm[new] = original node
+  std::vector<int32_t> iperm;  // iperm[orig] = new
+  std::vector<uint8_t> code;   // code[new] (kFree / kTop / kBot; bottom overrides top)
+  // SELL-64: slice s covers rows [64 s, 64 s + 64); its slots are
+  // slice_ptr[s] .. slice_ptr[s+1]-1; entry (slot t, lane l) lives at t*64 + l.
+  std::vector<int32_t> slice_ptr;  // n_slices + 1
+  std::vector<int32_t> row_len;    // per permuted row: incident (non-self-loop) elements
+  std::vector<int32_t> s_col;      // permuted neighbour row, -1 = pad
+  std::vector<int32_t> s_elem;     // element id (original order), -1 = pad
+  std::vector<int32_t> e2n_perm;   // E×2 permuted endpoints (-1,-1 for skipped elements)
+  std::vector<double> xyz_perm;    // N×3 coordinates in permuted order
+  std::vector<uint8_t> elem_valid; // 0 for elements skipped (out of range)
+  int64_t n_slices() const { return (int64_t)slice_ptr.size() - 1; }
+  int64_t n_slots() const { return slice_ptr.empty() ? 0 : (int64_t)slice_ptr.back(); }
+  bool planar = false;             // every z == 0
+};
+
+// Validates and builds.  Returns "" on success, else an error message.
+// skip_invalid: drop elements with out-of-range node ids (src/fea_petsc.cpp:241)
+// instead of failing (src/fea_solver.py:82-83 raises).
+std::string build_pattern(int64_t n_nodes, const double* xyz, int64_t n_elems, const int64_t* e2n,
+                          bool skip_invalid, const std::vector<int64_t>& top,
+                          const std::vector<int64_t>& bot, int sort_window, Pattern& P);
+
+// Scalar CSR over the 3·N DOFs in original order, pattern = the reference's
+// csr_matrix pattern for the active set (src/fea_solver.py:93-105):
+// block (n,m) present iff an active element joins n and m (or n == m and n has
+// an active incident element); all 9 entries of a present block are stored.
+// diag/vals are the device arrays copied back (6 symmetric components each).
+void export_csr(const Pattern& P, const std::vector<uint8_t>& active,
+                const std::vector<double>& diag6 /* 6×N SoA */,
+                const std::vector<double>& val6 /* 6×(slots·64) SoA */, std::vector<int64_t>& indptr,
+                std::vector<int32_t>& indices, std::vector<double>& data);
+
+}  // namespace mfea

@@ -1,0 +1,273 @@
+"""ctypes binding of libmfea.so (include/mfea.h).
+
+The HIP library is the product path: if it is missing this module raises
+ImportError at import time — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"mfea: HIP library not found at {LIB_PATH}; build it with "
+        f"`make -C mycelium-fea-project_amd` (or __graft_entry__.build())")
+_lib = C.CDLL(LIB_PATH)
+
+# error codes (mfea.h)
+OK, EINVAL, EDEVICE, ESTATE, EMAXIT, EBREAKDOWN, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5, -6, -7
+PC_JACOBI, PC_BLOCK_JACOBI = 0, 1
+NORM_UNPRECONDITIONED, NORM_PRECONDITIONED = 0, 1
+MESH_SKIP_INVALID = 1
+
+
+class SolveOpts(C.Structure):
+    _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("max_it", C.c_int32),
+                ("precond", C.c_int32), ("norm", C.c_int32), ("chunk", C.c_int32),
+                ("reg", C.c_double)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("iters", C.c_int32), ("status", C.c_int32), ("relres", C.c_double),
+                ("bnorm", C.c_double), ("n_free", C.c_int64), ("t_assemble_ms", C.c_double),
+                ("t_rhs_ms", C.c_double), ("t_solve_ms", C.c_double), ("t_post_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Info(C.Structure):
+    _fields_ = [("n_nodes", C.c_int64), ("n_elems", C.c_int64), ("n_free_nodes", C.c_int64),
+                ("n_top", C.c_int64), ("n_known", C.c_int64), ("n_slices", C.c_int64),
+                ("n_slots", C.c_int64), ("free_incidences", C.c_int64), ("planar", C.c_int32),
+                ("pad", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+_P = C.c_void_p
+_sig = {
+    "mfea_get_info": (C.c_int, [_P, C.POINTER(Info)]),
+    "mfea_profile_spmv": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double)]),
+    "mfea_abi_version": (C.c_int, []),
+    "mfea_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "mfea_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "mfea_destroy": (C.c_int, [_P]),
+    "mfea_set_material": (C.c_int, [_P, C.c_double, C.c_double, C.c_double]),
+    "mfea_set_mesh": (C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, C.c_uint32]),
+    "mfea_set_bc": (C.c_int, [_P, C.c_int64, _P, C.c_int64, _P]),
+    "mfea_set_active": (C.c_int, [_P, _P]),
+    "mfea_assemble": (C.c_int, [_P]),
+    "mfea_solve": (C.c_int, [_P, C.c_double, C.c_double, C.POINTER(SolveOpts), C.POINTER(Stats)]),
+    "mfea_post": (C.c_int, [_P, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "mfea_step": (C.c_int, [_P, C.c_double, C.c_double, C.POINTER(SolveOpts), C.c_double,
+                            C.POINTER(C.c_double), C.POINTER(C.c_int64), C.POINTER(Stats)]),
+    "mfea_get_displacement": (C.c_int, [_P, _P]),
+    "mfea_get_stress": (C.c_int, [_P, _P]),
+    "mfea_get_active": (C.c_int, [_P, _P]),
+    "mfea_element_stiffness": (C.c_int, [_P, C.c_int64, _P, _P, C.c_double, C.c_double,
+                                         C.c_double, _P, _P]),
+    "mfea_export_csr": (C.c_int, [_P, C.POINTER(C.c_int64), _P, _P, _P]),
+    "mfea_solve_csr": (C.c_int, [_P, C.c_int64, _P, _P, _P, C.c_int64, _P, _P,
+                                 C.POINTER(SolveOpts), _P, C.POINTER(Stats)]),
+    "mfea_dist_unique_id": (C.c_int, [_P]),
+    "mfea_dist_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(_lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_sig)
+
+
+class MfeaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mfea error {code}: {msg}")
+        self.code = code
+
+
+class SolverFailure(np.linalg.LinAlgError):
+    """PCG did not converge (max_it) or broke down.  Subclasses LinAlgError so
+    the reference driver's ``except np.linalg.LinAlgError`` (src/fea_solver.py:247)
+    catches it."""
+
+    def __init__(self, code, msg, stats=None):
+        super().__init__(f"mfea solver failure {code}: {msg}")
+        self.code = code
+        self.stats = stats
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(1024)
+    _lib.mfea_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def _check(rc, stats=None):
+    if rc == OK:
+        return
+    if rc in (EMAXIT, EBREAKDOWN):
+        raise SolverFailure(rc, last_error(), stats)
+    raise MfeaError(rc, last_error())
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P) if a is not None and a.size else None
+
+
+def abi_version() -> int:
+    return _lib.mfea_abi_version()
+
+
+def make_opts(rtol=1e-8, atol=0.0, max_it=100000, precond=PC_JACOBI, norm=NORM_UNPRECONDITIONED,
+              chunk=0, reg=1e-12) -> SolveOpts:
+    return SolveOpts(rtol, atol, int(max_it), int(precond), int(norm), int(chunk), reg)
+
+
+class Engine:
+    """One device handle (mfea_handle).  Host arrays are copied on every call."""
+
+    def __init__(self, device: int = 0):
+        h = _P()
+        _check(_lib.mfea_create(int(device), C.byref(h)))
+        self._h = h
+        self.n_nodes = 0
+        self.n_elems = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.mfea_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- setup --------------------------------------------------------------
+    def set_material(self, E, A, I):
+        _check(_lib.mfea_set_material(self._h, float(E), float(A), float(I)))
+
+    def set_mesh(self, xyz, e2n, skip_invalid=False):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float64).reshape(-1, 3)
+        e2n = np.ascontiguousarray(e2n, dtype=np.int64).reshape(-1, 2)
+        self._xyz, self._e2n = xyz, e2n
+        _check(_lib.mfea_set_mesh(self._h, xyz.shape[0], _ptr(xyz), e2n.shape[0], _ptr(e2n),
+                                  MESH_SKIP_INVALID if skip_invalid else 0))
+        self.n_nodes, self.n_elems = xyz.shape[0], e2n.shape[0]
+
+    def set_bc(self, top, bot):
+        top = np.ascontiguousarray(top, dtype=np.int64).ravel()
+        bot = np.ascontiguousarray(bot, dtype=np.int64).ravel()
+        _check(_lib.mfea_set_bc(self._h, top.size, _ptr(top), bot.size, _ptr(bot)))
+
+    def set_active(self, active=None):
+        if active is None:
+            _check(_lib.mfea_set_active(self._h, None))
+        else:
+            a = np.ascontiguousarray(active, dtype=np.uint8).ravel()
+            if a.size != self.n_elems:
+                raise ValueError("active must have one entry per element")
+            _check(_lib.mfea_set_active(self._h, _ptr(a)))
+
+    # ---- hot path -----------------------------------------------------------
+    def assemble(self):
+        _check(_lib.mfea_assemble(self._h))
+
+    def solve(self, dy_top, dy_bot, opts: SolveOpts | None = None) -> Stats:
+        st = Stats()
+        o = opts if opts is not None else make_opts()
+        _check(_lib.mfea_solve(self._h, float(dy_top), float(dy_bot), C.byref(o), C.byref(st)), st)
+        return st
+
+    def post(self, max_strain):
+        f = C.c_double()
+        n = C.c_int64()
+        _check(_lib.mfea_post(self._h, float(max_strain), C.byref(f), C.byref(n)))
+        return f.value, n.value
+
+    def step(self, dy_top, dy_bot, opts: SolveOpts | None, max_strain):
+        st = Stats()
+        f = C.c_double()
+        n = C.c_int64()
+        o = opts if opts is not None else make_opts()
+        _check(_lib.mfea_step(self._h, float(dy_top), float(dy_bot), C.byref(o), float(max_strain),
+                              C.byref(f), C.byref(n), C.byref(st)), st)
+        return f.value, n.value, st
+
+    # ---- results --------------------------------------------------------------
+    def displacement(self):
+        U = np.empty(3 * self.n_nodes)
+        _check(_lib.mfea_get_displacement(self._h, _ptr(U)))
+        return U
+
+    def stress(self):
+        s = np.empty(self.n_elems)
+        if self.n_elems:
+            _check(_lib.mfea_get_stress(self._h, _ptr(s)))
+        return s
+
+    def active(self):
+        a = np.empty(self.n_elems, dtype=np.uint8)
+        if self.n_elems:
+            _check(_lib.mfea_get_active(self._h, _ptr(a)))
+        return a.astype(bool)
+
+    def info(self) -> dict:
+        inf = Info()
+        _check(_lib.mfea_get_info(self._h, C.byref(inf)))
+        return inf.as_dict()
+
+    def profile_spmv(self, reps=50) -> float:
+        ms = C.c_double()
+        _check(_lib.mfea_profile_spmv(self._h, int(reps), C.byref(ms)))
+        return ms.value
+
+    # ---- reference-API helpers ------------------------------------------------
+    def element_stiffness(self, p1s, p2s, E, A, I):
+        p1 = np.ascontiguousarray(p1s, dtype=np.float64).reshape(-1, 3)
+        p2 = np.ascontiguousarray(p2s, dtype=np.float64).reshape(-1, 3)
+        n = p1.shape[0]
+        Ke = np.empty((n, 6, 6))
+        L = np.empty(n)
+        _check(_lib.mfea_element_stiffness(self._h, n, _ptr(p1), _ptr(p2), float(E), float(A),
+                                           float(I), _ptr(Ke), _ptr(L)))
+        return Ke, L
+
+    def export_csr(self):
+        nnz = C.c_int64(0)
+        _check(_lib.mfea_export_csr(self._h, C.byref(nnz), None, None, None))
+        indptr = np.empty(3 * self.n_nodes + 1, dtype=np.int64)
+        indices = np.empty(nnz.value, dtype=np.int32)
+        data = np.empty(nnz.value)
+        _check(_lib.mfea_export_csr(self._h, C.byref(nnz), indptr.ctypes.data_as(_P),
+                                    indices.ctypes.data_as(_P), data.ctypes.data_as(_P)))
+        return indptr, indices, data
+
+    def solve_csr(self, indptr, indices, data, known_dofs, known_vals, opts=None):
+        indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+        indices = np.ascontiguousarray(indices, dtype=np.int32)
+        data = np.ascontiguousarray(data, dtype=np.float64)
+        kd = np.ascontiguousarray(known_dofs, dtype=np.int64).ravel()
+        kv = np.ascontiguousarray(known_vals, dtype=np.float64).ravel()
+        n = indptr.size - 1
+        U = np.empty(n)
+        st = Stats()
+        o = opts if opts is not None else make_opts()
+        _check(_lib.mfea_solve_csr(self._h, n, indptr.ctypes.data_as(_P), _ptr(indices), _ptr(data),
+                                   kd.size, _ptr(kd), _ptr(kv), C.byref(o), _ptr(U), C.byref(st)), st)
+        return U, st

@@ -1,0 +1,46 @@
+import os
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "mycelium-fea-project_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, PKG, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")
+
+
+def read_rt(path):
+    """Round-trip float parsing for golden outputs."""
+    return pd.read_csv(path, float_precision="round_trip")
+
+
+def load_mesh(name):
+    """A committed mesh, parsed exactly as the reference parses it (pd.read_csv)."""
+    d = os.path.join(GOLDEN, "meshes", name)
+    nodes = pd.read_csv(os.path.join(d, "nodes.csv"))
+    elems = pd.read_csv(os.path.join(d, "elements.csv"))
+    return nodes, elems
+
+
+def load_gen(name):
+    z = np.load(os.path.join(GOLDEN, name))
+    out = {k: z[k] for k in z.files}
+    if "active" in out:
+        out["active"] = np.unpackbits(out["active"], axis=1)[:, : int(out["n_elems"])].astype(bool)
+    return out
+
+
+@pytest.fixture(scope="session")
+def engine():
+    from mfea import Engine
+    eng = Engine(0)
+    yield eng
+    eng.close()

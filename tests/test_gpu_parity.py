@@ -1,0 +1,272 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's golden vectors.  Tolerances (north_star): displacement within
+1e-10 relative L2 of the converged direct solve; node indexing bit-exact;
+assembly values within 4 ulp of the reference's csr_matrix.
+"""
+import os
+import shutil
+
+import numpy as np
+import pandas as pd
+import pytest
+import scipy.sparse as sp
+
+from conftest import GOLDEN, load_gen, load_mesh, read_rt
+
+pytestmark = pytest.mark.gpu
+
+import fea_oracle as fo  # noqa: E402  (checker only)
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def ulp_diff(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    sc = np.maximum(np.spacing(np.abs(a)), np.spacing(np.abs(b)))
+    return np.max(np.abs(a - b) / np.where(sc > 0, sc, 1e-300)) if a.size else 0.0
+
+
+# ---------------------------------------------------------------------------
+# element stiffness (src/fea_solver.py:30-68)
+# ---------------------------------------------------------------------------
+def test_element_stiffness_matches_oracle(engine):
+    rng = np.random.default_rng(7)
+    p1 = rng.normal(size=(20000, 3))
+    p2 = p1 + rng.normal(size=(20000, 3)) * rng.uniform(1e-3, 0.2, size=(20000, 1))
+    p2[:50] = p1[:50]                    # zero-length → L_safe clamp
+    p2[50:100, 2] = p1[50:100, 2]        # planar elements
+    Ke, L = engine.element_stiffness(p1, p2, fo.E_MOD, fo.AREA, fo.INERTIA)
+    Ko, Lo = fo.bar_stiffness_bulk(p1, p2)
+    assert np.array_equal(L, Lo)
+    # only L³ may differ (double-double cube vs NumPy pow, ≤1 ulp) → ≤ 2 ulp on Ke
+    assert ulp_diff(Ke, Ko) <= 2.0
+    assert np.mean(Ke == Ko) > 0.9
+
+
+# ---------------------------------------------------------------------------
+# assembly (src/fea_solver.py:74-106) — pattern identical, values ≤ 4 ulp
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mesh", ["test_X", "sim_20251117_175809", "sim_20251115_135507"])
+def test_assembly_matches_reference_K(engine, mesh):
+    nodes, elems = load_mesh(mesh)
+    z = np.load(os.path.join(GOLDEN, f"K0_{mesh}.npz"))
+    Kref = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=tuple(z["shape"]))
+    engine.set_mesh(nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values)
+    engine.set_bc([], [])
+    engine.set_active(None)
+    engine.assemble()
+    ip, ix, dv = engine.export_csr()
+    assert np.array_equal(ip, Kref.indptr)
+    assert np.array_equal(ix, Kref.indices)
+    assert ulp_diff(dv, Kref.data) <= 4.0
+
+
+def test_assembly_with_inactive_elements(engine):
+    nodes, elems = load_mesh("sim_20251117_175809")
+    xyz = nodes[["x", "y", "z"]].values
+    e2n = elems[["n1", "n2"]].values
+    rng = np.random.default_rng(3)
+    active = rng.random(len(e2n)) > 0.3
+    Kref = fo.assemble_global_stiffness(xyz, e2n, active)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc([], [])
+    engine.set_active(active)
+    engine.assemble()
+    ip, ix, dv = engine.export_csr()
+    assert np.array_equal(ip, Kref.indptr)
+    assert np.array_equal(ix, Kref.indices)
+    assert ulp_diff(dv, Kref.data) <= 4.0
+
+
+# ---------------------------------------------------------------------------
+# solve (src/fea_solver.py:112-135): ≤ 1e-10 relative L2 vs the direct solve
+# ---------------------------------------------------------------------------
+def _sim181147(engine):
+    nodes, elems = load_mesh("sim_20251117_181147")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    engine.set_mesh(xyz, elems[["n1", "n2"]].values)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    return xyz
+
+
+@pytest.mark.parametrize("precond", [0, 1])
+def test_solve_matches_direct(engine, precond):
+    from mfea import make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    _sim181147(engine)
+    engine.assemble()
+    st = engine.solve(float(sysz["dy"]), -float(sysz["dy"]),
+                      make_opts(rtol=1e-13, max_it=200000, precond=precond))
+    U = engine.displacement()
+    assert st.status == 0
+    assert rel(U, sysz["U"]) <= 1e-10
+    if precond == 0:
+        # Jacobi-PCG iteration count to 1e-8 = SciPy cg's (1644) within a few
+        st8 = engine.solve(float(sysz["dy"]), -float(sysz["dy"]), make_opts(rtol=1e-8))
+        assert abs(st8.iters - int(sysz["pcg_iters_1e8"])) <= 3
+
+
+def test_solve_deterministic(engine):
+    from mfea import make_opts
+    _sim181147(engine)
+    engine.assemble()
+    engine.solve(0.01, -0.01, make_opts(rtol=1e-10))
+    U1 = engine.displacement()
+    engine.assemble()
+    engine.solve(0.01, -0.01, make_opts(rtol=1e-10))
+    assert np.array_equal(U1, engine.displacement())
+
+
+def test_solve_csr_generic(engine):
+    """solve_system with a caller-supplied K (the reference's own API)."""
+    from mfea import make_opts
+    nodes, elems = load_mesh("sim_20251117_175809")
+    xyz = nodes[["x", "y", "z"]].values
+    K = fo.assemble_global_stiffness(xyz, elems[["n1", "n2"]].values, np.ones(len(elems), bool))
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    known, vals = fo.known_dof_map(top, bot, 0.01, -0.01)
+    Uref = fo.solve_system(K, known, vals)
+    U, st = engine.solve_csr(K.indptr, K.indices, K.data, known, vals,
+                             make_opts(rtol=1e-13, max_it=200000))
+    assert st.status == 0
+    assert rel(U, Uref) <= 1e-10
+    assert np.array_equal(U[known], vals)
+
+
+def test_fully_clamped_mesh_has_empty_solve(engine):
+    """test_I at GRIP_LENGTH 1.5: every node is a grip node, n_free = 0."""
+    from mfea import make_opts
+    nodes, elems = load_mesh("test_I")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    engine.set_mesh(xyz, elems[["n1", "n2"]].values)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    f, n_act, st = engine.step(0.01, -0.01, make_opts(rtol=1e-13), 0.018)
+    K = fo.assemble_global_stiffness(xyz, elems[["n1", "n2"]].values, np.ones(3, bool))
+    known, vals = fo.known_dof_map(top, bot, 0.01, -0.01)
+    Uref = fo.solve_system(K, known, vals)
+    assert st.n_free == 0 and st.iters == 0
+    assert np.array_equal(engine.displacement(), Uref)
+    Fref = (K @ Uref)[[3 * n + 1 for n in top]].sum()
+    assert abs(f - Fref) <= 1e-12 * max(1.0, abs(Fref))
+
+
+# ---------------------------------------------------------------------------
+# full drop-in runs against the reference's committed goldens
+# ---------------------------------------------------------------------------
+def _run_dropin(tmp_path, mesh, n_steps, dmax, grip, **kw):
+    import fea_solver as fs
+    d = tmp_path / mesh
+    shutil.copytree(os.path.join(GOLDEN, "meshes", mesh), d)
+    saved = (fs.N_STEPS, fs.DISPLACEMENT_MAX)
+    fs.N_STEPS, fs.DISPLACEMENT_MAX = n_steps, dmax
+    try:
+        fs.fea_solver(str(d), tol=grip, verbose=False, **kw)
+    finally:
+        fs.N_STEPS, fs.DISPLACEMENT_MAX = saved
+    return d / "fea_results"
+
+
+@pytest.mark.parametrize("mesh,n_steps", [("test_I", 40), ("test_X", 40), ("test_y", 100)])
+def test_dropin_reproduces_committed_goldens(tmp_path, mesh, n_steps):
+    out = _run_dropin(tmp_path, mesh, n_steps, 0.06, 0.5)
+    ref = os.path.join(GOLDEN, "ref", mesh)
+    for f in ("force_displacement.csv", "stress_record.csv", "node_displacements.csv",
+              "active_elements.csv"):
+        a, b = read_rt(out / f), read_rt(os.path.join(ref, f))
+        assert list(a.columns) == list(b.columns), f
+        assert a.shape == b.shape, f
+    U = read_rt(out / "node_displacements.csv").values[:, :-1]
+    Ur = read_rt(os.path.join(ref, "node_displacements.csv")).values[:, :-1]
+    for s in range(U.shape[0]):
+        assert rel(U[s], Ur[s]) <= 1e-10
+    F = read_rt(out / "force_displacement.csv").values
+    Fr = read_rt(os.path.join(ref, "force_displacement.csv")).values
+    assert np.array_equal(F[:, 0], Fr[:, 0])
+    assert rel(F[:, 1], Fr[:, 1]) <= 1e-10
+    S = read_rt(out / "stress_record.csv").values[:, :-1]
+    Sr = read_rt(os.path.join(ref, "stress_record.csv")).values[:, :-1]
+    assert rel(S, Sr) <= 1e-9
+    A = read_rt(out / "active_elements.csv")
+    Ar = read_rt(os.path.join(ref, "active_elements.csv"))
+    assert A.equals(Ar)
+
+
+def test_dropin_petsc_format_matches_cpp_golden(tmp_path):
+    out = _run_dropin(tmp_path, "test_I_cpp", 40, 0.06, 0.5, out_format="petsc")
+    ref = os.path.join(GOLDEN, "ref", "test_I_cpp")
+    for f in ("force_displacement.csv", "stress_record.csv", "node_displacements.csv",
+              "active_elements.csv"):
+        a = (out / f).read_text().splitlines()
+        b = open(os.path.join(ref, f)).read().splitlines()
+        assert a[0] == b[0] and len(a) == len(b), f
+    a = read_rt(out / "node_displacements.csv").values
+    b = read_rt(os.path.join(ref, "node_displacements.csv")).values
+    assert np.allclose(a, b, rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.parametrize("gen,mesh", [
+    ("gen_sim_20251117_175809_default.npz", "sim_20251117_175809"),
+    ("gen_sim_20251115_135507_grip05.npz", "sim_20251115_135507"),   # 3D mesh (z ≠ 0)
+    ("gen_test_X_default.npz", "test_X"),
+])
+def test_dropin_matches_reference_vectors(tmp_path, gen, mesh):
+    g = load_gen(gen)
+    res = _run_dropin(tmp_path, mesh, int(g["n_steps"]), float(g["dmax"]), float(g["grip"]))
+    F = read_rt(res / "force_displacement.csv").values
+    assert F.shape == g["force"].shape
+    assert rel(F[:, 1], g["force"][:, 1]) <= 1e-9
+    A = read_rt(res / "active_elements.csv").values[:, :-1].astype(bool)
+    assert np.array_equal(A, g["active"])
+    U = read_rt(res / "node_displacements.csv").values[:, :-1]
+    for k, s in enumerate(g["U_steps"]):
+        assert rel(U[s], g["U"][k]) <= 1e-10
+    S = read_rt(res / "stress_record.csv").values[:, :-1]
+    for s in range(S.shape[0]):
+        assert rel(S[s], g["stress"][s]) <= 1e-9
+
+
+def test_sim181147_force_and_failures_match_committed_golden(tmp_path):
+    """The reference's own 22k-DOF run (results/sim_20251117_181147/fea_results)."""
+    res = _run_dropin(tmp_path, "sim_20251117_181147", 40, 0.02, 1.5)
+    F = read_rt(res / "force_displacement.csv").values
+    Fr = read_rt(os.path.join(GOLDEN, "ref", "sim_20251117_181147", "force_displacement.csv")).values
+    assert rel(F[:, 1], Fr[:, 1]) <= 1e-9
+    z = np.load(os.path.join(GOLDEN, "ref", "sim_20251117_181147", "active_packed.npz"))
+    Ar = np.unpackbits(z["bits"], axis=1)[:, : int(z["n_elems"])].astype(bool)
+    A = read_rt(res / "active_elements.csv").values[:, :-1].astype(bool)
+    assert np.array_equal(A, Ar)
+
+
+# ---------------------------------------------------------------------------
+# full-size properties (C2 synthetic, 110k DOF)
+# ---------------------------------------------------------------------------
+def test_c2_properties(engine):
+    from mfea import make_opts, synth
+    xyz, e2n = synth.tiled_mesh(1, 5)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    st1 = engine.solve(0.005, -0.005, make_opts(rtol=1e-12, max_it=200000))
+    U1 = engine.displacement()
+    st2 = engine.solve(0.010, -0.010, make_opts(rtol=1e-12, max_it=200000))
+    U2 = engine.displacement()
+    assert st1.status == 0 and st2.status == 0
+    assert np.all(U1[2::3] == 0.0)                   # planar: z decouples exactly
+    assert rel(U2, 2 * U1) <= 1e-9                   # linearity in the load
+    # true residual of the free system, checked with the CPU oracle's K
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, 0.010, -0.010)
+    A, b, free = fo.free_system(K, known, vals)
+    assert np.linalg.norm(A @ U2[free] - b) <= 1e-10 * np.linalg.norm(b)

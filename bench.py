@@ -82,8 +82,8 @@ def main():
     eng.set_active(None)
     info = eng.info()
     dy = fs.DISPLACEMENT_MAX * a.load_step / (fs.N_STEPS - 1)
-    opts = make_opts(rtol=a.rtol, max_it=200000,
-                     precond=PC_BLOCK_JACOBI if a.precond == "bjacobi" else PC_JACOBI)
+    pc = PC_BLOCK_JACOBI if a.precond == "bjacobi" else PC_JACOBI
+    opts = make_opts(rtol=a.rtol, max_it=200000, precond=pc)
 
     def one_step():
         eng.set_active(None)                       # every step starts from the intact mesh
@@ -112,15 +112,18 @@ def main():
 
     force, n_active, st = stats[-1]
     iters = st.iters
-    # ---- roofline of the dominant kernel (SpMV), live HIP events on its stream
-    spmv_ms = eng.profile_spmv(reps=100)
+    # ---- roofline of the dominant kernel (fused SpMV + CG-CG iteration),
+    # live HIP events on the engine's stream
+    iter_ms = eng.profile_iteration(pc, reps=200)
     nf = info["n_free_nodes"]
     inc = info["free_incidences"]
-    # algorithmic bytes per SpMV launch: per free row
-    # diag block 48 B + row_len 4 B + p_i 24 B + q_i 24 B; per valid slot
-    # column 4 B + value block 48 B (neighbour p_j gathers are re-reads of p).
-    spmv_bytes = nf * (48 + 4 + 24 + 24) + inc * (4 + 48)
-    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    # algorithmic bytes per launch: per free row, vectors
+    # read r,s,w,p,x (5×24 B) + M⁻¹ (24 B Jacobi / 48 B block) and written
+    # p,x,s,r,w (5×24 B), diag block 48 B, row_len 4 B; per valid slot column
+    # 4 B + value block 48 B.  Neighbour gathers re-read vectors already counted.
+    minv = 48 if pc == PC_BLOCK_JACOBI else 24
+    iter_bytes = nf * (120 + minv + 120 + 48 + 4) + inc * (4 + 48)
+    achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(a.traffic):
         try:
@@ -154,15 +157,15 @@ def main():
         "step_breakdown_ms": {"assemble": st.t_assemble_ms, "rhs": st.t_rhs_ms,
                               "pcg": st.t_solve_ms, "post": st.t_post_ms},
         "roofline": {
-            "kernel": "k_spmv_sell",
+            "kernel": "k_cg_iter (fused SpMV + CG-CG update + reduction)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": PEAK_HBM_GBPS,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBPS,
             "traffic": traffic,
-            "alg_bytes_per_launch": spmv_bytes,
-            "avg_launch_us": spmv_ms * 1e3,
+            "alg_bytes_per_launch": iter_bytes,
+            "avg_launch_us": iter_ms * 1e3,
         },
     }
 

@@ -155,9 +155,11 @@ typedef struct {
   int32_t pad;
 } mfea_info;
 int mfea_get_info(mfea_handle* h, mfea_info* info);
-/* Launches the PCG SpMV kernel `reps` times on the handle's stream between two
- * HIP events (current p vector) and returns the average launch duration. */
-int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms);
+/* Launches the dominant kernel — the fused SpMV + single-reduction CG iteration —
+ * `reps` times on the handle's stream between two HIP events (on the current
+ * vectors, identical work each launch) and returns the average launch duration.
+ * Call after mfea_solve (it overwrites the solver state). */
+int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------- */
 /* Replaces the PETSC_COMM_WORLD row-block distribution of

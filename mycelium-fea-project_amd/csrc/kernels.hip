@@ -6,6 +6,7 @@
 // have products fused into adds behind our back.  The PCG kernels use explicit
 // fma() where fusion is wanted.
 #include "kernels.hpp"
+#include "device_util.hpp"
 
 #include <math.h>
 
@@ -20,79 +21,6 @@ int64_t grid_elementwise(int64_t n) {
   return g < 1 ? 1 : (g > 2048 ? 2048 : g);  // ≥ 8 blocks per CU, grid-stride beyond
 }
 
-// ---------------------------------------------------------------------------
-// deterministic block reduction + last-block finalize (agent-scope ticket).
-// Every block writes its partial sums, the block that draws the last ticket
-// sums all partials in a fixed order and writes `out`.  Result is bitwise
-// reproducible for a fixed grid size.  Protocol: cdna_hip_programming.md §6
-// Guideline 16 (release → drained wait → relaxed agent atomic; acquire in the
-// last block → wait → barrier → plain loads).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-template <int NV>
-__device__ __forceinline__ bool block_publish(double (&v)[NV], double* partials,
-                                              unsigned* ticket, double* out) {
-  __shared__ double lds[(kBlock / 64) * NV];
-  __shared__ int is_last;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned G = gridDim.x;
-#pragma unroll
-  for (int c = 0; c < NV; ++c) v[c] = wave_sum(v[c]);
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) lds[wid * NV + c] = v[c];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      double s = lds[c];
-      for (int w = 1; w < kBlock / 64; ++w) s += lds[w * NV + c];
-      partials[(size_t)c * G + blockIdx.x] = s;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (t == G - 1);
-  }
-  __syncthreads();
-  if (!is_last) return false;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  double s[NV];
-#pragma unroll
-  for (int c = 0; c < NV; ++c) s[c] = 0.0;
-  for (unsigned i = threadIdx.x; i < G; i += kBlock) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) s[c] += partials[(size_t)c * G + i];
-  }
-#pragma unroll
-  for (int c = 0; c < NV; ++c) s[c] = wave_sum(s[c]);
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) lds[wid * NV + c] = s[c];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      double t = lds[c];
-      for (int w = 1; w < kBlock / 64; ++w) t += lds[w * NV + c];
-      out[c] = t;
-    }
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return true;
-}
 
 // ---------------------------------------------------------------------------
 // Element stiffness S_e (the 3×3 block of Ke = [[S,−S],[−S,S]]),
@@ -174,25 +102,6 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __
 // x=0, r=b, z=M⁻¹b, p=z.  Known rows: x = prescribed (0, dy, 0), p = 0 so the
 // free-row SpMV sees K_fk·p = 0.  Reduces (r·z, b·b, z·z).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void sym_apply(const double B[6], const double v[3], double o[3]) {
-  o[0] = fma(B[0], v[0], fma(B[1], v[1], B[2] * v[2]));
-  o[1] = fma(B[1], v[0], fma(B[3], v[1], B[4] * v[2]));
-  o[2] = fma(B[2], v[0], fma(B[4], v[1], B[5] * v[2]));
-}
-
-__device__ __forceinline__ void sym_inverse(const double A[6], double B[6]) {
-  // adjugate / determinant of a symmetric 3×3 (SPD here)
-  const double c00 = A[3] * A[5] - A[4] * A[4];
-  const double c01 = A[2] * A[4] - A[1] * A[5];
-  const double c02 = A[1] * A[4] - A[2] * A[3];
-  const double c11 = A[0] * A[5] - A[2] * A[2];
-  const double c12 = A[1] * A[2] - A[0] * A[4];
-  const double c22 = A[0] * A[3] - A[1] * A[1];
-  const double det = A[0] * c00 + A[1] * c01 + A[2] * c02;
-  const double id = 1.0 / det;
-  B[0] = c00 * id; B[1] = c01 * id; B[2] = c02 * id;
-  B[3] = c11 * id; B[4] = c12 * id; B[5] = c22 * id;
-}
 
 __global__ __launch_bounds__(kBlock) void k_rhs_init(
     int64_t N, int64_t nf, const int32_t* __restrict__ slice_ptr, const int32_t* __restrict__ row_len,

@@ -21,12 +21,33 @@ constexpr int kBlock = 256;  // 4 wavefronts
 // PCG per-iteration scalar slot (see DESIGN.md "PCG scalar slots").
 // v[0] = p·q, v[1] = r·z, v[2] = r·r, v[3] = z·z (v[1..3] reduced together),
 // flag: 0 RUN, 1 STOP (propagated / after done), 2 BREAKDOWN.
+// Single-reduction CG (Chronopoulos–Gear) uses v[0] = γ = r·u, v[1] = δ = w·u,
+// v[2] = r·r, v[3] = u·u, and alpha = α of the iteration that consumed the slot.
 struct Slot {
   double v[4];
+  double alpha;
   int32_t flag;
-  int32_t pad[3];
+  int32_t pad;
 };
-enum SlotFlag : int32_t { kRun = 0, kStop = 1, kBreakdown = 2 };
+enum SlotFlag : int32_t { kRun = 0, kStop = 1, kBreakdown = 2, kInit = 3 };
+
+// Device pointers of the node-block (SELL-64) operator and the CG-CG state.
+struct SellOp {
+  int64_t N, nf, G;
+  const int32_t* slice_ptr;
+  const int32_t* row_len;
+  const int32_t* s_col;
+  const double* val;   // 6 × G
+  const double* diag;  // 6 × N
+};
+struct CgVecs {
+  double* x;     // 3N (known rows hold the prescribed values)
+  double* p;     // 3N
+  double* r[2];  // double-buffered by iteration parity
+  double* s[2];
+  double* w[2];
+  double* dinv;  // 3N (Jacobi) or 6N (3×3 block Jacobi); 0 on known rows
+};
 
 struct SolveState {
   double tol2;     // stopping threshold on the chosen norm²
@@ -98,6 +119,23 @@ void launch_spmv_csr(hipStream_t s, int j, int64_t n, const int64_t* indptr,
                      const int32_t* indices, const double* data, const uint8_t* known,
                      double reg, const double* p, double* q, Slot* slots, const SolveState* st,
                      double* partials, unsigned* ticket);
+
+// ---- single-reduction CG on the SELL operator (one kernel per iteration) ----
+// k_cg_rhs: b, M⁻¹, x, r₀ = b, p = s = w = 0; reduces (b·b, u₀·u₀) into red[0..1].
+void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double dy_top,
+                   double dy_bot, double reg, int precond, const CgVecs& v, double* partials,
+                   unsigned* ticket, double* red_out);
+// k_cg_first: w₀ = A u₀; (γ₀, δ₀, r·r, u·u) → slots[1]; slots[0].flag = kInit.
+void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
+                     Slot* slots, double* partials, unsigned* ticket);
+// iteration j of a chunk: reads slots[j], slots[j+1], writes slots[j+2].
+void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
+                    Slot* slots, const SolveState* st, double* partials, unsigned* ticket);
+void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st);
+void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
+                             int max_it, double reg, SolveState* st);
+int cg_block_size(int64_t rows);
+int64_t cg_grid(int64_t rows);
 
 int64_t grid_rows(int64_t rows);
 int64_t grid_elementwise(int64_t n);

@@ -85,6 +85,35 @@ def assemble_global_stiffness(coords, e2n, active):
     return sp.csr_matrix((Ke.ravel(), (rows, cols)), shape=(n_dof, n_dof))
 
 
+def stiffness_magnitude(p1s, p2s, E=E_MOD, A=AREA, I=INERTIA):
+    """|axial term| + |bending term| per Ke entry: the scale of the rounding
+    error of Ke.  S = t·k_ax + (δ−t)·k_b cancels catastrophically where
+    k_ax ≈ k_b (L ≈ 0.11 mm), so a 1-ulp difference in L³ (NumPy's SIMD pow is
+    ≤1 ulp, not correctly rounded) moves S by far more than 1 ulp of S."""
+    v = np.asarray(p2s, dtype=np.float64) - np.asarray(p1s, dtype=np.float64)
+    L = np.sqrt((v * v).sum(axis=1))
+    Ls = np.where(L < 1e-12, 1e-12, L)
+    n = v / Ls[:, None]
+    TT = n[:, :, None] * n[:, None, :]
+    m3 = np.abs(TT * ((E * A) / Ls)[:, None, None]) + \
+        np.abs((np.eye(3)[None] - TT) * (12 * E * I / Ls ** 3)[:, None, None])
+    return np.block([[m3, m3], [m3, m3]])
+
+
+def assemble_magnitude(coords, e2n, active):
+    """Σ over elements of stiffness_magnitude, in the CSR pattern of K."""
+    coords = np.asarray(coords, dtype=np.float64)
+    e2n = np.asarray(e2n, dtype=np.int64)
+    eidx = np.flatnonzero(np.asarray(active, dtype=bool))
+    n1, n2 = e2n[eidx, 0], e2n[eidx, 1]
+    M = stiffness_magnitude(coords[n1], coords[n2])
+    dof = np.concatenate([3 * n1[:, None] + np.arange(3), 3 * n2[:, None] + np.arange(3)], axis=1)
+    rows = np.repeat(dof, 6, axis=1).ravel()
+    cols = np.tile(dof, (1, 6)).ravel()
+    n = 3 * coords.shape[0]
+    return sp.csr_matrix((M.ravel(), (rows, cols)), shape=(n, n))
+
+
 def known_dof_map(top_nodes, bot_nodes, dy_top, dy_bot):
     """Prescribed DOFs, src/fea_solver.py:223-242.
 
@@ -170,15 +199,22 @@ def grip_nodes(coords, node_ids, tol=GRIP_LENGTH):
 
 
 def element_strain(coords, e2n, U):
-    """Axial strain of every element, src/fea_solver.py:260-270 (no L clamp)."""
-    n1 = e2n[:, 0]
-    n2 = e2n[:, 1]
-    v = coords[n2] - coords[n1]
-    L = np.sqrt((v * v).sum(axis=1))
-    with np.errstate(invalid="ignore", divide="ignore"):
-        n = v / L[:, None]
-        du = U.reshape(-1, 3)[n2] - U.reshape(-1, 3)[n1]
-        return ((n[:, 0] * du[:, 0] + n[:, 1] * du[:, 1]) + n[:, 2] * du[:, 2]) / L
+    """Axial strain of every element, src/fea_solver.py:260-270 (no L clamp).
+
+    The reference's ``np.dot(n, u2 - u1)`` on length-3 vectors is BLAS ddot, an
+    FMA chain; the oracle's C helper (cpu_fea.c:cpu_strain) restates it exactly."""
+    import ctypes as C
+    import cpu_fea
+    lib = cpu_fea.lib()
+    e2n = np.ascontiguousarray(e2n, dtype=np.int64)
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    U = np.ascontiguousarray(U, dtype=np.float64)
+    out = np.empty(e2n.shape[0])
+    P = C.c_void_p
+    lib.cpu_strain.argtypes = [C.c_int64, P, P, P, P]
+    lib.cpu_strain(e2n.shape[0], e2n.ctypes.data_as(P), coords.ctypes.data_as(P),
+                   U.ctypes.data_as(P), out.ctypes.data_as(P))
+    return out
 
 
 def run_fea(coords, node_ids, e2n, tol=GRIP_LENGTH, n_steps=N_STEPS,

@@ -44,9 +44,16 @@ def test_element_stiffness_matches_oracle(engine):
     Ke, L = engine.element_stiffness(p1, p2, fo.E_MOD, fo.AREA, fo.INERTIA)
     Ko, Lo = fo.bar_stiffness_bulk(p1, p2)
     assert np.array_equal(L, Lo)
-    # only L³ may differ (double-double cube vs NumPy pow, ≤1 ulp) → ≤ 2 ulp on Ke
-    assert ulp_diff(Ke, Ko) <= 2.0
+    # Only L³ may differ (double-double cube vs NumPy's ≤1-ulp pow); the bound is
+    # 4ε × (|axial term| + |bending term|) per entry — the rounding-error scale
+    # of S = t·k_ax + (δ−t)·k_b, which cancels where k_ax ≈ k_b.
+    M = fo.stiffness_magnitude(p1, p2)
+    assert np.all(np.abs(Ke - Ko) <= 4 * np.finfo(float).eps * M)
     assert np.mean(Ke == Ko) > 0.9
+
+
+def _assembly_bound(xyz, e2n, active):
+    return 4 * np.finfo(float).eps * fo.assemble_magnitude(xyz, e2n, active).data
 
 
 # ---------------------------------------------------------------------------
@@ -57,14 +64,16 @@ def test_assembly_matches_reference_K(engine, mesh):
     nodes, elems = load_mesh(mesh)
     z = np.load(os.path.join(GOLDEN, f"K0_{mesh}.npz"))
     Kref = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=tuple(z["shape"]))
-    engine.set_mesh(nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values)
+    xyz, e2n = nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values
+    engine.set_mesh(xyz, e2n)
     engine.set_bc([], [])
     engine.set_active(None)
     engine.assemble()
     ip, ix, dv = engine.export_csr()
     assert np.array_equal(ip, Kref.indptr)
     assert np.array_equal(ix, Kref.indices)
-    assert ulp_diff(dv, Kref.data) <= 4.0
+    assert np.all(np.abs(dv - Kref.data) <= _assembly_bound(xyz, e2n, np.ones(len(e2n), bool)))
+    assert np.mean(dv == Kref.data) > 0.9
 
 
 def test_assembly_with_inactive_elements(engine):
@@ -81,7 +90,7 @@ def test_assembly_with_inactive_elements(engine):
     ip, ix, dv = engine.export_csr()
     assert np.array_equal(ip, Kref.indptr)
     assert np.array_equal(ix, Kref.indices)
-    assert ulp_diff(dv, Kref.data) <= 4.0
+    assert np.all(np.abs(dv - Kref.data) <= _assembly_bound(xyz, e2n, active))
 
 
 # ---------------------------------------------------------------------------

@@ -256,6 +256,28 @@ int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, Solve
   return 0;
 }
 
+int finish_solve(mfea_handle* h, const mfea_solve_opts* o, int64_t nf, const SolveState& fin,
+                 mfea_stats* st) {
+  (void)o;
+  HIPC(hipEventRecord(h->ev[3], h->stream));
+  HIPC(hipEventSynchronize(h->ev[3]));
+  if (st) {
+    st->iters = fin.iters;
+    st->status = fin.status;
+    st->bnorm = std::sqrt(fin.bb0);
+    st->relres = fin.res0 > 0 ? std::sqrt(fin.res_final / fin.res0) : 0.0;
+    st->n_free = 3 * nf;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+    st->t_rhs_ms = ms;
+    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+    st->t_solve_ms = ms;
+  }
+  if (fin.status == -4) return fail(MFEA_EMAXIT, "PCG reached max_it without converging");
+  if (fin.status == -5) return fail(MFEA_EBREAKDOWN, "PCG breakdown (p·Ap <= 0 or non-finite)");
+  return 0;
+}
+
 int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
                mfea_stats* st) {
   const Pattern& P = h->P;
@@ -263,6 +285,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   const int64_t nf = P.n_free;
   const int precond = o->precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
   int chunk = o->chunk > 0 ? std::min(o->chunk, kMaxChunk) : 32;
+  chunk += chunk & 1;  // even: k_cg_iter takes the r/s/w buffer parity from j
   const SellOp op = sell_op(h);
   const CgVecs v = cg_vecs(h);
   HIPC(hipEventRecord(h->ev[1], s));
@@ -270,9 +293,26 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
                 h->tickets.ptr + 0, h->red.ptr);
   launch_cg_init_finalize(s, h->red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
                           h->state.ptr);
-  launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->partials.ptr, h->tickets.ptr + 2);
+  launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->state.ptr, h->partials.ptr,
+                  h->tickets.ptr + 2);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
+  // MFEA_NO_GRAPH=1: launch the chunk kernels eagerly (profilers that do not
+  // follow hipGraph replays; same kernels, same order)
+  static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  if (no_graph) {
+    SolveState fin;
+    int rc = drive_chunks(
+        h, chunk, o->max_it,
+        [&]() -> int {
+          enqueue_chunk_sell(h, chunk, precond);
+          HIPC(hipGetLastError());
+          return 0;
+        },
+        &fin);
+    if (rc) return rc;
+    return finish_solve(h, o, nf, fin, st);
+  }
   if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != precond) {
     destroy_graph(h);
     hipGraph_t g;
@@ -294,23 +334,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
       },
       &fin);
   if (rc) return rc;
-  HIPC(hipEventRecord(h->ev[3], s));
-  HIPC(hipEventSynchronize(h->ev[3]));
-  if (st) {
-    st->iters = fin.iters;
-    st->status = fin.status;
-    st->bnorm = std::sqrt(fin.bb0);
-    st->relres = fin.res0 > 0 ? std::sqrt(fin.res_final / fin.res0) : 0.0;
-    st->n_free = 3 * nf;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
-    st->t_rhs_ms = ms;
-    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
-    st->t_solve_ms = ms;
-  }
-  if (fin.status == -4) return fail(MFEA_EMAXIT, "PCG reached max_it without converging");
-  if (fin.status == -5) return fail(MFEA_EBREAKDOWN, "PCG breakdown (p·Ap <= 0 or non-finite)");
-  return 0;
+  return finish_solve(h, o, nf, fin, st);
 }
 
 int assemble_impl(mfea_handle* h, mfea_stats* st) {
@@ -739,6 +763,9 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   std::memset(two, 0, sizeof(two));
   two[0].flag = kInit;
   for (int c = 0; c < 4; ++c) two[1].v[c] = 1.0;
+  two[1].alpha = 1.0;
+  two[1].beta = 0.0;
+  two[1].res = 1.0;
   two[1].flag = kRun;
   HIPC(hipMemcpyAsync(h->slots.ptr, two, sizeof(two), hipMemcpyHostToDevice, s));
   launch_cg_iter(s, 0, op, pc, v, h->slots.ptr, h->state.ptr, h->partials.ptr,

@@ -5,13 +5,18 @@
 //   p_i = u_i + β_i p_{i−1}      s_i = w_i + β_i s_{i−1}
 //   x_{i+1} = x_i + α_i p_i      r_{i+1} = r_i − α_i s_i
 //   u_{i+1} = M⁻¹ r_{i+1}        w_{i+1} = A u_{i+1}
-//   γ = (r,u), δ = (w,u);  β_i = γ_i/γ_{i−1},  α_i = γ_i / (δ_i − β_i γ_i / α_{i−1})
+//   γ = (r,u), δ = (w,u);  β_{i+1} = γ_{i+1}/γ_i,  α_{i+1} = γ_{i+1} / (δ_{i+1} − β_{i+1} γ_{i+1} / α_i)
 // In exact arithmetic these are the iterates of textbook PCG (the reference's
 // KSPCG, src/fea_petsc.cpp:328); one fused reduction (γ, δ, ‖r‖², ‖u‖²) per
 // iteration instead of two.  The SpMV w = A u needs u_j of neighbour rows whose
 // owners update r, s, w in the same launch, so r, s, w are double-buffered by
 // iteration parity and each row recomputes its neighbours' u_j from the
 // previous-iteration values: u_j = M_j⁻¹ (r_j − α (w_j + β s_j)).
+//
+// Scalar hand-off: the block that completes an iteration's reduction (last
+// ticket) also forms α, β and the stopping norm for the next iteration and
+// writes them into the next slot, so an iteration kernel starts with plain
+// scalar loads and no divisions on its critical path.
 #include "device_util.hpp"
 #include "kernels.hpp"
 
@@ -54,6 +59,25 @@ __device__ __forceinline__ void block_mac(const double V[6], const double u[3], 
   y[0] = fma(V[0], u[0], fma(V[1], u[1], fma(V[2], u[2], y[0])));
   y[1] = fma(V[1], u[0], fma(V[3], u[1], fma(V[4], u[2], y[1])));
   y[2] = fma(V[2], u[0], fma(V[4], u[1], fma(V[5], u[2], y[2])));
+}
+
+// Finalize the scalars of slot `s` from its freshly reduced sums (thread 0 of
+// the reducing block).  prev = the slot whose α, γ the iteration consumed
+// (nullptr for the first reduction: β = 0, α = γ/δ).
+__device__ __forceinline__ void finalize_slot(Slot* s, const Slot* prev, int norm) {
+  const double g = s->v[0], d = s->v[1];
+  double beta = 0.0, den = d;
+  if (prev) {
+    beta = g / prev->v[0];
+    den = d - beta * g / prev->alpha;
+  }
+  const double alpha = g / den;
+  s->alpha = alpha;
+  s->beta = beta;
+  s->res = norm == 1 ? s->v[3] : s->v[2];
+  const bool ok = (den > 0.0) && isfinite(alpha) && isfinite(beta);
+  // γ = 0 ⇔ r = 0: converged, not a breakdown (the stopping test catches it)
+  s->flag = (ok || g == 0.0) ? kRun : kBreakdown;
 }
 
 // ---------------------------------------------------------------------------
@@ -153,10 +177,11 @@ __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, 
   st->status = 0;
 }
 
-// w₀ = A u₀ and the first fused reduction → slots[1]; slots[0] marks "no previous".
+// w₀ = A u₀ and the first fused reduction → slots[1] (α₀ = γ₀/δ₀, β₀ = 0).
 template <bool BLOCK, int BS>
 __global__ __launch_bounds__(BS) void k_cg_first(SellOp op, double reg, CgVecs v, Slot* slots,
-                                                 double* partials, unsigned* ticket) {
+                                                 const SolveState* st, double* partials,
+                                                 unsigned* ticket) {
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int64_t G = op.G;
@@ -193,19 +218,29 @@ __global__ __launch_bounds__(BS) void k_cg_first(SellOp op, double reg, CgVecs v
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    slots[0].flag = kInit;
-    slots[0].alpha = 0.0;
-  }
-  if (block_publish<4, BS>(acc, partials, ticket, slots[1].v) && threadIdx.x == 0) {
-    slots[1].flag = kRun;
-    slots[1].alpha = 0.0;
-  }
+  if (block_publish<4, BS>(acc, partials, ticket, slots[1].v) && threadIdx.x == 0)
+    finalize_slot(&slots[1], nullptr, st->norm);
 }
 
 __device__ __forceinline__ bool cg_running(const Slot& cur, const SolveState* st, int j) {
-  const double res = st->norm == 1 ? cur.v[3] : cur.v[2];
-  return cur.flag == kRun && res > st->tol2 && (st->base + j) < st->max_it;
+  return cur.flag == kRun && cur.res > st->tol2 && (st->base + j) < st->max_it;
+}
+
+// neighbour contribution y += V · M_c⁻¹ (r_c − α (w_c + β s_c))
+template <bool BLOCK>
+__device__ __forceinline__ void neighbour_mac(const double V[6], int64_t c, double alpha, double beta,
+                                              const double* __restrict__ r_old,
+                                              const double* __restrict__ s_old,
+                                              const double* __restrict__ w_old,
+                                              const double* __restrict__ dinv, double y[3]) {
+  double rc[3], sc[3], wc[3], uc[3];
+  load3(r_old, c, rc);
+  load3(s_old, c, sc);
+  load3(w_old, c, wc);
+#pragma unroll
+  for (int a = 0; a < 3; ++a) rc[a] = fma(-alpha, fma(beta, sc[a], wc[a]), rc[a]);
+  apply_minv<BLOCK>(dinv, c, rc, uc);
+  block_mac(V, uc, y);
 }
 
 // ---------------------------------------------------------------------------
@@ -218,48 +253,49 @@ template <bool BLOCK, int BS>
 __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
                                                 const SolveState* st, double* partials,
                                                 unsigned* ticket) {
-  const Slot cur = slots[j + 1];
-  if (!cg_running(cur, st, j)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) slots[j + 2].flag = kStop;
-    return;
-  }
-  const Slot prev = slots[j];
-  double beta, den;
-  if (prev.flag == kInit) {
-    beta = 0.0;
-    den = cur.v[1];
-  } else {
-    beta = cur.v[0] / prev.v[0];
-    den = cur.v[1] - beta * cur.v[0] / prev.alpha;
-  }
-  const double alpha = cur.v[0] / den;
-  if (!(den > 0.0) || !isfinite(alpha) || !isfinite(beta)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      slots[j + 2].v[0] = slots[j + 2].v[1] = slots[j + 2].v[2] = slots[j + 2].v[3] = 0.0;
-      slots[j + 2].flag = kBreakdown;
-    }
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) slots[j + 1].alpha = alpha;
-  const int par = (st->base + j) & 1;
+  const double alpha = slots[j + 1].alpha, beta = slots[j + 1].beta, res = slots[j + 1].res;
+  const int flag = slots[j + 1].flag;
+  const bool go = (flag == kRun) & (res > st->tol2) & ((st->base + j) < st->max_it);
+  const double reg = st->reg;
+  // chunks have even length and base is a multiple of the chunk, so the
+  // buffer parity is a launch constant: vector addresses need no scalar load
+  const int par = j & 1;
   const double* __restrict__ r_old = v.r[par];
   const double* __restrict__ s_old = v.s[par];
   const double* __restrict__ w_old = v.w[par];
   double* __restrict__ r_new = v.r[par ^ 1];
   double* __restrict__ s_new = v.s[par ^ 1];
   double* __restrict__ w_new = v.w[par ^ 1];
-  const double reg = st->reg;
-  const int64_t G = op.G;
+  double* __restrict__ xv = v.x;
+  double* __restrict__ pv = v.p;
+  const double* __restrict__ dinv = v.dinv;
+  const double* __restrict__ diag = op.diag;
+  const double* __restrict__ val = op.val;
+  const int32_t* __restrict__ s_col = op.s_col;
+  const int32_t* __restrict__ row_len = op.row_len;
+  const int32_t* __restrict__ slice_ptr = op.slice_ptr;
+  const int64_t G = op.G, N = op.N, nf = op.nf;
+  // No early exit on `go`: the scalar loads (SMEM) and the row's vector loads
+  // (VMEM) are in flight together and only the stores/publish are predicated.
+  // An iteration queued after convergence costs one wasted pass (≤ 2 chunks).
   const int64_t stride = (int64_t)gridDim.x * BS;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t row = (int64_t)blockIdx.x * BS + threadIdx.x; row < op.nf; row += stride) {
-    double ro[3], so[3], wo[3], pp[3], xx[3], uo[3], rn[3], un[3], sn[3];
+  for (int64_t row = (int64_t)blockIdx.x * BS + threadIdx.x; row - threadIdx.x % 64 < nf;
+       row += stride) {
+    // every lane of a wave shares the slice → scalar load of its slot offset
+    const int slice = __builtin_amdgcn_readfirstlane((int)(row >> 6));
+    const int64_t base = (int64_t)slice_ptr[slice] * 64 + (row & 63);
+    if (row >= nf) continue;
+    const int len = row_len[row];
+    double ro[3], so[3], wo[3], pp[3], xx[3], uo[3], rn[3], un[3], sn[3], D[6];
     load3(r_old, row, ro);
     load3(s_old, row, so);
     load3(w_old, row, wo);
-    load3(v.p, row, pp);
-    load3(v.x, row, xx);
-    apply_minv<BLOCK>(v.dinv, row, ro, uo);
+    load3(pv, row, pp);
+    load3(xv, row, xx);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) D[c] = diag[(int64_t)c * N + row];
+    apply_minv<BLOCK>(dinv, row, ro, uo);
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       pp[a] = fma(beta, pp[a], uo[a]);
@@ -267,36 +303,41 @@ __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot
       xx[a] = fma(alpha, pp[a], xx[a]);
       rn[a] = fma(-alpha, sn[a], ro[a]);
     }
-    apply_minv<BLOCK>(v.dinv, row, rn, un);
-    store3(v.p, row, pp);
-    store3(v.x, row, xx);
-    store3(s_new, row, sn);
-    store3(r_new, row, rn);
-    double D[6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) D[c] = op.diag[(int64_t)c * op.N + row];
+    apply_minv<BLOCK>(dinv, row, rn, un);
     D[0] += reg;
     D[3] += reg;
     D[5] += reg;
     double y[3] = {0.0, 0.0, 0.0};
     block_mac(D, un, y);
-    const int64_t base = (int64_t)op.slice_ptr[row >> 6] * 64 + (row & 63);
-    const int len = op.row_len[row];
-    for (int k = 0; k < len; ++k) {
-      const int64_t idx = base + (int64_t)k * 64;
-      const int64_t c = op.s_col[idx];
-      double V[6], rc[3], sc[3], wc[3], uc[3];
+    // slots two at a time: both columns, then both gathers, in flight together
+    int k = 0;
+    for (; k + 1 < len; k += 2) {
+      const int64_t i0 = base + (int64_t)k * 64, i1 = i0 + 64;
+      const int64_t c0 = s_col[i0], c1 = s_col[i1];
+      double V0[6], V1[6];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) V[q] = op.val[q * G + idx];
-      load3(r_old, c, rc);
-      load3(s_old, c, sc);
-      load3(w_old, c, wc);
-#pragma unroll
-      for (int a = 0; a < 3; ++a) rc[a] = fma(-alpha, fma(beta, sc[a], wc[a]), rc[a]);
-      apply_minv<BLOCK>(v.dinv, c, rc, uc);
-      block_mac(V, uc, y);
+      for (int q = 0; q < 6; ++q) {
+        V0[q] = val[q * G + i0];
+        V1[q] = val[q * G + i1];
+      }
+      neighbour_mac<BLOCK>(V0, c0, alpha, beta, r_old, s_old, w_old, dinv, y);
+      neighbour_mac<BLOCK>(V1, c1, alpha, beta, r_old, s_old, w_old, dinv, y);
     }
-    store3(w_new, row, y);
+    if (k < len) {
+      const int64_t i0 = base + (int64_t)k * 64;
+      const int64_t c0 = s_col[i0];
+      double V0[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) V0[q] = val[q * G + i0];
+      neighbour_mac<BLOCK>(V0, c0, alpha, beta, r_old, s_old, w_old, dinv, y);
+    }
+    if (go) {
+      store3(pv, row, pp);
+      store3(xv, row, xx);
+      store3(s_new, row, sn);
+      store3(r_new, row, rn);
+      store3(w_new, row, y);
+    }
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       acc[0] = fma(rn[a], un[a], acc[0]);
@@ -305,14 +346,18 @@ __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot
       acc[3] = fma(un[a], un[a], acc[3]);
     }
   }
-  if (block_publish<4, BS>(acc, partials, ticket, slots[j + 2].v) && threadIdx.x == 0) {
-    slots[j + 2].flag = kRun;
-    slots[j + 2].alpha = 0.0;
+  if (!go) {
+    // converged / stopped / max_it: propagate STOP (a breakdown was flagged by
+    // the reducing block of the previous iteration and stays in that slot)
+    if (blockIdx.x == 0 && threadIdx.x == 0) slots[j + 2].flag = kStop;
+    return;
   }
+  if (block_publish<4, BS>(acc, partials, ticket, slots[j + 2].v) && threadIdx.x == 0)
+    finalize_slot(&slots[j + 2], &slots[j + 1], st->norm);
 }
 
-// End of a chunk: record where the iteration stopped, or roll the two newest
-// slots to the front.  Once done, slots[1] is poisoned STOP so chunks the host
+// End of a chunk: record where the iteration stopped, or roll the newest slot
+// to the front.  Once done, slots[1] is poisoned STOP so chunks the host
 // already queued are no-ops.
 __global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -320,10 +365,10 @@ __global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st) {
   for (int j = 0; j <= chunk; ++j) {
     const Slot& cur = slots[j + 1];
     if (!cg_running(cur, st, j)) {
-      const double res = st->norm == 1 ? cur.v[3] : cur.v[2];
+      const double res = cur.res;
       st->iters = st->base + j;
       st->res_final = res;
-      if (cur.flag == kBreakdown) st->status = -5;
+      if (cur.flag == kBreakdown || (cur.flag == kRun && !isfinite(res))) st->status = -5;
       else if (cur.flag == kRun && res <= st->tol2) st->status = 0;
       else if (cur.flag == kRun) st->status = -4;
       else st->status = -5;
@@ -332,7 +377,6 @@ __global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st) {
       return;
     }
   }
-  slots[0] = slots[chunk];
   slots[1] = slots[chunk + 1];
   st->base += chunk;
 }
@@ -358,22 +402,22 @@ void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, doub
 
 template <int BS>
 static void first_bs(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, double* partials, unsigned* ticket) {
+                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
   const dim3 grid((unsigned)cg_grid(op.nf));
   if (precond == 1)
-    hipLaunchKernelGGL((k_cg_first<true, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, partials,
-                       ticket);
+    hipLaunchKernelGGL((k_cg_first<true, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, st,
+                       partials, ticket);
   else
-    hipLaunchKernelGGL((k_cg_first<false, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, partials,
-                       ticket);
+    hipLaunchKernelGGL((k_cg_first<false, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, st,
+                       partials, ticket);
 }
 
 void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, double* partials, unsigned* ticket) {
+                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
   if (cg_block_size(op.nf) == 64)
-    first_bs<64>(s, op, reg, precond, v, slots, partials, ticket);
+    first_bs<64>(s, op, reg, precond, v, slots, st, partials, ticket);
   else
-    first_bs<256>(s, op, reg, precond, v, slots, partials, ticket);
+    first_bs<256>(s, op, reg, precond, v, slots, st, partials, ticket);
 }
 
 template <int BS>

@@ -55,14 +55,27 @@ __device__ __forceinline__ bool block_publish(double (&v)[NV], double* partials,
   }
   __syncthreads();
   if (!is_last) return false;
+  // U partials per lane in flight per pass: one memory round trip covers
+  // BS·U blocks (the loads are independent; hipcc waits once per pass).
+  constexpr int U = BS >= 256 ? 8 : 16;
   double s[NV];
 #pragma unroll
   for (int c = 0; c < NV; ++c) s[c] = 0.0;
-  for (unsigned i = threadIdx.x; i < G; i += BS) {
+  for (unsigned i0 = threadIdx.x; i0 < G; i0 += BS * U) {
+    double t[U][NV];
 #pragma unroll
-    for (int c = 0; c < NV; ++c)
-      s[c] += __hip_atomic_load(&partials[(size_t)c * G + i], __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
+    for (int u = 0; u < U; ++u) {
+      const unsigned i = i0 + u * BS;
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        t[u][c] = i < G ? __hip_atomic_load(&partials[(size_t)c * G + i], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < NV; ++c) s[c] += t[u][c];
   }
 #pragma unroll
   for (int c = 0; c < NV; ++c) s[c] = wave_sum(s[c]);

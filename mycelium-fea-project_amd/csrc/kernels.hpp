@@ -22,10 +22,15 @@ constexpr int kBlock = 256;  // 4 wavefronts
 // v[0] = p·q, v[1] = r·z, v[2] = r·r, v[3] = z·z (v[1..3] reduced together),
 // flag: 0 RUN, 1 STOP (propagated / after done), 2 BREAKDOWN.
 // Single-reduction CG (Chronopoulos–Gear) uses v[0] = γ = r·u, v[1] = δ = w·u,
-// v[2] = r·r, v[3] = u·u, and alpha = α of the iteration that consumed the slot.
+// v[2] = r·r, v[3] = u·u (reduced together), and the scalars the next
+// iteration consumes, computed once by the reducing block: alpha, beta, res
+// (the stopping norm², r·r or u·u).  The HS kernels of the CSR path use
+// v[0] = p·q, v[1] = r·z, v[2] = r·r, v[3] = z·z.
 struct Slot {
   double v[4];
   double alpha;
+  double beta;
+  double res;
   int32_t flag;
   int32_t pad;
 };
@@ -127,7 +132,7 @@ void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double 
                    unsigned* ticket, double* red_out);
 // k_cg_first: w₀ = A u₀; (γ₀, δ₀, r·r, u·u) → slots[1]; slots[0].flag = kInit.
 void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, double* partials, unsigned* ticket);
+                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket);
 // iteration j of a chunk: reads slots[j], slots[j+1], writes slots[j+2].
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket);

@@ -397,7 +397,8 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
     if (act && a >= 0) {
       const double vx = xyz[3 * b] - xyz[3 * a], vy = xyz[3 * b + 1] - xyz[3 * a + 1],
                    vz = xyz[3 * b + 2] - xyz[3 * a + 2];
-      const double L = sqrt(vx * vx + vy * vy + vz * vz);
+      // np.linalg.norm of one 3-vector = sqrt(v·v) through BLAS ddot (py:266)
+      const double L = sqrt(fma(vz, vz, fma(vy, vy, vx * vx)));
       const double n0 = vx / L, n1 = vy / L, n2 = vz / L;
       const double du0 = u[3 * b] - u[3 * a], du1 = u[3 * b + 1] - u[3 * a + 1],
                    du2 = u[3 * b + 2] - u[3 * a + 2];

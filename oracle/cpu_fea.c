@@ -256,15 +256,17 @@ int cpu_fea_step(cpu_mesh *m, uint8_t *active, double dy_top, double dy_bot, dou
   return (rr > tol2) ? -1 : it;
 }
 
-/* Axial strain exactly as src/fea_solver.py:263-270 computes it: n = v/L (no
- * clamp), ε = np.dot(n, u2−u1)/L where NumPy's length-3 dot is BLAS ddot, an
- * FMA chain (x0·y0 → fma(x1,y1,·) → fma(x2,y2,·)). */
+/* Axial strain exactly as src/fea_solver.py:263-270 computes it: L =
+ * np.linalg.norm(v) = sqrt(v·v), n = v/L (no clamp), ε = np.dot(n, u2−u1)/L,
+ * where NumPy's length-3 dot is BLAS ddot, an FMA chain
+ * (x0·y0 → fma(x1,y1,·) → fma(x2,y2,·)). */
 void cpu_strain(int64_t E, const int64_t *e2n, const double *xyz, const double *U, double *out) {
   for (int64_t e = 0; e < E; ++e) {
     int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
     double v0 = xyz[3 * b] - xyz[3 * a], v1 = xyz[3 * b + 1] - xyz[3 * a + 1],
            v2 = xyz[3 * b + 2] - xyz[3 * a + 2];
-    double L = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+    /* np.linalg.norm of a 1-D vector is sqrt(x.dot(x)): ddot again (py:266) */
+    double L = sqrt(fma(v2, v2, fma(v1, v1, v0 * v0)));
     double n0 = v0 / L, n1 = v1 / L, n2 = v2 / L;
     double d0 = U[3 * b] - U[3 * a], d1 = U[3 * b + 1] - U[3 * a + 1], d2 = U[3 * b + 2] - U[3 * a + 2];
     out[e] = fma(n2, d2, fma(n1, d1, n0 * d0)) / L;

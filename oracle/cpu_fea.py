@@ -17,7 +17,7 @@ SRC = os.path.join(HERE, "cpu_fea.c")
 
 def build(force=False):
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.check_call(["gcc", "-O3", "-march=x86-64-v3", "-fopenmp", "-shared", "-fPIC",
+        subprocess.check_call(["gcc", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-fopenmp", "-shared", "-fPIC",
                                SRC, "-o", LIB, "-lm"])
     return LIB
 

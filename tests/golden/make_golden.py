@@ -114,10 +114,11 @@ def main():
 
     ref.N_STEPS, ref.DISPLACEMENT_MAX = defaults
 
-    # 4. assembled K at step 0 (all active) to pin assembly
+    # 4. assembled K at step 0 (all active) to pin assembly.  Meshes are parsed
+    # exactly as the reference parses them (pd.read_csv defaults, py:193-194).
     for mesh in ("test_X", "sim_20251117_175809", "sim_20251115_135507"):
-        n = rd(os.path.join(REF, "results", mesh, "nodes.csv"))
-        e = rd(os.path.join(REF, "results", mesh, "elements.csv"))
+        n = pd.read_csv(os.path.join(REF, "results", mesh, "nodes.csv"))
+        e = pd.read_csv(os.path.join(REF, "results", mesh, "elements.csv"))
         K = ref.assemble_global_stiffness(n[["x", "y", "z"]].values, e, np.ones(len(e), bool))
         np.savez_compressed(os.path.join(HERE, f"K0_{mesh}.npz"), indptr=K.indptr,
                             indices=K.indices, data=K.data, shape=np.array(K.shape))
@@ -125,8 +126,8 @@ def main():
 
     # 5. the step-20 linear system of the 22k-DOF mesh (solve parity + iteration counts)
     mesh = "sim_20251117_181147"
-    n = rd(os.path.join(REF, "results", mesh, "nodes.csv"))
-    e = rd(os.path.join(REF, "results", mesh, "elements.csv"))
+    n = pd.read_csv(os.path.join(REF, "results", mesh, "nodes.csv"))
+    e = pd.read_csv(os.path.join(REF, "results", mesh, "elements.csv"))
     coords = n[["x", "y", "z"]].values
     K = ref.assemble_global_stiffness(coords, e, np.ones(len(e), bool))
     y = coords[:, 1]

@@ -1,0 +1,93 @@
+// host_shim.cpp — TEST-ONLY C entry points over the host symbolic phase
+// (mycelium-fea-project_amd/csrc/symbolic.cpp) so its permutation, SELL-64
+// layout and CSR export can be checked on a machine without a GPU.  Element
+// blocks are formed here on the host with the same formula as the device
+// kernel (test input only; never part of libmfea.so).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "symbolic.hpp"
+
+using namespace mfea;
+
+static Pattern g_P;
+
+extern "C" {
+
+// returns 0 / -1 (error text in err); sizes: [n_free, n_top, n_known, n_slices, n_slots·64]
+int shim_build(int64_t N, const double* xyz, int64_t E, const int64_t* e2n, int skip,
+               int64_t ntop, const int64_t* top, int64_t nbot, const int64_t* bot, int window,
+               int64_t* sizes, char* err, int errn) {
+  std::vector<int64_t> t(top, top + ntop), b(bot, bot + nbot);
+  std::string e = build_pattern(N, xyz, E, e2n, skip != 0, t, b, window, g_P);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  sizes[0] = g_P.n_free;
+  sizes[1] = g_P.n_top;
+  sizes[2] = g_P.n_known;
+  sizes[3] = g_P.n_slices();
+  sizes[4] = g_P.n_slots() * kSlice;
+  return 0;
+}
+
+void shim_arrays(int32_t* perm, int32_t* row_len, int32_t* slice_ptr, int32_t* s_col,
+                 int32_t* s_elem, uint8_t* code) {
+  std::memcpy(perm, g_P.perm.data(), g_P.perm.size() * 4);
+  std::memcpy(row_len, g_P.row_len.data(), g_P.row_len.size() * 4);
+  std::memcpy(slice_ptr, g_P.slice_ptr.data(), g_P.slice_ptr.size() * 4);
+  std::memcpy(s_col, g_P.s_col.data(), g_P.s_col.size() * 4);
+  std::memcpy(s_elem, g_P.s_elem.data(), g_P.s_elem.size() * 4);
+  std::memcpy(code, g_P.code.data(), g_P.code.size());
+}
+
+// Host-side blocks for the last built pattern, then export_csr.  Call with
+// indptr == NULL to get nnz.
+int64_t shim_export(const uint8_t* active, double EA, double EI12, int64_t* indptr,
+                    int32_t* indices, double* data) {
+  const Pattern& P = g_P;
+  const int64_t N = P.n_nodes, G = P.n_slots() * kSlice;
+  std::vector<double> diag(6 * N, 0.0), val(6 * G, 0.0);
+  for (int64_t i = 0; i < N; ++i) {
+    const int64_t s = i / kSlice, lane = i % kSlice;
+    double d[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < P.row_len[i]; ++k) {
+      const int64_t idx = ((int64_t)P.slice_ptr[s] + k) * kSlice + lane;
+      const int32_t e = P.s_elem[idx], j = P.s_col[idx];
+      double S[6] = {0, 0, 0, 0, 0, 0};
+      if (active[e]) {
+        const double vx = P.xyz_perm[3 * j] - P.xyz_perm[3 * i];
+        const double vy = P.xyz_perm[3 * j + 1] - P.xyz_perm[3 * i + 1];
+        const double vz = P.xyz_perm[3 * j + 2] - P.xyz_perm[3 * i + 2];
+        double L = std::sqrt(vx * vx + vy * vy + vz * vz);
+        if (L < 1e-12) L = 1e-12;
+        const double n[3] = {vx / L, vy / L, vz / L};
+        const double kax = EA / L, kb = EI12 / (L * L * L);
+        const int ab[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+        for (int c = 0; c < 6; ++c) {
+          const double t = n[ab[c][0]] * n[ab[c][1]];
+          S[c] = t * kax + ((ab[c][0] == ab[c][1] ? 1.0 : 0.0) - t) * kb;
+          d[c] += S[c];
+        }
+      }
+      for (int c = 0; c < 6; ++c) val[c * G + idx] = -S[c];
+    }
+    for (int c = 0; c < 6; ++c) diag[c * N + i] = d[c];
+  }
+  std::vector<uint8_t> act(active, active + P.n_elems);
+  std::vector<int64_t> ip;
+  std::vector<int32_t> ix;
+  std::vector<double> dv;
+  export_csr(P, act, diag, val, ip, ix, dv);
+  if (indptr) {
+    std::memcpy(indptr, ip.data(), ip.size() * 8);
+    std::memcpy(indices, ix.data(), ix.size() * 4);
+    std::memcpy(data, dv.data(), dv.size() * 8);
+  }
+  return (int64_t)ix.size();
+}
+
+}  // extern "C"

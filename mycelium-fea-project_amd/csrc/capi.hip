@@ -75,6 +75,7 @@ struct mfea_handle {
   DevBuf<Slot> slots;
   DevBuf<SolveState> state;
   SolveState* h_state = nullptr;  // pinned, 2 entries
+  SolveState* d_host_state = nullptr;  // device view of h_state (mapped)
   double* h_red = nullptr;        // pinned
   int64_t G = 0;                  // slots·64
   // graph cache
@@ -93,6 +94,10 @@ struct mfea_handle {
 namespace {
 
 constexpr int kMaxChunk = 64;
+constexpr int kTicketSets = 16;
+
+// ticket set k (one per reducing kernel kind; see device_util.hpp layout)
+unsigned* tix(mfea_handle* h, int k) { return h->tickets.ptr + (size_t)k * kTicketStride; }
 
 void destroy_graph(mfea_handle* h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
@@ -133,7 +138,7 @@ int ensure_built(mfea_handle* h) {
   HIPC(h->cg_w1.alloc(3 * N));
   HIPC(h->dinv.alloc(6 * N));
   HIPC(h->stress.alloc(E));
-  HIPC(h->partials.alloc(4 * maxg));
+  HIPC(h->partials.alloc(4 * (maxg + 16)));
   HIPC(h->red.alloc(16));
   HIPC(h->slice_ptr.alloc(P.slice_ptr.size()));
   HIPC(h->row_len.alloc(N));
@@ -142,7 +147,7 @@ int ensure_built(mfea_handle* h) {
   HIPC(h->e2n_d.alloc(2 * E));
   HIPC(h->active.alloc(E));
   HIPC(h->code.alloc(N));
-  HIPC(h->tickets.alloc(16));
+  HIPC(h->tickets.alloc(kTicketSets * kTicketStride));
   HIPC(h->slots.alloc(kMaxChunk + 2));
   HIPC(h->state.alloc(1));
   hipStream_t s = h->stream;
@@ -156,7 +161,7 @@ int ensure_built(mfea_handle* h) {
   HIPC(up(h->s_elem.ptr, P.s_elem.data(), h->G * sizeof(int32_t)));
   HIPC(up(h->e2n_d.ptr, P.e2n_perm.data(), 2 * E * sizeof(int32_t)));
   HIPC(up(h->code.ptr, P.code.data(), N * sizeof(uint8_t)));
-  HIPC(hipMemsetAsync(h->tickets.ptr, 0, 16 * sizeof(unsigned), s));
+  HIPC(hipMemsetAsync(h->tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
   HIPC(hipMemsetAsync(h->x.ptr, 0, 3 * N * sizeof(double), s));
   HIPC(hipMemsetAsync(h->p.ptr, 0, 3 * N * sizeof(double), s));
   HIPC(hipMemsetAsync(h->q.ptr, 0, 3 * N * sizeof(double), s));
@@ -220,31 +225,37 @@ void enqueue_chunk_sell(mfea_handle* h, int chunk, int precond) {
   const CgVecs v = cg_vecs(h);
   for (int j = 0; j < chunk; ++j)
     launch_cg_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->partials.ptr,
-                   h->tickets.ptr + 1);
-  launch_cg_advance(s, chunk, h->slots.ptr, h->state.ptr);
+                   tix(h, 1));
+  launch_cg_advance(s, chunk, h->slots.ptr, h->state.ptr, h->d_host_state);
 }
 
 // Replays chunks until the device reports done; at most two chunks in flight.
 template <class Enqueue>
-int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, SolveState* out) {
+// mirror = true: the chunk's advance kernel writes the final state into the
+// mapped pinned h_state[0] itself (CG-CG path); otherwise copy it per chunk.
+int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, SolveState* out,
+                 bool mirror = false) {
   hipStream_t s = h->stream;
   const int64_t max_chunks = (int64_t)max_it / chunk + 3;
   int64_t k = 0;
   bool done = false;
+  volatile SolveState* hs = h->h_state;
+  if (mirror) hs[0].done = 0;
   while (!done && k < max_chunks) {
     int rc = enqueue();
     if (rc) return rc;
-    HIPC(hipMemcpyAsync(&h->h_state[k & 1], h->state.ptr, sizeof(SolveState),
-                        hipMemcpyDeviceToHost, s));
+    if (!mirror)
+      HIPC(hipMemcpyAsync(&h->h_state[k & 1], h->state.ptr, sizeof(SolveState),
+                          hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(h->poll[k & 1], s));
     if (k >= 1) {
       HIPC(hipEventSynchronize(h->poll[(k - 1) & 1]));
-      if (h->h_state[(k - 1) & 1].done) done = true;
+      if (hs[mirror ? 0 : (k - 1) & 1].done) done = true;
     }
     ++k;
   }
   HIPC(hipStreamSynchronize(s));
-  const SolveState& last = h->h_state[(k - 1) & 1];
+  const SolveState& last = h->h_state[mirror ? 0 : (k - 1) & 1];
   if (!last.done) {
     // should not happen (max_chunks covers max_it); report as maxit
     *out = last;
@@ -290,11 +301,11 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   const CgVecs v = cg_vecs(h);
   HIPC(hipEventRecord(h->ev[1], s));
   launch_cg_rhs(s, op, h->code.ptr, dy_top, dy_bot, o->reg, precond, v, h->partials.ptr,
-                h->tickets.ptr + 0, h->red.ptr);
+                tix(h, 0), h->red.ptr);
   launch_cg_init_finalize(s, h->red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
                           h->state.ptr);
   launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->state.ptr, h->partials.ptr,
-                  h->tickets.ptr + 2);
+                  tix(h, 2));
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
   // MFEA_NO_GRAPH=1: launch the chunk kernels eagerly (profilers that do not
@@ -309,7 +320,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
           HIPC(hipGetLastError());
           return 0;
         },
-        &fin);
+        &fin, /*mirror=*/true);
     if (rc) return rc;
     return finish_solve(h, o, nf, fin, st);
   }
@@ -332,7 +343,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
         HIPC(hipGraphLaunch(h->graph, s));
         return 0;
       },
-      &fin);
+      &fin, /*mirror=*/true);
   if (rc) return rc;
   return finish_solve(h, o, nf, fin, st);
 }
@@ -360,10 +371,10 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   hipStream_t s = h->stream;
   HIPC(hipEventRecord(h->ev[4], s));
   launch_reaction(s, P.n_free, P.n_top, P.n_nodes, h->slice_ptr.ptr, h->row_len.ptr, h->s_col.ptr,
-                  h->val.ptr, h->diag.ptr, h->G, h->x.ptr, h->partials.ptr, h->tickets.ptr + 3,
+                  h->val.ptr, h->diag.ptr, h->G, h->x.ptr, h->partials.ptr, tix(h, 3),
                   h->red.ptr + 4);
   launch_stress(s, P.n_elems, h->e2n_d.ptr, h->xyz_d.ptr, h->x.ptr, h->mat, max_strain,
-                h->active.ptr, h->stress.ptr, h->partials.ptr, h->tickets.ptr + 4, h->red.ptr + 5);
+                h->active.ptr, h->stress.ptr, h->partials.ptr, tix(h, 4), h->red.ptr + 5);
   HIPC(hipGetLastError());
   HIPC(hipMemcpyAsync(h->h_red, h->red.ptr + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPC(hipEventRecord(h->ev[5], s));
@@ -405,7 +416,9 @@ int mfea_create(int device, mfea_handle** out) {
   HIPC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   for (auto& ev : h->ev) HIPC(hipEventCreate(&ev));
   for (auto& ev : h->poll) HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  HIPC(hipHostMalloc(&h->h_state, 2 * sizeof(SolveState), hipHostMallocDefault));
+  HIPC(hipHostMalloc(&h->h_state, 2 * sizeof(SolveState),
+                     hipHostMallocMapped | hipHostMallocCoherent));
+  HIPC(hipHostGetDevicePointer((void**)&h->d_host_state, h->h_state, 0));
   HIPC(hipHostMalloc(&h->h_red, 16 * sizeof(double), hipHostMallocDefault));
   std::memset(h->h_state, 0, 2 * sizeof(SolveState));
   // reference constants src/fea_solver.py:14-20
@@ -665,12 +678,12 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
   HIPC(h->c_q.alloc(n));
   HIPC(h->c_dinv.alloc(n));
   const int64_t maxg = std::max<int64_t>(grid_rows(n), 2048);
-  if (h->partials.n < (size_t)(4 * maxg)) HIPC(h->partials.alloc(4 * maxg));
+  if (h->partials.n < (size_t)(4 * maxg)) HIPC(h->partials.alloc(4 * (maxg + 16)));
   HIPC(h->red.alloc(16));
-  HIPC(h->tickets.alloc(16));
+  HIPC(h->tickets.alloc(kTicketSets * kTicketStride));
   HIPC(h->slots.alloc(kMaxChunk + 2));
   HIPC(h->state.alloc(1));
-  if (h->dirty) HIPC(hipMemsetAsync(h->tickets.ptr, 0, 16 * sizeof(unsigned), s));
+  if (h->dirty) HIPC(hipMemsetAsync(h->tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
   HIPC(hipMemcpyAsync(h->c_indptr.ptr, indptr, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   if (nnz) {
     HIPC(hipMemcpyAsync(h->c_indices.ptr, indices, nnz * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -682,7 +695,7 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
   HIPC(hipEventRecord(h->ev[1], s));
   launch_csr_rhs_init(s, n, h->c_indptr.ptr, h->c_indices.ptr, h->c_data.ptr, h->c_known.ptr,
                       h->c_kval.ptr, o.reg, h->c_x.ptr, h->c_r.ptr, h->c_p.ptr, h->c_dinv.ptr,
-                      h->partials.ptr, h->tickets.ptr + 5, h->red.ptr);
+                      h->partials.ptr, tix(h, 5), h->red.ptr);
   launch_init_finalize(s, h->red.ptr, o.rtol, o.atol, o.norm, o.max_it, o.reg, h->slots.ptr,
                        h->state.ptr);
   HIPC(hipGetLastError());
@@ -695,9 +708,9 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
         for (int j = 0; j < chunk; ++j) {
           launch_spmv_csr(s, j, n, h->c_indptr.ptr, h->c_indices.ptr, h->c_data.ptr,
                           h->c_known.ptr, o.reg, h->c_p.ptr, h->c_q.ptr, h->slots.ptr,
-                          h->state.ptr, h->partials.ptr, h->tickets.ptr + 6);
+                          h->state.ptr, h->partials.ptr, tix(h, 6));
           launch_update(s, j, n, 0, h->c_x.ptr, h->c_r.ptr, h->c_p.ptr, h->c_q.ptr, h->c_dinv.ptr,
-                        h->slots.ptr, h->state.ptr, h->partials.ptr, h->tickets.ptr + 7);
+                        h->slots.ptr, h->state.ptr, h->partials.ptr, tix(h, 7));
           launch_direction(s, j, n, 0, h->c_r.ptr, h->c_p.ptr, h->c_dinv.ptr, h->slots.ptr,
                            h->state.ptr);
         }
@@ -769,11 +782,11 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   two[1].flag = kRun;
   HIPC(hipMemcpyAsync(h->slots.ptr, two, sizeof(two), hipMemcpyHostToDevice, s));
   launch_cg_iter(s, 0, op, pc, v, h->slots.ptr, h->state.ptr, h->partials.ptr,
-                 h->tickets.ptr + 1);  // warm
+                 tix(h, 1));  // warm
   HIPC(hipEventRecord(h->ev[0], s));
   for (int k = 0; k < reps; ++k)
     launch_cg_iter(s, 0, op, pc, v, h->slots.ptr, h->state.ptr, h->partials.ptr,
-                   h->tickets.ptr + 1);
+                   tix(h, 1));
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[1], s));
   HIPC(hipEventSynchronize(h->ev[1]));

@@ -359,23 +359,34 @@ __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot
 // End of a chunk: record where the iteration stopped, or roll the newest slot
 // to the front.  Once done, slots[1] is poisoned STOP so chunks the host
 // already queued are no-ops.
-__global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One wave: lane j checks slot j+1 in parallel, a ballot finds the first
+// iteration that did not run.  The final state is mirrored into mapped pinned
+// host memory (`host`), so the host polls without a copy kernel.
+__global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st, SolveState* host) {
+  if (blockIdx.x != 0) return;
+  const int lane = threadIdx.x;
   if (st->done) return;
-  for (int j = 0; j <= chunk; ++j) {
-    const Slot& cur = slots[j + 1];
-    if (!cg_running(cur, st, j)) {
-      const double res = cur.res;
-      st->iters = st->base + j;
-      st->res_final = res;
-      if (cur.flag == kBreakdown || (cur.flag == kRun && !isfinite(res))) st->status = -5;
-      else if (cur.flag == kRun && res <= st->tol2) st->status = 0;
-      else if (cur.flag == kRun) st->status = -4;
-      else st->status = -5;
-      st->done = 1;
-      slots[1].flag = kStop;
-      return;
-    }
+  int first = -1;
+  for (int j0 = 0; j0 <= chunk && first < 0; j0 += 64) {
+    const int j = j0 + lane;
+    const bool stop = j <= chunk && !cg_running(slots[j + 1], st, j);
+    const unsigned long long m = __ballot(stop);
+    if (m) first = j0 + __ffsll((long long)m) - 1;
+  }
+  if (lane != 0) return;
+  if (first >= 0) {
+    const Slot& cur = slots[first + 1];
+    const double res = cur.res;
+    st->iters = st->base + first;
+    st->res_final = res;
+    if (cur.flag == kBreakdown || (cur.flag == kRun && !isfinite(res))) st->status = -5;
+    else if (cur.flag == kRun && res <= st->tol2) st->status = 0;
+    else if (cur.flag == kRun) st->status = -4;
+    else st->status = -5;
+    st->done = 1;
+    slots[1].flag = kStop;
+    *host = *st;
+    return;
   }
   slots[1] = slots[chunk + 1];
   st->base += chunk;
@@ -440,8 +451,8 @@ void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const C
     iter_bs<256>(s, j, op, precond, v, slots, st, partials, ticket);
 }
 
-void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st) {
-  hipLaunchKernelGGL(k_cg_advance, dim3(1), dim3(64), 0, s, chunk, slots, st);
+void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host) {
+  hipLaunchKernelGGL(k_cg_advance, dim3(1), dim3(64), 0, s, chunk, slots, st, host);
 }
 
 }  // namespace mfea

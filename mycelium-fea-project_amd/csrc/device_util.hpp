@@ -1,100 +1,138 @@
 // device_util.hpp — device helpers shared by the mfea kernels (wave64 reductions,
-// fence-free last-block finalize, symmetric 3×3 block algebra).
+// fence-free sharded last-block finalize, symmetric 3×3 block algebra).
 #pragma once
 #include "kernels.hpp"
 
 namespace mfea {
 
-// ---------------------------------------------------------------------------
-// deterministic block reduction + last-block finalize (agent-scope ticket).
-// Every block writes its partial sums, the block that draws the last ticket
-// sums all partials in a fixed order and writes `out`.  Result is bitwise
-// reproducible for a fixed grid size.  Protocol: cdna_hip_programming.md §6
-// Guideline 16 (release → drained wait → relaxed agent atomic; acquire in the
-// last block → wait → barrier → plain loads).
-// ---------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
-// Hand-off without fences (MI355X_MICROARCH.md "Valid forms", table row 1):
-// the partials are stored write-through (sc1, via agent-scope atomic stores),
-// the storing lane drains them (s_waitcnt vmcnt(0)) before its agent-scope
-// ticket add, and the last arriver reads every partial with sc1 loads, so no
-// release/acquire fence (≈1.7 µs each) is paid on the per-iteration path.
-template <int NV, int BS = kBlock>
-__device__ __forceinline__ bool block_publish(double (&v)[NV], double* partials,
-                                              unsigned* ticket, double* out) {
+// Ticket layout: one ticket set = kTicketStride unsigned; shard s counter at
+// s·16 (64 B apart, separate lines), the top counter at kShards·16.
+constexpr int kShards = 8;
+static_assert((kShards + 1) * 16 <= kTicketStride, "ticket set too small");
+
+// Sum over the block of NV values, result on thread 0 (others: garbage).
+template <int NV, int BS>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* lds) {
   constexpr int NW = BS / 64;
-  __shared__ double lds[NW * NV];
-  __shared__ int is_last;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned G = gridDim.x;
 #pragma unroll
   for (int c = 0; c < NV; ++c) v[c] = wave_sum(v[c]);
   if (NW > 1) {
+    __syncthreads();
     if (lane == 0) {
 #pragma unroll
       for (int c = 0; c < NV; ++c) lds[wid * NV + c] = v[c];
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        double s = lds[c];
+        for (int w = 1; w < NW; ++w) s += lds[w * NV + c];
+        v[c] = s;
+      }
+    }
   }
+}
+
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic grid reduction finished inside the launch (no second kernel):
+// every block publishes its partial sums; the last arriver of each of
+// kShards shards (blocks ≡ s mod kShards) sums its shard's partials in block
+// order and publishes a shard sum; the last shard finisher sums the shard sums
+// in shard order and writes `out`.  Bitwise reproducible for a fixed grid.
+//
+// Two levels because same-address agent atomics serialize at ≈12 ns each
+// (MI355X_MICROARCH.md, row "fanin"): one counter for 1,300 blocks costs
+// ≈16 µs; eight shards of ≤165 plus a top counter of 8 cost ≈2 µs.
+//
+// Hand-off without fences (MI355X_MICROARCH.md "Valid forms", table row 1):
+// payload stored write-through (sc1, agent-scope atomic stores), the storing
+// lane drains it (s_waitcnt vmcnt(0)) before its agent-scope ticket add, the
+// last arriver reads every payload word with sc1 loads.  No ≈1.7 µs
+// release/acquire fence on the per-iteration path.
+// partials must hold NV·(gridDim + kShards) doubles.
+// ---------------------------------------------------------------------------
+template <int NV, int BS = kBlock>
+__device__ __forceinline__ bool block_publish(double (&v)[NV], double* partials,
+                                              unsigned* ticket, double* out) {
+  constexpr int NW = BS / 64;
+  __shared__ double lds[NW * NV];
+  __shared__ int flag;
+  const unsigned G = gridDim.x, b = blockIdx.x;
+  const unsigned S = G < (unsigned)kShards ? G : (unsigned)kShards;
+  const unsigned shard = b % S;
+  const unsigned nshard = (G - shard + S - 1) / S;
+  double* spart = partials + (size_t)NV * G;  // shard sums, [c][S]
+
+  block_sum<NV, BS>(v, lds);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      double s = NW > 1 ? lds[c] : v[c];
-      for (int w = 1; w < NW; ++w) s += lds[w * NV + c];
-      __hip_atomic_store(&partials[(size_t)c * G + blockIdx.x], s, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int c = 0; c < NV; ++c) store_sc1(&partials[(size_t)c * G + b], v[c]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (t == G - 1);
+    const unsigned t =
+        __hip_atomic_fetch_add(&ticket[shard * 16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (t == nshard - 1);
   }
   __syncthreads();
-  if (!is_last) return false;
-  // U partials per lane in flight per pass: one memory round trip covers
-  // BS·U blocks (the loads are independent; hipcc waits once per pass).
-  constexpr int U = BS >= 256 ? 8 : 16;
+  if (!flag) return false;
+
+  // ---- last block of this shard: sum its blocks' partials in block order
+  constexpr int U = BS >= 256 ? 4 : 8;
   double s[NV];
 #pragma unroll
   for (int c = 0; c < NV; ++c) s[c] = 0.0;
-  for (unsigned i0 = threadIdx.x; i0 < G; i0 += BS * U) {
+  for (unsigned k0 = threadIdx.x; k0 < nshard; k0 += BS * U) {
     double t[U][NV];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const unsigned i = i0 + u * BS;
+      const unsigned k = k0 + u * BS;
+      const unsigned blk = shard + k * S;
 #pragma unroll
-      for (int c = 0; c < NV; ++c)
-        t[u][c] = i < G ? __hip_atomic_load(&partials[(size_t)c * G + i], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT)
-                        : 0.0;
+      for (int c = 0; c < NV; ++c) t[u][c] = k < nshard ? load_sc1(&partials[(size_t)c * G + blk]) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int c = 0; c < NV; ++c) s[c] += t[u][c];
   }
-#pragma unroll
-  for (int c = 0; c < NV; ++c) s[c] = wave_sum(s[c]);
-  if (NW > 1) {
-    __syncthreads();
-    if (lane == 0) {
-#pragma unroll
-      for (int c = 0; c < NV; ++c) lds[wid * NV + c] = s[c];
-    }
-    __syncthreads();
-  }
+  block_sum<NV, BS>(s, lds);
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int c = 0; c < NV; ++c) {
-      double t = NW > 1 ? lds[c] : s[c];
-      for (int w = 1; w < NW; ++w) t += lds[w * NV + c];
-      out[c] = t;
-    }
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int c = 0; c < NV; ++c) store_sc1(&spart[c * S + shard], s[c]);
+    __hip_atomic_store(&ticket[shard * 16], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(&ticket[kShards * 16], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    flag = (t == S - 1);
+  }
+  __syncthreads();
+  if (!flag) return false;
+
+  // ---- last shard finisher: shard sums in shard order
+  if (threadIdx.x == 0) {
+    double r[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) r[c] = 0.0;
+    for (unsigned q = 0; q < S; ++q)
+#pragma unroll
+      for (int c = 0; c < NV; ++c) r[c] += load_sc1(&spart[c * S + q]);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) out[c] = r[c];
+    __hip_atomic_store(&ticket[kShards * 16], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return true;
 }

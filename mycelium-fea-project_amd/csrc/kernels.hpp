@@ -17,6 +17,7 @@
 namespace mfea {
 
 constexpr int kBlock = 256;  // 4 wavefronts
+constexpr int kTicketStride = 256;  // unsigned per reduction ticket set (device_util.hpp)
 
 // PCG per-iteration scalar slot (see DESIGN.md "PCG scalar slots").
 // v[0] = p·q, v[1] = r·z, v[2] = r·r, v[3] = z·z (v[1..3] reduced together),
@@ -136,7 +137,8 @@ void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, c
 // iteration j of a chunk: reads slots[j], slots[j+1], writes slots[j+2].
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket);
-void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st);
+// host: mapped pinned mirror of the final SolveState (written once, when done)
+void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host);
 void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
                              int max_it, double reg, SolveState* st);
 int cg_block_size(int64_t rows);

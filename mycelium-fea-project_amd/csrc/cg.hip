@@ -1,11 +1,11 @@
 // cg.hip — single-reduction preconditioned CG (Chronopoulos–Gear) on the SELL-64
-// node-block operator: ONE kernel per iteration.
+// node-block operator: ONE kernel per iteration, no atomics.
 //
 // Recurrences (x₀ = 0, u = M⁻¹r, w = A u, s = A p):
 //   p_i = u_i + β_i p_{i−1}      s_i = w_i + β_i s_{i−1}
 //   x_{i+1} = x_i + α_i p_i      r_{i+1} = r_i − α_i s_i
 //   u_{i+1} = M⁻¹ r_{i+1}        w_{i+1} = A u_{i+1}
-//   γ = (r,u), δ = (w,u);  β_{i+1} = γ_{i+1}/γ_i,  α_{i+1} = γ_{i+1} / (δ_{i+1} − β_{i+1} γ_{i+1} / α_i)
+//   γ = (r,u), δ = (w,u);  β_i = γ_i/γ_{i−1},  α_i = γ_i / (δ_i − β_i γ_i / α_{i−1})
 // In exact arithmetic these are the iterates of textbook PCG (the reference's
 // KSPCG, src/fea_petsc.cpp:328); one fused reduction (γ, δ, ‖r‖², ‖u‖²) per
 // iteration instead of two.  The SpMV w = A u needs u_j of neighbour rows whose
@@ -13,20 +13,27 @@
 // iteration parity and each row recomputes its neighbours' u_j from the
 // previous-iteration values: u_j = M_j⁻¹ (r_j − α (w_j + β s_j)).
 //
-// Scalar hand-off: the block that completes an iteration's reduction (last
-// ticket) also forms α, β and the stopping norm for the next iteration and
-// writes them into the next slot, so an iteration kernel starts with plain
-// scalar loads and no divisions on its critical path.
+// Cross-block reduction by the consumer: iteration j stores one partial
+// (γ, δ, ‖r‖², ‖u‖²) per block with plain stores; every wave of iteration j+1
+// loads all G ≤ 512 partials (one round trip, in flight together with its row
+// loads), sums them in block order and derives α, β and the stopping test
+// itself.  The kernel boundary is the only synchronisation: no atomics, no
+// last-block tail, no fences.  Every wave sums the same values in the same
+// order, so all waves (and, multi-GPU, all ranks after an all-reduce of the
+// partial array) agree bitwise.
 #include "device_util.hpp"
 #include "kernels.hpp"
 
 namespace mfea {
 
-int cg_block_size(int64_t rows) { return rows <= 64 * 1024 ? 64 : 256; }
+constexpr int kCgBS = 256;     // threads per block of the CG kernels
+constexpr int kCgMaxG = kCgMaxPartials;  // max blocks (= partials re-read by each wave)
+constexpr int kCgPU = kCgMaxG / 64;
+
+int cg_block_size(int64_t) { return kCgBS; }
 int64_t cg_grid(int64_t rows) {
-  const int bs = cg_block_size(rows);
-  int64_t g = (rows + bs - 1) / bs;
-  return g < 1 ? 1 : (g > 2048 ? 2048 : g);
+  int64_t g = (rows + kCgBS - 1) / kCgBS;
+  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
 }
 
 template <bool BLOCK>
@@ -61,24 +68,6 @@ __device__ __forceinline__ void block_mac(const double V[6], const double u[3], 
   y[2] = fma(V[2], u[0], fma(V[4], u[1], fma(V[5], u[2], y[2])));
 }
 
-// Finalize the scalars of slot `s` from its freshly reduced sums (thread 0 of
-// the reducing block).  prev = the slot whose α, γ the iteration consumed
-// (nullptr for the first reduction: β = 0, α = γ/δ).
-__device__ __forceinline__ void finalize_slot(Slot* s, const Slot* prev, int norm) {
-  const double g = s->v[0], d = s->v[1];
-  double beta = 0.0, den = d;
-  if (prev) {
-    beta = g / prev->v[0];
-    den = d - beta * g / prev->alpha;
-  }
-  const double alpha = g / den;
-  s->alpha = alpha;
-  s->beta = beta;
-  s->res = norm == 1 ? s->v[3] : s->v[2];
-  const bool ok = (den > 0.0) && isfinite(alpha) && isfinite(beta);
-  // γ = 0 ⇔ r = 0: converged, not a breakdown (the stopping test catches it)
-  s->flag = (ok || g == 0.0) ? kRun : kBreakdown;
-}
 
 // ---------------------------------------------------------------------------
 // Dirichlet elimination / RHS (src/fea_solver.py:115-125; src/fea_petsc.cpp:286-320)
@@ -177,15 +166,59 @@ __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, 
   st->status = 0;
 }
 
-// w₀ = A u₀ and the first fused reduction → slots[1] (α₀ = γ₀/δ₀, β₀ = 0).
-template <bool BLOCK, int BS>
-__global__ __launch_bounds__(BS) void k_cg_first(SellOp op, double reg, CgVecs v, Slot* slots,
-                                                 const SolveState* st, double* partials,
-                                                 unsigned* ticket) {
+// ---------------------------------------------------------------------------
+// Partial-sum protocol.  part = two parity buffers of [4][kCgMaxG] doubles.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double* part_buf(double* part, int par) {
+  return part + (size_t)par * 4 * kCgMaxG;
+}
+
+// Every lane ends with the grid total of the G partials (block order, then a
+// fixed butterfly): identical in every wave of every block.
+__device__ __forceinline__ void wave_partials(const double* __restrict__ p, int G, double s[4]) {
+  const int lane = threadIdx.x & 63;
+  // The buffer is always kCgMaxG wide: load every slot unconditionally (a
+  // guarded load makes hipcc branch + wait vmcnt(0) per element) and select.
+  double t[kCgPU][4];
+#pragma unroll
+  for (int k = 0; k < kCgPU; ++k) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[k][c] = p[c * kCgMaxG + lane + 64 * k];
+  }
+#pragma unroll
+  for (int k = 0; k < kCgPU; ++k) {
+    const bool in = lane + 64 * k < G;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[k][c] = in ? t[k][c] : 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < kCgPU; ++k) a += t[k][c];
+    s[c] = wave_sum(a);
+  }
+}
+
+// block partial (thread 0 stores it; the next launch's waves re-reduce)
+__device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __restrict__ p) {
+  __shared__ double lds[(kCgBS / 64) * 4];
+  block_sum<4, kCgBS>(acc, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p[c * kCgMaxG + blockIdx.x] = acc[c];
+  }
+}
+
+// w₀ = A u₀ and the first partials (γ₀, δ₀, ‖r₀‖², ‖u₀‖²) → parity 0;
+// slots[0] = INIT (no previous α, γ: iteration 0 uses β₀ = 0, α₀ = γ₀/δ₀).
+template <bool BLOCK>
+__global__ __launch_bounds__(kCgBS) void k_cg_first(SellOp op, double reg, CgVecs v, Slot* slots,
+                                                    double* part) {
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const int64_t stride = (int64_t)gridDim.x * BS;
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
   const int64_t G = op.G;
-  for (int64_t row = (int64_t)blockIdx.x * BS + threadIdx.x; row < op.nf; row += stride) {
+  for (int64_t row = (int64_t)blockIdx.x * kCgBS + threadIdx.x; row < op.nf; row += stride) {
     double r[3], u[3];
     load3(v.r[0], row, r);
     apply_minv<BLOCK>(v.dinv, row, r, u);
@@ -218,12 +251,15 @@ __global__ __launch_bounds__(BS) void k_cg_first(SellOp op, double reg, CgVecs v
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  if (block_publish<4, BS>(acc, partials, ticket, slots[1].v) && threadIdx.x == 0)
-    finalize_slot(&slots[1], nullptr, st->norm);
-}
-
-__device__ __forceinline__ bool cg_running(const Slot& cur, const SolveState* st, int j) {
-  return cur.flag == kRun && cur.res > st->tol2 && (st->base + j) < st->max_it;
+  store_block_partial(acc, part_buf(part, 0));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Slot s0;
+    s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
+    s0.alpha = s0.beta = s0.res = 0.0;
+    s0.flag = kInit;
+    s0.pad = 0;
+    slots[0] = s0;
+  }
 }
 
 // neighbour contribution y += V · M_c⁻¹ (r_c − α (w_c + β s_c))
@@ -244,22 +280,48 @@ __device__ __forceinline__ void neighbour_mac(const double V[6], int64_t c, doub
 }
 
 // ---------------------------------------------------------------------------
-// One CG-CG iteration.  Per free row (one lane per row, SELL-64 slot layout):
-// own-row vector updates, then w_new = (K_ii + reg) u_new + Σ_slots V u_j with
-// neighbour u_j recomputed from previous-iteration r, s, w.  HBM per row:
-// 11 × 24 B of vectors + 48 B diag + 52 B per slot.
+// One CG-CG iteration (iteration j of a chunk; chunks are even so the buffer
+// parity is j & 1).  Each wave first reduces the previous iteration's block
+// partials into (γ_j, δ_j, ‖r_j‖², ‖u_j‖²), forms α_j, β_j and the status of
+// iteration j; block 0 records them in slots[j+1].  Then per free row (one
+// lane per row, SELL-64 slot layout): own-row vector updates and
+// w_new = (K_ii + reg) u_new + Σ_slots V u_j with neighbour u_j recomputed from
+// previous-iteration r, s, w.  Stores are predicated on the status (an
+// iteration queued after convergence costs one wasted pass, ≤ 2 chunks).
+// HBM per free row: 11 × 24 B of vectors + 48 B diag + 52 B per slot.
 // ---------------------------------------------------------------------------
-template <bool BLOCK, int BS>
-__global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
-                                                const SolveState* st, double* partials,
-                                                unsigned* ticket) {
-  const double alpha = slots[j + 1].alpha, beta = slots[j + 1].beta, res = slots[j + 1].res;
-  const int flag = slots[j + 1].flag;
-  const bool go = (flag == kRun) & (res > st->tol2) & ((st->base + j) < st->max_it);
-  const double reg = st->reg;
-  // chunks have even length and base is a multiple of the chunk, so the
-  // buffer parity is a launch constant: vector addresses need no scalar load
+template <bool BLOCK>
+__global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
+                                                   const SolveState* st, double* part) {
   const int par = j & 1;
+  // scalar loads first in program order so they fly with the partial loads
+  const int f0 = __builtin_nontemporal_load(&slots[j].flag);
+  const double g0 = slots[j].v[0], a0 = slots[j].alpha;
+  const double tol2 = st->tol2, reg = st->reg;
+  const int base_it = st->base, max_it = st->max_it, norm = st->norm;
+  double S[4];
+  wave_partials(part_buf(part, par), (int)gridDim.x, S);
+  const double res = norm == 1 ? S[3] : S[2];
+  const bool first = f0 == kInit;
+  const double beta = first ? 0.0 : S[0] / g0;
+  const double den = first ? S[1] : S[1] - beta * S[0] / a0;
+  const double alpha = S[0] / den;
+  int status;
+  if (f0 != kRun && f0 != kInit) status = kStop;
+  else if (!(res > tol2)) status = isfinite(res) ? kConverged : kBreakdown;
+  else if (base_it + j >= max_it) status = kMaxit;
+  else status = ((den > 0.0) && isfinite(alpha) && isfinite(beta)) ? kRun : kBreakdown;
+  const bool go = status == kRun;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Slot sl;
+    sl.v[0] = S[0]; sl.v[1] = S[1]; sl.v[2] = S[2]; sl.v[3] = S[3];
+    sl.alpha = alpha;
+    sl.beta = beta;
+    sl.res = res;
+    sl.flag = status;
+    sl.pad = 0;
+    slots[j + 1] = sl;
+  }
   const double* __restrict__ r_old = v.r[par];
   const double* __restrict__ s_old = v.s[par];
   const double* __restrict__ w_old = v.w[par];
@@ -275,12 +337,9 @@ __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot
   const int32_t* __restrict__ row_len = op.row_len;
   const int32_t* __restrict__ slice_ptr = op.slice_ptr;
   const int64_t G = op.G, N = op.N, nf = op.nf;
-  // No early exit on `go`: the scalar loads (SMEM) and the row's vector loads
-  // (VMEM) are in flight together and only the stores/publish are predicated.
-  // An iteration queued after convergence costs one wasted pass (≤ 2 chunks).
-  const int64_t stride = (int64_t)gridDim.x * BS;
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t row = (int64_t)blockIdx.x * BS + threadIdx.x; row - threadIdx.x % 64 < nf;
+  for (int64_t row = (int64_t)blockIdx.x * kCgBS + threadIdx.x; row - threadIdx.x % 64 < nf;
        row += stride) {
     // every lane of a wave shares the slice → scalar load of its slot offset
     const int slice = __builtin_amdgcn_readfirstlane((int)(row >> 6));
@@ -346,49 +405,37 @@ __global__ __launch_bounds__(BS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot
       acc[3] = fma(un[a], un[a], acc[3]);
     }
   }
-  if (!go) {
-    // converged / stopped / max_it: propagate STOP (a breakdown was flagged by
-    // the reducing block of the previous iteration and stays in that slot)
-    if (blockIdx.x == 0 && threadIdx.x == 0) slots[j + 2].flag = kStop;
-    return;
-  }
-  if (block_publish<4, BS>(acc, partials, ticket, slots[j + 2].v) && threadIdx.x == 0)
-    finalize_slot(&slots[j + 2], &slots[j + 1], st->norm);
+  if (go) store_block_partial(acc, part_buf(part, par ^ 1));
 }
 
-// End of a chunk: record where the iteration stopped, or roll the newest slot
-// to the front.  Once done, slots[1] is poisoned STOP so chunks the host
-// already queued are no-ops.
-// One wave: lane j checks slot j+1 in parallel, a ballot finds the first
-// iteration that did not run.  The final state is mirrored into mapped pinned
-// host memory (`host`), so the host polls without a copy kernel.
+// End of a chunk: find the first iteration that did not run (one wave, one
+// slot per lane, ballot), record it, or roll slot `chunk` to the front.  The
+// final state is mirrored into mapped pinned host memory (`host`), so the host
+// polls without a copy kernel; slot 0 is then poisoned so already-queued
+// chunks do nothing.
 __global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st, SolveState* host) {
   if (blockIdx.x != 0) return;
   const int lane = threadIdx.x;
   if (st->done) return;
   int first = -1;
-  for (int j0 = 0; j0 <= chunk && first < 0; j0 += 64) {
+  for (int j0 = 0; j0 < chunk && first < 0; j0 += 64) {
     const int j = j0 + lane;
-    const bool stop = j <= chunk && !cg_running(slots[j + 1], st, j);
+    const bool stop = j < chunk && slots[j + 1].flag != kRun;
     const unsigned long long m = __ballot(stop);
     if (m) first = j0 + __ffsll((long long)m) - 1;
   }
   if (lane != 0) return;
   if (first >= 0) {
     const Slot& cur = slots[first + 1];
-    const double res = cur.res;
     st->iters = st->base + first;
-    st->res_final = res;
-    if (cur.flag == kBreakdown || (cur.flag == kRun && !isfinite(res))) st->status = -5;
-    else if (cur.flag == kRun && res <= st->tol2) st->status = 0;
-    else if (cur.flag == kRun) st->status = -4;
-    else st->status = -5;
+    st->res_final = cur.res;
+    st->status = cur.flag == kConverged ? 0 : (cur.flag == kMaxit ? -4 : -5);
     st->done = 1;
-    slots[1].flag = kStop;
+    slots[0].flag = kStop;
     *host = *st;
     return;
   }
-  slots[1] = slots[chunk + 1];
+  slots[0] = slots[chunk];
   st->base += chunk;
 }
 
@@ -411,44 +458,22 @@ void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, doub
                      reg, st);
 }
 
-template <int BS>
-static void first_bs(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
-  const dim3 grid((unsigned)cg_grid(op.nf));
-  if (precond == 1)
-    hipLaunchKernelGGL((k_cg_first<true, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, st,
-                       partials, ticket);
-  else
-    hipLaunchKernelGGL((k_cg_first<false, BS>), grid, dim3(BS), 0, s, op, reg, v, slots, st,
-                       partials, ticket);
-}
-
 void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
-  if (cg_block_size(op.nf) == 64)
-    first_bs<64>(s, op, reg, precond, v, slots, st, partials, ticket);
-  else
-    first_bs<256>(s, op, reg, precond, v, slots, st, partials, ticket);
-}
-
-template <int BS>
-static void iter_bs(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
+                     Slot* slots, double* part) {
   const dim3 grid((unsigned)cg_grid(op.nf));
   if (precond == 1)
-    hipLaunchKernelGGL((k_cg_iter<true, BS>), grid, dim3(BS), 0, s, j, op, v, slots, st, partials,
-                       ticket);
+    hipLaunchKernelGGL(k_cg_first<true>, grid, dim3(kCgBS), 0, s, op, reg, v, slots, part);
   else
-    hipLaunchKernelGGL((k_cg_iter<false, BS>), grid, dim3(BS), 0, s, j, op, v, slots, st, partials,
-                       ticket);
+    hipLaunchKernelGGL(k_cg_first<false>, grid, dim3(kCgBS), 0, s, op, reg, v, slots, part);
 }
 
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* partials, unsigned* ticket) {
-  if (cg_block_size(op.nf) == 64)
-    iter_bs<64>(s, j, op, precond, v, slots, st, partials, ticket);
+                    Slot* slots, const SolveState* st, double* part) {
+  const dim3 grid((unsigned)cg_grid(op.nf));
+  if (precond == 1)
+    hipLaunchKernelGGL(k_cg_iter<true>, grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
   else
-    iter_bs<256>(s, j, op, precond, v, slots, st, partials, ticket);
+    hipLaunchKernelGGL(k_cg_iter<false>, grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
 }
 
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host) {

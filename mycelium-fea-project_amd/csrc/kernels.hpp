@@ -35,7 +35,7 @@ struct Slot {
   int32_t flag;
   int32_t pad;
 };
-enum SlotFlag : int32_t { kRun = 0, kStop = 1, kBreakdown = 2, kInit = 3 };
+enum SlotFlag : int32_t { kRun = 0, kStop = 1, kBreakdown = 2, kInit = 3, kConverged = 4, kMaxit = 5 };
 
 // Device pointers of the node-block (SELL-64) operator and the CG-CG state.
 struct SellOp {
@@ -131,12 +131,16 @@ void launch_spmv_csr(hipStream_t s, int j, int64_t n, const int64_t* indptr,
 void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double dy_top,
                    double dy_bot, double reg, int precond, const CgVecs& v, double* partials,
                    unsigned* ticket, double* red_out);
-// k_cg_first: w₀ = A u₀; (γ₀, δ₀, r·r, u·u) → slots[1]; slots[0].flag = kInit.
+// part: 2 parity buffers × [4][kCgMaxPartials] block partials (cg.hip)
+constexpr int kCgMaxPartials = 512;
+// k_cg_first: w₀ = A u₀; block partials (γ₀, δ₀, r·r, u·u) → part parity 0;
+// slots[0].flag = kInit.
 void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,
-                     Slot* slots, const SolveState* st, double* partials, unsigned* ticket);
-// iteration j of a chunk: reads slots[j], slots[j+1], writes slots[j+2].
+                     Slot* slots, double* part);
+// iteration j of a chunk: reduces part parity j&1, records slots[j+1], writes
+// its partials to parity (j&1)^1.
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* partials, unsigned* ticket);
+                    Slot* slots, const SolveState* st, double* part);
 // host: mapped pinned mirror of the final SolveState (written once, when done)
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host);
 void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,

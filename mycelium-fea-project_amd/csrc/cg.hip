@@ -200,13 +200,27 @@ __device__ __forceinline__ void wave_partials(const double* __restrict__ p, int 
   }
 }
 
-// block partial (thread 0 stores it; the next launch's waves re-reduce)
+// block partial (thread 0 stores it; the next launch's waves re-reduce).
+// The cross-wave step uses a raw s_barrier behind an LDS-only wait: a
+// __syncthreads() would also wait for every outstanding vector store (vmcnt(0)).
 __device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __restrict__ p) {
-  __shared__ double lds[(kCgBS / 64) * 4];
-  block_sum<4, kCgBS>(acc, lds);
+  constexpr int NW = kCgBS / 64;
+  __shared__ double lds[NW * 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = wave_sum(acc[c]);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lds[wid * 4 + c] = acc[c];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) p[c * kCgMaxG + blockIdx.x] = acc[c];
+    for (int c = 0; c < 4; ++c) {
+      double s = lds[c];
+      for (int w = 1; w < NW; ++w) s += lds[w * 4 + c];
+      p[c * kCgMaxG + blockIdx.x] = s;
+    }
   }
 }
 
@@ -290,17 +304,80 @@ __device__ __forceinline__ void neighbour_mac(const double V[6], int64_t c, doub
 // iteration queued after convergence costs one wasted pass, ≤ 2 chunks).
 // HBM per free row: 11 × 24 B of vectors + 48 B diag + 52 B per slot.
 // ---------------------------------------------------------------------------
+// Own-row operands of one free row, loaded ahead of use (software prefetch).
+template <bool BLOCK>
+struct RowIn {
+  double ro[3], so[3], wo[3], pp[3], xx[3], D[6], M[BLOCK ? 6 : 3];
+  int len;
+  int64_t base;
+};
+
+template <bool BLOCK>
+__device__ __forceinline__ void load_row(int64_t row, const double* __restrict__ r_old,
+                                         const double* __restrict__ s_old,
+                                         const double* __restrict__ w_old,
+                                         const double* __restrict__ pv, const double* __restrict__ xv,
+                                         const double* __restrict__ diag,
+                                         const double* __restrict__ dinv,
+                                         const int32_t* __restrict__ row_len, int64_t N,
+                                         RowIn<BLOCK>& in) {
+  load3(r_old, row, in.ro);
+  load3(s_old, row, in.so);
+  load3(w_old, row, in.wo);
+  load3(pv, row, in.pp);
+  load3(xv, row, in.xx);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) in.D[c] = diag[(int64_t)c * N + row];
+#pragma unroll
+  for (int c = 0; c < (BLOCK ? 6 : 3); ++c) in.M[c] = dinv[(BLOCK ? 6 : 3) * row + c];
+  in.len = row_len[row];
+}
+
+template <bool BLOCK>
+__device__ __forceinline__ void apply_m(const double* M, const double r[3], double u[3]) {
+  if (BLOCK) {
+    sym_apply(M, r, u);
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) u[a] = M[a] * r[a];
+  }
+}
+
 template <bool BLOCK>
 __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
                                                    const SolveState* st, double* part) {
   const int par = j & 1;
-  // scalar loads first in program order so they fly with the partial loads
+  const double* __restrict__ r_old = v.r[par];
+  const double* __restrict__ s_old = v.s[par];
+  const double* __restrict__ w_old = v.w[par];
+  double* __restrict__ r_new = v.r[par ^ 1];
+  double* __restrict__ s_new = v.s[par ^ 1];
+  double* __restrict__ w_new = v.w[par ^ 1];
+  double* __restrict__ xv = v.x;
+  double* __restrict__ pv = v.p;
+  const double* __restrict__ dinv = v.dinv;
+  const double* __restrict__ diag = op.diag;
+  const double* __restrict__ val = op.val;
+  const int32_t* __restrict__ s_col = op.s_col;
+  const int32_t* __restrict__ row_len = op.row_len;
+  const int32_t* __restrict__ slice_ptr = op.slice_ptr;
+  const int64_t G = op.G, N = op.N, nf = op.nf;
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  const int64_t lane = threadIdx.x & 63;
+
+  // 1. the first row's operands, the scalars and the previous partials are
+  //    all independent loads: issue them together (one memory round trip)
+  int64_t row = (int64_t)blockIdx.x * kCgBS + threadIdx.x;
+  RowIn<BLOCK> in;
+  if (row < nf) load_row<BLOCK>(row, r_old, s_old, w_old, pv, xv, diag, dinv, row_len, N, in);
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
   const double g0 = slots[j].v[0], a0 = slots[j].alpha;
   const double tol2 = st->tol2, reg = st->reg;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
   wave_partials(part_buf(part, par), (int)gridDim.x, S);
+
+  // 2. α_j, β_j and the status of iteration j (identical in every wave)
   const double res = norm == 1 ? S[3] : S[2];
   const bool first = f0 == kInit;
   const double beta = first ? 0.0 : S[0] / g0;
@@ -322,52 +399,37 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
     sl.pad = 0;
     slots[j + 1] = sl;
   }
-  const double* __restrict__ r_old = v.r[par];
-  const double* __restrict__ s_old = v.s[par];
-  const double* __restrict__ w_old = v.w[par];
-  double* __restrict__ r_new = v.r[par ^ 1];
-  double* __restrict__ s_new = v.s[par ^ 1];
-  double* __restrict__ w_new = v.w[par ^ 1];
-  double* __restrict__ xv = v.x;
-  double* __restrict__ pv = v.p;
-  const double* __restrict__ dinv = v.dinv;
-  const double* __restrict__ diag = op.diag;
-  const double* __restrict__ val = op.val;
-  const int32_t* __restrict__ s_col = op.s_col;
-  const int32_t* __restrict__ row_len = op.row_len;
-  const int32_t* __restrict__ slice_ptr = op.slice_ptr;
-  const int64_t G = op.G, N = op.N, nf = op.nf;
-  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+
+  // 3. rows (grid-stride; the next row's operands are prefetched)
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t row = (int64_t)blockIdx.x * kCgBS + threadIdx.x; row - threadIdx.x % 64 < nf;
-       row += stride) {
+  for (; row - lane < nf; row += stride) {
     // every lane of a wave shares the slice → scalar load of its slot offset
     const int slice = __builtin_amdgcn_readfirstlane((int)(row >> 6));
     const int64_t base = (int64_t)slice_ptr[slice] * 64 + (row & 63);
-    if (row >= nf) continue;
-    const int len = row_len[row];
-    double ro[3], so[3], wo[3], pp[3], xx[3], uo[3], rn[3], un[3], sn[3], D[6];
-    load3(r_old, row, ro);
-    load3(s_old, row, so);
-    load3(w_old, row, wo);
-    load3(pv, row, pp);
-    load3(xv, row, xx);
-#pragma unroll
-    for (int c = 0; c < 6; ++c) D[c] = diag[(int64_t)c * N + row];
-    apply_minv<BLOCK>(dinv, row, ro, uo);
+    const bool mine = row < nf;
+    RowIn<BLOCK> cur = in;
+    const int64_t nrow = row + stride;
+    if (nrow < nf) load_row<BLOCK>(nrow, r_old, s_old, w_old, pv, xv, diag, dinv, row_len, N, in);
+    if (!mine) continue;
+    double uo[3], rn[3], un[3], sn[3], pp[3], xx[3];
+    apply_m<BLOCK>(cur.M, cur.ro, uo);
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      pp[a] = fma(beta, pp[a], uo[a]);
-      sn[a] = fma(beta, so[a], wo[a]);
-      xx[a] = fma(alpha, pp[a], xx[a]);
-      rn[a] = fma(-alpha, sn[a], ro[a]);
+      pp[a] = fma(beta, cur.pp[a], uo[a]);
+      sn[a] = fma(beta, cur.so[a], cur.wo[a]);
+      xx[a] = fma(alpha, pp[a], cur.xx[a]);
+      rn[a] = fma(-alpha, sn[a], cur.ro[a]);
     }
-    apply_minv<BLOCK>(dinv, row, rn, un);
+    apply_m<BLOCK>(cur.M, rn, un);
+    double D[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) D[c] = cur.D[c];
     D[0] += reg;
     D[3] += reg;
     D[5] += reg;
     double y[3] = {0.0, 0.0, 0.0};
     block_mac(D, un, y);
+    const int len = cur.len;
     // slots two at a time: both columns, then both gathers, in flight together
     int k = 0;
     for (; k + 1 < len; k += 2) {

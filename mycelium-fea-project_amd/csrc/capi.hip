@@ -112,6 +112,15 @@ int set_device(mfea_handle* h) {
   return 0;
 }
 
+// Row ordering of the free nodes: DFS by default; MFEA_ORDER=natural|<window>
+// for experiments (original order / degree sort inside windows).
+int order_mode() {
+  const char* e = std::getenv("MFEA_ORDER");
+  if (!e || !*e || std::strcmp(e, "dfs") == 0) return kOrderDFS;
+  if (std::strcmp(e, "natural") == 0) return 0;
+  return std::atoi(e);
+}
+
 // Build the symbolic pattern and (re)allocate + upload device state.
 int ensure_built(mfea_handle* h) {
   if (!h->has_mesh) return fail(MFEA_ESTATE, "no mesh: call mfea_set_mesh first");
@@ -119,7 +128,7 @@ int ensure_built(mfea_handle* h) {
   destroy_graph(h);
   std::string err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(),
                                   (h->mesh_flags & MFEA_MESH_SKIP_INVALID) != 0, h->top, h->bot,
-                                  /*sort_window=*/512, h->P);
+                                  order_mode(), h->P);
   if (!err.empty()) return fail(MFEA_EINVAL, err);
   const Pattern& P = h->P;
   const int64_t N = P.n_nodes, E = P.n_elems;

@@ -28,7 +28,7 @@ namespace mfea {
 
 constexpr int kCgBS = 256;     // threads per block of the CG kernels
 constexpr int kCgMaxG = kCgMaxPartials;  // max blocks (= partials re-read by each wave)
-constexpr int kCgPU = kCgMaxG / 64;
+static_assert(kCgMaxG == 512, "launch_cg_iter dispatches PU up to 8");
 
 int cg_block_size(int64_t) { return kCgBS; }
 int64_t cg_grid(int64_t rows) {
@@ -175,18 +175,21 @@ __device__ __forceinline__ double* part_buf(double* part, int par) {
 
 // Every lane ends with the grid total of the G partials (block order, then a
 // fixed butterfly): identical in every wave of every block.
+// PU = partial groups of 64 loaded per lane (G ≤ 64·PU); extra groups only
+// add exact zeros, so the result does not depend on PU.
+template <int PU>
 __device__ __forceinline__ void wave_partials(const double* __restrict__ p, int G, double s[4]) {
   const int lane = threadIdx.x & 63;
   // The buffer is always kCgMaxG wide: load every slot unconditionally (a
   // guarded load makes hipcc branch + wait vmcnt(0) per element) and select.
-  double t[kCgPU][4];
+  double t[PU][4];
 #pragma unroll
-  for (int k = 0; k < kCgPU; ++k) {
+  for (int k = 0; k < PU; ++k) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) t[k][c] = p[c * kCgMaxG + lane + 64 * k];
   }
 #pragma unroll
-  for (int k = 0; k < kCgPU; ++k) {
+  for (int k = 0; k < PU; ++k) {
     const bool in = lane + 64 * k < G;
 #pragma unroll
     for (int c = 0; c < 4; ++c) t[k][c] = in ? t[k][c] : 0.0;
@@ -195,7 +198,7 @@ __device__ __forceinline__ void wave_partials(const double* __restrict__ p, int 
   for (int c = 0; c < 4; ++c) {
     double a = 0.0;
 #pragma unroll
-    for (int k = 0; k < kCgPU; ++k) a += t[k][c];
+    for (int k = 0; k < PU; ++k) a += t[k][c];
     s[c] = wave_sum(a);
   }
 }
@@ -343,7 +346,7 @@ __device__ __forceinline__ void apply_m(const double* M, const double r[3], doub
   }
 }
 
-template <bool BLOCK>
+template <bool BLOCK, int PU>
 __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
                                                    const SolveState* st, double* part) {
   const int par = j & 1;
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
   const double tol2 = st->tol2, reg = st->reg;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
-  wave_partials(part_buf(part, par), (int)gridDim.x, S);
+  wave_partials<PU>(part_buf(part, par), (int)gridDim.x, S);
 
   // 2. α_j, β_j and the status of iteration j (identical in every wave)
   const double res = norm == 1 ? S[3] : S[2];
@@ -529,13 +532,23 @@ void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, c
     hipLaunchKernelGGL(k_cg_first<false>, grid, dim3(kCgBS), 0, s, op, reg, v, slots, part);
 }
 
-void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
+template <int PU>
+static void iter_pu(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
                     Slot* slots, const SolveState* st, double* part) {
   const dim3 grid((unsigned)cg_grid(op.nf));
   if (precond == 1)
-    hipLaunchKernelGGL(k_cg_iter<true>, grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
+    hipLaunchKernelGGL((k_cg_iter<true, PU>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
   else
-    hipLaunchKernelGGL(k_cg_iter<false>, grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
+    hipLaunchKernelGGL((k_cg_iter<false, PU>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
+}
+
+void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
+                    Slot* slots, const SolveState* st, double* part) {
+  const int64_t g = cg_grid(op.nf);
+  if (g <= 64) iter_pu<1>(s, j, op, precond, v, slots, st, part);
+  else if (g <= 128) iter_pu<2>(s, j, op, precond, v, slots, st, part);
+  else if (g <= 256) iter_pu<4>(s, j, op, precond, v, slots, st, part);
+  else iter_pu<8>(s, j, op, precond, v, slots, st, part);
 }
 
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host) {

@@ -40,6 +40,11 @@ struct Pattern {
   bool planar = false;             // every z == 0
 };
 
+// sort_window: 0/1 = original node order, kOrderDFS = depth-first order of the
+// free-node graph (default; chains contiguous), >1 = degree sort inside
+// windows of that many rows.
+constexpr int kOrderDFS = -1;
+
 // Validates and builds.  Returns "" on success, else an error message.
 // skip_invalid: drop elements with out-of-range node ids (src/fea_petsc.cpp:241)
 // instead of failing (src/fea_solver.py:82-83 raises).

@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--load-step", type=int, default=20, help="load step index of 40 (dy)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
+    ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
     return ap.parse_args()
 
@@ -125,6 +125,7 @@ def main():
     iter_bytes = nf * (120 + minv + 120 + 48 + 4) + inc * (4 + 48)
     achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
     traffic = None
+    a.traffic = a.traffic or os.path.join(REPO, "profiles", f"traffic_{a.config}.json")
     if os.path.exists(a.traffic):
         try:
             tj = json.load(open(a.traffic))

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 1
+#define MFEA_ABI_VERSION 2
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -152,7 +152,9 @@ typedef struct {
   int64_t n_slots;          /* slot rows × 64 = allocated slot entries              */
   int64_t free_incidences;  /* Σ row_len over free rows = valid slots the SpMV reads */
   int32_t planar;           /* all z == 0                                           */
-  int32_t pad;
+  int32_t cg_lanes;         /* 1: CG iterations run on the wave-local lane operator */
+  int64_t n_lanes;          /* lanes of that operator (owners + helpers + padding)   */
+  int64_t n_halo;           /* lanes with an out-of-wave slot (one push per iteration) */
 } mfea_info;
 int mfea_get_info(mfea_handle* h, mfea_info* info);
 /* Launches the dominant kernel — the fused SpMV + single-reduction CG iteration —

@@ -1,0 +1,23 @@
+/* mfea_debug.h — diagnostics of the mfea engine (not part of the reference's
+ * interface; no reference counterpart).  Same ABI rules as mfea.h. */
+#ifndef MFEA_DEBUG_H
+#define MFEA_DEBUG_H
+#include <stdint.h>
+
+#include "mfea.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One traced launch of the CG iteration kernel in the running state that
+ * mfea_profile_iteration sets up.  For every wave w (block·4 + wave), out[4w+k]
+ * holds s_memrealtime (100 MHz) at k = 0 entry, 1 partials reduced (α, β
+ * known), 2 SpMV of its last row done, 3 its stores drained.  cap >= 4·waves. */
+int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64_t cap,
+                               int64_t* n_waves);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

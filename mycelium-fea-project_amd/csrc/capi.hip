@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "kernels.hpp"
+#include "mfea_debug.h"
 #include "mfea.h"
 #include "symbolic.hpp"
 
@@ -73,6 +74,12 @@ struct mfea_handle {
   DevBuf<int32_t> slice_ptr, row_len, s_col, s_elem, e2n_d;
   DevBuf<uint8_t> active, code;
   DevBuf<unsigned> tickets;
+  // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
+  Ell L;
+  bool ell_ok = false;
+  DevBuf<uint32_t> e_code;
+  DevBuf<int32_t> e_partner, e_lane_row, e_src_pos, e_nbr_lane;
+  DevBuf<double> e_f;  // all lane-operator doubles, carved by ell_op / ell_vecs
   DevBuf<Slot> slots;
   DevBuf<SolveState> state;
   SolveState* h_state = nullptr;  // pinned, 2 entries
@@ -81,7 +88,7 @@ struct mfea_handle {
   int64_t G = 0;                  // slots·64
   // graph cache
   hipGraphExec_t graph = nullptr;
-  int graph_chunk = 0, graph_precond = -1;
+  int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipEvent_t ev[6] = {};
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
@@ -95,6 +102,9 @@ struct mfea_handle {
 namespace {
 
 constexpr int kMaxChunk = 64;
+// lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6, h × 2 18, hM 6
+constexpr int64_t kEllDoubles = 18 + 6 + 3 + 3 + 18 + 6 + 18 + 6;
+static_assert(kEllNone == kSrcNone && kEllHalo == kSrcHalo, "slot source codes");
 constexpr int kTicketSets = 16;
 
 // ticket set k (one per reducing kernel kind; see device_util.hpp layout)
@@ -105,6 +115,7 @@ void destroy_graph(mfea_handle* h) {
   h->graph = nullptr;
   h->graph_chunk = 0;
   h->graph_precond = -1;
+  h->graph_ell = -1;
 }
 
 int set_device(mfea_handle* h) {
@@ -184,10 +195,38 @@ int ensure_built(mfea_handle* h) {
   } else {
     HIPC(hipMemsetAsync(h->active.ptr, 1, E, s));
   }
+  // wave-local lanes (falls back to the SELL kernel when a row cannot be placed)
+  h->ell_ok = build_ell(P, h->L).empty() && P.n_free > 0;
+  if (h->ell_ok) {
+    const Ell& L = h->L;
+    const int64_t NL = L.n_lanes;
+    std::vector<uint32_t> code(NL);
+    for (int64_t l = 0; l < NL; ++l)
+      code[l] = (L.code[l] & 0xFFFFFFu) | (uint32_t)(uint8_t)(int8_t)L.info[l] << 24;
+    HIPC(h->e_code.alloc(NL));
+    HIPC(h->e_partner.alloc(NL));
+    HIPC(h->e_lane_row.alloc(NL));
+    HIPC(h->e_src_pos.alloc(3 * NL));
+    HIPC(h->e_nbr_lane.alloc(3 * NL));
+    HIPC(h->e_f.alloc(kEllDoubles * NL));
+    HIPC(up(h->e_code.ptr, code.data(), NL * sizeof(uint32_t)));
+    HIPC(up(h->e_partner.ptr, L.partner.data(), NL * sizeof(int32_t)));
+    HIPC(up(h->e_lane_row.ptr, L.lane_row.data(), NL * sizeof(int32_t)));
+    HIPC(up(h->e_src_pos.ptr, L.src_pos.data(), 3 * NL * sizeof(int32_t)));
+    HIPC(up(h->e_nbr_lane.ptr, L.nbr_lane.data(), 3 * NL * sizeof(int32_t)));
+    // halo records of lanes without a halo slot are read but never used
+    HIPC(hipMemsetAsync(h->e_f.ptr, 0, kEllDoubles * NL * sizeof(double), s));
+  }
   HIPC(hipStreamSynchronize(s));
   h->active_host.clear();
   h->dirty = false;
   return 0;
+}
+
+// MFEA_CG_KERNEL=sell forces the SELL iteration kernel (comparison runs)
+bool use_ell(const mfea_handle* h) {
+  const char* e = std::getenv("MFEA_CG_KERNEL");
+  return h->ell_ok && !(e && std::strcmp(e, "sell") == 0);
 }
 
 mfea_solve_opts default_opts() {
@@ -229,13 +268,64 @@ CgVecs cg_vecs(mfea_handle* h) {
   return v;
 }
 
+// planar meshes run the lanes with 2 DOFs per node (MFEA_LANE_DOF=3 forces 3)
+int lane_dofs(const mfea_handle* h) {
+  const char* e = std::getenv("MFEA_LANE_DOF");
+  return (h->P.planar && !(e && std::strcmp(e, "3") == 0)) ? 2 : 3;
+}
+
+EllOp ell_op(mfea_handle* h) {
+  EllOp op;
+  const int64_t NL = h->L.n_lanes;
+  op.NL = NL;
+  op.nd = lane_dofs(h);
+  op.code = h->e_code.ptr;
+  op.partner = h->e_partner.ptr;
+  op.lane_row = h->e_lane_row.ptr;
+  op.src_pos = h->e_src_pos.ptr;
+  op.nbr_lane = h->e_nbr_lane.ptr;
+  op.V = h->e_f.ptr;
+  op.D = op.V + 18 * NL;
+  return op;
+}
+
+EllVecs ell_vecs(mfea_handle* h) {
+  EllVecs v;
+  const int64_t NL = h->L.n_lanes;
+  double* f = h->e_f.ptr + 24 * NL;
+  auto take = [&](int64_t n) {
+    double* p = f;
+    f += n * NL;
+    return p;
+  };
+  v.x = take(3);
+  v.p = take(3);
+  for (int q = 0; q < 2; ++q) {
+    v.r[q] = take(3);
+    v.s[q] = take(3);
+    v.w[q] = take(3);
+  }
+  v.M = take(6);
+  v.h[0] = take(9);
+  v.h[1] = take(9);
+  v.hM = take(6);
+  return v;
+}
+
 // enqueue one chunk of single-reduction CG iterations (one kernel each)
-void enqueue_chunk_sell(mfea_handle* h, int chunk, int precond) {
+void enqueue_chunk(mfea_handle* h, int chunk, int precond, bool ell) {
   hipStream_t s = h->stream;
-  const SellOp op = sell_op(h);
-  const CgVecs v = cg_vecs(h);
-  for (int j = 0; j < chunk; ++j)
-    launch_cg_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+  if (ell) {
+    const EllOp op = ell_op(h);
+    const EllVecs v = ell_vecs(h);
+    for (int j = 0; j < chunk; ++j)
+      launch_ell_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+  } else {
+    const SellOp op = sell_op(h);
+    const CgVecs v = cg_vecs(h);
+    for (int j = 0; j < chunk; ++j)
+      launch_cg_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+  }
   launch_cg_advance(s, chunk, h->slots.ptr, h->state.ptr, h->d_host_state);
 }
 
@@ -314,46 +404,58 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
                 tix(h, 0), h->red.ptr);
   launch_cg_init_finalize(s, h->red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
                           h->state.ptr);
-  launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->cg_part.ptr);
+  HIPC(hipMemsetAsync(h->cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  const bool ell = use_ell(h);
+  if (ell) {
+    launch_ell_init(s, ell_op(h), op, precond, v, ell_vecs(h));
+    launch_ell_first(s, ell_op(h), o->reg, precond, ell_vecs(h), h->slots.ptr, h->cg_part.ptr);
+  } else {
+    launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->cg_part.ptr);
+  }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
   // MFEA_NO_GRAPH=1: launch the chunk kernels eagerly (profilers that do not
   // follow hipGraph replays; same kernels, same order)
   static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  SolveState fin;
+  int rc;
   if (no_graph) {
-    SolveState fin;
-    int rc = drive_chunks(
+    rc = drive_chunks(
         h, chunk, o->max_it,
         [&]() -> int {
-          enqueue_chunk_sell(h, chunk, precond);
+          enqueue_chunk(h, chunk, precond, ell);
           HIPC(hipGetLastError());
           return 0;
         },
         &fin, /*mirror=*/true);
-    if (rc) return rc;
-    return finish_solve(h, o, nf, fin, st);
+  } else {
+    if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != precond ||
+        h->graph_ell != (ell ? lane_dofs(h) : 0)) {
+      destroy_graph(h);
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      enqueue_chunk(h, chunk, precond, ell);
+      HIPC(hipStreamEndCapture(s, &g));
+      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_chunk = chunk;
+      h->graph_precond = precond;
+      h->graph_ell = ell ? lane_dofs(h) : 0;
+    }
+    rc = drive_chunks(
+        h, chunk, o->max_it,
+        [&]() -> int {
+          HIPC(hipGraphLaunch(h->graph, s));
+          return 0;
+        },
+        &fin, /*mirror=*/true);
   }
-  if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != precond) {
-    destroy_graph(h);
-    hipGraph_t g;
-    HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    enqueue_chunk_sell(h, chunk, precond);
-    HIPC(hipStreamEndCapture(s, &g));
-    hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    HIPC(e);
-    h->graph_chunk = chunk;
-    h->graph_precond = precond;
-  }
-  SolveState fin;
-  int rc = drive_chunks(
-      h, chunk, o->max_it,
-      [&]() -> int {
-        HIPC(hipGraphLaunch(h->graph, s));
-        return 0;
-      },
-      &fin, /*mirror=*/true);
   if (rc) return rc;
+  if (ell) {
+    launch_ell_finish(s, ell_op(h), ell_vecs(h), h->x.ptr);
+    HIPC(hipGetLastError());
+  }
   return finish_solve(h, o, nf, fin, st);
 }
 
@@ -764,7 +866,23 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
   for (int64_t i = 0; i < P.n_free; ++i) inc += P.row_len[i];
   info->free_incidences = inc;
   info->planar = P.planar ? 1 : 0;
+  info->cg_lanes = use_ell(h) ? 1 : 0;
+  info->n_lanes = h->ell_ok ? h->L.n_lanes : 0;
+  int64_t halo = 0;
+  if (h->ell_ok)
+    for (int32_t pt : h->L.partner) halo += pt >= 0;
+  info->n_halo = halo;
   return 0;
+}
+
+// iteration 0 of the active CG kernel (profiling / tracing)
+static void launch_iter0(mfea_handle* h, int pc, unsigned long long* trace) {
+  if (use_ell(h))
+    launch_ell_iter(h->stream, 0, ell_op(h), pc, ell_vecs(h), h->slots.ptr, h->state.ptr,
+                    h->cg_part.ptr, trace);
+  else
+    launch_cg_iter(h->stream, 0, sell_op(h), pc, cg_vecs(h), h->slots.ptr, h->state.ptr,
+                   h->cg_part.ptr, trace);
 }
 
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms) {
@@ -772,8 +890,6 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   if (int rc = set_device(h)) return rc;
   if (int rc = ensure_built(h)) return rc;
   hipStream_t s = h->stream;
-  const SellOp op = sell_op(h);
-  const CgVecs v = cg_vecs(h);
   const int pc = precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
   // Running state with tol 0: slots[0] = INIT and parity-0 partials of 1, so
   // γ = δ = ‖r‖² = ‖u‖² = G > 0, α = 1, β = 0.  Every launch is iteration 0
@@ -789,16 +905,36 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   std::memset(&s0, 0, sizeof(s0));
   s0.flag = kInit;
   HIPC(hipMemcpyAsync(h->slots.ptr, &s0, sizeof(s0), hipMemcpyHostToDevice, s));
-  launch_cg_iter(s, 0, op, pc, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);  // warm
+  launch_iter0(h, pc, nullptr);  // warm
   HIPC(hipEventRecord(h->ev[0], s));
-  for (int k = 0; k < reps; ++k)
-    launch_cg_iter(s, 0, op, pc, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+  for (int k = 0; k < reps; ++k) launch_iter0(h, pc, nullptr);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[1], s));
   HIPC(hipEventSynchronize(h->ev[1]));
   float ms = 0;
   HIPC(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
   *avg_ms = ms / reps;
+  return 0;
+}
+
+int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64_t cap,
+                               int64_t* n_waves) {
+  if (!h || !out || !n_waves || cap < 0) return fail(MFEA_EINVAL, "bad argument");
+  double ms = 0;
+  if (int rc = mfea_profile_iteration(h, precond, 20, &ms)) return rc;  // same running state
+  hipStream_t s = h->stream;
+  const int64_t g = cg_grid(use_ell(h) ? h->L.n_lanes : h->P.n_free);
+  const int64_t nw = g * (cg_block_size(0) / 64);
+  if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
+  unsigned long long* d = nullptr;
+  HIPC(hipMalloc(&d, nw * 4 * sizeof(unsigned long long)));
+  HIPC(hipMemsetAsync(d, 0, nw * 4 * sizeof(unsigned long long), s));
+  launch_iter0(h, precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0, d);
+  hipError_t e = hipMemcpyAsync(out, d, nw * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(MFEA_EDEVICE, hipGetErrorString(e));
+  *n_waves = nw;
   return 0;
 }
 

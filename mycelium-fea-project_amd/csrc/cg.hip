@@ -26,8 +26,6 @@
 
 namespace mfea {
 
-constexpr int kCgBS = 256;     // threads per block of the CG kernels
-constexpr int kCgMaxG = kCgMaxPartials;  // max blocks (= partials re-read by each wave)
 static_assert(kCgMaxG == 512, "launch_cg_iter dispatches PU up to 8");
 
 int cg_block_size(int64_t) { return kCgBS; }
@@ -61,12 +59,6 @@ __device__ __forceinline__ void store3(double* __restrict__ v, int64_t row, cons
   v[3 * row + 2] = o[2];
 }
 
-// y += V u with V the symmetric block (v0..v5)
-__device__ __forceinline__ void block_mac(const double V[6], const double u[3], double y[3]) {
-  y[0] = fma(V[0], u[0], fma(V[1], u[1], fma(V[2], u[2], y[0])));
-  y[1] = fma(V[1], u[0], fma(V[3], u[1], fma(V[4], u[2], y[1])));
-  y[2] = fma(V[2], u[0], fma(V[4], u[1], fma(V[5], u[2], y[2])));
-}
 
 
 // ---------------------------------------------------------------------------
@@ -164,67 +156,6 @@ __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, 
   st->done = 0;
   st->iters = 0;
   st->status = 0;
-}
-
-// ---------------------------------------------------------------------------
-// Partial-sum protocol.  part = two parity buffers of [4][kCgMaxG] doubles.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double* part_buf(double* part, int par) {
-  return part + (size_t)par * 4 * kCgMaxG;
-}
-
-// Every lane ends with the grid total of the G partials (block order, then a
-// fixed butterfly): identical in every wave of every block.
-// PU = partial groups of 64 loaded per lane (G ≤ 64·PU); extra groups only
-// add exact zeros, so the result does not depend on PU.
-template <int PU>
-__device__ __forceinline__ void wave_partials(const double* __restrict__ p, int G, double s[4]) {
-  const int lane = threadIdx.x & 63;
-  // The buffer is always kCgMaxG wide: load every slot unconditionally (a
-  // guarded load makes hipcc branch + wait vmcnt(0) per element) and select.
-  double t[PU][4];
-#pragma unroll
-  for (int k = 0; k < PU; ++k) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) t[k][c] = p[c * kCgMaxG + lane + 64 * k];
-  }
-#pragma unroll
-  for (int k = 0; k < PU; ++k) {
-    const bool in = lane + 64 * k < G;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) t[k][c] = in ? t[k][c] : 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    double a = 0.0;
-#pragma unroll
-    for (int k = 0; k < PU; ++k) a += t[k][c];
-    s[c] = wave_sum(a);
-  }
-}
-
-// block partial (thread 0 stores it; the next launch's waves re-reduce).
-// The cross-wave step uses a raw s_barrier behind an LDS-only wait: a
-// __syncthreads() would also wait for every outstanding vector store (vmcnt(0)).
-__device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __restrict__ p) {
-  constexpr int NW = kCgBS / 64;
-  __shared__ double lds[NW * 4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) acc[c] = wave_sum(acc[c]);
-  if (lane == 0) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) lds[wid * 4 + c] = acc[c];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      double s = lds[c];
-      for (int w = 1; w < NW; ++w) s += lds[w * 4 + c];
-      p[c * kCgMaxG + blockIdx.x] = s;
-    }
-  }
 }
 
 // w₀ = A u₀ and the first partials (γ₀, δ₀, ‖r₀‖², ‖u₀‖²) → parity 0;
@@ -336,19 +267,13 @@ __device__ __forceinline__ void load_row(int64_t row, const double* __restrict__
   in.len = row_len[row];
 }
 
-template <bool BLOCK>
-__device__ __forceinline__ void apply_m(const double* M, const double r[3], double u[3]) {
-  if (BLOCK) {
-    sym_apply(M, r, u);
-  } else {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) u[a] = M[a] * r[a];
-  }
-}
 
-template <bool BLOCK, int PU>
+
+template <bool BLOCK, int PU, bool TRACE = false>
 __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, Slot* slots,
-                                                   const SolveState* st, double* part) {
+                                                   const SolveState* st, double* part,
+                                                   unsigned long long* trace) {
+  trace_point<TRACE>(trace, 0, 0.0);
   const int par = j & 1;
   const double* __restrict__ r_old = v.r[par];
   const double* __restrict__ s_old = v.s[par];
@@ -378,33 +303,18 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
   const double tol2 = st->tol2, reg = st->reg;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
-  wave_partials<PU>(part_buf(part, par), (int)gridDim.x, S);
+  wave_partials<PU>(part_buf(part, par), S);
+  trace_point<TRACE>(trace, 1, S[0]);
 
   // 2. α_j, β_j and the status of iteration j (identical in every wave)
-  const double res = norm == 1 ? S[3] : S[2];
-  const bool first = f0 == kInit;
-  const double beta = first ? 0.0 : S[0] / g0;
-  const double den = first ? S[1] : S[1] - beta * S[0] / a0;
-  const double alpha = S[0] / den;
-  int status;
-  if (f0 != kRun && f0 != kInit) status = kStop;
-  else if (!(res > tol2)) status = isfinite(res) ? kConverged : kBreakdown;
-  else if (base_it + j >= max_it) status = kMaxit;
-  else status = ((den > 0.0) && isfinite(alpha) && isfinite(beta)) ? kRun : kBreakdown;
-  const bool go = status == kRun;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    Slot sl;
-    sl.v[0] = S[0]; sl.v[1] = S[1]; sl.v[2] = S[2]; sl.v[3] = S[3];
-    sl.alpha = alpha;
-    sl.beta = beta;
-    sl.res = res;
-    sl.flag = status;
-    sl.pad = 0;
-    slots[j + 1] = sl;
-  }
+  const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
+  const double alpha = cs.alpha, beta = cs.beta;
+  const bool go = cs.status == kRun;
+  cg_record(slots, j, S, cs);
 
   // 3. rows (grid-stride; the next row's operands are prefetched)
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double ylast = 0.0;
   for (; row - lane < nf; row += stride) {
     // every lane of a wave shares the slice → scalar load of its slot offset
     const int slice = __builtin_amdgcn_readfirstlane((int)(row >> 6));
@@ -424,6 +334,13 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
       rn[a] = fma(-alpha, sn[a], cur.ro[a]);
     }
     apply_m<BLOCK>(cur.M, rn, un);
+    // own-row results leave now: their write-back overlaps the gathers below
+    if (go) {
+      store3(pv, row, pp);
+      store3(xv, row, xx);
+      store3(s_new, row, sn);
+      store3(r_new, row, rn);
+    }
     double D[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) D[c] = cur.D[c];
@@ -455,13 +372,8 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
       for (int q = 0; q < 6; ++q) V0[q] = val[q * G + i0];
       neighbour_mac<BLOCK>(V0, c0, alpha, beta, r_old, s_old, w_old, dinv, y);
     }
-    if (go) {
-      store3(pv, row, pp);
-      store3(xv, row, xx);
-      store3(s_new, row, sn);
-      store3(r_new, row, rn);
-      store3(w_new, row, y);
-    }
+    if (TRACE) ylast = y[0];
+    if (go) store3(w_new, row, y);
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       acc[0] = fma(rn[a], un[a], acc[0]);
@@ -470,7 +382,12 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
       acc[3] = fma(un[a], un[a], acc[3]);
     }
   }
+  trace_point<TRACE>(trace, 2, ylast);
   if (go) store_block_partial(acc, part_buf(part, par ^ 1));
+  if (TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    trace_point<TRACE>(trace, 3, acc[0]);
+  }
 }
 
 // End of a chunk: find the first iteration that did not run (one wave, one
@@ -532,23 +449,33 @@ void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, c
     hipLaunchKernelGGL(k_cg_first<false>, grid, dim3(kCgBS), 0, s, op, reg, v, slots, part);
 }
 
-template <int PU>
+template <int PU, bool TRACE>
 static void iter_pu(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* part) {
+                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
   const dim3 grid((unsigned)cg_grid(op.nf));
   if (precond == 1)
-    hipLaunchKernelGGL((k_cg_iter<true, PU>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
+    hipLaunchKernelGGL((k_cg_iter<true, PU, TRACE>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st,
+                       part, trace);
   else
-    hipLaunchKernelGGL((k_cg_iter<false, PU>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st, part);
+    hipLaunchKernelGGL((k_cg_iter<false, PU, TRACE>), grid, dim3(kCgBS), 0, s, j, op, v, slots, st,
+                       part, trace);
+}
+
+template <bool TRACE>
+static void iter_dispatch(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
+                          Slot* slots, const SolveState* st, double* part,
+                          unsigned long long* trace) {
+  const int64_t g = cg_grid(op.nf);
+  if (g <= 64) iter_pu<1, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else if (g <= 128) iter_pu<2, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else if (g <= 256) iter_pu<4, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else iter_pu<8, TRACE>(s, j, op, precond, v, slots, st, part, trace);
 }
 
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* part) {
-  const int64_t g = cg_grid(op.nf);
-  if (g <= 64) iter_pu<1>(s, j, op, precond, v, slots, st, part);
-  else if (g <= 128) iter_pu<2>(s, j, op, precond, v, slots, st, part);
-  else if (g <= 256) iter_pu<4>(s, j, op, precond, v, slots, st, part);
-  else iter_pu<8>(s, j, op, precond, v, slots, st, part);
+                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
+  if (trace) iter_dispatch<true>(s, j, op, precond, v, slots, st, part, trace);
+  else iter_dispatch<false>(s, j, op, precond, v, slots, st, part, nullptr);
 }
 
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host) {

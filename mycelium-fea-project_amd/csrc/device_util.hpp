@@ -11,6 +11,31 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// DPP move of a double (two 32-bit halves), all lanes active
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+// Wave total in every lane, in a fixed order (identical in every wave):
+// quad sums by quad_perm, 8- and 16-lane sums by row_half_mirror / row_mirror
+// (each step pairs two equal-order partial sums, so all lanes of a row agree
+// bitwise), then the four row sums read out as scalars.  VALU only: no LDS
+// round trips (a __shfl_xor butterfly is 12 ds_bpermute_b32 per double).
+__device__ __forceinline__ double wave_allsum(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+
 // Ticket layout: one ticket set = kTicketStride unsigned; shard s counter at
 // s·16 (64 B apart, separate lines), the top counter at kShards·16.
 constexpr int kShards = 8;
@@ -155,6 +180,134 @@ __device__ __forceinline__ void sym_inverse(const double A[6], double B[6]) {
   const double id = 1.0 / det;
   B[0] = c00 * id; B[1] = c01 * id; B[2] = c02 * id;
   B[3] = c11 * id; B[4] = c12 * id; B[5] = c22 * id;
+}
+
+// ---------------------------------------------------------------------------
+// Shared pieces of the CG iteration kernels (cg.hip: SELL operator, ell.hip:
+// wave-local lanes).
+// ---------------------------------------------------------------------------
+constexpr int kCgBS = 256;               // threads per block of the CG kernels
+constexpr int kCgMaxG = kCgMaxPartials;  // max blocks (= partials re-read by each wave)
+
+// y += V u with V the symmetric block (v0..v5)
+__device__ __forceinline__ void block_mac(const double V[6], const double u[3], double y[3]) {
+  y[0] = fma(V[0], u[0], fma(V[1], u[1], fma(V[2], u[2], y[0])));
+  y[1] = fma(V[1], u[0], fma(V[3], u[1], fma(V[4], u[2], y[1])));
+  y[2] = fma(V[2], u[0], fma(V[4], u[1], fma(V[5], u[2], y[2])));
+}
+
+template <bool BLOCK>
+__device__ __forceinline__ void apply_m(const double* M, const double r[3], double u[3]) {
+  if (BLOCK) {
+    sym_apply(M, r, u);
+  } else {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) u[a] = M[a] * r[a];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Partial-sum protocol.  part = two parity buffers of [4][kCgMaxG] doubles.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double* part_buf(double* part, int par) {
+  return part + (size_t)par * 4 * kCgMaxG;
+}
+
+// Every lane ends with the grid total of the partials (block order, then a
+// fixed butterfly): identical in every wave of every block.  PU = partial
+// groups of 64 loaded per lane (G ≤ 64·PU).  The buffer is zeroed at the start
+// of every solve and only blocks < G write it, so the slots ≥ G add exact
+// zeros: every load is unconditional (a guarded or selected load makes hipcc
+// branch and wait vmcnt(0) on all outstanding loads).
+template <int PU>
+__device__ __forceinline__ void wave_partials(const double* __restrict__ p, double s[4]) {
+  const int lane = threadIdx.x & 63;
+  double t[PU][4];
+#pragma unroll
+  for (int k = 0; k < PU; ++k) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[k][c] = p[c * kCgMaxG + lane + 64 * k];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double a = 0.0;
+#pragma unroll
+    for (int k = 0; k < PU; ++k) a += t[k][c];
+    s[c] = wave_allsum(a);
+  }
+}
+
+// block partial (thread 0 stores it; the next launch's waves re-reduce).
+// The cross-wave step uses a raw s_barrier behind an LDS-only wait: a
+// __syncthreads() would also wait for every outstanding vector store (vmcnt(0)).
+__device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __restrict__ p) {
+  constexpr int NW = kCgBS / 64;
+  __shared__ double lds[NW * 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = wave_allsum(acc[c]);
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lds[wid * 4 + c] = acc[c];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double s = lds[c];
+      for (int w = 1; w < NW; ++w) s += lds[w * 4 + c];
+      p[c * kCgMaxG + blockIdx.x] = s;
+    }
+  }
+}
+
+// α_j, β_j and the status of iteration j from the reduced partials S and the
+// previous slot (identical in every wave of every block).
+struct CgScalars {
+  double alpha, beta, res;
+  int status;
+};
+__device__ __forceinline__ CgScalars cg_scalars(const double S[4], int f0, double g0, double a0,
+                                                double tol2, int it, int max_it, int norm) {
+  CgScalars c;
+  c.res = norm == 1 ? S[3] : S[2];
+  const bool first = f0 == kInit;
+  c.beta = first ? 0.0 : S[0] / g0;
+  const double den = first ? S[1] : S[1] - c.beta * S[0] / a0;
+  c.alpha = S[0] / den;
+  if (f0 != kRun && f0 != kInit) c.status = kStop;
+  else if (!(c.res > tol2)) c.status = isfinite(c.res) ? kConverged : kBreakdown;
+  else if (it >= max_it) c.status = kMaxit;
+  else c.status = ((den > 0.0) && isfinite(c.alpha) && isfinite(c.beta)) ? kRun : kBreakdown;
+  return c;
+}
+
+// block 0 records iteration j's scalars in slots[j + 1]
+__device__ __forceinline__ void cg_record(Slot* slots, int j, const double S[4],
+                                          const CgScalars& c) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Slot sl;
+    sl.v[0] = S[0]; sl.v[1] = S[1]; sl.v[2] = S[2]; sl.v[3] = S[3];
+    sl.alpha = c.alpha;
+    sl.beta = c.beta;
+    sl.res = c.res;
+    sl.flag = c.status;
+    sl.pad = 0;
+    slots[j + 1] = sl;
+  }
+}
+
+// TRACE: lane 0 of every wave records s_memrealtime (100 MHz) at entry, once
+// the partials are reduced, once the last row's SpMV is done, and after its
+// stores have drained: trace[(block·4 + wave)·4 + point] (diagnostics only).
+template <bool TRACE>
+__device__ __forceinline__ void trace_point(unsigned long long* trace, int point, double dep) {
+  if (TRACE) {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
+    if ((threadIdx.x & 63) == 0)
+      trace[((size_t)blockIdx.x * (kCgBS / 64) + (threadIdx.x >> 6)) * 4 + point] = t;
+  }
 }
 
 }  // namespace mfea

@@ -1,0 +1,523 @@
+// ell.hip — single-reduction PCG (Chronopoulos–Gear, as in cg.hip) on the
+// wave-local lane operator of symbolic.hpp ("Ell"): ONE memory round trip per
+// iteration.
+//
+// The SELL kernel (cg.hip) pays a chain of dependent loads per iteration:
+// slot offset → neighbour column → neighbour r, s, w (≈ 2.7 µs measured with
+// tools/trace_iter.py on C2, after the 2.4 µs hop that brings the row's own
+// operands and the partials).  Here every operand a lane needs sits at an
+// address computable from its lane index alone:
+//   - own vectors, M, the diagonal block and three slot blocks (k-major);
+//   - a neighbour owned by a lane of the SAME wave: its fresh u_j is read from
+//     the wave's LDS exchange row after that lane wrote it;
+//   - an out-of-wave neighbour (slot 0 only): its previous-iteration r, s, w
+//     (and its M) were pushed into this lane's halo record by the partner lane
+//     in the previous launch; u_j = M_j (r_j − α (w_j + β s_j)) is recomputed
+//     with exactly the owner's operations, so every lane sees bitwise the u_j
+//     its owner uses.
+// Helper lanes (rows with more than three slots or several halo slots) add
+// their partial A u into the owner lane in a fixed order; they carry no vector
+// state (all zero) and never store.
+//
+// ND = 2: planar meshes (all z = 0).  The z DOFs decouple exactly (xz, yz
+// couplings are exactly 0 and b_z = 0), so every z
+// component of every Krylov vector stays exactly 0 and contributes exact
+// zeros to every sum: dropping them gives bitwise the 3-DOF iterates with
+// 40 % fewer bytes per lane.  Symmetric blocks then hold (xx, xy, yy).
+#include "device_util.hpp"
+#include "kernels.hpp"
+
+namespace mfea {
+
+template <int ND>
+struct Dof {
+  static constexpr int NB = ND == 3 ? 6 : 3;  // components of a symmetric block
+  static constexpr int LDSW = ND == 3 ? 4 : 2;  // doubles per lane in an LDS row
+};
+template <int ND, bool BLOCK>
+constexpr int n_minv() { return BLOCK ? Dof<ND>::NB : ND; }
+// SELL / row-order component of lane-block component c (2-D: xx, xy, yy)
+template <int ND>
+__device__ __forceinline__ int blk_src(int c) { return ND == 3 ? c : (c == 2 ? 3 : c); }
+
+template <int ND>
+__device__ __forceinline__ void lload(const double* __restrict__ v, int64_t NL, int64_t l,
+                                      double* o) {
+#pragma unroll
+  for (int c = 0; c < ND; ++c) o[c] = v[c * NL + l];
+}
+template <int ND>
+__device__ __forceinline__ void lstore(double* __restrict__ v, int64_t NL, int64_t l,
+                                       const double* o) {
+#pragma unroll
+  for (int c = 0; c < ND; ++c) v[c * NL + l] = o[c];
+}
+
+// y += V u (symmetric block)
+template <int ND>
+__device__ __forceinline__ void bmac(const double* V, const double* u, double* y) {
+  if (ND == 3) {
+    block_mac(V, u, y);
+  } else {  // = block_mac with V_xz = V_yz = 0, u_z = 0
+    y[0] = fma(V[0], u[0], fma(V[1], u[1], y[0]));
+    y[1] = fma(V[1], u[0], fma(V[2], u[1], y[1]));
+  }
+}
+// u = M r
+template <int ND, bool BLOCK>
+__device__ __forceinline__ void mapply(const double* M, const double* r, double* u) {
+  if (!BLOCK) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) u[a] = M[a] * r[a];
+  } else if (ND == 3) {
+    sym_apply(M, r, u);
+  } else {  // = sym_apply with B_xz = B_yz = 0, r_z = 0
+    u[0] = fma(M[0], r[0], M[1] * r[1]);
+    u[1] = fma(M[1], r[0], M[2] * r[1]);
+  }
+}
+
+__device__ __forceinline__ int group_info(uint32_t code) { return (int)(int8_t)(code >> 24); }
+
+__device__ __forceinline__ int wave_max_i(int m) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, 64));
+  return m;
+}
+
+// LDS stores of this wave visible to its own later LDS loads (DS ops of one
+// wave execute in order; the wait keeps the compiler from reordering too)
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// Lane operator values and initial vectors (once per solve).
+// ---------------------------------------------------------------------------
+template <int ND, bool BLOCK>
+__global__ __launch_bounds__(kCgBS) void k_ell_init(EllOp op, SellOp sop, CgVecs rv, EllVecs v) {
+  constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>();
+  const int64_t NL = op.NL;
+  const double zero[3] = {0.0, 0.0, 0.0};
+  for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l < NL;
+       l += (int64_t)gridDim.x * kCgBS) {
+    const int32_t row = op.lane_row[l];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int32_t sp = op.src_pos[k * NL + l];
+#pragma unroll
+      for (int c = 0; c < NB; ++c)
+        op.V[(c * 3 + k) * NL + l] = sp >= 0 ? sop.val[(int64_t)blk_src<ND>(c) * sop.G + sp] : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+      op.D[c * NL + l] = row >= 0 ? sop.diag[(int64_t)blk_src<ND>(c) * sop.N + row] : 0.0;
+#pragma unroll
+    for (int c = 0; c < NM; ++c)
+      v.M[c * NL + l] = row >= 0 ? rv.dinv[(int64_t)(BLOCK ? 6 : 3) * row + (BLOCK ? blk_src<ND>(c) : c)]
+                                 : 0.0;
+    double b[3] = {0.0, 0.0, 0.0};
+    if (row >= 0) {
+#pragma unroll
+      for (int c = 0; c < ND; ++c) b[c] = rv.r[0][3 * (int64_t)row + c];
+    }
+    lstore<ND>(v.r[0], NL, l, b);
+    lstore<ND>(v.r[1], NL, l, zero);
+    lstore<ND>(v.x, NL, l, zero);
+    lstore<ND>(v.p, NL, l, zero);
+    for (int q = 0; q < 2; ++q) {
+      lstore<ND>(v.s[q], NL, l, zero);
+      lstore<ND>(v.w[q], NL, l, zero);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// w₀ = A u₀ with the neighbours pulled through nbr_lane (the only gather of
+// the solve), halo records of parity 0 (r₀, s₀ = 0, w₀ and M), partials
+// (γ₀, δ₀, ‖r₀‖², ‖u₀‖²) → parity 0, slots[0] = INIT.
+// ---------------------------------------------------------------------------
+template <int ND, bool BLOCK>
+__global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
+                                                     double* part) {
+  constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>();
+  const int64_t NL = op.NL;
+  const int lane = threadIdx.x & 63;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l - lane < NL;
+       l += (int64_t)gridDim.x * kCgBS) {
+    double r[ND], M[NM], u[ND], D[NB];
+    lload<ND>(v.r[0], NL, l, r);
+#pragma unroll
+    for (int c = 0; c < NM; ++c) M[c] = v.M[c * NL + l];
+    mapply<ND, BLOCK>(M, r, u);
+#pragma unroll
+    for (int c = 0; c < NB; ++c) D[c] = op.D[c * NL + l];
+    D[0] += reg;
+    D[ND == 3 ? 3 : 2] += reg;
+    if (ND == 3) D[5] += reg;
+    double y[ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0;
+    bmac<ND>(D, u, y);
+    for (int k = 0; k < 3; ++k) {
+      const int32_t nl = op.nbr_lane[k * NL + l];
+      if (nl < 0) continue;
+      double rc[ND], Mc[NM], uc[ND], V[NB];
+      lload<ND>(v.r[0], NL, nl, rc);
+#pragma unroll
+      for (int c = 0; c < NM; ++c) Mc[c] = v.M[c * NL + nl];
+      mapply<ND, BLOCK>(Mc, rc, uc);
+#pragma unroll
+      for (int c = 0; c < NB; ++c) V[c] = op.V[(c * 3 + k) * NL + l];
+      bmac<ND>(V, uc, y);
+    }
+    const int info = group_info(op.code[l]);
+    const int maxh = wave_max_i(info > 0 ? info : 0);
+    for (int t = 1; t <= maxh; ++t) {
+      double yt[ND];
+#pragma unroll
+      for (int a = 0; a < ND; ++a) yt[a] = __shfl(y[a], (lane + t) & 63, 64);
+      if (t <= info) {
+#pragma unroll
+        for (int a = 0; a < ND; ++a) y[a] += yt[a];
+      }
+    }
+    if (info >= 0) lstore<ND>(v.w[0], NL, l, y);
+    // halo push: the owner's r₀, s₀ = 0, w₀ and M
+    const int ow = info < 0 ? lane + info : lane;
+    double ro[ND], yo[ND], Mo[NM];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      ro[a] = __shfl(r[a], ow, 64);
+      yo[a] = __shfl(y[a], ow, 64);
+    }
+#pragma unroll
+    for (int c = 0; c < NM; ++c) Mo[c] = __shfl(M[c], ow, 64);
+    const int32_t pt = op.partner[l];
+    if (pt >= 0) {
+      double* h = v.h[0];
+#pragma unroll
+      for (int c = 0; c < ND; ++c) {
+        h[c * NL + pt] = ro[c];
+        h[(3 + c) * NL + pt] = 0.0;
+        h[(6 + c) * NL + pt] = yo[c];
+      }
+#pragma unroll
+      for (int c = 0; c < NM; ++c) v.hM[c * NL + pt] = Mo[c];
+    }
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {  // helper lanes: r = u = 0
+      acc[0] = fma(r[a], u[a], acc[0]);
+      acc[1] = fma(y[a], u[a], acc[1]);
+      acc[2] = fma(r[a], r[a], acc[2]);
+      acc[3] = fma(u[a], u[a], acc[3]);
+    }
+  }
+  store_block_partial(acc, part_buf(part, 0));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Slot s0;
+    s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
+    s0.alpha = s0.beta = s0.res = 0.0;
+    s0.flag = kInit;
+    s0.pad = 0;
+    slots[0] = s0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One CG-CG iteration (iteration j of a chunk, buffer parity j & 1).
+// Per lane, all loads independent of each other and of α, β:
+//   own r, s, w, p, x (5·ND), diagonal block (NB), M, three slot blocks
+//   (3·NB), code + partner, halo record r, s, w (3·ND) + M, and the G block
+//   partials.  Then α, β; own update (p, x, s, r, u); u → LDS; A u from the
+//   LDS row and the halo record; helper partials → owner through LDS; stores;
+//   halo push.
+// HBM per lane, Jacobi: ND = 3: 440 B read, 120 B written; ND = 2: 264 B
+// read, 80 B written (+24·ND B per halo push).
+// ---------------------------------------------------------------------------
+template <int ND, bool BLOCK>
+struct LaneIn {
+  double ro[ND], so[ND], wo[ND], pp[ND], xx[ND], D[Dof<ND>::NB], M[n_minv<ND, BLOCK>()];
+  double V[3][Dof<ND>::NB];
+  double h[3 * ND], hM[n_minv<ND, BLOCK>()];
+  uint32_t code;
+  int32_t partner;
+};
+
+template <int ND, bool BLOCK>
+__device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, const EllVecs& v,
+                                          LaneIn<ND, BLOCK>& in) {
+  constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>();
+  const int64_t NL = op.NL;
+  lload<ND>(v.r[par], NL, l, in.ro);
+  lload<ND>(v.s[par], NL, l, in.so);
+  lload<ND>(v.w[par], NL, l, in.wo);
+  lload<ND>(v.p, NL, l, in.pp);
+  lload<ND>(v.x, NL, l, in.xx);
+#pragma unroll
+  for (int c = 0; c < NB; ++c) in.D[c] = op.D[c * NL + l];
+#pragma unroll
+  for (int c = 0; c < NM; ++c) in.M[c] = v.M[c * NL + l];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int c = 0; c < NB; ++c) in.V[k][c] = op.V[(c * 3 + k) * NL + l];
+  in.code = op.code[l];
+  in.partner = op.partner[l];
+  const double* __restrict__ h = v.h[par];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int c = 0; c < ND; ++c) in.h[q * ND + c] = h[(q * 3 + c) * NL + l];
+#pragma unroll
+  for (int c = 0; c < NM; ++c) in.hM[c] = v.hM[c * NL + l];
+}
+
+template <int ND, bool BLOCK, int PU, bool TRACE = false>
+__global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, Slot* slots,
+                                                    const SolveState* st, double* part,
+                                                    unsigned long long* trace) {
+  constexpr int NB = Dof<ND>::NB, LW = Dof<ND>::LDSW;
+  constexpr int NW = kCgBS / 64;
+  __shared__ double lds_u[NW][64][LW];       // fresh u of every lane
+  __shared__ double lds_y[NW][64][LW];       // helper partials of A u
+  __shared__ double lds_b[NW][64][3 * ND];   // owner r, s, w for helper pushes
+  trace_point<TRACE>(trace, 0, 0.0);
+  const int par = j & 1;
+  const int64_t NL = op.NL;
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double* __restrict__ r_new = v.r[par ^ 1];
+  double* __restrict__ s_new = v.s[par ^ 1];
+  double* __restrict__ w_new = v.w[par ^ 1];
+  double* __restrict__ h_new = v.h[par ^ 1];
+
+  int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x;
+  LaneIn<ND, BLOCK> in;
+  if (l - lane < NL) load_lane<ND, BLOCK>(l, par, op, v, in);
+  const int f0 = __builtin_nontemporal_load(&slots[j].flag);
+  const double g0 = slots[j].v[0], a0 = slots[j].alpha;
+  const double tol2 = st->tol2, reg = st->reg;
+  const int base_it = st->base, max_it = st->max_it, norm = st->norm;
+  double S[4];
+  wave_partials<PU>(part_buf(part, par), S);
+  trace_point<TRACE>(trace, 1, S[0]);
+
+  const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
+  const double alpha = cs.alpha, beta = cs.beta;
+  const bool go = cs.status == kRun;
+  cg_record(slots, j, S, cs);
+
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double ylast = 0.0;
+  for (bool first = true; l - lane < NL; l += stride, first = false) {  // wave-uniform
+    if (!first) load_lane<ND, BLOCK>(l, par, op, v, in);
+    const int info = group_info(in.code);
+    const bool owner = info >= 0;
+    double uo[ND], rn[ND], un[ND], sn[ND], pp[ND], xx[ND];
+    mapply<ND, BLOCK>(in.M, in.ro, uo);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      pp[a] = fma(beta, in.pp[a], uo[a]);
+      sn[a] = fma(beta, in.so[a], in.wo[a]);
+      xx[a] = fma(alpha, pp[a], in.xx[a]);
+      rn[a] = fma(-alpha, sn[a], in.ro[a]);
+    }
+    mapply<ND, BLOCK>(in.M, rn, un);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) lds_u[wv][lane][a] = un[a];
+    if (go && owner) {
+      lstore<ND>(v.p, NL, l, pp);
+      lstore<ND>(v.x, NL, l, xx);
+      lstore<ND>(s_new, NL, l, sn);
+      lstore<ND>(r_new, NL, l, rn);
+    }
+    double D[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) D[c] = in.D[c];
+    D[0] += reg;
+    D[ND == 3 ? 3 : 2] += reg;
+    if (ND == 3) D[5] += reg;
+    double y[ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0;
+    bmac<ND>(D, un, y);
+    // halo neighbour of slot 0: the owner's operations on the pushed record
+    double uh[ND];
+    {
+      double t[ND];
+#pragma unroll
+      for (int a = 0; a < ND; ++a)
+        t[a] = fma(-alpha, fma(beta, in.h[ND + a], in.h[2 * ND + a]), in.h[a]);
+      mapply<ND, BLOCK>(in.hM, t, uh);
+    }
+    lds_fence();
+    double uk[3][ND];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int src = (int)((in.code >> (8 * k)) & 63);
+#pragma unroll
+      for (int a = 0; a < ND; ++a) uk[k][a] = lds_u[wv][src][a];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t src = (in.code >> (8 * k)) & 0xFF;
+      if (k == 0 && src == kSrcHalo) {
+#pragma unroll
+        for (int a = 0; a < ND; ++a) uk[0][a] = uh[a];
+      }
+      if (src != kSrcNone) bmac<ND>(in.V[k], uk[k], y);
+    }
+    // helper lanes → owner (t order)
+    if (__ballot(info > 0)) {
+#pragma unroll
+      for (int a = 0; a < ND; ++a) lds_y[wv][lane][a] = y[a];
+      lds_fence();
+      for (int t0 = 1; __ballot(info >= t0); t0 += 4) {
+        double yt[4][ND];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int src = min(lane + t0 + q, 63);
+#pragma unroll
+          for (int a = 0; a < ND; ++a) yt[q][a] = lds_y[wv][src][a];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (t0 + q <= info) {
+#pragma unroll
+            for (int a = 0; a < ND; ++a) y[a] += yt[q][a];
+          }
+      }
+    }
+    if (TRACE) ylast = y[0];
+    if (go && owner) lstore<ND>(w_new, NL, l, y);
+    // halo push of the owner's r, s, w; a helper takes them from its owner's
+    // LDS row (only waves where a helper pushes pay for it)
+    double rsy[3 * ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      rsy[a] = rn[a];
+      rsy[ND + a] = sn[a];
+      rsy[2 * ND + a] = y[a];
+    }
+    if (__ballot(in.partner >= 0 && !owner)) {
+#pragma unroll
+      for (int c = 0; c < 3 * ND; ++c) lds_b[wv][lane][c] = rsy[c];
+      lds_fence();
+      const int ow = owner ? lane : lane + info;
+#pragma unroll
+      for (int c = 0; c < 3 * ND; ++c) rsy[c] = lds_b[wv][ow][c];
+    }
+    if (go && in.partner >= 0) {
+      const int64_t pt = in.partner;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int c = 0; c < ND; ++c) h_new[(q * 3 + c) * NL + pt] = rsy[q * ND + c];
+    }
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {  // helper lanes contribute exact zeros
+      acc[0] = fma(rn[a], un[a], acc[0]);
+      acc[1] = fma(y[a], un[a], acc[1]);
+      acc[2] = fma(rn[a], rn[a], acc[2]);
+      acc[3] = fma(un[a], un[a], acc[3]);
+    }
+    // the LDS rows are rewritten next pass: all reads of this pass are done
+    lds_fence();
+  }
+  trace_point<TRACE>(trace, 2, ylast);
+  if (go) store_block_partial(acc, part_buf(part, par ^ 1));
+  if (TRACE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    trace_point<TRACE>(trace, 3, acc[0]);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kCgBS) void k_ell_finish(EllOp op, EllVecs v, double* x_row) {
+  const int64_t NL = op.NL;
+  for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l < NL;
+       l += (int64_t)gridDim.x * kCgBS) {
+    const int32_t row = op.lane_row[l];
+    if (row < 0) continue;
+    double xx[3] = {0.0, 0.0, 0.0};  // 2-D: z stays exactly 0
+    lload<ND>(v.x, NL, l, xx);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) x_row[3 * (int64_t)row + c] = xx[c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+static dim3 ell_grid(const EllOp& op) { return dim3((unsigned)cg_grid(op.NL)); }
+static dim3 ell_grid_ew(const EllOp& op) { return dim3((unsigned)grid_rows(op.NL > 0 ? op.NL : 1)); }
+
+template <int ND>
+static void init_nd(hipStream_t s, const EllOp& op, const SellOp& sop, int precond,
+                    const CgVecs& rv, const EllVecs& v) {
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_init<ND, true>), ell_grid_ew(op), dim3(kCgBS), 0, s, op, sop, rv, v);
+  else
+    hipLaunchKernelGGL((k_ell_init<ND, false>), ell_grid_ew(op), dim3(kCgBS), 0, s, op, sop, rv, v);
+}
+void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int precond,
+                     const CgVecs& rv, const EllVecs& v) {
+  if (op.nd == 2) init_nd<2>(s, op, sop, precond, rv, v);
+  else init_nd<3>(s, op, sop, precond, rv, v);
+}
+
+template <int ND>
+static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
+                     Slot* slots, double* part) {
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_first<ND, true>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v, slots,
+                       part);
+  else
+    hipLaunchKernelGGL((k_ell_first<ND, false>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v, slots,
+                       part);
+}
+void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
+                      Slot* slots, double* part) {
+  if (op.nd == 2) first_nd<2>(s, op, reg, precond, v, slots, part);
+  else first_nd<3>(s, op, reg, precond, v, slots, part);
+}
+
+template <int ND, int PU, bool TRACE>
+static void iter_launch(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                        Slot* slots, const SolveState* st, double* part,
+                        unsigned long long* trace) {
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE>), ell_grid(op), dim3(kCgBS), 0, s, j, op,
+                       v, slots, st, part, trace);
+  else
+    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE>), ell_grid(op), dim3(kCgBS), 0, s, j, op,
+                       v, slots, st, part, trace);
+}
+
+template <int ND, bool TRACE>
+static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
+  const int64_t g = cg_grid(op.NL);
+  if (g <= 64) iter_launch<ND, 1, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else if (g <= 128) iter_launch<ND, 2, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else if (g <= 256) iter_launch<ND, 4, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  else iter_launch<ND, 8, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+}
+
+void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
+  if (op.nd == 2) {
+    if (trace) iter_pu<2, true>(s, j, op, precond, v, slots, st, part, trace);
+    else iter_pu<2, false>(s, j, op, precond, v, slots, st, part, nullptr);
+  } else {
+    if (trace) iter_pu<3, true>(s, j, op, precond, v, slots, st, part, trace);
+    else iter_pu<3, false>(s, j, op, precond, v, slots, st, part, nullptr);
+  }
+}
+
+void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row) {
+  if (op.nd == 2)
+    hipLaunchKernelGGL(k_ell_finish<2>, ell_grid_ew(op), dim3(kCgBS), 0, s, op, v, x_row);
+  else
+    hipLaunchKernelGGL(k_ell_finish<3>, ell_grid_ew(op), dim3(kCgBS), 0, s, op, v, x_row);
+}
+
+}  // namespace mfea

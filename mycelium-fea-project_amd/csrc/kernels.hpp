@@ -140,13 +140,51 @@ void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, c
 // iteration j of a chunk: reduces part parity j&1, records slots[j+1], writes
 // its partials to parity (j&1)^1.
 void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const CgVecs& v,
-                    Slot* slots, const SolveState* st, double* part);
+                    Slot* slots, const SolveState* st, double* part,
+                    unsigned long long* trace = nullptr);
 // host: mapped pinned mirror of the final SolveState (written once, when done)
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host);
 void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
                              int max_it, double reg, SolveState* st);
 int cg_block_size(int64_t rows);
 int64_t cg_grid(int64_t rows);
+
+// ---- single-reduction CG on the wave-local lane operator (ell.hip) --------
+constexpr uint32_t kSrcNone = 0xFF, kSrcHalo = 0xFE;  // slot source codes (symbolic.hpp)
+// Lane arrays are component-major: a[c·NL + lane].  See symbolic.hpp "Ell".
+struct EllOp {
+  int64_t NL;                // lanes, multiple of 64
+  int nd;                    // DOFs per node in the lanes: 2 (planar mesh) or 3
+  const uint32_t* code;      // bytes 0..2: slot sources; byte 3: int8 group info
+  const int32_t* partner;    // halo push target of slot 0, -1
+  const int32_t* lane_row;   // owner lane → free row, -1
+  const int32_t* src_pos;    // [3][NL] SELL position of each slot, -1
+  const int32_t* nbr_lane;   // [3][NL] neighbour owner lane (first iteration only)
+  double* V;                 // [NB][3][NL] slot blocks (component c, slot k: (c·3+k)·NL)
+  double* D;                 // [NB][NL] diagonal block (unregularised), 0 off owners
+                             // NB = 6 (xx xy xz yy yz zz) or, nd = 2, 3 (xx xy yy)
+};
+struct EllVecs {  // component c of a lane vector at [c·NL + lane], c < nd
+  double* x;      // [3][NL]
+  double* p;      // [3][NL]
+  double* r[2];   // [3][NL] by iteration parity
+  double* s[2];
+  double* w[2];
+  double* M;      // [3|6][NL] Jacobi / block-Jacobi inverse, 0 off owners
+  double* h[2];   // [9][NL] halo records by parity: r, s, w of the slot-0 neighbour at (q·3+c)·NL
+  double* hM;     // [3|6][NL] halo record of the slot-0 neighbour's M
+};
+// values and lane vectors from the SELL operator and k_cg_rhs's row-order b, M⁻¹
+void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int precond,
+                     const CgVecs& rv, const EllVecs& v);
+// w₀ = A u₀ (neighbours pulled once), halo records of parity 0, partials, slots[0] = INIT
+void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
+                      Slot* slots, double* part);
+void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                     Slot* slots, const SolveState* st, double* part,
+                     unsigned long long* trace = nullptr);
+// x of the owner lanes → row-order x (free rows)
+void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
 
 int64_t grid_rows(int64_t rows);
 int64_t grid_elementwise(int64_t n);

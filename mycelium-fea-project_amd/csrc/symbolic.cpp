@@ -179,6 +179,120 @@ std::string build_pattern(int64_t N, const double* xyz, int64_t E, const int64_t
   return "";
 }
 
+// ---------------------------------------------------------------------------
+std::string build_ell(const Pattern& P, Ell& L) {
+  L = Ell();
+  const int64_t nf = P.n_free;
+  if (nf == 0) return "";
+  const auto pos_of = [&](int64_t i, int k) {
+    return ((int64_t)P.slice_ptr[i / kSlice] + k) * kSlice + i % kSlice;
+  };
+  // free-neighbour slots of every free row, in slot (= element) order
+  std::vector<int64_t> fptr(nf + 1, 0);
+  for (int64_t i = 0; i < nf; ++i) {
+    int c = 0;
+    for (int k = 0; k < P.row_len[i]; ++k) c += P.s_col[pos_of(i, k)] < nf;
+    fptr[i + 1] = fptr[i] + c;
+  }
+  std::vector<int64_t> fpos(fptr[nf]);
+  for (int64_t i = 0, q = 0; i < nf; ++i)
+    for (int k = 0; k < P.row_len[i]; ++k) {
+      const int64_t pos = pos_of(i, k);
+      if (P.s_col[pos] < nf) fpos[q++] = pos;
+    }
+  // Waves are filled greedily with consecutive rows: for a candidate wave
+  // [a, b) a row's halo slots are exactly its slots to rows outside [a, b),
+  // and its group needs max(⌈slots/3⌉, halo slots) lanes.  Take the longest
+  // [a, b) whose groups fit 64 lanes (with a short look-ahead, since adding a
+  // row can turn earlier halo slots local).
+  std::vector<int32_t> need(nf, 1), lane(nf, -1), wave(nf, -1);
+  const auto row_need = [&](int64_t i, int32_t w) {
+    const int64_t ns = fptr[i + 1] - fptr[i];
+    int64_t halo = 0;
+    for (int64_t q = fptr[i]; q < fptr[i + 1]; ++q) halo += wave[P.s_col[fpos[q]]] != w;
+    return (int32_t)std::max<int64_t>({1, (ns + kEllSlots - 1) / kEllSlots, halo});
+  };
+  int64_t n_lanes = 0;
+  int32_t w = 0;
+  for (int64_t a = 0; a < nf; ++w) {
+    int64_t best = -1;
+    for (int64_t b = a + 1; b <= nf && b <= a + kSlice; ++b) {
+      wave[b - 1] = w;
+      int64_t total = 0;
+      for (int64_t i = a; i < b; ++i) total += row_need(i, w);
+      if (total <= kSlice) best = b;
+      else if (best > 0 && b - best >= 8) break;
+    }
+    if (best < 0) return "a row needs more than 64 lanes (out-of-wave degree too high)";
+    for (int64_t i = best; i < nf && i < a + kSlice; ++i) wave[i] = -1;
+    int64_t pos = (int64_t)w * kSlice;
+    for (int64_t i = a; i < best; ++i) {
+      need[i] = row_need(i, w);
+      lane[i] = (int32_t)pos;
+      pos += need[i];
+    }
+    a = best;
+    n_lanes = (int64_t)(w + 1) * kSlice;
+  }
+  if (n_lanes > INT32_MAX / 8) return "mesh too large for the lane layout";
+  L.n_lanes = n_lanes;
+  L.lane_row.assign(n_lanes, -1);
+  L.row_lane = lane;
+  L.info.assign(n_lanes, 0);
+  L.code.assign(n_lanes, kEllNone | kEllNone << 8 | kEllNone << 16);
+  L.partner.assign(n_lanes, -1);
+  L.src_pos.assign(kEllSlots * n_lanes, -1);
+  L.nbr_lane.assign(kEllSlots * n_lanes, -1);
+  std::vector<int32_t> lane_of_pos(P.s_col.size(), -1);
+  for (int64_t i = 0; i < nf; ++i) {
+    const int32_t l0 = lane[i], g = need[i];
+    L.lane_row[l0] = (int32_t)i;
+    L.info[l0] = g - 1;
+    for (int t = 1; t < g; ++t) L.info[l0 + t] = -t;
+    // halo slots first (one per lane, slot 0), then the in-wave slots in order
+    std::vector<int64_t> halo, local;
+    for (int64_t q = fptr[i]; q < fptr[i + 1]; ++q)
+      (lane[P.s_col[fpos[q]]] / kSlice != l0 / kSlice ? halo : local).push_back(fpos[q]);
+    size_t hq = 0, lq = 0;
+    for (int t = 0; t < g; ++t) {
+      const int32_t l = l0 + t;
+      for (int k = 0; k < kEllSlots; ++k) {
+        int64_t pos = -1;
+        bool is_halo = false;
+        if (k == 0 && hq < halo.size()) {
+          pos = halo[hq++];
+          is_halo = true;
+        } else if (lq < local.size()) {
+          pos = local[lq++];
+        }
+        if (pos < 0) continue;
+        const int32_t j = P.s_col[pos];
+        const uint32_t src = is_halo ? kEllHalo : (uint32_t)(lane[j] % kSlice);
+        L.code[l] = (L.code[l] & ~(0xFFu << (8 * k))) | src << (8 * k);
+        L.src_pos[(int64_t)k * n_lanes + l] = (int32_t)pos;
+        L.nbr_lane[(int64_t)k * n_lanes + l] = lane[j];
+        lane_of_pos[pos] = l;
+      }
+    }
+    if (hq != halo.size() || lq != local.size()) return "internal: group too small for its slots";
+  }
+  // halo partners: the lane holding the mirror slot (same element, seen from j)
+  for (int64_t l = 0; l < n_lanes; ++l) {
+    if ((L.code[l] & 0xFF) != kEllHalo) continue;
+    const int64_t pos = L.src_pos[l];
+    const int32_t j = P.s_col[pos], e = P.s_elem[pos];
+    const int32_t i = L.lane_row[l] >= 0 ? L.lane_row[l] : L.lane_row[l + L.info[l]];
+    int32_t mirror = -1;
+    for (int k = 0; k < P.row_len[j]; ++k) {
+      const int64_t pj = pos_of(j, k);
+      if (P.s_elem[pj] == e && P.s_col[pj] == i) mirror = lane_of_pos[pj];
+    }
+    if (mirror < 0 || (L.code[mirror] & 0xFF) != kEllHalo) return "internal: halo mirror missing";
+    L.partner[l] = mirror;
+  }
+  return "";
+}
+
 // symmetric component index of (a,b): xx xy xz yy yz zz
 static inline int sym(int a, int b) {
   if (a > b) std::swap(a, b);

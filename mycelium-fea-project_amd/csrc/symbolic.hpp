@@ -52,6 +52,37 @@ std::string build_pattern(int64_t n_nodes, const double* xyz, int64_t n_elems, c
                           bool skip_invalid, const std::vector<int64_t>& top,
                           const std::vector<int64_t>& bot, int sort_window, Pattern& P);
 
+// ---------------------------------------------------------------------------
+// Wave-local CG operator ("ELL-3 lanes") over the free rows [0, n_free).
+//
+// One lane = one wavefront lane of the CG iteration kernel.  A free row gets
+// an OWNER lane, plus HELPER lanes directly after it when it has more than
+// three free-neighbour slots or more than one out-of-wave neighbour; a group
+// never straddles a 64-lane wave (inert padding lanes).  Every lane holds up
+// to three slots (k-major arrays [k][n_lanes]); slots to grip (known) rows
+// are dropped (u = 0 there).  A slot's neighbour u_j comes from
+//   - the lane of j's owner in the SAME wave: a cross-lane permute, or
+//   - a halo record (slot 0 only, ≤ 1 per lane) that j's group pushed in the
+//     previous launch: partner[lane] is the lane whose record this lane's
+//     slot-0 partner reads, i.e. where this lane pushes its owner's (r, s, w).
+// So an iteration needs no neighbour index loads: one memory round trip.
+constexpr int kEllSlots = 3;
+constexpr uint32_t kEllNone = 0xFF, kEllHalo = 0xFE;  // = kSrcNone / kSrcHalo (kernels.hpp)
+
+struct Ell {
+  int64_t n_lanes = 0;            // multiple of 64 (0 when n_free == 0)
+  std::vector<int32_t> lane_row;  // owner lane → row; helper / inert → -1
+  std::vector<int32_t> row_lane;  // free row → owner lane
+  std::vector<int32_t> info;      // owner: #helpers; helper: -(distance to owner); inert: 0
+  std::vector<uint32_t> code;     // byte k = source of slot k: lane 0..63, kEllHalo, kEllNone
+  std::vector<int32_t> partner;   // push target lane of slot 0 (halo), -1
+  std::vector<int32_t> src_pos;   // [k][n_lanes] SELL position of the slot, -1
+  std::vector<int32_t> nbr_lane;  // [k][n_lanes] owner lane of the neighbour, -1
+};
+
+// Builds the lanes for P's free rows.  Returns "" on success.
+std::string build_ell(const Pattern& P, Ell& L);
+
 // Scalar CSR over the 3·N DOFs in original order, pattern = the reference's
 // csr_matrix pattern for the active set (src/fea_solver.py:93-105):
 // block (n,m) present iff an active element joins n and m (or n == m and n has

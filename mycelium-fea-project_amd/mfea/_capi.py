@@ -45,10 +45,10 @@ class Info(C.Structure):
     _fields_ = [("n_nodes", C.c_int64), ("n_elems", C.c_int64), ("n_free_nodes", C.c_int64),
                 ("n_top", C.c_int64), ("n_known", C.c_int64), ("n_slices", C.c_int64),
                 ("n_slots", C.c_int64), ("free_incidences", C.c_int64), ("planar", C.c_int32),
-                ("pad", C.c_int32)]
+                ("cg_lanes", C.c_int32), ("n_lanes", C.c_int64), ("n_halo", C.c_int64)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _P = C.c_void_p
@@ -78,6 +78,8 @@ _sig = {
                                  C.POINTER(SolveOpts), _P, C.POINTER(Stats)]),
     "mfea_dist_unique_id": (C.c_int, [_P]),
     "mfea_dist_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    # include/mfea_debug.h
+    "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(_lib, _name)
@@ -237,6 +239,15 @@ class Engine:
         ms = C.c_double()
         _check(_lib.mfea_profile_iteration(self._h, int(precond), int(reps), C.byref(ms)))
         return ms.value
+
+    def trace_iteration(self, precond=PC_JACOBI, cap=1 << 16):
+        """Per-wave s_memrealtime stamps (100 MHz) of one CG iteration launch:
+        (waves, 4) = entry, partials reduced, SpMV done, stores drained."""
+        out = np.zeros(4 * cap, dtype=np.uint64)
+        nw = C.c_int64()
+        _check(_lib.mfea_debug_trace_iteration(self._h, int(precond), out.ctypes.data, out.size,
+                                               C.byref(nw)))
+        return out[:4 * nw.value].reshape(-1, 4)
 
     # ---- reference-API helpers ------------------------------------------------
     def element_stiffness(self, p1s, p2s, E, A, I):

@@ -90,4 +90,28 @@ int64_t shim_export(const uint8_t* active, double EA, double EI12, int64_t* indp
   return (int64_t)ix.size();
 }
 
+// Wave-local lanes of the last built pattern: returns n_lanes (or -1, error in
+// err); with lane_row == NULL only the size is returned.
+static Ell g_L;
+int64_t shim_ell(int32_t* lane_row, int32_t* row_lane, int32_t* info, uint32_t* code,
+                 int32_t* partner, int32_t* src_pos, int32_t* nbr_lane, char* err, int errn) {
+  if (!lane_row) {
+    std::string e = build_ell(g_P, g_L);
+    if (!e.empty()) {
+      std::snprintf(err, errn, "%s", e.c_str());
+      return -1;
+    }
+    return g_L.n_lanes;
+  }
+  const int64_t n = g_L.n_lanes;
+  std::memcpy(lane_row, g_L.lane_row.data(), n * 4);
+  std::memcpy(row_lane, g_L.row_lane.data(), g_L.row_lane.size() * 4);
+  std::memcpy(info, g_L.info.data(), n * 4);
+  std::memcpy(code, g_L.code.data(), n * 4);
+  std::memcpy(partner, g_L.partner.data(), n * 4);
+  std::memcpy(src_pos, g_L.src_pos.data(), kEllSlots * n * 4);
+  std::memcpy(nbr_lane, g_L.nbr_lane.data(), kEllSlots * n * 4);
+  return n;
+}
+
 }  // extern "C"

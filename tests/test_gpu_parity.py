@@ -294,3 +294,124 @@ def test_c2_properties(engine):
     known, vals = fo.known_dof_map(top, bot, 0.010, -0.010)
     A, b, free = fo.free_system(K, known, vals)
     assert np.linalg.norm(A @ U2[free] - b) <= 1e-10 * np.linalg.norm(b)
+
+
+# ---------------------------------------------------------------------------
+# the two CG iteration kernels: wave-local lanes (default) and SELL (reference
+# layout); same algorithm, so same iterates up to summation order
+# ---------------------------------------------------------------------------
+def _solve_with(engine, kernel, dy, opts):
+    old = os.environ.get("MFEA_CG_KERNEL")
+    try:
+        if kernel == "sell":
+            os.environ["MFEA_CG_KERNEL"] = "sell"
+        else:
+            os.environ.pop("MFEA_CG_KERNEL", None)
+        st = engine.solve(dy, -dy, opts)
+        assert engine.info()["cg_lanes"] == (kernel == "lanes")
+        return st, engine.displacement()
+    finally:
+        if old is None:
+            os.environ.pop("MFEA_CG_KERNEL", None)
+        else:
+            os.environ["MFEA_CG_KERNEL"] = old
+
+
+@pytest.mark.parametrize("precond", [0, 1])
+def test_lane_kernel_matches_sell_and_direct(engine, precond):
+    from mfea import make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    _sim181147(engine)
+    engine.assemble()
+    dy = float(sysz["dy"])
+    st_l, U_l = _solve_with(engine, "lanes", dy, make_opts(rtol=1e-13, max_it=200000, precond=precond))
+    st_s, U_s = _solve_with(engine, "sell", dy, make_opts(rtol=1e-13, max_it=200000, precond=precond))
+    assert st_l.status == 0 and st_s.status == 0
+    assert rel(U_l, sysz["U"]) <= 1e-10 and rel(U_s, sysz["U"]) <= 1e-10
+    s8l, _ = _solve_with(engine, "lanes", dy, make_opts(rtol=1e-8, precond=precond))
+    s8s, _ = _solve_with(engine, "sell", dy, make_opts(rtol=1e-8, precond=precond))
+    assert abs(s8l.iters - s8s.iters) <= 3
+    if precond == 0:
+        assert abs(s8l.iters - int(sysz["pcg_iters_1e8"])) <= 3
+
+
+def _direct(xyz, e2n, top, bot, dy):
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    return fo.solve_system(K, known, vals)
+
+
+def _true_relres(xyz, e2n, top, bot, dy, U):
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    A, b, free = fo.free_system(K, known, vals)
+    return np.linalg.norm(A @ U[free] - b) / np.linalg.norm(b)
+
+
+def test_lane_kernel_high_degree_and_multiedges(engine):
+    """A hub of degree 40 (helper lanes spanning most of a wave), duplicated
+    elements, shortcuts, and a chain across several waves; hyphal lengths
+    (0.05 mm) keep the system well conditioned (cond ≈ 2e6), so both kernels
+    must reach the direct solve."""
+    from mfea import make_opts
+    n = 400
+    xyz = np.zeros((n, 3))
+    ang = 2 * np.pi * np.arange(1, 41) / 40
+    xyz[1:41, 0] = 0.05 * np.cos(ang)
+    xyz[1:41, 1] = 0.05 * np.sin(ang)
+    i = np.arange(41, n)
+    xyz[41:, 0] = 0.01 * np.sin(i)
+    xyz[41:, 1] = 0.06 + 0.05 * (i - 41)
+    e2n = [(0, i) for i in range(1, 41)] + [(i, i + 1) for i in range(41, n - 1)]
+    e2n += [(5, 41), (5, 41), (60, 62), (7, 45), (41, 43), (20, 200)]
+    e2n = np.array(e2n)
+    top = np.arange(380, 400)
+    bot = np.arange(41, 46)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    assert engine.info()["n_lanes"] > engine.info()["n_free_nodes"] + 10   # helper lanes
+    opts = make_opts(rtol=1e-13, max_it=200000)
+    st_l, U_l = _solve_with(engine, "lanes", 0.01, opts)
+    st_s, U_s = _solve_with(engine, "sell", 0.01, opts)
+    assert st_l.status == 0 and st_s.status == 0
+    Uref = _direct(xyz, e2n, top, bot, 0.01)
+    assert rel(U_l, Uref) <= 1e-10 and rel(U_s, Uref) <= 1e-10
+    assert _true_relres(xyz, e2n, top, bot, 0.01, U_l) <= 1e-12
+    assert abs(st_l.iters - st_s.iters) <= 3
+
+
+def test_lane_kernel_natural_order_many_halos(engine, monkeypatch):
+    """Natural (export) row order: most neighbours are out of wave, so most
+    slots go through pushed halo records and groups grow helper lanes."""
+    from mfea import make_opts, synth
+    monkeypatch.setenv("MFEA_ORDER", "natural")
+    xyz, e2n = synth.tiled_mesh(1, 1)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    info = engine.info()
+    assert info["cg_lanes"] == 1 and info["n_halo"] > info["n_free_nodes"] // 2
+    Uref = _direct(xyz, e2n, top, bot, 0.01)
+    st, U = _solve_with(engine, "lanes", 0.01, make_opts(rtol=1e-13, max_it=200000))
+    assert st.status == 0
+    assert rel(U, Uref) <= 1e-10
+
+
+@pytest.mark.parametrize("precond", [0, 1])
+def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
+    """On a planar mesh the 2-DOF lanes drop z components that are exactly 0
+    in every iterate: U must equal the 3-DOF lanes' U bit for bit."""
+    from mfea import make_opts
+    _sim181147(engine)
+    engine.assemble()
+    opts = make_opts(rtol=1e-10, max_it=200000, precond=precond)
+    st2, U2 = _solve_with(engine, "lanes", 0.01, opts)
+    monkeypatch.setenv("MFEA_LANE_DOF", "3")
+    st3, U3 = _solve_with(engine, "lanes", 0.01, opts)
+    assert st2.status == 0 and st3.status == 0 and st2.iters == st3.iters
+    assert np.array_equal(U2, U3)
+    assert np.all(U2[2::3] == 0.0)

@@ -2,6 +2,7 @@
 SELL-64 node-block layout), the CSR export, the C ABI surface, the CPU
 baseline, the synthetic generator and the CSV writers."""
 import ctypes as C
+import glob
 import os
 import re
 
@@ -162,7 +163,7 @@ def test_self_loop_elements_are_excluded():
 
 # ---------------------------------------------------------------------------
 def test_library_exports_every_declared_symbol():
-    header = open(os.path.join(REPO, "include", "mfea.h")).read()
+    header = "".join(open(f).read() for f in glob.glob(os.path.join(REPO, "include", "*.h")))
     declared = set(re.findall(r"^\s*int\s+(mfea_\w+)\s*\(", header, re.M))
     assert len(declared) >= 20
     lib = C.CDLL(os.path.join(PKG, "libmfea.so"))
@@ -170,7 +171,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     from mfea import _capi
     assert declared == set(_capi.EXPORTED)
-    assert _capi.abi_version() == 1
+    assert _capi.abi_version() == 2
 
 
 def test_create_without_gpu_fails_cleanly():

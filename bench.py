@@ -43,6 +43,29 @@ def parse():
     return ap.parse_args()
 
 
+def iteration_bytes(info, block):
+    """Algorithmic HBM bytes of one iteration launch.
+
+    Lane kernel (ell.hip), nd DOFs per node, NB = 3 (nd 2) or 6 block
+    components, NM = nd (Jacobi) or NB (block-Jacobi) M components:
+      per lane read  8·(5·nd + NB + NM + 3·NB + 3·nd + NM) + 8 (r s w p x, D, M,
+                     three slot blocks, halo record + its M, code + partner)
+      per free row   written 8·5·nd (p x s r w)
+      per halo lane  written 8·3·nd (the partner's record)
+    SELL kernel (cg.hip): per free row 120 + minv + 120 + 48 + 4 B, per slot 52 B.
+    """
+    if info["cg_lanes"]:
+        nd = 2 if info["planar"] else 3
+        nb = 3 if nd == 2 else 6
+        nm = nb if block else nd
+        per_lane = 8 * (5 * nd + nb + nm + 3 * nb + 3 * nd + nm) + 8
+        b = info["n_lanes"] * per_lane + info["n_free_nodes"] * 40 * nd + info["n_halo"] * 24 * nd
+        return b, f"k_ell_iter (lanes, {nd} DOF/node: update + SpMV + reduction)"
+    minv = 48 if block else 24
+    b = info["n_free_nodes"] * (120 + minv + 120 + 48 + 4) + info["free_incidences"] * 52
+    return b, "k_cg_iter (SELL: update + SpMV + reduction)"
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -112,30 +135,26 @@ def main():
 
     force, n_active, st = stats[-1]
     iters = st.iters
-    # ---- roofline of the dominant kernel (fused SpMV + CG-CG iteration),
-    # live HIP events on the engine's stream
+    # ---- roofline of the dominant kernel (one CG-CG iteration launch), live
+    # HIP events on the engine's stream; algorithmic bytes per launch as in
+    # DESIGN.md §Roofline
     iter_ms = eng.profile_iteration(pc, reps=200)
+    iter_bytes, kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
     nf = info["n_free_nodes"]
-    inc = info["free_incidences"]
-    # algorithmic bytes per launch: per free row, vectors
-    # read r,s,w,p,x (5×24 B) + M⁻¹ (24 B Jacobi / 48 B block) and written
-    # p,x,s,r,w (5×24 B), diag block 48 B, row_len 4 B; per valid slot column
-    # 4 B + value block 48 B.  Neighbour gathers re-read vectors already counted.
-    minv = 48 if pc == PC_BLOCK_JACOBI else 24
-    iter_bytes = nf * (120 + minv + 120 + 48 + 4) + inc * (4 + 48)
     achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
     traffic = None
     a.traffic = a.traffic or os.path.join(REPO, "profiles", f"traffic_{a.config}.json")
     if os.path.exists(a.traffic):
         try:
             tj = json.load(open(a.traffic))
-            if tj.get("config") == a.config:
+            # only a profile of the same config AND the same iteration kernel
+            if tj.get("config") == a.config and kernel.split()[0] in tj.get("iter_kernel", ""):
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
 
     out = {
-        "metric": "DOF solved/sec (full load step, Jacobi-PCG to rtol 1e-8)",
+        "metric": "DOF solved/sec + CG iters to 1e-8; SpMV achieved HBM GB/s vs roofline",
         "value": n_dof * a.steps * world / dt,
         "unit": "DOF/s",
         "n_gpus": world,
@@ -152,13 +171,14 @@ def main():
                         f"{info['n_elems']} elements, load step {a.load_step}/40",
             "n_dof": n_dof, "n_free_dof": 3 * nf, "n_elems": info["n_elems"],
             "precond": a.precond, "rtol": a.rtol, "parallelism": f"replicas{world}" if world > 1 else "1gpu",
+            "cg_kernel": "lanes" if info["cg_lanes"] else "sell", "n_lanes": info["n_lanes"],
         },
         "cg_iters": iters,
         "relres": st.relres,
         "step_breakdown_ms": {"assemble": st.t_assemble_ms, "rhs": st.t_rhs_ms,
                               "pcg": st.t_solve_ms, "post": st.t_post_ms},
         "roofline": {
-            "kernel": "k_cg_iter (fused SpMV + CG-CG update + reduction)",
+            "kernel": kernel,
             "bound": "hbm",
             "achieved": achieved,
             "peak": PEAK_HBM_GBPS,

@@ -109,10 +109,10 @@ int mfea_assemble(mfea_handle* h);
  * Replaces solve_system (src/fea_solver.py:112-135) and MatZeroRowsColumnsIS +
  * diag regularisation + KSPSolve (src/fea_petsc.cpp:286-357).
  * Returns MFEA_EMAXIT / MFEA_EBREAKDOWN on solver failure (stats still filled);
- * the Python shim maps them to np.linalg.LinAlgError (src/fea_solver.py:247-249). */
+ * the Python shim maps them to np.linalg.LinAlgError (src/fea_solver.py:250-254). */
 int mfea_solve(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
                mfea_stats* st);
-/* Reaction + stress/failure on device.  Replaces src/fea_solver.py:252-274 and
+/* Reaction + stress/failure on device.  Replaces src/fea_solver.py:256-284 and
  * src/fea_petsc.cpp:360-406: total_force = Σ_{top} (K·U)[3n+1] on the
  * unregularised K; stress = E·ε for elements active at step start (0 else);
  * elements with |ε| > max_strain are deactivated for the next step. */

@@ -394,7 +394,7 @@ def test_lane_kernel_natural_order_many_halos(engine, monkeypatch):
     engine.set_active(None)
     engine.assemble()
     info = engine.info()
-    assert info["cg_lanes"] == 1 and info["n_halo"] > info["n_free_nodes"] // 2
+    assert info["cg_lanes"] == 1 and info["n_halo"] > info["n_free_nodes"] // 4
     Uref = _direct(xyz, e2n, top, bot, 0.01)
     st, U = _solve_with(engine, "lanes", 0.01, make_opts(rtol=1e-13, max_it=200000))
     assert st.status == 0

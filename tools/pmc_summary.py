@@ -18,7 +18,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "k_cg_iter"
+KERNELS = ("k_ell_iter", "k_cg_iter")  # lane kernel, SELL kernel (whichever ran)
 
 
 def rows(d, pattern):
@@ -55,8 +55,9 @@ def main():
         res["kernel_stats"] = [
             {"name": r["Name"][:120], "calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
              "pct": float(r["Percentage"])} for r in tr[:12]]
-        it = [r for r in tr if KERNEL in r["Name"]]
+        it = [r for r in tr if any(k in r["Name"] for k in KERNELS)]
         if it:
+            res["iter_kernel"] = it[0]["Name"][:120]
             res["iter_avg_us_rocprof"] = float(it[0]["AverageNs"]) / 1e3
     # --- calibration: KB counted per byte moved, 8-B and 3×8-B per lane reads, 24-B writes
     cal_b = 768 << 20
@@ -74,8 +75,13 @@ def main():
             fac["k_write24"] = cal_b / (v * 1024.0)
     res["calibration_bytes_per_counted_byte"] = fac
     # --- traffic of the dominant kernel
-    f = pick(counter_by_kernel(os.path.join(prof, "fetch"), "FETCH_SIZE"), KERNEL)
-    w = pick(counter_by_kernel(os.path.join(prof, "write"), "WRITE_SIZE"), KERNEL)
+    fk = counter_by_kernel(os.path.join(prof, "fetch"), "FETCH_SIZE")
+    wk = counter_by_kernel(os.path.join(prof, "write"), "WRITE_SIZE")
+    f = w = None
+    for k in KERNELS:
+        if pick(fk, k) is not None:
+            f, w = pick(fk, k), pick(wk, k)
+            break
     if f is not None and w is not None:
         rf = fac.get("k_read24", 1.0)
         rw = fac.get("k_write24", 1.0)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 2
+#define MFEA_ABI_VERSION 3
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -155,6 +155,10 @@ typedef struct {
   int32_t cg_lanes;         /* 1: CG iterations run on the wave-local lane operator */
   int64_t n_lanes;          /* lanes of that operator (owners + helpers + padding)   */
   int64_t n_halo;           /* lanes with an out-of-wave slot (one push per iteration) */
+  int32_t n_parts;          /* partitions of the solve (ranks, or mfea_debug_set_parts)  */
+  int32_t part;             /* this handle's (first) partition                         */
+  int64_t n_pairs;          /* cut free-free elements of that partition (records/iter)  */
+  int64_t n_ghost;          /* its ghost rows (other partitions' nodes)                */
 } mfea_info;
 int mfea_get_info(mfea_handle* h, mfea_info* info);
 /* Launches the dominant kernel — the fused SpMV + single-reduction CG iteration —
@@ -165,11 +169,23 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------- */
 /* Replaces the PETSC_COMM_WORLD row-block distribution of
- * src/fea_petsc_parallel.cpp:169-171, 234-268, 330-409.  unique_id: the 128-byte
- * ncclUniqueId made by rank 0 (mfea_dist_unique_id) and broadcast by the caller.
- * Must precede mfea_set_mesh; each rank then owns one y-band of nodes. */
+ * src/fea_petsc_parallel.cpp:169-171, 234-268, 330-409 and its MPI reductions.
+ * unique_id: the 128-byte ncclUniqueId made by rank 0 (mfea_dist_unique_id)
+ * and broadcast by the caller.  Every rank then passes the WHOLE mesh and the
+ * same grips to mfea_set_mesh / mfea_set_bc; the handle keeps the strip of
+ * nodes it owns (partition.hpp: equal free-node counts along one axis), the
+ * elements touching them and the far ends of cut elements as ghost rows.
+ * Each CG iteration runs one kernel per GPU plus one RCCL group (cut-row CG
+ * records to the strip neighbours + the 4 partial sums to every rank); all
+ * ranks derive bitwise identical α, β and stopping decisions.
+ * Partitioned handles: mfea_get_displacement writes the owned nodes' entries,
+ * mfea_get_stress / mfea_get_active the entries of elements whose first node
+ * is owned (others untouched); mfea_post returns the global force and count. */
 int mfea_dist_unique_id(uint8_t* unique_id /* 128 bytes */);
 int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id);
+/* Strip axis of the partition: 0 = x, 1 = y, -1 (default) = the longer
+ * bounding-box extent.  Takes effect at the next build. */
+int mfea_set_partition_axis(mfea_handle* h, int axis);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,12 @@ extern "C" {
 int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64_t cap,
                                int64_t* n_waves);
 
+/* Runs the partitioned solve of mfea_dist_init with `nparts` partitions held
+ * by this one handle on its one device: the same partition plan, kernels and
+ * exchange schedule, with device copies in place of RCCL (tests the
+ * multi-GPU path on one GPU).  axis as mfea_set_partition_axis. */
+int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
+
 #ifdef __cplusplus
 }
 #endif

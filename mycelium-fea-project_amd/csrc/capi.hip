@@ -1,18 +1,26 @@
 // capi.hip — the C ABI of include/mfea.h: handle, device memory, the on-device
-// step loop (assemble → RHS → PCG in hipGraph-captured chunks → reaction/stress).
+// step loop (assemble → RHS → PCG in hipGraph-captured chunks → reaction/stress),
+// and the multi-partition driver (partition.hpp): one partition per GPU joined
+// over RCCL (mfea_dist_init), or several partitions on one device exchanging
+// through device copies (mfea_debug_set_parts; the same kernels and the same
+// exchange schedule, used to test the partitioned solve on one GPU).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.hpp"
 #include "mfea_debug.h"
 #include "mfea.h"
+#include "partition.hpp"
 #include "symbolic.hpp"
 
 using namespace mfea;
@@ -33,10 +41,25 @@ int fail(int code, const std::string& msg) {
       return fail(MFEA_EDEVICE, std::string(#call) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
+#define NCCLC(call)                                                                       \
+  do {                                                                                    \
+    ncclResult_t r_ = (call);                                                             \
+    if (r_ != ncclSuccess)                                                                \
+      return fail(MFEA_ECOMM, std::string(#call) + ": " + ncclGetErrorString(r_));        \
+  } while (0)
+
+#define RC(call)                  \
+  do {                            \
+    if (int rc_ = (call)) return rc_; \
+  } while (0)
+
 template <class T>
 struct DevBuf {
   T* ptr = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
     if (ptr) (void)hipFree(ptr);
@@ -53,26 +76,17 @@ struct DevBuf {
 
 }  // namespace
 
-struct mfea_handle {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  double E = 2500.0, A = 0.0, I = 0.0;
-  Material mat{};
-  // host-side mesh/BC
-  int64_t N = 0, Ecount = 0;
-  std::vector<double> xyz;
-  std::vector<int64_t> e2n;
-  uint32_t mesh_flags = 0;
-  std::vector<int64_t> top, bot;
-  bool has_mesh = false, dirty = true;
-  std::vector<uint8_t> active_host;  // pending upload (empty = none)
-  Pattern P;
-  // device
+// One partition's operator, vectors and solver state on the handle's device.
+// Single-GPU handles hold one partition covering the whole mesh.
+struct Part {
+  int rank = 0;   // partition index = rank in the partitioned solve
+  Pattern P;      // local pattern (the whole mesh when not partitioned)
+  PartPlan plan;  // partitioned only
   DevBuf<double> xyz_d, val, diag, x, r, p, q, dinv, stress, partials, red;
   DevBuf<double> cg_r1, cg_s0, cg_s1, cg_w0, cg_w1;  // CG-CG double buffers (r0 = r)
   DevBuf<double> cg_part;                            // CG-CG block partials, 2 parities
   DevBuf<int32_t> slice_ptr, row_len, s_col, s_elem, e2n_d;
-  DevBuf<uint8_t> active, code;
+  DevBuf<uint8_t> active, code, elem_own;
   DevBuf<unsigned> tickets;
   // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
   Ell L;
@@ -81,12 +95,46 @@ struct mfea_handle {
   DevBuf<int32_t> e_partner, e_lane_row, e_src_pos, e_nbr_lane;
   DevBuf<double> e_f;  // all lane-operator doubles, carved by ell_op / ell_vecs
   DevBuf<Slot> slots;
-  DevBuf<SolveState> state;
-  SolveState* h_state = nullptr;  // pinned, 2 entries
+  DevBuf<SolveState> state, state_mirror;
+  SolveState* mirror = nullptr;  // where k_cg_advance publishes the final state
+  int64_t G = 0;                 // slots·64
+  // partitioned solve: exchange buffers
+  DevBuf<double> xrec;  // xs[2] | xr[2] | mr
+  DevBuf<double> gbuf;  // gall[2] | gsend | gred
+  DevBuf<double> xh;    // displacement halo: send | recv
+  DevBuf<int32_t> xsend_rows, xrecv_rows;
+  DistVecs dv{};
+  double* gred = nullptr;  // [64][4] gathered scalars (RHS norms, reaction, #active)
+  double* xh_send = nullptr;
+  double* xh_recv = nullptr;
+};
+
+struct mfea_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  double E = 2500.0, A = 0.0, I = 0.0;
+  Material mat{};
+  // host-side mesh/BC (original order)
+  int64_t N = 0, Ecount = 0;
+  std::vector<double> xyz;
+  std::vector<int64_t> e2n;
+  uint32_t mesh_flags = 0;
+  bool planar = false;  // every z == 0 (the whole mesh)
+  std::vector<int64_t> top, bot;
+  int64_t n_free_global = 0;
+  bool has_mesh = false, dirty = true;
+  std::vector<uint8_t> active_host;  // pending upload, original element order (empty = none)
+  std::vector<std::unique_ptr<Part>> parts;
+  // partitioning: nparts partitions on this device (world == 1), or this
+  // process's partition `rank` of `world` (RCCL)
+  int nparts = 1, axis = -1;
+  int world = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  double dist_timeout_s = 300.0;
+  SolveState* h_state = nullptr;       // pinned, 2 entries
   SolveState* d_host_state = nullptr;  // device view of h_state (mapped)
-  double* h_red = nullptr;        // pinned
-  int64_t G = 0;                  // slots·64
-  // graph cache
+  double* h_red = nullptr;             // pinned
+  // graph cache (single partition)
   hipGraphExec_t graph = nullptr;
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipEvent_t ev[6] = {};
@@ -105,10 +153,17 @@ constexpr int kMaxChunk = 64;
 // lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6, h × 2 18, hM 6
 constexpr int64_t kEllDoubles = 18 + 6 + 3 + 3 + 18 + 6 + 18 + 6;
 static_assert(kEllNone == kSrcNone && kEllHalo == kSrcHalo, "slot source codes");
+static_assert(kGhost == 3, "k_cg_rhs treats code 3 as a ghost free row");
 constexpr int kTicketSets = 16;
+constexpr int64_t kRecMax = 9, kMMax = 6;  // record / M widths at nd = 3, block Jacobi
+
+Part& part0(mfea_handle* h) { return *h->parts[0]; }
+bool partitioned(const mfea_handle* h) { return h->parts.size() > 1 || h->world > 1; }
+int nranks(const mfea_handle* h) { return h->world > 1 ? h->world : (int)h->parts.size(); }
 
 // ticket set k (one per reducing kernel kind; see device_util.hpp layout)
-unsigned* tix(mfea_handle* h, int k) { return h->tickets.ptr + (size_t)k * kTicketStride; }
+unsigned* tix(Part& pt, int k) { return pt.tickets.ptr + (size_t)k * kTicketStride; }
+double* cg_part_buf(Part& pt, int par) { return pt.cg_part.ptr + (size_t)par * 4 * kCgMaxPartials; }
 
 void destroy_graph(mfea_handle* h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
@@ -132,101 +187,223 @@ int order_mode() {
   return std::atoi(e);
 }
 
-// Build the symbolic pattern and (re)allocate + upload device state.
-int ensure_built(mfea_handle* h) {
-  if (!h->has_mesh) return fail(MFEA_ESTATE, "no mesh: call mfea_set_mesh first");
-  if (!h->dirty) return 0;
-  destroy_graph(h);
-  std::string err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(),
-                                  (h->mesh_flags & MFEA_MESH_SKIP_INVALID) != 0, h->top, h->bot,
-                                  order_mode(), h->P);
-  if (!err.empty()) return fail(MFEA_EINVAL, err);
-  const Pattern& P = h->P;
+// planar meshes run the lanes with 2 DOFs per node (MFEA_LANE_DOF=3 forces 3);
+// decided on the whole mesh so every partition exchanges records of one width
+int lane_dofs(const mfea_handle* h) {
+  const char* e = std::getenv("MFEA_LANE_DOF");
+  return (h->planar && !(e && std::strcmp(e, "3") == 0)) ? 2 : 3;
+}
+
+// Waits for an event.  Partitioned over RCCL: polls with a deadline and the
+// communicator's error state, so a lost peer ends the call instead of hanging.
+int wait_event(mfea_handle* h, hipEvent_t ev) {
+  if (h->world <= 1 || !h->comm) {
+    HIPC(hipEventSynchronize(ev));
+    return 0;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) return fail(MFEA_EDEVICE, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    ncclResult_t ar = ncclSuccess;
+    if (ncclCommGetAsyncError(h->comm, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) {
+      (void)ncclCommAbort(h->comm);
+      h->comm = nullptr;
+      return fail(MFEA_ECOMM, std::string("RCCL: ") + ncclGetErrorString(ar));
+    }
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt > h->dist_timeout_s) {
+      (void)ncclCommAbort(h->comm);
+      h->comm = nullptr;
+      return fail(MFEA_ECOMM, "RCCL: no progress before the deadline (peer lost?)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+int sync_stream(mfea_handle* h) {
+  HIPC(hipEventRecord(h->ev[5], h->stream));
+  return wait_event(h, h->ev[5]);
+}
+
+// ---------------------------------------------------------------------------
+// Build one partition: symbolic pattern + lanes (host), allocate and upload.
+// ---------------------------------------------------------------------------
+int upload_part(mfea_handle* h, Part& pt, bool dm) {
+  const Pattern& P = pt.P;
   const int64_t N = P.n_nodes, E = P.n_elems;
-  h->G = P.n_slots() * kSlice;
+  pt.G = P.n_slots() * kSlice;
   const int64_t maxg = std::max<int64_t>({grid_rows(N), grid_rows(E), 2048, 1});
-  HIPC(h->xyz_d.alloc(3 * N));
-  HIPC(h->val.alloc(6 * h->G));
-  HIPC(h->diag.alloc(6 * N));
-  HIPC(h->x.alloc(3 * N));
-  HIPC(h->r.alloc(3 * N));
-  HIPC(h->p.alloc(3 * N));
-  HIPC(h->q.alloc(3 * N));
-  HIPC(h->cg_r1.alloc(3 * N));
-  HIPC(h->cg_s0.alloc(3 * N));
-  HIPC(h->cg_s1.alloc(3 * N));
-  HIPC(h->cg_w0.alloc(3 * N));
-  HIPC(h->cg_w1.alloc(3 * N));
-  HIPC(h->cg_part.alloc(2 * 4 * kCgMaxPartials));
-  HIPC(h->dinv.alloc(6 * N));
-  HIPC(h->stress.alloc(E));
-  HIPC(h->partials.alloc(4 * (maxg + 16)));
-  HIPC(h->red.alloc(16));
-  HIPC(h->slice_ptr.alloc(P.slice_ptr.size()));
-  HIPC(h->row_len.alloc(N));
-  HIPC(h->s_col.alloc(h->G));
-  HIPC(h->s_elem.alloc(h->G));
-  HIPC(h->e2n_d.alloc(2 * E));
-  HIPC(h->active.alloc(E));
-  HIPC(h->code.alloc(N));
-  HIPC(h->tickets.alloc(kTicketSets * kTicketStride));
-  HIPC(h->slots.alloc(kMaxChunk + 2));
-  HIPC(h->state.alloc(1));
+  HIPC(pt.xyz_d.alloc(3 * N));
+  HIPC(pt.val.alloc(6 * pt.G));
+  HIPC(pt.diag.alloc(6 * N));
+  HIPC(pt.x.alloc(3 * N));
+  HIPC(pt.r.alloc(3 * N));
+  HIPC(pt.p.alloc(3 * N));
+  HIPC(pt.q.alloc(3 * N));
+  HIPC(pt.cg_r1.alloc(3 * N));
+  HIPC(pt.cg_s0.alloc(3 * N));
+  HIPC(pt.cg_s1.alloc(3 * N));
+  HIPC(pt.cg_w0.alloc(3 * N));
+  HIPC(pt.cg_w1.alloc(3 * N));
+  HIPC(pt.cg_part.alloc(2 * 4 * kCgMaxPartials));
+  HIPC(pt.dinv.alloc(6 * N));
+  HIPC(pt.stress.alloc(E));
+  HIPC(pt.partials.alloc(4 * (maxg + 16)));
+  HIPC(pt.red.alloc(16));
+  HIPC(pt.slice_ptr.alloc(P.slice_ptr.size()));
+  HIPC(pt.row_len.alloc(N));
+  HIPC(pt.s_col.alloc(pt.G));
+  HIPC(pt.s_elem.alloc(pt.G));
+  HIPC(pt.e2n_d.alloc(2 * E));
+  HIPC(pt.active.alloc(E));
+  HIPC(pt.code.alloc(N));
+  HIPC(pt.tickets.alloc(kTicketSets * kTicketStride));
+  HIPC(pt.slots.alloc(kMaxChunk + 2));
+  HIPC(pt.state.alloc(1));
   hipStream_t s = h->stream;
   auto up = [&](void* d, const void* src, size_t bytes) {
     return bytes ? hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
   };
-  HIPC(up(h->xyz_d.ptr, P.xyz_perm.data(), 3 * N * sizeof(double)));
-  HIPC(up(h->slice_ptr.ptr, P.slice_ptr.data(), P.slice_ptr.size() * sizeof(int32_t)));
-  HIPC(up(h->row_len.ptr, P.row_len.data(), N * sizeof(int32_t)));
-  HIPC(up(h->s_col.ptr, P.s_col.data(), h->G * sizeof(int32_t)));
-  HIPC(up(h->s_elem.ptr, P.s_elem.data(), h->G * sizeof(int32_t)));
-  HIPC(up(h->e2n_d.ptr, P.e2n_perm.data(), 2 * E * sizeof(int32_t)));
-  HIPC(up(h->code.ptr, P.code.data(), N * sizeof(uint8_t)));
-  HIPC(hipMemsetAsync(h->tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
-  HIPC(hipMemsetAsync(h->x.ptr, 0, 3 * N * sizeof(double), s));
-  HIPC(hipMemsetAsync(h->p.ptr, 0, 3 * N * sizeof(double), s));
-  HIPC(hipMemsetAsync(h->q.ptr, 0, 3 * N * sizeof(double), s));
-  HIPC(hipMemsetAsync(h->stress.ptr, 0, E * sizeof(double), s));
-  HIPC(hipMemsetAsync(h->val.ptr, 0, 6 * h->G * sizeof(double), s));
-  HIPC(hipMemsetAsync(h->diag.ptr, 0, 6 * N * sizeof(double), s));
-  if (h->active_host.size() == (size_t)E) {
-    HIPC(up(h->active.ptr, h->active_host.data(), E));
+  HIPC(up(pt.xyz_d.ptr, P.xyz_perm.data(), 3 * N * sizeof(double)));
+  HIPC(up(pt.slice_ptr.ptr, P.slice_ptr.data(), P.slice_ptr.size() * sizeof(int32_t)));
+  HIPC(up(pt.row_len.ptr, P.row_len.data(), N * sizeof(int32_t)));
+  HIPC(up(pt.s_col.ptr, P.s_col.data(), pt.G * sizeof(int32_t)));
+  HIPC(up(pt.s_elem.ptr, P.s_elem.data(), pt.G * sizeof(int32_t)));
+  HIPC(up(pt.e2n_d.ptr, P.e2n_perm.data(), 2 * E * sizeof(int32_t)));
+  HIPC(up(pt.code.ptr, P.code.data(), N * sizeof(uint8_t)));
+  HIPC(hipMemsetAsync(pt.tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
+  HIPC(hipMemsetAsync(pt.red.ptr, 0, 16 * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.x.ptr, 0, 3 * N * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.p.ptr, 0, 3 * N * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.q.ptr, 0, 3 * N * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.stress.ptr, 0, E * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.val.ptr, 0, 6 * pt.G * sizeof(double), s));
+  HIPC(hipMemsetAsync(pt.diag.ptr, 0, 6 * N * sizeof(double), s));
+  std::vector<uint8_t> act;
+  if (h->active_host.size() == (size_t)h->Ecount) {
+    if (dm) {
+      act.resize(E);
+      for (int64_t le = 0; le < E; ++le) act[le] = h->active_host[pt.plan.elem_g[le]];
+    } else {
+      act = h->active_host;
+    }
+    HIPC(up(pt.active.ptr, act.data(), E));
   } else {
-    HIPC(hipMemsetAsync(h->active.ptr, 1, E, s));
+    HIPC(hipMemsetAsync(pt.active.ptr, 1, E, s));
   }
-  // wave-local lanes (falls back to the SELL kernel when a row cannot be placed)
-  h->ell_ok = build_ell(P, h->L).empty() && P.n_free > 0;
-  if (h->ell_ok) {
-    const Ell& L = h->L;
+  // wave-local lanes (single partition: falls back to the SELL kernel when a
+  // row cannot be placed; partitioned: required)
+  const std::string lerr = build_ell(P, pt.L, dm ? &pt.plan.elem_pair : nullptr);
+  pt.ell_ok = lerr.empty() && (dm || P.n_free > 0);
+  if (dm && !lerr.empty()) return fail(MFEA_EINVAL, "partition " + std::to_string(pt.rank) + ": " + lerr);
+  if (pt.ell_ok) {
+    const Ell& L = pt.L;
     const int64_t NL = L.n_lanes;
     std::vector<uint32_t> code(NL);
     for (int64_t l = 0; l < NL; ++l)
       code[l] = (L.code[l] & 0xFFFFFFu) | (uint32_t)(uint8_t)(int8_t)L.info[l] << 24;
-    HIPC(h->e_code.alloc(NL));
-    HIPC(h->e_partner.alloc(NL));
-    HIPC(h->e_lane_row.alloc(NL));
-    HIPC(h->e_src_pos.alloc(3 * NL));
-    HIPC(h->e_nbr_lane.alloc(3 * NL));
-    HIPC(h->e_f.alloc(kEllDoubles * NL));
-    HIPC(up(h->e_code.ptr, code.data(), NL * sizeof(uint32_t)));
-    HIPC(up(h->e_partner.ptr, L.partner.data(), NL * sizeof(int32_t)));
-    HIPC(up(h->e_lane_row.ptr, L.lane_row.data(), NL * sizeof(int32_t)));
-    HIPC(up(h->e_src_pos.ptr, L.src_pos.data(), 3 * NL * sizeof(int32_t)));
-    HIPC(up(h->e_nbr_lane.ptr, L.nbr_lane.data(), 3 * NL * sizeof(int32_t)));
+    HIPC(pt.e_code.alloc(NL));
+    HIPC(pt.e_partner.alloc(NL));
+    HIPC(pt.e_lane_row.alloc(NL));
+    HIPC(pt.e_src_pos.alloc(3 * NL));
+    HIPC(pt.e_nbr_lane.alloc(3 * NL));
+    HIPC(pt.e_f.alloc(kEllDoubles * NL));
+    HIPC(up(pt.e_code.ptr, code.data(), NL * sizeof(uint32_t)));
+    HIPC(up(pt.e_partner.ptr, L.partner.data(), NL * sizeof(int32_t)));
+    HIPC(up(pt.e_lane_row.ptr, L.lane_row.data(), NL * sizeof(int32_t)));
+    HIPC(up(pt.e_src_pos.ptr, L.src_pos.data(), 3 * NL * sizeof(int32_t)));
+    HIPC(up(pt.e_nbr_lane.ptr, L.nbr_lane.data(), 3 * NL * sizeof(int32_t)));
     // halo records of lanes without a halo slot are read but never used
-    HIPC(hipMemsetAsync(h->e_f.ptr, 0, kEllDoubles * NL * sizeof(double), s));
+    if (NL) HIPC(hipMemsetAsync(pt.e_f.ptr, 0, kEllDoubles * NL * sizeof(double), s));
+  }
+  if (dm) {
+    const PartPlan& pl = pt.plan;
+    const int64_t NX = std::max<int64_t>(pl.n_pairs, 1);
+    HIPC(pt.xrec.alloc(4 * NX * kRecMax + NX * kMMax));
+    pt.dv.xs[0] = pt.xrec.ptr;
+    pt.dv.xs[1] = pt.xrec.ptr + NX * kRecMax;
+    pt.dv.xr[0] = pt.xrec.ptr + 2 * NX * kRecMax;
+    pt.dv.xr[1] = pt.xrec.ptr + 3 * NX * kRecMax;
+    pt.dv.mr = pt.xrec.ptr + 4 * NX * kRecMax;
+    HIPC(hipMemsetAsync(pt.xrec.ptr, 0, pt.xrec.n * sizeof(double), s));
+    HIPC(pt.gbuf.alloc(2 * 4 * kMaxRanks + 4 + 4 * kMaxRanks));
+    pt.dv.gall[0] = pt.gbuf.ptr;
+    pt.dv.gall[1] = pt.gbuf.ptr + 4 * kMaxRanks;
+    pt.dv.gsend = pt.gbuf.ptr + 8 * kMaxRanks;
+    pt.gred = pt.gbuf.ptr + 8 * kMaxRanks + 4;
+    HIPC(hipMemsetAsync(pt.gbuf.ptr, 0, pt.gbuf.n * sizeof(double), s));
+    const int64_t ns = (int64_t)pl.xsend_node.size(), nr = (int64_t)pl.xrecv_node.size();
+    HIPC(pt.xh.alloc(3 * (ns + nr)));
+    pt.xh_send = pt.xh.ptr;
+    pt.xh_recv = pt.xh.ptr + 3 * ns;
+    std::vector<int32_t> rs(ns), rr(nr);
+    for (int64_t i = 0; i < ns; ++i) rs[i] = P.iperm[pl.xsend_node[i]];
+    for (int64_t i = 0; i < nr; ++i) rr[i] = P.iperm[pl.xrecv_node[i]];
+    HIPC(pt.xsend_rows.alloc(ns));
+    HIPC(pt.xrecv_rows.alloc(nr));
+    HIPC(up(pt.xsend_rows.ptr, rs.data(), ns * sizeof(int32_t)));
+    HIPC(up(pt.xrecv_rows.ptr, rr.data(), nr * sizeof(int32_t)));
+    HIPC(pt.elem_own.alloc(E));
+    HIPC(up(pt.elem_own.ptr, pl.elem_own.data(), E));
   }
   HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// Build the symbolic pattern(s) and (re)allocate + upload device state.
+int ensure_built(mfea_handle* h) {
+  if (!h->has_mesh) return fail(MFEA_ESTATE, "no mesh: call mfea_set_mesh first");
+  if (!h->dirty) return 0;
+  destroy_graph(h);
+  const bool dm = h->world > 1 || h->nparts > 1;
+  const int np = h->world > 1 ? 1 : h->nparts;
+  const bool skip = (h->mesh_flags & MFEA_MESH_SKIP_INVALID) != 0;
+  h->parts.clear();
+  for (int i = 0; i < np; ++i) {
+    h->parts.push_back(std::make_unique<Part>());
+    Part& pt = *h->parts.back();
+    pt.rank = h->world > 1 ? h->rank : i;
+    std::string err;
+    if (!dm) {
+      err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(), skip, h->top, h->bot,
+                          order_mode(), pt.P);
+    } else {
+      err = build_partition(h->N, h->xyz.data(), h->Ecount, h->e2n.data(), skip, h->top, h->bot,
+                            h->world > 1 ? h->world : np, pt.rank, h->axis, pt.plan);
+      if (err.empty())
+        err = build_pattern((int64_t)pt.plan.node_g.size(), pt.plan.xyz.data(),
+                            (int64_t)pt.plan.elem_g.size(), pt.plan.e2n.data(), false, pt.plan.top,
+                            pt.plan.bot, order_mode(), pt.P, &pt.plan.ghost);
+    }
+    if (!err.empty()) {
+      h->parts.resize(1);
+      return fail(MFEA_EINVAL, err);
+    }
+    if (i == 0) {
+      pt.mirror = h->d_host_state;
+    } else {
+      HIPC(pt.state_mirror.alloc(1));
+      pt.mirror = pt.state_mirror.ptr;
+    }
+    RC(upload_part(h, pt, dm));
+  }
+  {  // free DOFs of the whole mesh (reported in mfea_stats)
+    std::vector<uint8_t> known(h->N, 0);
+    for (int64_t t : h->top) known[t] = 1;
+    for (int64_t b : h->bot) known[b] = 1;
+    h->n_free_global = h->N - (int64_t)std::count(known.begin(), known.end(), 1);
+  }
   h->active_host.clear();
   h->dirty = false;
   return 0;
 }
 
 // MFEA_CG_KERNEL=sell forces the SELL iteration kernel (comparison runs)
-bool use_ell(const mfea_handle* h) {
+bool use_ell(const Part& pt) {
   const char* e = std::getenv("MFEA_CG_KERNEL");
-  return h->ell_ok && !(e && std::strcmp(e, "sell") == 0);
+  return pt.ell_ok && !(e && std::strcmp(e, "sell") == 0);
 }
 
 mfea_solve_opts default_opts() {
@@ -241,58 +418,52 @@ mfea_solve_opts default_opts() {
   return o;
 }
 
-SellOp sell_op(mfea_handle* h) {
+SellOp sell_op(Part& pt) {
   SellOp op;
-  op.N = h->P.n_nodes;
-  op.nf = h->P.n_free;
-  op.G = h->G;
-  op.slice_ptr = h->slice_ptr.ptr;
-  op.row_len = h->row_len.ptr;
-  op.s_col = h->s_col.ptr;
-  op.val = h->val.ptr;
-  op.diag = h->diag.ptr;
+  op.N = pt.P.n_nodes;
+  op.nf = pt.P.n_free;
+  op.G = pt.G;
+  op.slice_ptr = pt.slice_ptr.ptr;
+  op.row_len = pt.row_len.ptr;
+  op.s_col = pt.s_col.ptr;
+  op.val = pt.val.ptr;
+  op.diag = pt.diag.ptr;
   return op;
 }
 
-CgVecs cg_vecs(mfea_handle* h) {
+CgVecs cg_vecs(Part& pt) {
   CgVecs v;
-  v.x = h->x.ptr;
-  v.p = h->p.ptr;
-  v.r[0] = h->r.ptr;
-  v.r[1] = h->cg_r1.ptr;
-  v.s[0] = h->cg_s0.ptr;
-  v.s[1] = h->cg_s1.ptr;
-  v.w[0] = h->cg_w0.ptr;
-  v.w[1] = h->cg_w1.ptr;
-  v.dinv = h->dinv.ptr;
+  v.x = pt.x.ptr;
+  v.p = pt.p.ptr;
+  v.r[0] = pt.r.ptr;
+  v.r[1] = pt.cg_r1.ptr;
+  v.s[0] = pt.cg_s0.ptr;
+  v.s[1] = pt.cg_s1.ptr;
+  v.w[0] = pt.cg_w0.ptr;
+  v.w[1] = pt.cg_w1.ptr;
+  v.dinv = pt.dinv.ptr;
   return v;
 }
 
-// planar meshes run the lanes with 2 DOFs per node (MFEA_LANE_DOF=3 forces 3)
-int lane_dofs(const mfea_handle* h) {
-  const char* e = std::getenv("MFEA_LANE_DOF");
-  return (h->P.planar && !(e && std::strcmp(e, "3") == 0)) ? 2 : 3;
-}
-
-EllOp ell_op(mfea_handle* h) {
+EllOp ell_op(const mfea_handle* h, Part& pt) {
   EllOp op;
-  const int64_t NL = h->L.n_lanes;
+  const int64_t NL = pt.L.n_lanes;
   op.NL = NL;
   op.nd = lane_dofs(h);
-  op.code = h->e_code.ptr;
-  op.partner = h->e_partner.ptr;
-  op.lane_row = h->e_lane_row.ptr;
-  op.src_pos = h->e_src_pos.ptr;
-  op.nbr_lane = h->e_nbr_lane.ptr;
-  op.V = h->e_f.ptr;
+  op.code = pt.e_code.ptr;
+  op.partner = pt.e_partner.ptr;
+  op.lane_row = pt.e_lane_row.ptr;
+  op.src_pos = pt.e_src_pos.ptr;
+  op.nbr_lane = pt.e_nbr_lane.ptr;
+  op.V = pt.e_f.ptr;
   op.D = op.V + 18 * NL;
   return op;
 }
 
-EllVecs ell_vecs(mfea_handle* h) {
+EllVecs ell_vecs(Part& pt) {
   EllVecs v;
-  const int64_t NL = h->L.n_lanes;
-  double* f = h->e_f.ptr + 24 * NL;
+  const int64_t NL = pt.L.n_lanes;
+  double* f = pt.e_f.ptr + 24 * NL;
   auto take = [&](int64_t n) {
     double* p = f;
     f += n * NL;
@@ -312,30 +483,164 @@ EllVecs ell_vecs(mfea_handle* h) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// Exchanges of the partitioned solve.  Over RCCL: one group of point-to-point
+// transfers on the handle's stream (the partial-sum all-gather is done with
+// send/recv pairs too, so one group per iteration carries everything).
+// Partitions on one device: device copies on the same stream.
+// ---------------------------------------------------------------------------
+// CG records of parity q (xs[q] → the peers' xr[q]); gather: this rank's
+// partial sums (gsend) → row `rank` of every rank's gall[q].
+int xchg_records(mfea_handle* h, int q, bool gather) {
+  const int64_t RW = 3 * lane_dofs(h);
+  hipStream_t s = h->stream;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    const PartPlan& pl = pt.plan;
+    NCCLC(ncclGroupStart());
+    for (size_t i = 0; i < pl.peers.size(); ++i) {
+      const size_t n = (size_t)(pl.peer_cnt[i] * RW);
+      NCCLC(ncclSend(pt.dv.xs[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
+      NCCLC(ncclRecv(pt.dv.xr[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
+    }
+    if (gather)
+      for (int r = 0; r < h->world; ++r) {
+        if (r == h->rank) continue;
+        NCCLC(ncclSend(pt.dv.gsend, 4, ncclFloat64, r, h->comm, s));
+        NCCLC(ncclRecv(pt.dv.gall[q] + 4 * r, 4, ncclFloat64, r, h->comm, s));
+      }
+    NCCLC(ncclGroupEnd());
+    return 0;
+  }
+  for (auto& a : h->parts) {
+    const PartPlan& pa = a->plan;
+    for (size_t i = 0; i < pa.peers.size(); ++i) {
+      Part& b = *h->parts[pa.peers[i]];
+      const PartPlan& pb = b.plan;
+      const auto it = std::lower_bound(pb.peers.begin(), pb.peers.end(), a->rank);
+      const size_t jb = (size_t)(it - pb.peers.begin());
+      if (it == pb.peers.end() || *it != a->rank || pb.peer_cnt[jb] != pa.peer_cnt[i])
+        return fail(MFEA_EINVAL, "internal: asymmetric exchange plan");
+      HIPC(hipMemcpyAsync(b.dv.xr[q] + pb.peer_off[jb] * RW, a->dv.xs[q] + pa.peer_off[i] * RW,
+                          pa.peer_cnt[i] * RW * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    if (gather)
+      for (auto& b : h->parts)
+        if (b != a)
+          HIPC(hipMemcpyAsync(b->dv.gall[q] + 4 * a->rank, a->dv.gsend, 4 * sizeof(double),
+                              hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
+}
+
+// displacement halo: xh_send (packed owned rows) → the peers' xh_recv
+int xchg_xhalo(mfea_handle* h) {
+  hipStream_t s = h->stream;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    const PartPlan& pl = pt.plan;
+    NCCLC(ncclGroupStart());
+    for (size_t i = 0; i < pl.xpeers.size(); ++i) {
+      if (pl.xsend_cnt[i])
+        NCCLC(ncclSend(pt.xh_send + 3 * pl.xsend_off[i], (size_t)(3 * pl.xsend_cnt[i]), ncclFloat64,
+                       pl.xpeers[i], h->comm, s));
+      if (pl.xrecv_cnt[i])
+        NCCLC(ncclRecv(pt.xh_recv + 3 * pl.xrecv_off[i], (size_t)(3 * pl.xrecv_cnt[i]), ncclFloat64,
+                       pl.xpeers[i], h->comm, s));
+    }
+    NCCLC(ncclGroupEnd());
+    return 0;
+  }
+  for (auto& a : h->parts) {
+    const PartPlan& pa = a->plan;
+    for (size_t i = 0; i < pa.xpeers.size(); ++i) {
+      if (!pa.xsend_cnt[i]) continue;
+      Part& b = *h->parts[pa.xpeers[i]];
+      const PartPlan& pb = b.plan;
+      const auto it = std::lower_bound(pb.xpeers.begin(), pb.xpeers.end(), a->rank);
+      const size_t jb = (size_t)(it - pb.xpeers.begin());
+      if (it == pb.xpeers.end() || *it != a->rank || pb.xrecv_cnt[jb] != pa.xsend_cnt[i])
+        return fail(MFEA_EINVAL, "internal: asymmetric displacement halo");
+      HIPC(hipMemcpyAsync(b.xh_recv + 3 * pb.xrecv_off[jb], a->xh_send + 3 * pa.xsend_off[i],
+                          3 * pa.xsend_cnt[i] * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+  }
+  return 0;
+}
+
+// 4 doubles at red + off of every partition → row `rank` of every gred
+int gather4(mfea_handle* h, int off) {
+  hipStream_t s = h->stream;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    HIPC(hipMemcpyAsync(pt.gred + 4 * h->rank, pt.red.ptr + off, 4 * sizeof(double),
+                        hipMemcpyDeviceToDevice, s));
+    NCCLC(ncclGroupStart());
+    for (int r = 0; r < h->world; ++r) {
+      if (r == h->rank) continue;
+      NCCLC(ncclSend(pt.red.ptr + off, 4, ncclFloat64, r, h->comm, s));
+      NCCLC(ncclRecv(pt.gred + 4 * r, 4, ncclFloat64, r, h->comm, s));
+    }
+    NCCLC(ncclGroupEnd());
+    return 0;
+  }
+  for (auto& a : h->parts)
+    for (auto& b : h->parts)
+      HIPC(hipMemcpyAsync(b->gred + 4 * a->rank, a->red.ptr + off, 4 * sizeof(double),
+                          hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // enqueue one chunk of single-reduction CG iterations (one kernel each)
 void enqueue_chunk(mfea_handle* h, int chunk, int precond, bool ell) {
   hipStream_t s = h->stream;
+  Part& pt = part0(h);
   if (ell) {
-    const EllOp op = ell_op(h);
-    const EllVecs v = ell_vecs(h);
+    const EllOp op = ell_op(h, pt);
+    const EllVecs v = ell_vecs(pt);
     for (int j = 0; j < chunk; ++j)
-      launch_ell_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+      launch_ell_iter(s, j, op, precond, v, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
   } else {
-    const SellOp op = sell_op(h);
-    const CgVecs v = cg_vecs(h);
+    const SellOp op = sell_op(pt);
+    const CgVecs v = cg_vecs(pt);
     for (int j = 0; j < chunk; ++j)
-      launch_cg_iter(s, j, op, precond, v, h->slots.ptr, h->state.ptr, h->cg_part.ptr);
+      launch_cg_iter(s, j, op, precond, v, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
   }
-  launch_cg_advance(s, chunk, h->slots.ptr, h->state.ptr, h->d_host_state);
+  launch_cg_advance(s, chunk, pt.slots.ptr, pt.state.ptr, pt.mirror);
+}
+
+// partitioned: per iteration, every partition's iteration kernel, its partial
+// sums, then one exchange of records + sums (launched eagerly)
+int enqueue_chunk_dist(mfea_handle* h, int chunk, int precond) {
+  hipStream_t s = h->stream;
+  for (int j = 0; j < chunk; ++j) {
+    const int q = (j & 1) ^ 1;
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_ell_iter(s, j, ell_op(h, pt), precond, ell_vecs(pt), pt.slots.ptr, pt.state.ptr,
+                      pt.cg_part.ptr, nullptr, &pt.dv);
+    }
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_psum(s, pt.L.n_lanes, cg_part_buf(pt, q), pt.dv.gall[q] + 4 * pt.rank, pt.dv.gsend);
+    }
+    HIPC(hipGetLastError());
+    RC(xchg_records(h, q, true));
+  }
+  for (auto& pp : h->parts) launch_cg_advance(s, chunk, pp->slots.ptr, pp->state.ptr, pp->mirror);
+  HIPC(hipGetLastError());
+  return 0;
 }
 
 // Replays chunks until the device reports done; at most two chunks in flight.
-template <class Enqueue>
 // mirror = true: the chunk's advance kernel writes the final state into the
 // mapped pinned h_state[0] itself (CG-CG path); otherwise copy it per chunk.
+template <class Enqueue>
 int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, SolveState* out,
                  bool mirror = false) {
   hipStream_t s = h->stream;
+  Part& pt = part0(h);
   const int64_t max_chunks = (int64_t)max_it / chunk + 3;
   int64_t k = 0;
   bool done = false;
@@ -345,16 +650,16 @@ int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, Solve
     int rc = enqueue();
     if (rc) return rc;
     if (!mirror)
-      HIPC(hipMemcpyAsync(&h->h_state[k & 1], h->state.ptr, sizeof(SolveState),
+      HIPC(hipMemcpyAsync(&h->h_state[k & 1], pt.state.ptr, sizeof(SolveState),
                           hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(h->poll[k & 1], s));
     if (k >= 1) {
-      HIPC(hipEventSynchronize(h->poll[(k - 1) & 1]));
+      RC(wait_event(h, h->poll[(k - 1) & 1]));
       if (hs[mirror ? 0 : (k - 1) & 1].done) done = true;
     }
     ++k;
   }
-  HIPC(hipStreamSynchronize(s));
+  RC(sync_stream(h));
   const SolveState& last = h->h_state[mirror ? 0 : (k - 1) & 1];
   if (!last.done) {
     // should not happen (max_chunks covers max_it); report as maxit
@@ -367,17 +672,15 @@ int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, Solve
   return 0;
 }
 
-int finish_solve(mfea_handle* h, const mfea_solve_opts* o, int64_t nf, const SolveState& fin,
-                 mfea_stats* st) {
-  (void)o;
+int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
   HIPC(hipEventRecord(h->ev[3], h->stream));
-  HIPC(hipEventSynchronize(h->ev[3]));
+  RC(wait_event(h, h->ev[3]));
   if (st) {
     st->iters = fin.iters;
     st->status = fin.status;
     st->bnorm = std::sqrt(fin.bb0);
     st->relres = fin.res0 > 0 ? std::sqrt(fin.res_final / fin.res0) : 0.0;
-    st->n_free = 3 * nf;
+    st->n_free = 3 * h->n_free_global;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
     st->t_rhs_ms = ms;
@@ -389,28 +692,31 @@ int finish_solve(mfea_handle* h, const mfea_solve_opts* o, int64_t nf, const Sol
   return 0;
 }
 
+int solve_chunk_size(const mfea_solve_opts* o) {
+  int chunk = o->chunk > 0 ? std::min(o->chunk, kMaxChunk) : 32;
+  return chunk + (chunk & 1);  // even: the iteration kernels take the buffer parity from j
+}
+
 int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
                mfea_stats* st) {
-  const Pattern& P = h->P;
+  Part& pt = part0(h);
   hipStream_t s = h->stream;
-  const int64_t nf = P.n_free;
   const int precond = o->precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
-  int chunk = o->chunk > 0 ? std::min(o->chunk, kMaxChunk) : 32;
-  chunk += chunk & 1;  // even: k_cg_iter takes the r/s/w buffer parity from j
-  const SellOp op = sell_op(h);
-  const CgVecs v = cg_vecs(h);
+  const int chunk = solve_chunk_size(o);
+  const SellOp op = sell_op(pt);
+  const CgVecs v = cg_vecs(pt);
   HIPC(hipEventRecord(h->ev[1], s));
-  launch_cg_rhs(s, op, h->code.ptr, dy_top, dy_bot, o->reg, precond, v, h->partials.ptr,
-                tix(h, 0), h->red.ptr);
-  launch_cg_init_finalize(s, h->red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
-                          h->state.ptr);
-  HIPC(hipMemsetAsync(h->cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
-  const bool ell = use_ell(h);
+  launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, precond, v, pt.partials.ptr, tix(pt, 0),
+                pt.red.ptr);
+  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
+                          pt.state.ptr);
+  HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  const bool ell = use_ell(pt);
   if (ell) {
-    launch_ell_init(s, ell_op(h), op, precond, v, ell_vecs(h));
-    launch_ell_first(s, ell_op(h), o->reg, precond, ell_vecs(h), h->slots.ptr, h->cg_part.ptr);
+    launch_ell_init(s, ell_op(h, pt), op, precond, v, ell_vecs(pt));
+    launch_ell_first(s, ell_op(h, pt), o->reg, precond, ell_vecs(pt), pt.slots.ptr, pt.cg_part.ptr);
   } else {
-    launch_cg_first(s, op, o->reg, precond, v, h->slots.ptr, h->cg_part.ptr);
+    launch_cg_first(s, op, o->reg, precond, v, pt.slots.ptr, pt.cg_part.ptr);
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
@@ -453,22 +759,80 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   }
   if (rc) return rc;
   if (ell) {
-    launch_ell_finish(s, ell_op(h), ell_vecs(h), h->x.ptr);
+    launch_ell_finish(s, ell_op(h, pt), ell_vecs(pt), pt.x.ptr);
     HIPC(hipGetLastError());
   }
-  return finish_solve(h, o, nf, fin, st);
+  return finish_solve(h, fin, st);
+}
+
+// The partitioned solve: the same CG-CG iterations on every partition's lanes,
+// with the exchanges of partition.hpp between kernels.
+int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
+               mfea_stats* st) {
+  hipStream_t s = h->stream;
+  const int precond = o->precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
+  const int chunk = solve_chunk_size(o);
+  const int W = nranks(h);
+  HIPC(hipEventRecord(h->ev[1], s));
+  // RHS, M⁻¹ and the global (‖b‖², ‖M⁻¹b‖²)
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, precond, cg_vecs(pt),
+                  pt.partials.ptr, tix(pt, 0), pt.red.ptr);
+  }
+  RC(gather4(h, 0));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
+    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg,
+                            pt.state.ptr);
+    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+    launch_ell_init(s, ell_op(h, pt), sell_op(pt), precond, cg_vecs(pt), ell_vecs(pt));
+    launch_ell_pack0(s, ell_op(h, pt), precond, ell_vecs(pt), pt.dv);
+  }
+  RC(xchg_records(h, 1, false));  // [r₀ | M] of the cut rows
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_ell_first(s, ell_op(h, pt), o->reg, precond, ell_vecs(pt), pt.slots.ptr, pt.cg_part.ptr,
+                     &pt.dv);
+    launch_psum(s, pt.L.n_lanes, cg_part_buf(pt, 0), pt.dv.gall[0] + 4 * pt.rank, pt.dv.gsend);
+  }
+  RC(xchg_records(h, 0, true));
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(h->ev[2], s));
+  SolveState fin;
+  RC(drive_chunks(
+      h, chunk, o->max_it, [&]() -> int { return enqueue_chunk_dist(h, chunk, precond); }, &fin,
+      /*mirror=*/true));
+  // x to row order, then the displacement halo (ghost rows of the post kernels)
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_ell_finish(s, ell_op(h, pt), ell_vecs(pt), pt.x.ptr);
+    launch_rows_pack(s, pt.xsend_rows.ptr, (int64_t)pt.plan.xsend_node.size(), pt.x.ptr, pt.xh_send);
+  }
+  RC(xchg_xhalo(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rows_unpack(s, pt.xrecv_rows.ptr, (int64_t)pt.plan.xrecv_node.size(), pt.xh_recv,
+                       pt.x.ptr);
+  }
+  HIPC(hipGetLastError());
+  return finish_solve(h, fin, st);
 }
 
 int assemble_impl(mfea_handle* h, mfea_stats* st) {
-  const Pattern& P = h->P;
   hipStream_t s = h->stream;
   HIPC(hipEventRecord(h->ev[0], s));
-  launch_assemble(s, P.n_nodes, h->xyz_d.ptr, h->slice_ptr.ptr, h->row_len.ptr, h->s_col.ptr,
-                  h->s_elem.ptr, h->active.ptr, h->mat, h->G, h->val.ptr, h->diag.ptr);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Pattern& P = pt.P;
+    launch_assemble(s, P.n_nodes, pt.xyz_d.ptr, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr,
+                    pt.s_elem.ptr, pt.active.ptr, h->mat, pt.G, pt.val.ptr, pt.diag.ptr);
+  }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[1], s));
   if (st) {
-    HIPC(hipEventSynchronize(h->ev[1]));
+    RC(wait_event(h, h->ev[1]));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
     st->t_assemble_ms = ms;
@@ -478,20 +842,32 @@ int assemble_impl(mfea_handle* h, mfea_stats* st) {
 
 int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
               mfea_stats* st) {
-  const Pattern& P = h->P;
   hipStream_t s = h->stream;
+  const bool dm = partitioned(h);
   HIPC(hipEventRecord(h->ev[4], s));
-  launch_reaction(s, P.n_free, P.n_top, P.n_nodes, h->slice_ptr.ptr, h->row_len.ptr, h->s_col.ptr,
-                  h->val.ptr, h->diag.ptr, h->G, h->x.ptr, h->partials.ptr, tix(h, 3),
-                  h->red.ptr + 4);
-  launch_stress(s, P.n_elems, h->e2n_d.ptr, h->xyz_d.ptr, h->x.ptr, h->mat, max_strain,
-                h->active.ptr, h->stress.ptr, h->partials.ptr, tix(h, 4), h->red.ptr + 5);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Pattern& P = pt.P;
+    launch_reaction(s, P.n_free, P.n_top, P.n_nodes, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr,
+                    pt.val.ptr, pt.diag.ptr, pt.G, pt.x.ptr, pt.partials.ptr, tix(pt, 3),
+                    pt.red.ptr + 4);
+    launch_stress(s, P.n_elems, pt.e2n_d.ptr, pt.xyz_d.ptr, pt.x.ptr, h->mat, max_strain,
+                  pt.active.ptr, pt.stress.ptr, pt.partials.ptr, tix(pt, 4), pt.red.ptr + 5,
+                  dm ? pt.elem_own.ptr : nullptr);
+  }
   HIPC(hipGetLastError());
-  HIPC(hipMemcpyAsync(h->h_red, h->red.ptr + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+  Part& p0 = part0(h);
+  if (dm) {  // (force, #active) of every partition, summed in rank order
+    RC(gather4(h, 4));
+    launch_rank_sum(s, p0.gred, nranks(h), p0.red.ptr + 12);
+    HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 12, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+  } else {
+    HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
   HIPC(hipEventRecord(h->ev[5], s));
-  HIPC(hipEventSynchronize(h->ev[5]));
-  if (P.n_top == 0) h->h_red[0] = 0.0;
-  if (P.n_elems == 0) h->h_red[1] = 0.0;
+  RC(wait_event(h, h->ev[5]));
+  if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
+  if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
@@ -499,6 +875,29 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[4], h->ev[5]);
     st->t_post_ms = ms;
+  }
+  return 0;
+}
+
+int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
+              mfea_stats* st) {
+  return partitioned(h) ? solve_dist(h, dy_top, dy_bot, o, st) : solve_impl(h, dy_top, dy_bot, o, st);
+}
+
+// current element activity in original order (elements no partition of this
+// process holds stay 1)
+int gather_active(mfea_handle* h, std::vector<uint8_t>& out) {
+  out.assign(h->Ecount, 1);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int64_t E = pt.P.n_elems;
+    std::vector<uint8_t> a(E);
+    if (E) HIPC(hipMemcpy(a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    if (!partitioned(h)) {
+      out = a;
+      return 0;
+    }
+    for (int64_t le = 0; le < E; ++le) out[pt.plan.elem_g[le]] = a[le];
   }
   return 0;
 }
@@ -532,6 +931,8 @@ int mfea_create(int device, mfea_handle** out) {
   HIPC(hipHostGetDevicePointer((void**)&h->d_host_state, h->h_state, 0));
   HIPC(hipHostMalloc(&h->h_red, 16 * sizeof(double), hipHostMallocDefault));
   std::memset(h->h_state, 0, 2 * sizeof(SolveState));
+  h->parts.push_back(std::make_unique<Part>());  // scratch of mfea_solve_csr until a mesh is set
+  h->parts[0]->mirror = h->d_host_state;
   // reference constants src/fea_solver.py:14-20
   const double d = 0.0002, t = 0.000001;
   const double A = 3.14 * (std::pow(d / 2, 2) - std::pow(d / 2 - t, 2));
@@ -545,6 +946,8 @@ int mfea_destroy(mfea_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   destroy_graph(h);
+  h->parts.clear();
+  if (h->comm) (void)ncclCommDestroy(h->comm);
   for (auto& ev : h->ev)
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : h->poll)
@@ -572,7 +975,7 @@ int mfea_set_mesh(mfea_handle* h, int64_t n_nodes, const double* xyz, int64_t n_
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
   if (n_nodes < 0 || n_elems < 0) return fail(MFEA_EINVAL, "negative size");
   if ((n_nodes && !xyz) || (n_elems && !e2n)) return fail(MFEA_EINVAL, "NULL mesh array");
-  if (int rc = set_device(h)) return rc;
+  RC(set_device(h));
   h->N = n_nodes;
   h->Ecount = n_elems;
   h->xyz.assign(xyz, xyz + 3 * n_nodes);
@@ -581,6 +984,9 @@ int mfea_set_mesh(mfea_handle* h, int64_t n_nodes, const double* xyz, int64_t n_
   h->has_mesh = true;
   h->dirty = true;
   h->active_host.clear();
+  h->planar = true;
+  for (int64_t n = 0; n < n_nodes; ++n)
+    if (xyz[3 * n + 2] != 0.0) h->planar = false;
   // validate now so errors surface at the call that caused them
   Pattern tmp;
   std::string err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(),
@@ -603,10 +1009,7 @@ int mfea_set_bc(mfea_handle* h, int64_t n_top, const int64_t* top, int64_t n_bot
   for (int64_t i = 0; i < n_bot; ++i)
     if (bot[i] < 0 || bot[i] >= h->N) return fail(MFEA_EINVAL, "bottom grip node out of range");
   // keep the current activity across the rebuild
-  if (!h->dirty && h->Ecount) {
-    h->active_host.resize(h->Ecount);
-    (void)hipMemcpy(h->active_host.data(), h->active.ptr, h->Ecount, hipMemcpyDeviceToHost);
-  }
+  if (!h->dirty && h->Ecount) RC(gather_active(h, h->active_host));
   h->top.assign(top, top + n_top);
   h->bot.assign(bot, bot + n_bot);
   h->dirty = true;
@@ -615,57 +1018,62 @@ int mfea_set_bc(mfea_handle* h, int64_t n_top, const int64_t* top, int64_t n_bot
 
 int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
+  RC(set_device(h));
+  RC(ensure_built(h));
   if (h->Ecount == 0) return 0;
-  if (active) {
-    std::vector<uint8_t> a(active, active + h->Ecount);
-    for (auto& v : a) v = v ? 1 : 0;
-    HIPC(hipMemcpy(h->active.ptr, a.data(), h->Ecount, hipMemcpyHostToDevice));
-  } else {
-    HIPC(hipMemset(h->active.ptr, 1, h->Ecount));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int64_t E = pt.P.n_elems;
+    if (!E) continue;
+    if (active) {
+      std::vector<uint8_t> a(E);
+      for (int64_t le = 0; le < E; ++le)
+        a[le] = active[partitioned(h) ? pt.plan.elem_g[le] : le] ? 1 : 0;
+      HIPC(hipMemcpy(pt.active.ptr, a.data(), E, hipMemcpyHostToDevice));
+    } else {
+      HIPC(hipMemset(pt.active.ptr, 1, E));
+    }
   }
   return 0;
 }
 
 int mfea_assemble(mfea_handle* h) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  if (int rc = assemble_impl(h, nullptr)) return rc;
-  HIPC(hipStreamSynchronize(h->stream));
-  return 0;
+  RC(set_device(h));
+  RC(ensure_built(h));
+  RC(assemble_impl(h, nullptr));
+  return sync_stream(h);
 }
 
 int mfea_solve(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
                mfea_stats* st) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
+  RC(set_device(h));
+  RC(ensure_built(h));
   mfea_solve_opts o = opts ? *opts : default_opts();
   if (st) std::memset(st, 0, sizeof(*st));
-  return solve_impl(h, dy_top, dy_bot, &o, st);
+  return solve_any(h, dy_top, dy_bot, &o, st);
 }
 
 int mfea_post(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
+  RC(set_device(h));
+  RC(ensure_built(h));
   return post_impl(h, max_strain, total_force, n_active, nullptr);
 }
 
 int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
               double max_strain, double* total_force, int64_t* n_active, mfea_stats* st) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
+  RC(set_device(h));
+  RC(ensure_built(h));
   mfea_solve_opts o = opts ? *opts : default_opts();
   if (st) std::memset(st, 0, sizeof(*st));
-  if (int rc = assemble_impl(h, nullptr)) return rc;
-  int rc = solve_impl(h, dy_top, dy_bot, &o, st);
-  if (rc && rc != MFEA_EMAXIT && rc != MFEA_EBREAKDOWN) return rc;
-  if (rc) return rc;  // the reference stops the step loop here (src/fea_petsc.cpp:346-354)
-  if (int rc2 = post_impl(h, max_strain, total_force, n_active, st)) return rc2;
+  RC(assemble_impl(h, nullptr));
+  // a solver failure stops the step loop here, as the reference does
+  // (src/fea_petsc.cpp:346-354)
+  RC(solve_any(h, dy_top, dy_bot, &o, st));
+  RC(post_impl(h, max_strain, total_force, n_active, st));
   if (st) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
@@ -676,37 +1084,69 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
 
 int mfea_get_displacement(mfea_handle* h, double* U) {
   if (!h || !U) return fail(MFEA_EINVAL, "NULL argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  const int64_t N = h->P.n_nodes;
-  std::vector<double> xp(3 * N);
-  if (N) HIPC(hipMemcpy(xp.data(), h->x.ptr, 3 * N * sizeof(double), hipMemcpyDeviceToHost));
-  for (int64_t i = 0; i < N; ++i)
-    for (int a = 0; a < 3; ++a) U[3 * (int64_t)h->P.perm[i] + a] = xp[3 * i + a];
+  RC(set_device(h));
+  RC(ensure_built(h));
+  const bool dm = partitioned(h);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Pattern& P = pt.P;
+    const int64_t N = P.n_nodes;
+    std::vector<double> xp(3 * N);
+    if (N) HIPC(hipMemcpy(xp.data(), pt.x.ptr, 3 * N * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < N; ++i) {
+      const int64_t ln = P.perm[i];
+      if (dm && pt.plan.ghost[ln]) continue;
+      const int64_t g = dm ? pt.plan.node_g[ln] : ln;
+      for (int a = 0; a < 3; ++a) U[3 * g + a] = xp[3 * i + a];
+    }
+  }
   return 0;
 }
 
 int mfea_get_stress(mfea_handle* h, double* stress) {
   if (!h || !stress) return fail(MFEA_EINVAL, "NULL argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  if (h->Ecount)
-    HIPC(hipMemcpy(stress, h->stress.ptr, h->Ecount * sizeof(double), hipMemcpyDeviceToHost));
+  RC(set_device(h));
+  RC(ensure_built(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int64_t E = pt.P.n_elems;
+    if (!E) continue;
+    if (!partitioned(h)) {
+      HIPC(hipMemcpy(stress, pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
+      continue;
+    }
+    std::vector<double> sl(E);
+    HIPC(hipMemcpy(sl.data(), pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t le = 0; le < E; ++le)
+      if (pt.plan.elem_own[le]) stress[pt.plan.elem_g[le]] = sl[le];
+  }
   return 0;
 }
 
 int mfea_get_active(mfea_handle* h, uint8_t* active) {
   if (!h || !active) return fail(MFEA_EINVAL, "NULL argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  if (h->Ecount) HIPC(hipMemcpy(active, h->active.ptr, h->Ecount, hipMemcpyDeviceToHost));
+  RC(set_device(h));
+  RC(ensure_built(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int64_t E = pt.P.n_elems;
+    if (!E) continue;
+    if (!partitioned(h)) {
+      HIPC(hipMemcpy(active, pt.active.ptr, E, hipMemcpyDeviceToHost));
+      continue;
+    }
+    std::vector<uint8_t> al(E);
+    HIPC(hipMemcpy(al.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    for (int64_t le = 0; le < E; ++le)
+      if (pt.plan.elem_own[le]) active[pt.plan.elem_g[le]] = al[le];
+  }
   return 0;
 }
 
 int mfea_element_stiffness(mfea_handle* h, int64_t n, const double* p1s, const double* p2s,
                            double E, double A, double I, double* Ke, double* L) {
   if (!h || n < 0 || (n && (!p1s || !p2s || !Ke || !L))) return fail(MFEA_EINVAL, "bad argument");
-  if (int rc = set_device(h)) return rc;
+  RC(set_device(h));
   if (n == 0) return 0;
   Material m;
   m.EA = E * A;
@@ -730,15 +1170,17 @@ int mfea_element_stiffness(mfea_handle* h, int64_t n, const double* p1s, const d
 int mfea_export_csr(mfea_handle* h, int64_t* nnz, int64_t* indptr, int32_t* indices,
                     double* data) {
   if (!h || !nnz) return fail(MFEA_EINVAL, "NULL argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  const Pattern& P = h->P;
+  RC(set_device(h));
+  RC(ensure_built(h));
+  if (partitioned(h)) return fail(MFEA_ESTATE, "mfea_export_csr: single-partition handles only");
+  Part& pt = part0(h);
+  const Pattern& P = pt.P;
   const int64_t N = P.n_nodes, E = P.n_elems;
-  std::vector<double> diag6(6 * N), val6(6 * h->G);
+  std::vector<double> diag6(6 * N), val6(6 * pt.G);
   std::vector<uint8_t> act(E);
-  if (N) HIPC(hipMemcpy(diag6.data(), h->diag.ptr, 6 * N * sizeof(double), hipMemcpyDeviceToHost));
-  if (h->G) HIPC(hipMemcpy(val6.data(), h->val.ptr, 6 * h->G * sizeof(double), hipMemcpyDeviceToHost));
-  if (E) HIPC(hipMemcpy(act.data(), h->active.ptr, E, hipMemcpyDeviceToHost));
+  if (N) HIPC(hipMemcpy(diag6.data(), pt.diag.ptr, 6 * N * sizeof(double), hipMemcpyDeviceToHost));
+  if (pt.G) HIPC(hipMemcpy(val6.data(), pt.val.ptr, 6 * pt.G * sizeof(double), hipMemcpyDeviceToHost));
+  if (E) HIPC(hipMemcpy(act.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
   std::vector<int64_t> ip;
   std::vector<int32_t> ix;
   std::vector<double> dv;
@@ -761,7 +1203,8 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
                    mfea_stats* st) {
   if (!h || n < 0 || (n && (!indptr || !U)) || n_known < 0 || (n_known && (!known_dofs || !known_vals)))
     return fail(MFEA_EINVAL, "bad argument");
-  if (int rc = set_device(h)) return rc;
+  RC(set_device(h));
+  if (h->world > 1) return fail(MFEA_ESTATE, "mfea_solve_csr: not on a partitioned (RCCL) handle");
   mfea_solve_opts o = opts ? *opts : default_opts();
   if (o.precond != MFEA_PC_JACOBI) return fail(MFEA_EINVAL, "CSR path supports Jacobi only");
   if (st) std::memset(st, 0, sizeof(*st));
@@ -778,6 +1221,7 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
     kval[k] = known_vals[i];
   }
   hipStream_t s = h->stream;
+  Part& pt = part0(h);  // its reduction scratch, slots and state
   HIPC(h->c_indptr.alloc(n + 1));
   HIPC(h->c_indices.alloc(nnz));
   HIPC(h->c_data.alloc(nnz));
@@ -789,12 +1233,17 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
   HIPC(h->c_q.alloc(n));
   HIPC(h->c_dinv.alloc(n));
   const int64_t maxg = std::max<int64_t>(grid_rows(n), 2048);
-  if (h->partials.n < (size_t)(4 * maxg)) HIPC(h->partials.alloc(4 * (maxg + 16)));
-  HIPC(h->red.alloc(16));
-  HIPC(h->tickets.alloc(kTicketSets * kTicketStride));
-  HIPC(h->slots.alloc(kMaxChunk + 2));
-  HIPC(h->state.alloc(1));
-  if (h->dirty) HIPC(hipMemsetAsync(h->tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
+  if (pt.partials.n < (size_t)(4 * maxg)) HIPC(pt.partials.alloc(4 * (maxg + 16)));
+  if (!pt.red.ptr) {
+    HIPC(pt.red.alloc(16));
+    HIPC(hipMemsetAsync(pt.red.ptr, 0, 16 * sizeof(double), s));
+  }
+  if (!pt.tickets.ptr) {
+    HIPC(pt.tickets.alloc(kTicketSets * kTicketStride));
+    HIPC(hipMemsetAsync(pt.tickets.ptr, 0, kTicketSets * kTicketStride * sizeof(unsigned), s));
+  }
+  HIPC(pt.slots.alloc(kMaxChunk + 2));
+  HIPC(pt.state.alloc(1));
   HIPC(hipMemcpyAsync(h->c_indptr.ptr, indptr, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   if (nnz) {
     HIPC(hipMemcpyAsync(h->c_indices.ptr, indices, nnz * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -806,9 +1255,9 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
   HIPC(hipEventRecord(h->ev[1], s));
   launch_csr_rhs_init(s, n, h->c_indptr.ptr, h->c_indices.ptr, h->c_data.ptr, h->c_known.ptr,
                       h->c_kval.ptr, o.reg, h->c_x.ptr, h->c_r.ptr, h->c_p.ptr, h->c_dinv.ptr,
-                      h->partials.ptr, tix(h, 5), h->red.ptr);
-  launch_init_finalize(s, h->red.ptr, o.rtol, o.atol, o.norm, o.max_it, o.reg, h->slots.ptr,
-                       h->state.ptr);
+                      pt.partials.ptr, tix(pt, 5), pt.red.ptr);
+  launch_init_finalize(s, pt.red.ptr, o.rtol, o.atol, o.norm, o.max_it, o.reg, pt.slots.ptr,
+                       pt.state.ptr);
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
   const int chunk = o.chunk > 0 ? std::min(o.chunk, kMaxChunk) : 32;
@@ -818,14 +1267,14 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
       [&]() -> int {
         for (int j = 0; j < chunk; ++j) {
           launch_spmv_csr(s, j, n, h->c_indptr.ptr, h->c_indices.ptr, h->c_data.ptr,
-                          h->c_known.ptr, o.reg, h->c_p.ptr, h->c_q.ptr, h->slots.ptr,
-                          h->state.ptr, h->partials.ptr, tix(h, 6));
+                          h->c_known.ptr, o.reg, h->c_p.ptr, h->c_q.ptr, pt.slots.ptr,
+                          pt.state.ptr, pt.partials.ptr, tix(pt, 6));
           launch_update(s, j, n, 0, h->c_x.ptr, h->c_r.ptr, h->c_p.ptr, h->c_q.ptr, h->c_dinv.ptr,
-                        h->slots.ptr, h->state.ptr, h->partials.ptr, tix(h, 7));
-          launch_direction(s, j, n, 0, h->c_r.ptr, h->c_p.ptr, h->c_dinv.ptr, h->slots.ptr,
-                           h->state.ptr);
+                        pt.slots.ptr, pt.state.ptr, pt.partials.ptr, tix(pt, 7));
+          launch_direction(s, j, n, 0, h->c_r.ptr, h->c_p.ptr, h->c_dinv.ptr, pt.slots.ptr,
+                           pt.state.ptr);
         }
-        launch_advance(s, chunk, h->slots.ptr, h->state.ptr);
+        launch_advance(s, chunk, pt.slots.ptr, pt.state.ptr);
         HIPC(hipGetLastError());
         return 0;
       },
@@ -851,9 +1300,10 @@ int mfea_solve_csr(mfea_handle* h, int64_t n, const int64_t* indptr, const int32
 
 int mfea_get_info(mfea_handle* h, mfea_info* info) {
   if (!h || !info) return fail(MFEA_EINVAL, "NULL argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
-  const Pattern& P = h->P;
+  RC(set_device(h));
+  RC(ensure_built(h));
+  Part& pt = part0(h);
+  const Pattern& P = pt.P;
   std::memset(info, 0, sizeof(*info));
   info->n_nodes = P.n_nodes;
   info->n_elems = P.n_elems;
@@ -861,34 +1311,41 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
   info->n_top = P.n_top;
   info->n_known = P.n_known;
   info->n_slices = P.n_slices();
-  info->n_slots = h->G;
+  info->n_slots = pt.G;
   int64_t inc = 0;
   for (int64_t i = 0; i < P.n_free; ++i) inc += P.row_len[i];
   info->free_incidences = inc;
-  info->planar = P.planar ? 1 : 0;
-  info->cg_lanes = use_ell(h) ? 1 : 0;
-  info->n_lanes = h->ell_ok ? h->L.n_lanes : 0;
+  info->planar = h->planar ? 1 : 0;
+  info->cg_lanes = use_ell(pt) ? 1 : 0;
+  info->n_lanes = pt.ell_ok ? pt.L.n_lanes : 0;
   int64_t halo = 0;
-  if (h->ell_ok)
-    for (int32_t pt : h->L.partner) halo += pt >= 0;
+  if (pt.ell_ok)
+    for (int32_t p : pt.L.partner) halo += p != -1;
   info->n_halo = halo;
+  info->n_parts = nranks(h);
+  info->part = pt.rank;
+  info->n_pairs = pt.plan.n_pairs;
+  info->n_ghost = P.n_ghost;
   return 0;
 }
 
-// iteration 0 of the active CG kernel (profiling / tracing)
+// iteration 0 of the active CG kernel of partition 0 (profiling / tracing;
+// partitioned handles: the per-GPU kernel without its exchange)
 static void launch_iter0(mfea_handle* h, int pc, unsigned long long* trace) {
-  if (use_ell(h))
-    launch_ell_iter(h->stream, 0, ell_op(h), pc, ell_vecs(h), h->slots.ptr, h->state.ptr,
-                    h->cg_part.ptr, trace);
+  Part& pt = part0(h);
+  if (use_ell(pt))
+    launch_ell_iter(h->stream, 0, ell_op(h, pt), pc, ell_vecs(pt), pt.slots.ptr, pt.state.ptr,
+                    pt.cg_part.ptr, trace);
   else
-    launch_cg_iter(h->stream, 0, sell_op(h), pc, cg_vecs(h), h->slots.ptr, h->state.ptr,
-                   h->cg_part.ptr, trace);
+    launch_cg_iter(h->stream, 0, sell_op(pt), pc, cg_vecs(pt), pt.slots.ptr, pt.state.ptr,
+                   pt.cg_part.ptr, trace);
 }
 
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms) {
   if (!h || !avg_ms || reps <= 0) return fail(MFEA_EINVAL, "bad argument");
-  if (int rc = set_device(h)) return rc;
-  if (int rc = ensure_built(h)) return rc;
+  RC(set_device(h));
+  RC(ensure_built(h));
+  Part& pt = part0(h);
   hipStream_t s = h->stream;
   const int pc = precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
   // Running state with tol 0: slots[0] = INIT and parity-0 partials of 1, so
@@ -896,15 +1353,15 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   // (same parity), so it reads the same buffers and does identical work
   // (including all stores); only x and p drift.
   const double ones[2] = {1.0, 1.0};
-  HIPC(hipMemcpyAsync(h->red.ptr + 8, ones, sizeof(ones), hipMemcpyHostToDevice, s));
-  launch_cg_init_finalize(s, h->red.ptr + 8, 0.0, 0.0, 0, 1 << 30, 1e-12, h->state.ptr);
+  HIPC(hipMemcpyAsync(pt.red.ptr + 8, ones, sizeof(ones), hipMemcpyHostToDevice, s));
+  launch_cg_init_finalize(s, pt.red.ptr + 8, 0.0, 0.0, 0, 1 << 30, 1e-12, pt.state.ptr);
   std::vector<double> pones(4 * kCgMaxPartials, 1.0);
-  HIPC(hipMemcpyAsync(h->cg_part.ptr, pones.data(), pones.size() * sizeof(double),
+  HIPC(hipMemcpyAsync(pt.cg_part.ptr, pones.data(), pones.size() * sizeof(double),
                       hipMemcpyHostToDevice, s));
   Slot s0;
   std::memset(&s0, 0, sizeof(s0));
   s0.flag = kInit;
-  HIPC(hipMemcpyAsync(h->slots.ptr, &s0, sizeof(s0), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(pt.slots.ptr, &s0, sizeof(s0), hipMemcpyHostToDevice, s));
   launch_iter0(h, pc, nullptr);  // warm
   HIPC(hipEventRecord(h->ev[0], s));
   for (int k = 0; k < reps; ++k) launch_iter0(h, pc, nullptr);
@@ -921,9 +1378,10 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
                                int64_t* n_waves) {
   if (!h || !out || !n_waves || cap < 0) return fail(MFEA_EINVAL, "bad argument");
   double ms = 0;
-  if (int rc = mfea_profile_iteration(h, precond, 20, &ms)) return rc;  // same running state
+  RC(mfea_profile_iteration(h, precond, 20, &ms));  // same running state
   hipStream_t s = h->stream;
-  const int64_t g = cg_grid(use_ell(h) ? h->L.n_lanes : h->P.n_free);
+  Part& pt = part0(h);
+  const int64_t g = cg_grid(use_ell(pt) ? pt.L.n_lanes : pt.P.n_free);
   const int64_t nw = g * (cg_block_size(0) / 64);
   if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
   unsigned long long* d = nullptr;
@@ -938,17 +1396,53 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   return 0;
 }
 
+int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis) {
+  if (!h) return fail(MFEA_EINVAL, "NULL handle");
+  if (nparts < 1 || nparts > kMaxRanks) return fail(MFEA_EINVAL, "nparts must be in [1, 64]");
+  if (axis < -1 || axis > 1) return fail(MFEA_EINVAL, "axis must be -1, 0 or 1");
+  if (h->world > 1 && nparts > 1) return fail(MFEA_ESTATE, "handle already joined an RCCL world");
+  h->nparts = nparts;
+  h->axis = axis;
+  h->dirty = true;
+  return 0;
+}
+
+int mfea_set_partition_axis(mfea_handle* h, int axis) {
+  if (!h) return fail(MFEA_EINVAL, "NULL handle");
+  if (axis < -1 || axis > 1) return fail(MFEA_EINVAL, "axis must be -1, 0 or 1");
+  h->axis = axis;
+  h->dirty = true;
+  return 0;
+}
+
 int mfea_dist_unique_id(uint8_t* unique_id) {
-  (void)unique_id;
-  return fail(MFEA_ESTATE, "multi-GPU path not built in this version");
+  if (!unique_id) return fail(MFEA_EINVAL, "NULL argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId u;
+  NCCLC(ncclGetUniqueId(&u));
+  std::memcpy(unique_id, &u, sizeof(u));
+  return 0;
 }
 
 int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id) {
-  (void)h;
-  (void)rank;
-  (void)world;
-  (void)unique_id;
-  return fail(MFEA_ESTATE, "multi-GPU path not built in this version");
+  if (!h || !unique_id) return fail(MFEA_EINVAL, "NULL argument");
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world)
+    return fail(MFEA_EINVAL, "bad rank / world size");
+  if (h->comm) return fail(MFEA_ESTATE, "handle already joined an RCCL world");
+  if (h->nparts > 1) return fail(MFEA_ESTATE, "handle holds several partitions");
+  RC(set_device(h));
+  if (const char* t = std::getenv("MFEA_DIST_TIMEOUT_S")) h->dist_timeout_s = std::atof(t);
+  if (world > 1) {
+    ncclUniqueId u;
+    std::memcpy(&u, unique_id, sizeof(u));
+    ncclComm_t c = nullptr;
+    NCCLC(ncclCommInitRank(&c, world, u, rank));
+    h->comm = c;
+  }
+  h->world = world;
+  h->rank = rank;
+  h->dirty = true;
+  return 0;
 }
 
 }  // extern "C"

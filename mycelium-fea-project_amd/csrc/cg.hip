@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_rhs(SellOp op, const uint8_t* __r
     for (int k = 0; k < len; ++k) {
       const int64_t idx = base + (int64_t)k * 64;
       const int32_t j = op.s_col[idx];
-      if (j >= op.nf) {
+      if (j >= op.nf && code[j] != 3) {  // a known neighbour (3 = ghost free row: x₀ = 0)
         const double dy = code[j] == 2 ? dy_bot : dy_top;
         kx = fma(op.val[1 * G + idx], dy, kx);
         ky = fma(op.val[3 * G + idx], dy, ky);
@@ -120,7 +120,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_rhs(SellOp op, const uint8_t* __r
       acc[1] = fma(u[a], u[a], acc[1]);
     }
   } else if (row < op.N) {
-    const double xk[3] = {0.0, code[row] == 2 ? dy_bot : dy_top, 0.0};
+    // ghost free rows (3) hold 0 until the solve's displacement halo fills them
+    const double xk[3] = {0.0, code[row] == 3 ? 0.0 : (code[row] == 2 ? dy_bot : dy_top), 0.0};
     store3(v.x, row, xk);
     store3(v.p, row, zero);
     for (int b = 0; b < 2; ++b) {

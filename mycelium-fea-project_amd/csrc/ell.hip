@@ -89,6 +89,20 @@ __device__ __forceinline__ int wave_max_i(int m) {
 // wave execute in order; the wait keeps the compiler from reordering too)
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Multi-partition: every lane of every wave ends with the total of the gathered
+// per-rank partial sums, summed in one fixed order (DPP tree over the rank
+// rows) — identical on every rank, since the gathered rows are bitwise copies.
+__device__ __forceinline__ void wave_gall(const double* __restrict__ g, double s[4]) {
+  const int lane = threadIdx.x & 63;
+  double t[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t[c] = g[lane * 4 + c];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s[c] = wave_allsum(t[c]);
+}
+
+__device__ __forceinline__ int64_t pair_of(int32_t partner) { return -2 - (int64_t)partner; }
+
 // ---------------------------------------------------------------------------
 // Lane operator values and initial vectors (once per solve).
 // ---------------------------------------------------------------------------
@@ -131,19 +145,57 @@ __global__ __launch_bounds__(kCgBS) void k_ell_init(EllOp op, SellOp sop, CgVecs
 }
 
 // ---------------------------------------------------------------------------
+// Multi-partition, before w₀ = A u₀: each remote-halo lane sends its owner's
+// [r₀ | M] (helpers take them from the owner lane) into its pair's slot of
+// the parity-1 send records.
+// ---------------------------------------------------------------------------
+template <int ND, bool BLOCK>
+__global__ __launch_bounds__(kCgBS) void k_ell_pack0(EllOp op, EllVecs v, DistVecs dv) {
+  constexpr int NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
+  const int64_t NL = op.NL;
+  const int lane = threadIdx.x & 63;
+  for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l - lane < NL;
+       l += (int64_t)gridDim.x * kCgBS) {
+    double r[ND], M[NM];
+    lload<ND>(v.r[0], NL, l, r);
+#pragma unroll
+    for (int c = 0; c < NM; ++c) M[c] = v.M[c * NL + l];
+    const int info = group_info(op.code[l]);
+    const int ow = info < 0 ? lane + info : lane;
+    double ro[ND], Mo[NM];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) ro[a] = __shfl(r[a], ow, 64);
+#pragma unroll
+    for (int c = 0; c < NM; ++c) Mo[c] = __shfl(M[c], ow, 64);
+    const int32_t pt = op.partner[l];
+    if (pt <= -2) {
+      double* rec = dv.xs[1] + pair_of(pt) * RW;
+#pragma unroll
+      for (int a = 0; a < ND; ++a) rec[a] = ro[a];
+#pragma unroll
+      for (int c = 0; c < NM; ++c) rec[ND + c] = Mo[c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // w₀ = A u₀ with the neighbours pulled through nbr_lane (the only gather of
 // the solve), halo records of parity 0 (r₀, s₀ = 0, w₀ and M), partials
 // (γ₀, δ₀, ‖r₀‖², ‖u₀‖²) → parity 0, slots[0] = INIT.
+// DIST: a remote slot-0 neighbour's [r₀ | M] comes from the received parity-1
+// records (its M is kept in dv.mr for the iterations), and the lane's own
+// parity-0 record goes to its pair's send slot.
 // ---------------------------------------------------------------------------
-template <int ND, bool BLOCK>
+template <int ND, bool BLOCK, bool DIST>
 __global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
-                                                     double* part) {
-  constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>();
+                                                     double* part, DistVecs dv) {
+  constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
   const int64_t NL = op.NL;
   const int lane = threadIdx.x & 63;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l - lane < NL;
        l += (int64_t)gridDim.x * kCgBS) {
+    const int32_t pt = op.partner[l];
     double r[ND], M[NM], u[ND], D[NB];
     lload<ND>(v.r[0], NL, l, r);
 #pragma unroll
@@ -160,11 +212,23 @@ __global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVe
     bmac<ND>(D, u, y);
     for (int k = 0; k < 3; ++k) {
       const int32_t nl = op.nbr_lane[k * NL + l];
-      if (nl < 0) continue;
       double rc[ND], Mc[NM], uc[ND], V[NB];
-      lload<ND>(v.r[0], NL, nl, rc);
+      if (nl >= 0) {
+        lload<ND>(v.r[0], NL, nl, rc);
 #pragma unroll
-      for (int c = 0; c < NM; ++c) Mc[c] = v.M[c * NL + nl];
+        for (int c = 0; c < NM; ++c) Mc[c] = v.M[c * NL + nl];
+      } else if (DIST && k == 0 && pt <= -2) {
+        const double* rec = dv.xr[1] + pair_of(pt) * RW;
+#pragma unroll
+        for (int a = 0; a < ND; ++a) rc[a] = rec[a];
+#pragma unroll
+        for (int c = 0; c < NM; ++c) {
+          Mc[c] = rec[ND + c];
+          dv.mr[pair_of(pt) * NM + c] = Mc[c];
+        }
+      } else {
+        continue;
+      }
       mapply<ND, BLOCK>(Mc, rc, uc);
 #pragma unroll
       for (int c = 0; c < NB; ++c) V[c] = op.V[(c * 3 + k) * NL + l];
@@ -192,7 +256,6 @@ __global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVe
     }
 #pragma unroll
     for (int c = 0; c < NM; ++c) Mo[c] = __shfl(M[c], ow, 64);
-    const int32_t pt = op.partner[l];
     if (pt >= 0) {
       double* h = v.h[0];
 #pragma unroll
@@ -203,6 +266,14 @@ __global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVe
       }
 #pragma unroll
       for (int c = 0; c < NM; ++c) v.hM[c * NL + pt] = Mo[c];
+    } else if (DIST && pt <= -2) {
+      double* rec = dv.xs[0] + pair_of(pt) * RW;
+#pragma unroll
+      for (int c = 0; c < ND; ++c) {
+        rec[c] = ro[c];
+        rec[ND + c] = 0.0;
+        rec[2 * ND + c] = yo[c];
+      }
     }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {  // helper lanes: r = u = 0
@@ -272,11 +343,16 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
   for (int c = 0; c < NM; ++c) in.hM[c] = v.hM[c * NL + l];
 }
 
-template <int ND, bool BLOCK, int PU, bool TRACE = false>
+// DIST (multi-partition): α, β come from the gathered rank partial sums; a
+// remote slot-0 neighbour's record is read from the received records of its
+// pair (an index-dependent load: only waves holding such lanes pay a second
+// round trip), and the lane's record for the peer goes to the send slot.
+template <int ND, bool BLOCK, int PU, bool TRACE = false, bool DIST = false>
 __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, Slot* slots,
                                                     const SolveState* st, double* part,
-                                                    unsigned long long* trace) {
+                                                    unsigned long long* trace, DistVecs dv) {
   constexpr int NB = Dof<ND>::NB, LW = Dof<ND>::LDSW;
+  constexpr int NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
   constexpr int NW = kCgBS / 64;
   __shared__ double lds_u[NW][64][LW];       // fresh u of every lane
   __shared__ double lds_y[NW][64][LW];       // helper partials of A u
@@ -299,7 +375,10 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
   const double tol2 = st->tol2, reg = st->reg;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
-  wave_partials<PU>(part_buf(part, par), S);
+  if (DIST)
+    wave_gall(dv.gall[par], S);
+  else
+    wave_partials<PU>(part_buf(part, par), S);
   trace_point<TRACE>(trace, 1, S[0]);
 
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
@@ -311,6 +390,14 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
   double ylast = 0.0;
   for (bool first = true; l - lane < NL; l += stride, first = false) {  // wave-uniform
     if (!first) load_lane<ND, BLOCK>(l, par, op, v, in);
+    if (DIST && in.partner <= -2) {
+      const int64_t k = pair_of(in.partner);
+      const double* __restrict__ rec = dv.xr[par] + k * RW;
+#pragma unroll
+      for (int q = 0; q < RW; ++q) in.h[q] = rec[q];
+#pragma unroll
+      for (int c = 0; c < NM; ++c) in.hM[c] = dv.mr[k * NM + c];
+    }
     const int info = group_info(in.code);
     const bool owner = info >= 0;
     double uo[ND], rn[ND], un[ND], sn[ND], pp[ND], xx[ND];
@@ -399,7 +486,7 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
       rsy[ND + a] = sn[a];
       rsy[2 * ND + a] = y[a];
     }
-    if (__ballot(in.partner >= 0 && !owner)) {
+    if (__ballot(in.partner != -1 && !owner)) {
 #pragma unroll
       for (int c = 0; c < 3 * ND; ++c) lds_b[wv][lane][c] = rsy[c];
       lds_fence();
@@ -413,6 +500,11 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
       for (int q = 0; q < 3; ++q)
 #pragma unroll
         for (int c = 0; c < ND; ++c) h_new[(q * 3 + c) * NL + pt] = rsy[q * ND + c];
+    }
+    if (DIST && go && in.partner <= -2) {
+      double* __restrict__ rec = dv.xs[par ^ 1] + pair_of(in.partner) * RW;
+#pragma unroll
+      for (int q = 0; q < RW; ++q) rec[q] = rsy[q];
     }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {  // helper lanes contribute exact zeros
@@ -447,6 +539,52 @@ __global__ __launch_bounds__(kCgBS) void k_ell_finish(EllOp op, EllVecs v, doubl
 }
 
 // ---------------------------------------------------------------------------
+// Multi-partition helpers (one wave / tiny grids; off the per-lane path).
+// ---------------------------------------------------------------------------
+template <int PU>
+__global__ __launch_bounds__(64) void k_psum(const double* __restrict__ p, double* row,
+                                             double* gsend) {
+  double S[4];
+  wave_partials<PU>(p, S);  // block order, the order wave_partials uses single-GPU
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      row[c] = S[c];
+      gsend[c] = S[c];
+    }
+  }
+}
+
+__global__ void k_rank_sum(const double* __restrict__ g, int world, double* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int c = 0; c < 4; ++c) {
+    double s = 0.0;
+    for (int r = 0; r < world; ++r) s += g[4 * r + c];
+    out[c] = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rows_pack(const int32_t* __restrict__ rows, int64_t n,
+                                                      const double* __restrict__ x,
+                                                      double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[3 * i + c] = x[3 * r + c];
+}
+
+__global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restrict__ rows, int64_t n,
+                                                        const double* __restrict__ in,
+                                                        double* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) x[3 * r + c] = in[3 * i + c];
+}
+
+// ---------------------------------------------------------------------------
 static dim3 ell_grid(const EllOp& op) { return dim3((unsigned)cg_grid(op.NL)); }
 static dim3 ell_grid_ew(const EllOp& op) { return dim3((unsigned)grid_rows(op.NL > 0 ? op.NL : 1)); }
 
@@ -464,53 +602,101 @@ void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int prec
   else init_nd<3>(s, op, sop, precond, rv, v);
 }
 
-template <int ND>
+template <int ND, bool DIST>
 static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
-                     Slot* slots, double* part) {
+                     Slot* slots, double* part, const DistVecs& dv) {
   if (precond == 1)
-    hipLaunchKernelGGL((k_ell_first<ND, true>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v, slots,
-                       part);
+    hipLaunchKernelGGL((k_ell_first<ND, true, DIST>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v,
+                       slots, part, dv);
   else
-    hipLaunchKernelGGL((k_ell_first<ND, false>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v, slots,
-                       part);
+    hipLaunchKernelGGL((k_ell_first<ND, false, DIST>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v,
+                       slots, part, dv);
 }
 void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
-                      Slot* slots, double* part) {
-  if (op.nd == 2) first_nd<2>(s, op, reg, precond, v, slots, part);
-  else first_nd<3>(s, op, reg, precond, v, slots, part);
+                      Slot* slots, double* part, const DistVecs* dv) {
+  const DistVecs d = dv ? *dv : DistVecs{};
+  if (op.nd == 2) {
+    if (dv) first_nd<2, true>(s, op, reg, precond, v, slots, part, d);
+    else first_nd<2, false>(s, op, reg, precond, v, slots, part, d);
+  } else {
+    if (dv) first_nd<3, true>(s, op, reg, precond, v, slots, part, d);
+    else first_nd<3, false>(s, op, reg, precond, v, slots, part, d);
+  }
 }
 
-template <int ND, int PU, bool TRACE>
+template <int ND>
+static void pack0_nd(hipStream_t s, const EllOp& op, int precond, const EllVecs& v,
+                     const DistVecs& dv) {
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_pack0<ND, true>), ell_grid(op), dim3(kCgBS), 0, s, op, v, dv);
+  else
+    hipLaunchKernelGGL((k_ell_pack0<ND, false>), ell_grid(op), dim3(kCgBS), 0, s, op, v, dv);
+}
+void launch_ell_pack0(hipStream_t s, const EllOp& op, int precond, const EllVecs& v,
+                      const DistVecs& dv) {
+  if (op.nd == 2) pack0_nd<2>(s, op, precond, v, dv);
+  else pack0_nd<3>(s, op, precond, v, dv);
+}
+
+template <int ND, int PU, bool TRACE, bool DIST>
 static void iter_launch(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                         Slot* slots, const SolveState* st, double* part,
-                        unsigned long long* trace) {
+                        unsigned long long* trace, const DistVecs& dv) {
   if (precond == 1)
-    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE>), ell_grid(op), dim3(kCgBS), 0, s, j, op,
-                       v, slots, st, part, trace);
+    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST>), ell_grid(op), dim3(kCgBS), 0, s, j,
+                       op, v, slots, st, part, trace, dv);
   else
-    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE>), ell_grid(op), dim3(kCgBS), 0, s, j, op,
-                       v, slots, st, part, trace);
+    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE, DIST>), ell_grid(op), dim3(kCgBS), 0, s, j,
+                       op, v, slots, st, part, trace, dv);
 }
 
 template <int ND, bool TRACE>
 static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
-                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
+                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
+                    const DistVecs& dv) {
   const int64_t g = cg_grid(op.NL);
-  if (g <= 64) iter_launch<ND, 1, TRACE>(s, j, op, precond, v, slots, st, part, trace);
-  else if (g <= 128) iter_launch<ND, 2, TRACE>(s, j, op, precond, v, slots, st, part, trace);
-  else if (g <= 256) iter_launch<ND, 4, TRACE>(s, j, op, precond, v, slots, st, part, trace);
-  else iter_launch<ND, 8, TRACE>(s, j, op, precond, v, slots, st, part, trace);
+  if (g <= 64) iter_launch<ND, 1, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
+  else if (g <= 128) iter_launch<ND, 2, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
+  else if (g <= 256) iter_launch<ND, 4, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
+  else iter_launch<ND, 8, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
 }
 
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
-                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace) {
-  if (op.nd == 2) {
-    if (trace) iter_pu<2, true>(s, j, op, precond, v, slots, st, part, trace);
-    else iter_pu<2, false>(s, j, op, precond, v, slots, st, part, nullptr);
-  } else {
-    if (trace) iter_pu<3, true>(s, j, op, precond, v, slots, st, part, trace);
-    else iter_pu<3, false>(s, j, op, precond, v, slots, st, part, nullptr);
+                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
+                     const DistVecs* dv) {
+  if (dv) {  // the rank partial sums replace the block partials: PU unused
+    if (op.nd == 2) iter_launch<2, 1, false, true>(s, j, op, precond, v, slots, st, part, nullptr, *dv);
+    else iter_launch<3, 1, false, true>(s, j, op, precond, v, slots, st, part, nullptr, *dv);
+    return;
   }
+  const DistVecs d{};
+  if (op.nd == 2) {
+    if (trace) iter_pu<2, true>(s, j, op, precond, v, slots, st, part, trace, d);
+    else iter_pu<2, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
+  } else {
+    if (trace) iter_pu<3, true>(s, j, op, precond, v, slots, st, part, trace, d);
+    else iter_pu<3, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
+  }
+}
+
+void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend) {
+  const int64_t g = cg_grid(NL);
+  if (g <= 64) hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend);
+  else if (g <= 128) hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend);
+  else if (g <= 256) hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend);
+  else hipLaunchKernelGGL(k_psum<8>, dim3(1), dim3(64), 0, s, p, row, gsend);
+}
+
+void launch_rank_sum(hipStream_t s, const double* g, int world, double* out) {
+  hipLaunchKernelGGL(k_rank_sum, dim3(1), dim3(64), 0, s, g, world, out);
+}
+
+void launch_rows_pack(hipStream_t s, const int32_t* rows, int64_t n, const double* x, double* out) {
+  if (n > 0) hipLaunchKernelGGL(k_rows_pack, dim3((unsigned)grid_rows(n)), dim3(kBlock), 0, s, rows, n, x, out);
+}
+
+void launch_rows_unpack(hipStream_t s, const int32_t* rows, int64_t n, const double* in, double* x) {
+  if (n > 0) hipLaunchKernelGGL(k_rows_unpack, dim3((unsigned)grid_rows(n)), dim3(kBlock), 0, s, rows, n, in, x);
 }
 
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row) {

@@ -387,7 +387,8 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
                                                    const double* __restrict__ u, Material m,
                                                    double max_strain, uint8_t* __restrict__ active,
                                                    double* __restrict__ stress, double* partials,
-                                                   unsigned* ticket, double* red_out) {
+                                                   unsigned* ticket, double* red_out,
+                                                   const uint8_t* __restrict__ owned) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cnt[1] = {0.0};
   if (e < E) {
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
       active[e] = act;
     }
     stress[e] = sg;
-    cnt[0] = act ? 1.0 : 0.0;
+    cnt[0] = (act && (!owned || owned[e])) ? 1.0 : 0.0;
   }
   block_publish<1>(cnt, partials, ticket, red_out);
 }
@@ -560,9 +561,10 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
 
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
-                   double* stress, double* partials, unsigned* ticket, double* red_out) {
+                   double* stress, double* partials, unsigned* ticket, double* red_out,
+                   const uint8_t* owned) {
   hipLaunchKernelGGL(k_stress, MFEA_GRID(grid_rows(E > 0 ? E : 1)), E, e2n, xyz, u, m, max_strain,
-                     active, stress, partials, ticket, red_out);
+                     active, stress, partials, ticket, red_out, owned);
 }
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,

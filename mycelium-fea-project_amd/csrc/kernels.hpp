@@ -109,9 +109,11 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
                      const double* val, const double* diag, int64_t G, const double* u,
                      double* partials, unsigned* ticket, double* red_out);
 
+// owned (multi-partition): count only elements this partition reports; NULL = all
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
-                   double* stress, double* partials, unsigned* ticket, double* red_out);
+                   double* stress, double* partials, unsigned* ticket, double* red_out,
+                   const uint8_t* owned = nullptr);
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,
                               Material m, double* Ke, double* L);
@@ -174,17 +176,43 @@ struct EllVecs {  // component c of a lane vector at [c·NL + lane], c < nd
   double* h[2];   // [9][NL] halo records by parity: r, s, w of the slot-0 neighbour at (q·3+c)·NL
   double* hM;     // [3|6][NL] halo record of the slot-0 neighbour's M
 };
+// ---- multi-partition CG (partition.hpp; one partition per GPU) -------------
+// Cross-partition halo records, pair k (partition.hpp) at rec[k·RW + q·nd + c]
+// with RW = 3·nd (q = 0 r, 1 s, 2 w).  The exchange before w₀ = A u₀ carries
+// [r₀ | M] in the parity-1 slots.  Rank partial sums: gall[par] = [64][4]
+// (row = rank, rows >= world stay 0), summed by every wave in a fixed order,
+// so every rank derives bitwise the same α, β and stopping decision.
+struct DistVecs {
+  double* xs[2];    // [NX][RW] records this partition sends, by parity
+  double* xr[2];    // [NX][RW] records received from the peers
+  double* mr;       // [NX][NM] the peers' M (kept from the first exchange)
+  double* gall[2];  // [64][4] partial sums of every rank, by parity
+  double* gsend;    // [4] this partition's partial sums
+};
+constexpr int kMaxRanks = 64;
+
 // values and lane vectors from the SELL operator and k_cg_rhs's row-order b, M⁻¹
 void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int precond,
                      const CgVecs& rv, const EllVecs& v);
+// multi-partition: [r₀ | M] of each remote-halo lane's owner → xs[1]
+void launch_ell_pack0(hipStream_t s, const EllOp& op, int precond, const EllVecs& v,
+                      const DistVecs& dv);
 // w₀ = A u₀ (neighbours pulled once), halo records of parity 0, partials, slots[0] = INIT
 void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
-                      Slot* slots, double* part);
+                      Slot* slots, double* part, const DistVecs* dv = nullptr);
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                      Slot* slots, const SolveState* st, double* part,
-                     unsigned long long* trace = nullptr);
+                     unsigned long long* trace = nullptr, const DistVecs* dv = nullptr);
 // x of the owner lanes → row-order x (free rows)
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
+// this partition's block partials of the iteration (parity buffer `p`, the
+// iteration kernel's grid for NL lanes) → row[0..3] and gsend[0..3]
+void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend);
+// out[c] = Σ_{r < world} g[4r + c] in rank order
+void launch_rank_sum(hipStream_t s, const double* g, int world, double* out);
+// out[3i + c] = x[3 rows[i] + c] / x[3 rows[i] + c] = in[3i + c]
+void launch_rows_pack(hipStream_t s, const int32_t* rows, int64_t n, const double* x, double* out);
+void launch_rows_unpack(hipStream_t s, const int32_t* rows, int64_t n, const double* in, double* x);
 
 int64_t grid_rows(int64_t rows);
 int64_t grid_elementwise(int64_t n);

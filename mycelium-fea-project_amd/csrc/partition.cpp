@@ -1,0 +1,165 @@
+// partition.cpp — see partition.hpp.  Pure host C++ (no HIP), unit-tested on CPU.
+#include "partition.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <utility>
+
+namespace mfea {
+
+std::vector<int32_t> node_owner(int64_t N, const double* xyz, const std::vector<int64_t>& top,
+                                const std::vector<int64_t>& bot, int world, int axis,
+                                int* axis_used) {
+  std::vector<uint8_t> known(N, 0);
+  for (int64_t t : top) known[t] = 1;
+  for (int64_t b : bot) known[b] = 1;
+  if (axis < 0) {
+    double lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+    for (int64_t n = 0; n < N; ++n)
+      for (int c = 0; c < 2; ++c) {
+        lo[c] = std::min(lo[c], xyz[3 * n + c]);
+        hi[c] = std::max(hi[c], xyz[3 * n + c]);
+      }
+    axis = (N > 0 && hi[1] - lo[1] > hi[0] - lo[0]) ? 1 : 0;
+  }
+  if (axis_used) *axis_used = axis;
+  std::vector<int64_t> ord(N);
+  std::iota(ord.begin(), ord.end(), (int64_t)0);
+  std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+    const double xa = xyz[3 * a + axis], xb = xyz[3 * b + axis];
+    return xa < xb || (xa == xb && a < b);
+  });
+  int64_t nfree = 0;
+  for (int64_t n = 0; n < N; ++n) nfree += !known[n];
+  // the k-th free node along the axis goes to rank ⌊k·world / nfree⌋; a known
+  // node joins the strip of the free nodes around it
+  std::vector<int32_t> own(N, 0);
+  int64_t seen = 0;
+  for (int64_t q = 0; q < N; ++q) {
+    const int64_t n = ord[q];
+    const int64_t r = nfree ? seen * world / nfree : 0;
+    own[n] = (int32_t)std::min<int64_t>(r, world - 1);
+    seen += !known[n];
+  }
+  return own;
+}
+
+std::string build_partition(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
+                            bool skip_invalid, const std::vector<int64_t>& top,
+                            const std::vector<int64_t>& bot, int world, int rank, int axis,
+                            PartPlan& plan) {
+  if (world < 1 || rank < 0 || rank >= world) return "bad rank / world size";
+  if (N < 0 || E < 0) return "negative mesh size";
+  if (N > INT32_MAX / 4 || E > INT32_MAX / 4) return "mesh too large for int32 indexing";
+  for (int64_t t : top)
+    if (t < 0 || t >= N) return "top grip node out of range";
+  for (int64_t b : bot)
+    if (b < 0 || b >= N) return "bottom grip node out of range";
+  plan = PartPlan();
+  plan.world = world;
+  plan.rank = rank;
+  const std::vector<int32_t> own = node_owner(N, xyz, top, bot, world, axis, &plan.axis);
+  std::vector<uint8_t> known(N, 0);
+  for (int64_t t : top) known[t] = 1;
+  for (int64_t b : bot) known[b] = 1;
+
+  // ---- local mesh: owned nodes, elements with an owned endpoint, their far ends
+  std::vector<uint8_t> valid(E, 1), local_e(E, 0), local_n(N, 0);
+  for (int64_t n = 0; n < N; ++n) local_n[n] = own[n] == rank;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
+    if (a < 0 || a >= N || b < 0 || b >= N) {
+      if (!skip_invalid)
+        return "element " + std::to_string(e) + " references node out of range [0," +
+               std::to_string(N) + ")";
+      valid[e] = 0;
+      continue;
+    }
+    if (own[a] == rank || own[b] == rank) {
+      local_e[e] = 1;
+      local_n[a] = local_n[b] = 1;
+    }
+  }
+  std::vector<int64_t> g2l(N, -1);
+  for (int64_t n = 0; n < N; ++n) {
+    if (!local_n[n]) continue;
+    g2l[n] = (int64_t)plan.node_g.size();
+    plan.node_g.push_back(n);
+    plan.ghost.push_back(own[n] != rank);
+    for (int c = 0; c < 3; ++c) plan.xyz.push_back(xyz[3 * n + c]);
+  }
+  for (int64_t e = 0; e < E; ++e) {
+    if (!local_e[e]) continue;
+    const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
+    plan.elem_g.push_back(e);
+    plan.e2n.push_back(g2l[a]);
+    plan.e2n.push_back(g2l[b]);
+    plan.elem_own.push_back(own[a] == rank);
+  }
+  for (int64_t t : top)
+    if (local_n[t]) plan.top.push_back(g2l[t]);
+  for (int64_t b : bot)
+    if (local_n[b]) plan.bot.push_back(g2l[b]);
+
+  // ---- CG record pairs: cut elements between two free nodes, (peer, element) order
+  const int64_t EL = (int64_t)plan.elem_g.size();
+  plan.elem_pair.assign(EL, -1);
+  std::vector<std::pair<int32_t, int64_t>> pr;  // (peer, local element)
+  for (int64_t le = 0; le < EL; ++le) {
+    const int64_t e = plan.elem_g[le];
+    const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
+    if (a == b || known[a] || known[b] || own[a] == own[b]) continue;
+    pr.emplace_back(own[a] == rank ? own[b] : own[a], le);
+  }
+  // local elements are in ascending global id: a stable sort by peer keeps that order
+  std::stable_sort(pr.begin(), pr.end(),
+                   [](const auto& x, const auto& y) { return x.first < y.first; });
+  for (size_t k = 0; k < pr.size(); ++k) {
+    plan.elem_pair[pr[k].second] = (int32_t)k;
+    if (plan.peers.empty() || plan.peers.back() != pr[k].first) {
+      plan.peers.push_back(pr[k].first);
+      plan.peer_off.push_back((int64_t)k);
+      plan.peer_cnt.push_back(0);
+    }
+    plan.peer_cnt.back()++;
+  }
+  plan.n_pairs = (int64_t)pr.size();
+
+  // ---- displacement halo: A sends B its free nodes adjacent to B's nodes; B
+  // receives exactly those as its ghost free nodes.  Both sorted by node id.
+  std::vector<std::pair<int32_t, int64_t>> snd, rcv;  // (peer, global node)
+  for (int64_t e = 0; e < E; ++e) {
+    if (!valid[e]) continue;
+    const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
+    if (a == b || own[a] == own[b]) continue;
+    for (int s = 0; s < 2; ++s) {
+      const int64_t m = s ? b : a, o = s ? a : b;
+      if (known[m]) continue;
+      if (own[m] == rank) snd.emplace_back(own[o], m);
+      if (own[o] == rank) rcv.emplace_back(own[m], m);
+    }
+  }
+  for (auto* v : {&snd, &rcv}) {
+    std::sort(v->begin(), v->end());
+    v->erase(std::unique(v->begin(), v->end()), v->end());
+  }
+  std::vector<int32_t> xp;
+  for (const auto& s : snd) xp.push_back(s.first);
+  for (const auto& r : rcv) xp.push_back(r.first);
+  std::sort(xp.begin(), xp.end());
+  xp.erase(std::unique(xp.begin(), xp.end()), xp.end());
+  plan.xpeers = xp;
+  size_t is = 0, ir = 0;
+  for (int32_t p : xp) {
+    plan.xsend_off.push_back((int64_t)plan.xsend_node.size());
+    for (; is < snd.size() && snd[is].first == p; ++is) plan.xsend_node.push_back(g2l[snd[is].second]);
+    plan.xsend_cnt.push_back((int64_t)plan.xsend_node.size() - plan.xsend_off.back());
+    plan.xrecv_off.push_back((int64_t)plan.xrecv_node.size());
+    for (; ir < rcv.size() && rcv[ir].first == p; ++ir) plan.xrecv_node.push_back(g2l[rcv[ir].second]);
+    plan.xrecv_cnt.push_back((int64_t)plan.xrecv_node.size() - plan.xrecv_off.back());
+  }
+  return "";
+}
+
+}  // namespace mfea

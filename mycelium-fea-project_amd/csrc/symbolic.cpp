@@ -9,8 +9,11 @@ namespace mfea {
 
 std::string build_pattern(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
                           bool skip_invalid, const std::vector<int64_t>& top,
-                          const std::vector<int64_t>& bot, int sort_window, Pattern& P) {
+                          const std::vector<int64_t>& bot, int sort_window, Pattern& P,
+                          const std::vector<uint8_t>* ghost) {
   if (N < 0 || E < 0) return "negative mesh size";
+  if (ghost && (int64_t)ghost->size() != N) return "internal: ghost mask size mismatch";
+  const auto is_ghost = [&](int64_t n) { return ghost && (*ghost)[n]; };
   if (N > INT32_MAX / 4 || E > INT32_MAX / 4) return "mesh too large for int32 indexing";
   P = Pattern();
   P.n_nodes = N;
@@ -36,7 +39,8 @@ std::string build_pattern(int64_t N, const double* xyz, int64_t E, const int64_t
     if (b < 0 || b >= N) return "bottom grip node out of range";
     in_bot[b] = 1;
   }
-  for (int64_t n = 0; n < N; ++n) code_orig[n] = in_bot[n] ? kBot : (in_top[n] ? kTop : kFree);
+  for (int64_t n = 0; n < N; ++n)
+    code_orig[n] = in_bot[n] ? kBot : (in_top[n] ? kTop : (is_ghost(n) ? kGhost : kFree));
 
   // ---- degree (incident elements, self-loops excluded: they add exactly 0)
   std::vector<int32_t> deg(N, 0);
@@ -108,15 +112,20 @@ std::string build_pattern(int64_t N, const double* xyz, int64_t E, const int64_t
   P.n_free = (int64_t)free_nodes.size();
   std::vector<uint8_t> placed(N, 0);
   for (int64_t t : top)
-    if (!placed[t]) {
+    if (!placed[t] && !is_ghost(t)) {
       placed[t] = 1;
       P.perm.push_back((int32_t)t);
     }
   P.n_top = (int64_t)P.perm.size() - P.n_free;
   for (int64_t b : bot)
-    if (!placed[b] && code_orig[b] != kFree) {
+    if (!placed[b] && code_orig[b] != kFree && !is_ghost(b)) {
       placed[b] = 1;
       P.perm.push_back((int32_t)b);
+    }
+  for (int64_t n = 0; n < N; ++n)
+    if (is_ghost(n)) {
+      P.perm.push_back((int32_t)n);
+      P.n_ghost++;
     }
   P.n_known = N - P.n_free;
   if ((int64_t)P.perm.size() != N) return "internal: permutation size mismatch";
@@ -180,26 +189,34 @@ std::string build_pattern(int64_t N, const double* xyz, int64_t E, const int64_t
 }
 
 // ---------------------------------------------------------------------------
-std::string build_ell(const Pattern& P, Ell& L) {
+std::string build_ell(const Pattern& P, Ell& L, const std::vector<int32_t>* elem_pair) {
   L = Ell();
   const int64_t nf = P.n_free;
   if (nf == 0) return "";
   const auto pos_of = [&](int64_t i, int k) {
     return ((int64_t)P.slice_ptr[i / kSlice] + k) * kSlice + i % kSlice;
   };
-  // free-neighbour slots of every free row, in slot (= element) order
+  // a slot to another partition's free node (multi-GPU)
+  const auto remote = [&](int64_t pos) {
+    const int32_t j = P.s_col[pos];
+    return elem_pair && j >= nf && P.code[j] == kGhost;
+  };
+  // free-neighbour (and remote) slots of every free row, in slot (= element) order
   std::vector<int64_t> fptr(nf + 1, 0);
   for (int64_t i = 0; i < nf; ++i) {
     int c = 0;
-    for (int k = 0; k < P.row_len[i]; ++k) c += P.s_col[pos_of(i, k)] < nf;
+    for (int k = 0; k < P.row_len[i]; ++k) c += P.s_col[pos_of(i, k)] < nf || remote(pos_of(i, k));
     fptr[i + 1] = fptr[i] + c;
   }
   std::vector<int64_t> fpos(fptr[nf]);
   for (int64_t i = 0, q = 0; i < nf; ++i)
     for (int k = 0; k < P.row_len[i]; ++k) {
       const int64_t pos = pos_of(i, k);
-      if (P.s_col[pos] < nf) fpos[q++] = pos;
+      if (P.s_col[pos] < nf || remote(pos)) fpos[q++] = pos;
     }
+  for (int64_t q = 0; q < fptr[nf]; ++q)
+    if (remote(fpos[q]) && (*elem_pair)[P.s_elem[fpos[q]]] < 0)
+      return "internal: remote slot without an exchange pair";
   // Waves are filled greedily with consecutive rows: for a candidate wave
   // [a, b) a row's halo slots are exactly its slots to rows outside [a, b),
   // and its group needs max(⌈slots/3⌉, halo slots) lanes.  Take the longest
@@ -209,7 +226,8 @@ std::string build_ell(const Pattern& P, Ell& L) {
   const auto row_need = [&](int64_t i, int32_t w) {
     const int64_t ns = fptr[i + 1] - fptr[i];
     int64_t halo = 0;
-    for (int64_t q = fptr[i]; q < fptr[i + 1]; ++q) halo += wave[P.s_col[fpos[q]]] != w;
+    for (int64_t q = fptr[i]; q < fptr[i + 1]; ++q)
+      halo += remote(fpos[q]) || wave[P.s_col[fpos[q]]] != w;
     return (int32_t)std::max<int64_t>({1, (ns + kEllSlots - 1) / kEllSlots, halo});
   };
   int64_t n_lanes = 0;
@@ -252,7 +270,8 @@ std::string build_ell(const Pattern& P, Ell& L) {
     // halo slots first (one per lane, slot 0), then the in-wave slots in order
     std::vector<int64_t> halo, local;
     for (int64_t q = fptr[i]; q < fptr[i + 1]; ++q)
-      (lane[P.s_col[fpos[q]]] / kSlice != l0 / kSlice ? halo : local).push_back(fpos[q]);
+      (remote(fpos[q]) || lane[P.s_col[fpos[q]]] / kSlice != l0 / kSlice ? halo : local)
+          .push_back(fpos[q]);
     size_t hq = 0, lq = 0;
     for (int t = 0; t < g; ++t) {
       const int32_t l = l0 + t;
@@ -270,7 +289,7 @@ std::string build_ell(const Pattern& P, Ell& L) {
         const uint32_t src = is_halo ? kEllHalo : (uint32_t)(lane[j] % kSlice);
         L.code[l] = (L.code[l] & ~(0xFFu << (8 * k))) | src << (8 * k);
         L.src_pos[(int64_t)k * n_lanes + l] = (int32_t)pos;
-        L.nbr_lane[(int64_t)k * n_lanes + l] = lane[j];
+        L.nbr_lane[(int64_t)k * n_lanes + l] = remote(pos) ? -1 : lane[j];
         lane_of_pos[pos] = l;
       }
     }
@@ -281,6 +300,10 @@ std::string build_ell(const Pattern& P, Ell& L) {
     if ((L.code[l] & 0xFF) != kEllHalo) continue;
     const int64_t pos = L.src_pos[l];
     const int32_t j = P.s_col[pos], e = P.s_elem[pos];
+    if (remote(pos)) {  // the peer rank's lane of the same cut element
+      L.partner[l] = -2 - (*elem_pair)[e];
+      continue;
+    }
     const int32_t i = L.lane_row[l] >= 0 ? L.lane_row[l] : L.lane_row[l + L.info[l]];
     int32_t mirror = -1;
     for (int k = 0; k < P.row_len[j]; ++k) {

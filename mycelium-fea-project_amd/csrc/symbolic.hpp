@@ -16,13 +16,16 @@ namespace mfea {
 
 constexpr int kSlice = 64;  // rows per slice = wavefront width on CDNA4
 
-enum NodeCode : uint8_t { kFree = 0, kTop = 1, kBot = 2 };
+// kGhost: a free node owned by another partition (multi-GPU); its row holds
+// coordinates and, after a solve, the owner's displacement — never solved here.
+enum NodeCode : uint8_t { kFree = 0, kTop = 1, kBot = 2, kGhost = 3 };
 
 struct Pattern {
   int64_t n_nodes = 0, n_elems = 0;
   int64_t n_free = 0;   // free nodes occupy permuted rows [0, n_free)
   int64_t n_top = 0;    // top grip rows [n_free, n_free + n_top) in top-list order
-  int64_t n_known = 0;  // known rows [n_free, n_nodes)
+  int64_t n_known = 0;  // known rows [n_free, n_nodes) (ghost rows included)
+  int64_t n_ghost = 0;  // rows of other partitions' nodes, [n_nodes - n_ghost, n_nodes)
   std::vector<int32_t> perm;   // perm[new] = original node
   std::vector<int32_t> iperm;  // iperm[orig] = new
   std::vector<uint8_t> code;   // code[new] (kFree / kTop / kBot; bottom overrides top)
@@ -48,9 +51,14 @@ constexpr int kOrderDFS = -1;
 // Validates and builds.  Returns "" on success, else an error message.
 // skip_invalid: drop elements with out-of-range node ids (src/fea_petsc.cpp:241)
 // instead of failing (src/fea_solver.py:82-83 raises).
+// ghost (multi-GPU, partition.hpp): nodes owned by another partition.  They
+// take the last rows — a ghost grip node keeps its kTop / kBot code (its value
+// is prescribed), a ghost free node gets kGhost — and never enter the free,
+// top or bottom blocks.
 std::string build_pattern(int64_t n_nodes, const double* xyz, int64_t n_elems, const int64_t* e2n,
                           bool skip_invalid, const std::vector<int64_t>& top,
-                          const std::vector<int64_t>& bot, int sort_window, Pattern& P);
+                          const std::vector<int64_t>& bot, int sort_window, Pattern& P,
+                          const std::vector<uint8_t>* ghost = nullptr);
 
 // ---------------------------------------------------------------------------
 // Wave-local CG operator ("ELL-3 lanes") over the free rows [0, n_free).
@@ -81,7 +89,11 @@ struct Ell {
 };
 
 // Builds the lanes for P's free rows.  Returns "" on success.
-std::string build_ell(const Pattern& P, Ell& L);
+// elem_pair (multi-GPU): per element, its cross-partition pair index
+// (partition.hpp).  A slot to a kGhost row is a REMOTE halo slot: always slot 0
+// of its lane, and partner = -2 - pair (the lane sends its owner's record to
+// that pair's send slot and reads the peer's record from the receive slot).
+std::string build_ell(const Pattern& P, Ell& L, const std::vector<int32_t>* elem_pair = nullptr);
 
 // Scalar CSR over the 3·N DOFs in original order, pattern = the reference's
 // csr_matrix pattern for the active set (src/fea_solver.py:93-105):

@@ -119,7 +119,7 @@ def _grips(nodes, coords, tol):
 
 
 def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=None,
-               out_format="python", verbose=True):
+               out_format="python", verbose=True, nparts=1):
     """The reference step loop (src/fea_solver.py:186-335) with the hot path on device.
 
     Reads <results_dir>/nodes.csv + elements.csv, runs N_STEPS load steps and
@@ -127,7 +127,8 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     node_displacements,force_displacement}.csv, runtime.txt and
     solve_runtime.txt.  Module constants are read at call time, as in the
     reference.  out_format='petsc' writes the fea_petsc.cpp formatting instead
-    (src/fea_petsc.cpp:433-516)."""
+    (src/fea_petsc.cpp:433-516).  nparts > 1 runs the multi-GPU partitioned
+    solve with that many partitions on this one device (mfea_debug_set_parts)."""
     start_time = time.time()
     say = print if verbose else (lambda *a, **k: None)
     say(f"🔧 Running FEA on geometry from {results_dir}")
@@ -147,6 +148,7 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     say(f"Top nodes: {len(top)}, Bottom nodes: {len(bot)}")
 
     eng = get_engine()
+    eng.set_parts(nparts)
     eng.set_material(E_mod, A, I)
     eng.set_mesh(coords, e2n)
     eng.set_bc(top, bot)
@@ -226,11 +228,13 @@ def main(argv=None):
     ap.add_argument("--reg", type=float, default=REG)
     ap.add_argument("--pc", choices=["jacobi", "bjacobi"], default="jacobi")
     ap.add_argument("--format", choices=["python", "petsc"], default="python")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="partitions of the multi-GPU solve, all on this device")
     a = ap.parse_args(argv)
     N_STEPS, DISPLACEMENT_MAX, MAX_STRAIN, REG = a.n_steps, a.disp_max, a.max_strain, a.reg
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,
                precond=_capi.PC_BLOCK_JACOBI if a.pc == "bjacobi" else _capi.PC_JACOBI,
-               out_format=a.format)
+               out_format=a.format, nparts=a.parts)
 
 
 if __name__ == "__main__":

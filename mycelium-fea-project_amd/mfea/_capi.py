@@ -45,7 +45,9 @@ class Info(C.Structure):
     _fields_ = [("n_nodes", C.c_int64), ("n_elems", C.c_int64), ("n_free_nodes", C.c_int64),
                 ("n_top", C.c_int64), ("n_known", C.c_int64), ("n_slices", C.c_int64),
                 ("n_slots", C.c_int64), ("free_incidences", C.c_int64), ("planar", C.c_int32),
-                ("cg_lanes", C.c_int32), ("n_lanes", C.c_int64), ("n_halo", C.c_int64)]
+                ("cg_lanes", C.c_int32), ("n_lanes", C.c_int64), ("n_halo", C.c_int64),
+                ("n_parts", C.c_int32), ("part", C.c_int32), ("n_pairs", C.c_int64),
+                ("n_ghost", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -78,8 +80,10 @@ _sig = {
                                  C.POINTER(SolveOpts), _P, C.POINTER(Stats)]),
     "mfea_dist_unique_id": (C.c_int, [_P]),
     "mfea_dist_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    "mfea_set_partition_axis": (C.c_int, [_P, C.c_int]),
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
+    "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(_lib, _name)
@@ -128,6 +132,13 @@ def abi_version() -> int:
     return _lib.mfea_abi_version()
 
 
+def dist_unique_id() -> bytes:
+    """The 128-byte RCCL unique id (rank 0 makes it, the launcher broadcasts it)."""
+    buf = (C.c_uint8 * 128)()
+    _check(_lib.mfea_dist_unique_id(buf))
+    return bytes(buf)
+
+
 def make_opts(rtol=1e-8, atol=0.0, max_it=100000, precond=PC_JACOBI, norm=NORM_UNPRECONDITIONED,
               chunk=0, reg=1e-12) -> SolveOpts:
     return SolveOpts(rtol, atol, int(max_it), int(precond), int(norm), int(chunk), reg)
@@ -159,6 +170,22 @@ class Engine:
 
     def __exit__(self, *exc):
         self.close()
+
+    # ---- partitioning -------------------------------------------------------
+    def dist_init(self, rank: int, world: int, unique_id: bytes):
+        """Join an RCCL world (one process per GPU); call before set_mesh."""
+        if len(unique_id) != 128:
+            raise ValueError("unique_id must be 128 bytes")
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        _check(_lib.mfea_dist_init(self._h, int(rank), int(world), buf))
+
+    def set_partition_axis(self, axis: int = -1):
+        _check(_lib.mfea_set_partition_axis(self._h, int(axis)))
+
+    def set_parts(self, nparts: int, axis: int = -1):
+        """nparts partitions of the multi-GPU solve held by this handle on one
+        device (mfea_debug_set_parts: the partitioned path, testable on one GPU)."""
+        _check(_lib.mfea_debug_set_parts(self._h, int(nparts), int(axis)))
 
     # ---- setup --------------------------------------------------------------
     def set_material(self, E, A, I):

@@ -1,0 +1,142 @@
+"""GPU parity of the multi-GPU partitioned solve (partition.hpp).
+
+The partitions run on ONE device here (mfea_debug_set_parts): the same
+partition plan, lane kernels (DIST variants) and exchange schedule as the
+one-process-per-GPU RCCL path, with device copies standing in for the RCCL
+group.  Bars: the displacement within 1e-10 relative L2 of the direct solve,
+Jacobi-PCG iteration counts within ±3 of SciPy's, and the drop-in CSV records
+equal to the reference's golden vectors, for 2-4 partitions along x and y,
+planar (2 DOF lanes) and 3-D (3 DOF lanes) meshes, with element failures
+crossing partition boundaries.
+"""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_gen, load_mesh, read_rt
+from test_gpu_parity import STRESS_RTOL, force_close, rel
+
+pytestmark = pytest.mark.gpu
+
+import fea_oracle as fo  # noqa: E402  (checker only)
+
+
+@pytest.fixture(scope="module")
+def peng():
+    from mfea import Engine
+    eng = Engine(0)
+    yield eng
+    eng.close()
+
+
+def _sim181147(eng, nparts, axis=-1):
+    nodes, elems = load_mesh("sim_20251117_181147")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    eng.set_parts(nparts, axis)
+    eng.set_mesh(xyz, elems[["n1", "n2"]].values)
+    eng.set_bc(top, bot)
+    eng.set_active(None)
+    return xyz, elems[["n1", "n2"]].values, top, bot
+
+
+@pytest.mark.parametrize("nparts,axis,precond", [(2, -1, 0), (3, 0, 0), (4, 1, 0), (3, -1, 1)])
+def test_partitioned_solve_matches_direct(peng, nparts, axis, precond):
+    from mfea import make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    _sim181147(peng, nparts, axis)
+    info = peng.info()
+    assert info["n_parts"] == nparts and info["n_pairs"] > 0 and info["n_ghost"] > 0
+    peng.assemble()
+    dy = float(sysz["dy"])
+    st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=200000, precond=precond))
+    U = peng.displacement()
+    assert st.status == 0
+    assert rel(U, sysz["U"]) <= 1e-10
+    if precond == 0:
+        st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8))
+        assert abs(st8.iters - int(sysz["pcg_iters_1e8"])) <= 3
+
+
+def test_partitioned_solve_deterministic(peng):
+    from mfea import make_opts
+    _sim181147(peng, 3)
+    peng.assemble()
+    peng.solve(0.01, -0.01, make_opts(rtol=1e-10))
+    U1 = peng.displacement()
+    peng.assemble()
+    peng.solve(0.01, -0.01, make_opts(rtol=1e-10))
+    assert np.array_equal(U1, peng.displacement())
+
+
+def test_partitioned_step_matches_single_partition(peng, engine):
+    """One full load step (assembly → PCG → reaction, stress, failures) of the
+    C2-shaped network (1×5 tiles, 110k DOF) on 4 partitions vs 1."""
+    from mfea import make_opts, synth
+    xyz, e2n = synth.tiled_mesh(1, 5)
+    top, bot = synth.grips(xyz)
+    out = []
+    for eng, npart in ((engine, 1), (peng, 4)):
+        eng.set_parts(npart)
+        eng.set_mesh(xyz, e2n)
+        eng.set_bc(top, bot)
+        eng.set_active(None)
+        f, n_act, st = eng.step(0.0102564, -0.0102564, make_opts(rtol=1e-13, max_it=200000), 0.018)
+        out.append((f, n_act, st.iters, eng.displacement(), eng.stress(), eng.active()))
+    engine.set_parts(1)
+    (f1, n1, it1, U1, S1, A1), (f4, n4, it4, U4, S4, A4) = out
+    assert abs(it1 - it4) <= 3
+    assert rel(U4, U1) <= 1e-10
+    # the reaction is a sum of K·U over the grip rows with heavy cancellation
+    # (|f| ≈ 1e-5 of Σ|terms|): relative agreement is ~1e5 × the U error
+    assert abs(f4 - f1) <= 1e-8 * abs(f1)
+    assert n4 == n1 and np.array_equal(A4, A1)
+    assert rel(S4, S1) <= 1e-8
+
+
+def _run_dropin(tmp_path, mesh, n_steps, dmax, grip, nparts):
+    import fea_solver as fs
+    d = tmp_path / mesh
+    shutil.copytree(os.path.join(GOLDEN, "meshes", mesh), d)
+    saved = (fs.N_STEPS, fs.DISPLACEMENT_MAX)
+    fs.N_STEPS, fs.DISPLACEMENT_MAX = n_steps, dmax
+    try:
+        fs.fea_solver(str(d), tol=grip, verbose=False, nparts=nparts)
+    finally:
+        fs.N_STEPS, fs.DISPLACEMENT_MAX = saved
+        fs.get_engine().set_parts(1)
+    return d / "fea_results"
+
+
+@pytest.mark.parametrize("gen,mesh,nparts", [
+    ("gen_sim_20251117_175809_default.npz", "sim_20251117_175809", 3),
+    ("gen_sim_20251115_135507_grip05.npz", "sim_20251115_135507", 2),   # 3D mesh (z ≠ 0)
+])
+def test_partitioned_dropin_matches_reference_vectors(tmp_path, gen, mesh, nparts):
+    g = load_gen(gen)
+    res = _run_dropin(tmp_path, mesh, int(g["n_steps"]), float(g["dmax"]), float(g["grip"]), nparts)
+    F = read_rt(res / "force_displacement.csv").values
+    assert F.shape == g["force"].shape
+    assert force_close(F[:, 1], g["force"][:, 1])
+    A = read_rt(res / "active_elements.csv").values[:, :-1].astype(bool)
+    assert np.array_equal(A, g["active"])
+    U = read_rt(res / "node_displacements.csv").values[:, :-1]
+    for k, s in enumerate(g["U_steps"]):
+        assert rel(U[s], g["U"][k]) <= 1e-10
+    S = read_rt(res / "stress_record.csv").values[:, :-1]
+    for s in range(S.shape[0]):
+        assert rel(S[s], g["stress"][s]) <= STRESS_RTOL
+
+
+def test_partitioned_failures_match_committed_golden(tmp_path):
+    """The reference's 22k-DOF run with element failures, on 2 partitions."""
+    res = _run_dropin(tmp_path, "sim_20251117_181147", 40, 0.02, 1.5, 2)
+    F = read_rt(res / "force_displacement.csv").values
+    Fr = read_rt(os.path.join(GOLDEN, "ref", "sim_20251117_181147", "force_displacement.csv")).values
+    assert rel(F[:, 1], Fr[:, 1]) <= 1e-9
+    z = np.load(os.path.join(GOLDEN, "ref", "sim_20251117_181147", "active_packed.npz"))
+    Ar = np.unpackbits(z["bits"], axis=1)[:, : int(z["n_elems"])].astype(bool)
+    A = read_rt(res / "active_elements.csv").values[:, :-1].astype(bool)
+    assert np.array_equal(A, Ar)

@@ -6,6 +6,13 @@ A "step" = one pass of the hot path over the synthetic mesh: device assembly
 the timed region; no CSV IO.  Workload (BASELINE.json configs[1]): the 100k-DOF
 synthetic network = 1×5 tiles of results/sim_20251117_181147 (110,625 DOF).
 
+N > 1 (one process per GPU, launched by torch.distributed.run): the
+partitioned solve over RCCL with weak scaling — the network is
+N×5 tiles (≈ 110k DOF per GPU) cut into N strips along x, one per GPU;
+`value` is the whole network's DOF/s.  `--mode replicas` runs N independent
+copies of the 1-GPU step instead.  torch.distributed (gloo) only carries the
+RCCL unique id, the barriers and the max-over-ranks time.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2_100k]
 
 Prints ONE JSON line on rank 0.
@@ -22,7 +29,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "mycelium-fea-project_amd"))
 
-import numpy as np  # noqa: E402
+import numpy as np  # noqa: E402,F401
 
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
@@ -40,6 +47,10 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
+    ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
+                    help="N > 1: one network cut over the GPUs, or N independent copies")
+    ap.add_argument("--parts", type=int, default=1,
+                    help="1 GPU: run the partitioned solve with this many partitions on it")
     return ap.parse_args()
 
 
@@ -84,21 +95,35 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo")
 
-    from mfea import Engine, make_opts, PC_BLOCK_JACOBI, PC_JACOBI, synth
+    from mfea import Engine, make_opts, PC_BLOCK_JACOBI, PC_JACOBI, dist_unique_id, synth
     from mfea.synth import CONFIGS
+    import fea_solver as fs
 
     nx, ny = CONFIGS[a.config]
+    mode = a.mode if world > 1 else ("parts" if a.parts > 1 else "1gpu")
+    note = None
+    eng = Engine(local)
+    if mode == "partitioned":
+        nx *= world  # weak scaling: one tile column (≈ the 1-GPU network) per GPU
+        try:
+            uid = [dist_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            eng.dist_init(rank, world, uid[0])
+            eng.set_partition_axis(0)
+        except Exception as ex:  # noqa: BLE001  (reported in the JSON, then replicas)
+            note = f"partitioned init failed ({ex}); replicas instead"
+            mode, nx = "replicas", nx // world
+            eng.close()
+            eng = Engine(local)
+    elif mode == "parts":
+        eng.set_parts(a.parts, 0)
     xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
     top, bot = synth.grips(xyz)
     n_dof = 3 * len(xyz)
 
-    import fea_solver as fs
-    eng = Engine(local)
     eng.set_material(fs.E_mod, fs.A, fs.I)
     eng.set_mesh(xyz, e2n)
     eng.set_bc(top, bot)
@@ -115,7 +140,8 @@ def main():
     def barrier_sync():
         if dist is not None:
             import torch
-            torch.cuda.synchronize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
             dist.barrier()
 
     for _ in range(a.warmup):
@@ -129,22 +155,24 @@ def main():
     dt = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # DOF of the whole job: the one (partitioned) network, or N copies
+    job_dof = n_dof * (world if mode == "replicas" else 1)
 
     force, n_active, st = stats[-1]
     iters = st.iters
     # ---- roofline of the dominant kernel (one CG-CG iteration launch), live
     # HIP events on the engine's stream; algorithmic bytes per launch as in
-    # DESIGN.md §Roofline
+    # DESIGN.md §Roofline (partitioned: rank 0's partition, without exchange)
     iter_ms = eng.profile_iteration(pc, reps=200)
     iter_bytes, kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
     nf = info["n_free_nodes"]
     achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
     traffic = None
     a.traffic = a.traffic or os.path.join(REPO, "profiles", f"traffic_{a.config}.json")
-    if os.path.exists(a.traffic):
+    if os.path.exists(a.traffic) and mode == "1gpu":
         try:
             tj = json.load(open(a.traffic))
             # only a profile of the same config AND the same iteration kernel
@@ -153,9 +181,19 @@ def main():
         except Exception:
             traffic = None
 
+    parallelism = {"1gpu": "1gpu", "parts": f"parts{a.parts}@1gpu",
+                   "partitioned": f"partitioned{world} (RCCL)", "replicas": f"replicas{world}"}[mode]
+    workload = (f"{a.config}: {nx}x{ny} tiles, {n_dof} DOF, {st.n_free} free DOF, {len(e2n)} elements, "
+                f"load step {a.load_step}/40")
+    if mode == "partitioned":
+        workload += f", cut into {world} x-strips (one per GPU)"
+    elif mode == "parts":
+        workload += f", {a.parts} partitions on 1 GPU"
+    elif mode == "replicas":
+        workload += f", one copy per GPU ({world} GPUs)"
     out = {
         "metric": "DOF solved/sec + CG iters to 1e-8; SpMV achieved HBM GB/s vs roofline",
-        "value": n_dof * a.steps * world / dt,
+        "value": job_dof * a.steps / dt,
         "unit": "DOF/s",
         "n_gpus": world,
         "steps": a.steps,
@@ -167,11 +205,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (tiled copies of results/sim_20251117_181147; no RNG)",
         "config": {
-            "workload": f"{a.config}: {nx}x{ny} tiles, {n_dof} DOF, {info['n_free_nodes'] * 3} free DOF, "
-                        f"{info['n_elems']} elements, load step {a.load_step}/40",
-            "n_dof": n_dof, "n_free_dof": 3 * nf, "n_elems": info["n_elems"],
-            "precond": a.precond, "rtol": a.rtol, "parallelism": f"replicas{world}" if world > 1 else "1gpu",
+            "workload": workload,
+            "n_dof": n_dof, "n_free_dof": st.n_free, "n_elems": len(e2n),
+            "precond": a.precond, "rtol": a.rtol, "parallelism": parallelism,
             "cg_kernel": "lanes" if info["cg_lanes"] else "sell", "n_lanes": info["n_lanes"],
+            "rank0_part": {"free_dof": 3 * nf, "n_pairs": info["n_pairs"], "n_ghost": info["n_ghost"]},
         },
         "cg_iters": iters,
         "relres": st.relres,
@@ -189,8 +227,10 @@ def main():
             "avg_launch_us": iter_ms * 1e3,
         },
     }
+    if note:
+        out["note"] = note
 
-    if rank == 0 and not a.no_cpu:
+    if rank == 0 and not a.no_cpu and world == 1:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import cpu_fea  # baseline leg only
         cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)

@@ -167,6 +167,25 @@ int mfea_get_info(mfea_handle* h, mfea_info* info);
  * Call after mfea_solve (it overwrites the solver state). */
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms);
 
+/* ---- record writer (host only: needs no device, no handle) ------------------ */
+/* Writes one of the driver's end-of-run CSV records, byte-identical to the
+ * reference's writers: src/fea_solver.py:297-316 (pandas to_csv — shortest
+ * round-trip floats as numpy/Python repr, NaN as an empty field, True/False,
+ * node_displacements headed 0..n_cols-1) with style MFEA_CSV_PANDAS, or
+ * src/fea_petsc.cpp:433-516 (setprecision(12), 1/0, node_i_x…node_i_z header)
+ * with MFEA_CSV_PETSC.  values: n_rows×n_cols row-major f64 (STRESS, DISP,
+ * FORCE); flags: n_rows×n_cols bytes (ACTIVE).  Rows get the 1-based step
+ * column, except FORCE (n_cols = 2: total_displacement, total_force).
+ * n_threads formats column chunks in parallel (output identical for any). */
+#define MFEA_CSV_PANDAS 0
+#define MFEA_CSV_PETSC 1
+#define MFEA_REC_STRESS 0 /* stress_record.csv       */
+#define MFEA_REC_ACTIVE 1 /* active_elements.csv     */
+#define MFEA_REC_DISP 2   /* node_displacements.csv  */
+#define MFEA_REC_FORCE 3  /* force_displacement.csv  */
+int mfea_write_record_csv(const char* path, int style, int kind, int64_t n_rows, int64_t n_cols,
+                          const double* values, const uint8_t* flags, int n_threads);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------- */
 /* Replaces the PETSC_COMM_WORLD row-block distribution of
  * src/fea_petsc_parallel.cpp:169-171, 234-268, 330-409 and its MPI reductions.

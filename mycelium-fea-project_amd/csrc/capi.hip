@@ -21,6 +21,7 @@
 #include "mfea_debug.h"
 #include "mfea.h"
 #include "partition.hpp"
+#include "records.hpp"
 #include "symbolic.hpp"
 
 using namespace mfea;
@@ -130,7 +131,7 @@ struct mfea_handle {
   int nparts = 1, axis = -1;
   int world = 1, rank = 0;
   ncclComm_t comm = nullptr;
-  double dist_timeout_s = 300.0;
+  double dist_timeout_s = 60.0;  // per wait; MFEA_DIST_TIMEOUT_S
   SolveState* h_state = nullptr;       // pinned, 2 entries
   SolveState* d_host_state = nullptr;  // device view of h_state (mapped)
   double* h_red = nullptr;             // pinned
@@ -490,26 +491,25 @@ EllVecs ell_vecs(Part& pt) {
 // Partitions on one device: device copies on the same stream.
 // ---------------------------------------------------------------------------
 // CG records of parity q (xs[q] → the peers' xr[q]); gather: this rank's
-// partial sums (gsend) → row `rank` of every rank's gall[q].
+// partial sums (gsend) → row `rank` of every rank's gall[q].  The sums travel
+// by all-gather (a pure copy: every rank then adds the same bits in the same
+// order), never by an all-reduce whose summation order may differ per rank.
 int xchg_records(mfea_handle* h, int q, bool gather) {
   const int64_t RW = 3 * lane_dofs(h);
   hipStream_t s = h->stream;
   if (h->world > 1) {
     Part& pt = part0(h);
     const PartPlan& pl = pt.plan;
-    NCCLC(ncclGroupStart());
-    for (size_t i = 0; i < pl.peers.size(); ++i) {
-      const size_t n = (size_t)(pl.peer_cnt[i] * RW);
-      NCCLC(ncclSend(pt.dv.xs[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
-      NCCLC(ncclRecv(pt.dv.xr[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
-    }
-    if (gather)
-      for (int r = 0; r < h->world; ++r) {
-        if (r == h->rank) continue;
-        NCCLC(ncclSend(pt.dv.gsend, 4, ncclFloat64, r, h->comm, s));
-        NCCLC(ncclRecv(pt.dv.gall[q] + 4 * r, 4, ncclFloat64, r, h->comm, s));
+    if (!pl.peers.empty()) {
+      NCCLC(ncclGroupStart());
+      for (size_t i = 0; i < pl.peers.size(); ++i) {
+        const size_t n = (size_t)(pl.peer_cnt[i] * RW);
+        NCCLC(ncclSend(pt.dv.xs[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
+        NCCLC(ncclRecv(pt.dv.xr[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
       }
-    NCCLC(ncclGroupEnd());
+      NCCLC(ncclGroupEnd());
+    }
+    if (gather) NCCLC(ncclAllGather(pt.dv.gsend, pt.dv.gall[q], 4, ncclFloat64, h->comm, s));
     return 0;
   }
   for (auto& a : h->parts) {
@@ -573,15 +573,7 @@ int gather4(mfea_handle* h, int off) {
   hipStream_t s = h->stream;
   if (h->world > 1) {
     Part& pt = part0(h);
-    HIPC(hipMemcpyAsync(pt.gred + 4 * h->rank, pt.red.ptr + off, 4 * sizeof(double),
-                        hipMemcpyDeviceToDevice, s));
-    NCCLC(ncclGroupStart());
-    for (int r = 0; r < h->world; ++r) {
-      if (r == h->rank) continue;
-      NCCLC(ncclSend(pt.red.ptr + off, 4, ncclFloat64, r, h->comm, s));
-      NCCLC(ncclRecv(pt.gred + 4 * r, 4, ncclFloat64, r, h->comm, s));
-    }
-    NCCLC(ncclGroupEnd());
+    NCCLC(ncclAllGather(pt.red.ptr + off, pt.gred, 4, ncclFloat64, h->comm, s));
     return 0;
   }
   for (auto& a : h->parts)
@@ -800,10 +792,42 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   RC(xchg_records(h, 0, true));
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
+  // MFEA_DIST_GRAPH=1: replay each chunk (kernels + exchanges) as one hipGraph
+  static const bool dist_graph = [] {
+    const char* e = std::getenv("MFEA_DIST_GRAPH");
+    return e && *e == '1';
+  }();
   SolveState fin;
-  RC(drive_chunks(
-      h, chunk, o->max_it, [&]() -> int { return enqueue_chunk_dist(h, chunk, precond); }, &fin,
-      /*mirror=*/true));
+  if (dist_graph) {
+    const int tag = -10 - lane_dofs(h);  // graph_ell key of the partitioned chunk
+    if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != precond ||
+        h->graph_ell != tag) {
+      destroy_graph(h);
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int rc = enqueue_chunk_dist(h, chunk, precond);
+      const hipError_t ce = hipStreamEndCapture(s, &g);
+      if (rc) return rc;
+      HIPC(ce);
+      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_chunk = chunk;
+      h->graph_precond = precond;
+      h->graph_ell = tag;
+    }
+    RC(drive_chunks(
+        h, chunk, o->max_it,
+        [&]() -> int {
+          HIPC(hipGraphLaunch(h->graph, s));
+          return 0;
+        },
+        &fin, /*mirror=*/true));
+  } else {
+    RC(drive_chunks(
+        h, chunk, o->max_it, [&]() -> int { return enqueue_chunk_dist(h, chunk, precond); }, &fin,
+        /*mirror=*/true));
+  }
   // x to row order, then the displacement halo (ghost rows of the post kernels)
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -1413,6 +1437,13 @@ int mfea_set_partition_axis(mfea_handle* h, int axis) {
   h->axis = axis;
   h->dirty = true;
   return 0;
+}
+
+int mfea_write_record_csv(const char* path, int style, int kind, int64_t n_rows, int64_t n_cols,
+                          const double* values, const uint8_t* flags, int n_threads) {
+  const std::string err =
+      write_record_csv(path, style, kind, n_rows, n_cols, values, flags, n_threads);
+  return err.empty() ? 0 : fail(MFEA_EINVAL, err);
 }
 
 int mfea_dist_unique_id(uint8_t* unique_id) {

@@ -194,25 +194,20 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
 
 def write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_record,
                   force_disp_curve, out_format="python"):
-    """CSV writers, src/fea_solver.py:297-316 (pandas) / src/fea_petsc.cpp:433-516."""
-    if out_format == "petsc":
-        from mfea.io_csv import write_petsc_records
-        write_petsc_records(fea_dir, n_nodes, n_elems, stress_record, active_record,
-                            disp_record, force_disp_curve)
-        return
-    cols = [f"elem_{i}" for i in range(n_elems)]
-    stress_df = pd.DataFrame(stress_record, columns=cols)
-    stress_df["step"] = np.arange(1, len(stress_record) + 1)
-    stress_df.to_csv(os.path.join(fea_dir, "stress_record.csv"), index=False)
-    active_df = pd.DataFrame(active_record, columns=cols)
-    active_df["step"] = np.arange(1, len(active_record) + 1)
-    active_df.to_csv(os.path.join(fea_dir, "active_elements.csv"), index=False)
-    ncol = len(disp_record[0]) if disp_record else 3 * n_nodes
-    disp_df = pd.DataFrame(disp_record, columns=np.arange(ncol))
-    disp_df["step"] = np.arange(1, len(disp_record) + 1)
-    disp_df.to_csv(os.path.join(fea_dir, "node_displacements.csv"), index=False)
-    fd_df = pd.DataFrame(force_disp_curve, columns=["total_displacement", "total_force"])
-    fd_df.to_csv(os.path.join(fea_dir, "force_displacement.csv"), index=False)
+    """CSV writers, src/fea_solver.py:297-316 (pandas) / src/fea_petsc.cpp:433-516,
+    through the native multi-threaded writer (mfea_write_record_csv), which
+    reproduces both byte for byte.  The C++ driver writes a record file only
+    when it holds at least one step (src/fea_petsc.cpp:435, 457, 477, 508)."""
+    petsc = out_format == "petsc"
+    style = _capi.CSV_PETSC if petsc else _capi.CSV_PANDAS
+    files = (("stress_record.csv", _capi.REC_STRESS, stress_record, n_elems),
+             ("active_elements.csv", _capi.REC_ACTIVE, active_record, n_elems),
+             ("node_displacements.csv", _capi.REC_DISP, disp_record, 3 * n_nodes),
+             ("force_displacement.csv", _capi.REC_FORCE, force_disp_curve, 2))
+    for name, kind, rec, ncol in files:
+        if petsc and not len(rec):
+            continue
+        _capi.write_record_csv(os.path.join(fea_dir, name), style, kind, rec, n_cols=ncol)
 
 
 def main(argv=None):

@@ -81,6 +81,8 @@ _sig = {
     "mfea_dist_unique_id": (C.c_int, [_P]),
     "mfea_dist_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "mfea_set_partition_axis": (C.c_int, [_P, C.c_int]),
+    "mfea_write_record_csv": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _P, _P,
+                                        C.c_int]),
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
@@ -137,6 +139,28 @@ def dist_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()
     _check(_lib.mfea_dist_unique_id(buf))
     return bytes(buf)
+
+
+CSV_PANDAS, CSV_PETSC = 0, 1
+REC_STRESS, REC_ACTIVE, REC_DISP, REC_FORCE = 0, 1, 2, 3
+
+
+def write_record_csv(path, style, kind, records, n_cols=None, threads=None):
+    """One end-of-run record file through the native writer (mfea_write_record_csv):
+    byte-identical to the reference's pandas / ostream writers.  records: list
+    of per-step rows (or a 2-D array)."""
+    flags = kind == REC_ACTIVE
+    dt = np.uint8 if flags else np.float64
+    if len(records):
+        a = np.ascontiguousarray(np.asarray(records), dtype=dt).reshape(len(records), -1)
+    else:
+        a = np.zeros((0, n_cols or 0), dtype=dt)
+    nr, nc = a.shape
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    p = a.ctypes.data_as(_P) if a.size else None
+    _check(_lib.mfea_write_record_csv(os.fsencode(path), int(style), int(kind), nr, nc,
+                                      None if flags else p, p if flags else None, int(threads)))
 
 
 def make_opts(rtol=1e-8, atol=0.0, max_it=100000, precond=PC_JACOBI, norm=NORM_UNPRECONDITIONED,

@@ -34,7 +34,8 @@ def build_host_shim():
     import subprocess
     d = os.path.join(REPO, "tests", "native")
     out = os.path.join(d, "libhostshim.so")
-    srcs = [os.path.join(d, "host_shim.cpp"), os.path.join(PKG, "csrc", "symbolic.cpp")]
+    srcs = [os.path.join(d, "host_shim.cpp"), os.path.join(PKG, "csrc", "symbolic.cpp"),
+            os.path.join(PKG, "csrc", "partition.cpp")]
     if not os.path.exists(out) or any(os.path.getmtime(s) > os.path.getmtime(out) for s in srcs):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC",
                                "-I" + os.path.join(PKG, "csrc"), *srcs, "-o", out])

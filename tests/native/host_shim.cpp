@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "partition.hpp"
 #include "symbolic.hpp"
 
 using namespace mfea;
@@ -112,6 +113,52 @@ int64_t shim_ell(int32_t* lane_row, int32_t* row_lane, int32_t* info, uint32_t* 
   std::memcpy(src_pos, g_L.src_pos.data(), kEllSlots * n * 4);
   std::memcpy(nbr_lane, g_L.nbr_lane.data(), kEllSlots * n * 4);
   return n;
+}
+
+// Multi-GPU partition plan of one rank (partition.cpp), for the world-size-2
+// gloo tests.  sizes: [local nodes, local elements, pairs, peers, xpeers,
+// xsend nodes, xrecv nodes, axis used].
+static PartPlan g_plan;
+int shim_part(int64_t N, const double* xyz, int64_t E, const int64_t* e2n, int64_t ntop,
+              const int64_t* top, int64_t nbot, const int64_t* bot, int world, int rank, int axis,
+              int64_t* sizes, char* err, int errn) {
+  std::vector<int64_t> t(top, top + ntop), b(bot, bot + nbot);
+  std::string e = build_partition(N, xyz, E, e2n, false, t, b, world, rank, axis, g_plan);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  sizes[0] = (int64_t)g_plan.node_g.size();
+  sizes[1] = (int64_t)g_plan.elem_g.size();
+  sizes[2] = g_plan.n_pairs;
+  sizes[3] = (int64_t)g_plan.peers.size();
+  sizes[4] = (int64_t)g_plan.xpeers.size();
+  sizes[5] = (int64_t)g_plan.xsend_node.size();
+  sizes[6] = (int64_t)g_plan.xrecv_node.size();
+  sizes[7] = g_plan.axis;
+  return 0;
+}
+
+void shim_part_arrays(int64_t* node_g, uint8_t* ghost, int64_t* elem_g, uint8_t* elem_own,
+                      int32_t* elem_pair, int32_t* peers, int64_t* peer_cnt, int32_t* xpeers,
+                      int64_t* xsend_cnt, int64_t* xrecv_cnt, int64_t* xsend_node,
+                      int64_t* xrecv_node) {
+  const PartPlan& p = g_plan;
+  auto cp = [](void* dst, const auto& v) {
+    if (!v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+  };
+  cp(node_g, p.node_g);
+  cp(ghost, p.ghost);
+  cp(elem_g, p.elem_g);
+  cp(elem_own, p.elem_own);
+  cp(elem_pair, p.elem_pair);
+  cp(peers, p.peers);
+  cp(peer_cnt, p.peer_cnt);
+  cp(xpeers, p.xpeers);
+  cp(xsend_cnt, p.xsend_cnt);
+  cp(xrecv_cnt, p.xrecv_cnt);
+  cp(xsend_node, p.xsend_node);
+  cp(xrecv_node, p.xrecv_node);
 }
 
 }  // extern "C"

@@ -1405,8 +1405,9 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   RC(mfea_profile_iteration(h, precond, 20, &ms));  // same running state
   hipStream_t s = h->stream;
   Part& pt = part0(h);
-  const int64_t g = cg_grid(use_ell(pt) ? pt.L.n_lanes : pt.P.n_free);
-  const int64_t nw = g * (cg_block_size(0) / 64);
+  const bool ell = use_ell(pt);
+  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes) : cg_grid(pt.P.n_free);
+  const int64_t nw = g * ((ell ? ell_block_size(pt.L.n_lanes) : cg_block_size(0)) / 64);
   if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
   unsigned long long* d = nullptr;
   HIPC(hipMalloc(&d, nw * 4 * sizeof(unsigned long long)));

@@ -240,8 +240,9 @@ __device__ __forceinline__ void wave_partials(const double* __restrict__ p, doub
 // block partial (thread 0 stores it; the next launch's waves re-reduce).
 // The cross-wave step uses a raw s_barrier behind an LDS-only wait: a
 // __syncthreads() would also wait for every outstanding vector store (vmcnt(0)).
+template <int BS = kCgBS>
 __device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __restrict__ p) {
-  constexpr int NW = kCgBS / 64;
+  constexpr int NW = BS / 64;
   __shared__ double lds[NW * 4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -250,7 +251,8 @@ __device__ __forceinline__ void store_block_partial(double (&acc)[4], double* __
 #pragma unroll
     for (int c = 0; c < 4; ++c) lds[wid * 4 + c] = acc[c];
   }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (NW > 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -300,13 +302,13 @@ __device__ __forceinline__ void cg_record(Slot* slots, int j, const double S[4],
 // TRACE: lane 0 of every wave records s_memrealtime (100 MHz) at entry, once
 // the partials are reduced, once the last row's SpMV is done, and after its
 // stores have drained: trace[(block·4 + wave)·4 + point] (diagnostics only).
-template <bool TRACE>
+template <bool TRACE, int BS = kCgBS>
 __device__ __forceinline__ void trace_point(unsigned long long* trace, int point, double dep) {
   if (TRACE) {
     unsigned long long t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
     if ((threadIdx.x & 63) == 0)
-      trace[((size_t)blockIdx.x * (kCgBS / 64) + (threadIdx.x >> 6)) * 4 + point] = t;
+      trace[((size_t)blockIdx.x * (BS / 64) + (threadIdx.x >> 6)) * 4 + point] = t;
   }
 }
 

@@ -24,6 +24,8 @@
 // component of every Krylov vector stays exactly 0 and contributes exact
 // zeros to every sum: dropping them gives bitwise the 3-DOF iterates with
 // 40 % fewer bytes per lane.  Symmetric blocks then hold (xx, xy, yy).
+#include <cstdlib>
+
 #include "device_util.hpp"
 #include "kernels.hpp"
 
@@ -186,15 +188,15 @@ __global__ __launch_bounds__(kCgBS) void k_ell_pack0(EllOp op, EllVecs v, DistVe
 // records (its M is kept in dv.mr for the iterations), and the lane's own
 // parity-0 record goes to its pair's send slot.
 // ---------------------------------------------------------------------------
-template <int ND, bool BLOCK, bool DIST>
-__global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
-                                                     double* part, DistVecs dv) {
+template <int ND, bool BLOCK, bool DIST, int BS>
+__global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
+                                                  double* part, DistVecs dv) {
   constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
   const int64_t NL = op.NL;
   const int lane = threadIdx.x & 63;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x; l - lane < NL;
-       l += (int64_t)gridDim.x * kCgBS) {
+  for (int64_t l = (int64_t)blockIdx.x * BS + threadIdx.x; l - lane < NL;
+       l += (int64_t)gridDim.x * BS) {
     const int32_t pt = op.partner[l];
     double r[ND], M[NM], u[ND], D[NB];
     lload<ND>(v.r[0], NL, l, r);
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(kCgBS) void k_ell_first(EllOp op, double reg, EllVe
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  store_block_partial(acc, part_buf(part, 0));
+  store_block_partial<BS>(acc, part_buf(part, 0));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;
     s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
@@ -326,8 +328,10 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
   lload<ND>(v.x, NL, l, in.xx);
 #pragma unroll
   for (int c = 0; c < NB; ++c) in.D[c] = op.D[c * NL + l];
+  if (BLOCK) {
 #pragma unroll
-  for (int c = 0; c < NM; ++c) in.M[c] = v.M[c * NL + l];
+    for (int c = 0; c < NM; ++c) in.M[c] = v.M[c * NL + l];
+  }
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -347,27 +351,27 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
 // remote slot-0 neighbour's record is read from the received records of its
 // pair (an index-dependent load: only waves holding such lanes pay a second
 // round trip), and the lane's record for the peer goes to the send slot.
-template <int ND, bool BLOCK, int PU, bool TRACE = false, bool DIST = false>
-__global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, Slot* slots,
-                                                    const SolveState* st, double* part,
-                                                    unsigned long long* trace, DistVecs dv) {
+template <int ND, bool BLOCK, int PU, bool TRACE, bool DIST, int BS>
+__global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slot* slots,
+                                                 const SolveState* st, double* part,
+                                                 unsigned long long* trace, DistVecs dv) {
   constexpr int NB = Dof<ND>::NB, LW = Dof<ND>::LDSW;
   constexpr int NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
-  constexpr int NW = kCgBS / 64;
+  constexpr int NW = BS / 64;
   __shared__ double lds_u[NW][64][LW];       // fresh u of every lane
   __shared__ double lds_y[NW][64][LW];       // helper partials of A u
   __shared__ double lds_b[NW][64][3 * ND];   // owner r, s, w for helper pushes
-  trace_point<TRACE>(trace, 0, 0.0);
+  trace_point<TRACE, BS>(trace, 0, 0.0);
   const int par = j & 1;
   const int64_t NL = op.NL;
-  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* __restrict__ r_new = v.r[par ^ 1];
   double* __restrict__ s_new = v.s[par ^ 1];
   double* __restrict__ w_new = v.w[par ^ 1];
   double* __restrict__ h_new = v.h[par ^ 1];
 
-  int64_t l = (int64_t)blockIdx.x * kCgBS + threadIdx.x;
+  int64_t l = (int64_t)blockIdx.x * BS + threadIdx.x;
   LaneIn<ND, BLOCK> in;
   if (l - lane < NL) load_lane<ND, BLOCK>(l, par, op, v, in);
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
     wave_gall(dv.gall[par], S);
   else
     wave_partials<PU>(part_buf(part, par), S);
-  trace_point<TRACE>(trace, 1, S[0]);
+  trace_point<TRACE, BS>(trace, 1, S[0]);
 
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
   const double alpha = cs.alpha, beta = cs.beta;
@@ -400,6 +404,16 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
     }
     const int info = group_info(in.code);
     const bool owner = info >= 0;
+    if (!BLOCK) {
+      // PCJACOBI: M = 1 / (K_ii + reg), bitwise k_cg_rhs's dinv (no M load).
+      // A zero diagonal (helper / inert lanes, rows without active elements)
+      // has r = 0 throughout, so M = 0 gives the same u = 0 (and no inf·0).
+#pragma unroll
+      for (int a = 0; a < ND; ++a) {
+        const double d = in.D[ND == 3 ? (a == 0 ? 0 : (a == 1 ? 3 : 5)) : 2 * a];
+        in.M[a] = d != 0.0 ? 1.0 / (d + reg) : 0.0;
+      }
+    }
     double uo[ND], rn[ND], un[ND], sn[ND], pp[ND], xx[ND];
     mapply<ND, BLOCK>(in.M, in.ro, uo);
 #pragma unroll
@@ -516,11 +530,11 @@ __global__ __launch_bounds__(kCgBS) void k_ell_iter(int j, EllOp op, EllVecs v, 
     // the LDS rows are rewritten next pass: all reads of this pass are done
     lds_fence();
   }
-  trace_point<TRACE>(trace, 2, ylast);
-  if (go) store_block_partial(acc, part_buf(part, par ^ 1));
+  trace_point<TRACE, BS>(trace, 2, ylast);
+  if (go) store_block_partial<BS>(acc, part_buf(part, par ^ 1));
   if (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    trace_point<TRACE>(trace, 3, acc[0]);
+    trace_point<TRACE, BS>(trace, 3, acc[0]);
   }
 }
 
@@ -585,8 +599,38 @@ __global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-static dim3 ell_grid(const EllOp& op) { return dim3((unsigned)cg_grid(op.NL)); }
+// ---------------------------------------------------------------------------
+// Launch geometry of the lane kernels.  A launch needs ≥ 256 blocks to put
+// work on every CU (256 CUs in 8 XCDs): the per-CU memory pipe, not HBM, is
+// what a small system saturates (C2: 557 waves in 140 blocks of 256 left 116
+// CUs idle and loaded ≈ 68 KB per busy CU).  So: the largest block (256, 128
+// or 64 threads) whose grid still covers the CUs; block partials ≤ 512.
+// MFEA_ELL_BS=64|128|256 overrides (experiments).
+// ---------------------------------------------------------------------------
+static int env_bs() {
+  static const int v = [] {
+    const char* e = std::getenv("MFEA_ELL_BS");
+    const int b = e ? std::atoi(e) : 0;
+    return (b == 64 || b == 128 || b == 256) ? b : 0;
+  }();
+  return v;
+}
+int ell_block_size(int64_t NL) {
+  if (const int b = env_bs()) return b;
+  for (int b : {256, 128})
+    if ((NL + b - 1) / b >= 256) return b;
+  return 64;
+}
+int64_t ell_grid_size(int64_t NL) {
+  const int b = ell_block_size(NL);
+  const int64_t g = (NL + b - 1) / b;
+  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
+}
+// partial groups of 64 each wave loads: ≥ grid / 64
+static int pu_of(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : g <= 320 ? 5 : 8; }
+
 static dim3 ell_grid_ew(const EllOp& op) { return dim3((unsigned)grid_rows(op.NL > 0 ? op.NL : 1)); }
+static dim3 ell_grid_cg(const EllOp& op) { return dim3((unsigned)cg_grid(op.NL)); }
 
 template <int ND>
 static void init_nd(hipStream_t s, const EllOp& op, const SellOp& sop, int precond,
@@ -602,15 +646,25 @@ void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int prec
   else init_nd<3>(s, op, sop, precond, rv, v);
 }
 
+template <int ND, bool DIST, int BS>
+static void first_bs(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
+                     Slot* slots, double* part, const DistVecs& dv) {
+  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
+                       part, dv);
+  else
+    hipLaunchKernelGGL((k_ell_first<ND, false, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
+                       part, dv);
+}
 template <int ND, bool DIST>
 static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                      Slot* slots, double* part, const DistVecs& dv) {
-  if (precond == 1)
-    hipLaunchKernelGGL((k_ell_first<ND, true, DIST>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v,
-                       slots, part, dv);
-  else
-    hipLaunchKernelGGL((k_ell_first<ND, false, DIST>), ell_grid(op), dim3(kCgBS), 0, s, op, reg, v,
-                       slots, part, dv);
+  switch (ell_block_size(op.NL)) {
+    case 64: first_bs<ND, DIST, 64>(s, op, reg, precond, v, slots, part, dv); break;
+    case 128: first_bs<ND, DIST, 128>(s, op, reg, precond, v, slots, part, dv); break;
+    default: first_bs<ND, DIST, 256>(s, op, reg, precond, v, slots, part, dv); break;
+  }
 }
 void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                       Slot* slots, double* part, const DistVecs* dv) {
@@ -628,9 +682,9 @@ template <int ND>
 static void pack0_nd(hipStream_t s, const EllOp& op, int precond, const EllVecs& v,
                      const DistVecs& dv) {
   if (precond == 1)
-    hipLaunchKernelGGL((k_ell_pack0<ND, true>), ell_grid(op), dim3(kCgBS), 0, s, op, v, dv);
+    hipLaunchKernelGGL((k_ell_pack0<ND, true>), ell_grid_cg(op), dim3(kCgBS), 0, s, op, v, dv);
   else
-    hipLaunchKernelGGL((k_ell_pack0<ND, false>), ell_grid(op), dim3(kCgBS), 0, s, op, v, dv);
+    hipLaunchKernelGGL((k_ell_pack0<ND, false>), ell_grid_cg(op), dim3(kCgBS), 0, s, op, v, dv);
 }
 void launch_ell_pack0(hipStream_t s, const EllOp& op, int precond, const EllVecs& v,
                       const DistVecs& dv) {
@@ -638,53 +692,80 @@ void launch_ell_pack0(hipStream_t s, const EllOp& op, int precond, const EllVecs
   else pack0_nd<3>(s, op, precond, v, dv);
 }
 
-template <int ND, int PU, bool TRACE, bool DIST>
+template <int ND, int PU, bool TRACE, bool DIST, int BS>
 static void iter_launch(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                         Slot* slots, const SolveState* st, double* part,
                         unsigned long long* trace, const DistVecs& dv) {
+  const dim3 grid((unsigned)ell_grid_size(op.NL));
   if (precond == 1)
-    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST>), ell_grid(op), dim3(kCgBS), 0, s, j,
-                       op, v, slots, st, part, trace, dv);
+    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST, BS>), grid, dim3(BS), 0, s, j, op, v,
+                       slots, st, part, trace, dv);
   else
-    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE, DIST>), ell_grid(op), dim3(kCgBS), 0, s, j,
-                       op, v, slots, st, part, trace, dv);
+    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE, DIST, BS>), grid, dim3(BS), 0, s, j, op, v,
+                       slots, st, part, trace, dv);
 }
 
-template <int ND, bool TRACE>
+template <int ND, bool TRACE, int BS>
 static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                     const DistVecs& dv) {
-  const int64_t g = cg_grid(op.NL);
-  if (g <= 64) iter_launch<ND, 1, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
-  else if (g <= 128) iter_launch<ND, 2, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
-  else if (g <= 256) iter_launch<ND, 4, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
-  else iter_launch<ND, 8, TRACE, false>(s, j, op, precond, v, slots, st, part, trace, dv);
+  switch (pu_of(ell_grid_size(op.NL))) {
+    case 1: iter_launch<ND, 1, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    case 2: iter_launch<ND, 2, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    case 4: iter_launch<ND, 4, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    case 5: iter_launch<ND, 5, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    default: iter_launch<ND, 8, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+  }
+}
+
+template <int ND, bool TRACE>
+static void iter_bs(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                    Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
+                    const DistVecs& dv) {
+  switch (ell_block_size(op.NL)) {
+    case 64: iter_pu<ND, TRACE, 64>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    case 128: iter_pu<ND, TRACE, 128>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    default: iter_pu<ND, TRACE, 256>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+  }
+}
+
+template <int ND>
+static void iter_dist(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                      Slot* slots, const SolveState* st, double* part, const DistVecs& dv) {
+  // the rank partial sums replace the block partials: PU unused
+  switch (ell_block_size(op.NL)) {
+    case 64: iter_launch<ND, 1, false, true, 64>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
+    case 128: iter_launch<ND, 1, false, true, 128>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
+    default: iter_launch<ND, 1, false, true, 256>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
+  }
 }
 
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                      Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                      const DistVecs* dv) {
-  if (dv) {  // the rank partial sums replace the block partials: PU unused
-    if (op.nd == 2) iter_launch<2, 1, false, true>(s, j, op, precond, v, slots, st, part, nullptr, *dv);
-    else iter_launch<3, 1, false, true>(s, j, op, precond, v, slots, st, part, nullptr, *dv);
+  if (dv) {
+    if (op.nd == 2) iter_dist<2>(s, j, op, precond, v, slots, st, part, *dv);
+    else iter_dist<3>(s, j, op, precond, v, slots, st, part, *dv);
     return;
   }
   const DistVecs d{};
   if (op.nd == 2) {
-    if (trace) iter_pu<2, true>(s, j, op, precond, v, slots, st, part, trace, d);
-    else iter_pu<2, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
+    if (trace) iter_bs<2, true>(s, j, op, precond, v, slots, st, part, trace, d);
+    else iter_bs<2, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
   } else {
-    if (trace) iter_pu<3, true>(s, j, op, precond, v, slots, st, part, trace, d);
-    else iter_pu<3, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
+    if (trace) iter_bs<3, true>(s, j, op, precond, v, slots, st, part, trace, d);
+    else iter_bs<3, false>(s, j, op, precond, v, slots, st, part, nullptr, d);
   }
 }
 
 void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend) {
-  const int64_t g = cg_grid(NL);
-  if (g <= 64) hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend);
-  else if (g <= 128) hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend);
-  else if (g <= 256) hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend);
-  else hipLaunchKernelGGL(k_psum<8>, dim3(1), dim3(64), 0, s, p, row, gsend);
+  switch (pu_of(ell_grid_size(NL))) {
+    case 1: hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
+    case 2: hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
+    case 4: hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
+    case 5: hipLaunchKernelGGL(k_psum<5>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
+    default: hipLaunchKernelGGL(k_psum<8>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
+  }
 }
 
 void launch_rank_sum(hipStream_t s, const double* g, int world, double* out) {

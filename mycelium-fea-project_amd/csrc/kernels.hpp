@@ -203,6 +203,9 @@ void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, c
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                      Slot* slots, const SolveState* st, double* part,
                      unsigned long long* trace = nullptr, const DistVecs* dv = nullptr);
+// launch geometry of the lane CG kernels (block size 64/128/256, grid ≤ 512)
+int ell_block_size(int64_t NL);
+int64_t ell_grid_size(int64_t NL);
 // x of the owner lanes → row-order x (free rows)
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
 // this partition's block partials of the iteration (parity buffer `p`, the

@@ -59,20 +59,23 @@ def iteration_bytes(info, block):
 
     Lane kernel (ell.hip), nd DOFs per node, NB = 3 (nd 2) or 6 block
     components, NM = nd (Jacobi) or NB (block-Jacobi) M components:
-      per lane read  8·(5·nd + NB + NL_M + 3·NB + 3·nd + NM) + 8 (r s w p x, D,
-                     the lane's M — NL_M = NB for block Jacobi, 0 for Jacobi,
-                     whose M = 1/(D_ii + reg) is formed in registers — three
-                     slot blocks, halo record + its M, code + partner)
+      per lane read  8·(5·nd + NB + NL_M + 3·NB) + 8 (r s w p x, D, the lane's
+                     M — NL_M = NB for block Jacobi, 0 for Jacobi, whose
+                     M = 1/(D_ii + reg) is formed in registers — three slot
+                     blocks, code + partner)
+      per halo lane  read 8·(3·nd + NM) (its compact record: r s w + M of the
+                     out-of-wave neighbour), written 8·3·nd (the record it fills)
+      per wave       read 16 (halo mask + record base)
       per free row   written 8·5·nd (p x s r w)
-      per halo lane  written 8·3·nd (the partner's record)
     SELL kernel (cg.hip): per free row 120 + minv + 120 + 48 + 4 B, per slot 52 B.
     """
     if info["cg_lanes"]:
         nd = 2 if info["planar"] else 3
         nb = 3 if nd == 2 else 6
         nm = nb if block else nd
-        per_lane = 8 * (5 * nd + nb + (nb if block else 0) + 3 * nb + 3 * nd + nm) + 8
-        b = info["n_lanes"] * per_lane + info["n_free_nodes"] * 40 * nd + info["n_halo"] * 24 * nd
+        per_lane = 8 * (5 * nd + nb + (nb if block else 0) + 3 * nb) + 8
+        b = (info["n_lanes"] * per_lane + info["n_lanes"] // 64 * 16 + info["n_free_nodes"] * 40 * nd
+             + info["n_halo"] * (8 * (3 * nd + nm) + 24 * nd))
         return b, f"k_ell_iter (lanes, {nd} DOF/node: update + SpMV + reduction)"
     minv = 48 if block else 24
     b = info["n_free_nodes"] * (120 + minv + 120 + 48 + 4) + info["free_incidences"] * 52

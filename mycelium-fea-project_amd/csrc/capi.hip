@@ -93,8 +93,10 @@ struct Part {
   Ell L;
   bool ell_ok = false;
   DevBuf<uint32_t> e_code;
-  DevBuf<int32_t> e_partner, e_lane_row, e_src_pos, e_nbr_lane;
+  DevBuf<int32_t> e_partner, e_lane_row, e_src_pos, e_nbr_lane, e_hbase;
+  DevBuf<uint64_t> e_hmask;
   DevBuf<double> e_f;  // all lane-operator doubles, carved by ell_op / ell_vecs
+  DevBuf<double> e_fin;  // in-launch reduction of large systems: [2][4] out | partials
   DevBuf<Slot> slots;
   DevBuf<SolveState> state, state_mirror;
   SolveState* mirror = nullptr;  // where k_cg_advance publishes the final state
@@ -151,7 +153,8 @@ struct mfea_handle {
 namespace {
 
 constexpr int kMaxChunk = 64;
-// lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6, h × 2 18, hM 6
+// lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6; plus per
+// compact halo record (ell_vecs): h × 2 18, hM 6
 constexpr int64_t kEllDoubles = 18 + 6 + 3 + 3 + 18 + 6 + 18 + 6;
 static_assert(kEllNone == kSrcNone && kEllHalo == kSrcHalo, "slot source codes");
 static_assert(kGhost == 3, "k_cg_rhs treats code 3 as a ghost free row");
@@ -310,14 +313,23 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(pt.e_lane_row.alloc(NL));
     HIPC(pt.e_src_pos.alloc(3 * NL));
     HIPC(pt.e_nbr_lane.alloc(3 * NL));
-    HIPC(pt.e_f.alloc(kEllDoubles * NL));
+    HIPC(pt.e_f.alloc((kEllDoubles - 24) * NL + 24 * (L.n_hrec + 1)));
     HIPC(up(pt.e_code.ptr, code.data(), NL * sizeof(uint32_t)));
-    HIPC(up(pt.e_partner.ptr, L.partner.data(), NL * sizeof(int32_t)));
+    // the device partner is the record the lane fills: its mirror's record
+    std::vector<int32_t> push(NL);
+    for (int64_t l = 0; l < NL; ++l) push[l] = L.partner[l] >= 0 ? L.hrec[L.partner[l]] : L.partner[l];
+    HIPC(up(pt.e_partner.ptr, push.data(), NL * sizeof(int32_t)));
+    HIPC(pt.e_hmask.alloc(NL / 64));
+    HIPC(pt.e_hbase.alloc(NL / 64));
+    HIPC(up(pt.e_hmask.ptr, L.hmask.data(), NL / 64 * sizeof(uint64_t)));
+    HIPC(up(pt.e_hbase.ptr, L.hbase.data(), NL / 64 * sizeof(int32_t)));
     HIPC(up(pt.e_lane_row.ptr, L.lane_row.data(), NL * sizeof(int32_t)));
     HIPC(up(pt.e_src_pos.ptr, L.src_pos.data(), 3 * NL * sizeof(int32_t)));
     HIPC(up(pt.e_nbr_lane.ptr, L.nbr_lane.data(), 3 * NL * sizeof(int32_t)));
-    // halo records of lanes without a halo slot are read but never used
-    if (NL) HIPC(hipMemsetAsync(pt.e_f.ptr, 0, kEllDoubles * NL * sizeof(double), s));
+    // zero records: a lane without a halo slot reads its neighbour's (unused)
+    if (NL) HIPC(hipMemsetAsync(pt.e_f.ptr, 0, pt.e_f.n * sizeof(double), s));
+    HIPC(pt.e_fin.alloc(8 + 4 * (NL / 64 + 16)));
+    HIPC(hipMemsetAsync(pt.e_fin.ptr, 0, pt.e_fin.n * sizeof(double), s));
   }
   if (dm) {
     const PartPlan& pl = pt.plan;
@@ -458,6 +470,12 @@ EllOp ell_op(const mfea_handle* h, Part& pt) {
   op.nbr_lane = pt.e_nbr_lane.ptr;
   op.V = pt.e_f.ptr;
   op.D = op.V + 18 * NL;
+  op.NR = pt.L.n_hrec + 1;  // + the spare record the last wave's non-halo lanes read
+  op.fin_out = pt.e_fin.ptr;
+  op.fin_part = pt.e_fin.ptr + 8;
+  op.fin_ticket = tix(pt, 8);
+  op.hmask = pt.e_hmask.ptr;
+  op.hbase = pt.e_hbase.ptr;
   return op;
 }
 
@@ -478,9 +496,10 @@ EllVecs ell_vecs(Part& pt) {
     v.w[q] = take(3);
   }
   v.M = take(6);
-  v.h[0] = take(9);
-  v.h[1] = take(9);
-  v.hM = take(6);
+  const int64_t NR = pt.L.n_hrec + 1;  // compact halo records (ell_op)
+  v.h[0] = f;
+  v.h[1] = f + 9 * NR;
+  v.hM = f + 18 * NR;
   return v;
 }
 
@@ -1382,6 +1401,8 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   std::vector<double> pones(4 * kCgMaxPartials, 1.0);
   HIPC(hipMemcpyAsync(pt.cg_part.ptr, pones.data(), pones.size() * sizeof(double),
                       hipMemcpyHostToDevice, s));
+  if (pt.ell_ok) HIPC(hipMemcpyAsync(pt.e_fin.ptr, pones.data(), 4 * sizeof(double),
+                                     hipMemcpyHostToDevice, s));  // FIN: parity-0 sums
   Slot s0;
   std::memset(&s0, 0, sizeof(s0));
   s0.flag = kInit;
@@ -1406,7 +1427,7 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   hipStream_t s = h->stream;
   Part& pt = part0(h);
   const bool ell = use_ell(pt);
-  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes) : cg_grid(pt.P.n_free);
+  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes, ell_fin(pt.L.n_lanes)) : cg_grid(pt.P.n_free);
   const int64_t nw = g * ((ell ? ell_block_size(pt.L.n_lanes) : cg_block_size(0)) / 64);
   if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
   unsigned long long* d = nullptr;

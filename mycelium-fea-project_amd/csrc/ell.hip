@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kCgBS) void k_ell_pack0(EllOp op, EllVecs v, DistVe
 // records (its M is kept in dv.mr for the iterations), and the lane's own
 // parity-0 record goes to its pair's send slot.
 // ---------------------------------------------------------------------------
-template <int ND, bool BLOCK, bool DIST, int BS>
+template <int ND, bool BLOCK, bool DIST, int BS, bool FIN>
 __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
                                                   double* part, DistVecs dv) {
   constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs 
     for (int c = 0; c < NB; ++c) D[c] = op.D[c * NL + l];
     D[0] += reg;
     D[ND == 3 ? 3 : 2] += reg;
-    if (ND == 3) D[5] += reg;
+    if constexpr (ND == 3) D[5] += reg;
     double y[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
@@ -258,16 +258,17 @@ __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs 
     }
 #pragma unroll
     for (int c = 0; c < NM; ++c) Mo[c] = __shfl(M[c], ow, 64);
-    if (pt >= 0) {
+    if (pt >= 0) {  // pt = the compact record this lane fills
       double* h = v.h[0];
+      const int64_t NR = op.NR;
 #pragma unroll
       for (int c = 0; c < ND; ++c) {
-        h[c * NL + pt] = ro[c];
-        h[(3 + c) * NL + pt] = 0.0;
-        h[(6 + c) * NL + pt] = yo[c];
+        h[c * NR + pt] = ro[c];
+        h[(3 + c) * NR + pt] = 0.0;
+        h[(6 + c) * NR + pt] = yo[c];
       }
 #pragma unroll
-      for (int c = 0; c < NM; ++c) v.hM[c * NL + pt] = Mo[c];
+      for (int c = 0; c < NM; ++c) v.hM[c * NR + pt] = Mo[c];
     } else if (DIST && pt <= -2) {
       double* rec = dv.xs[0] + pair_of(pt) * RW;
 #pragma unroll
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs 
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  store_block_partial<BS>(acc, part_buf(part, 0));
+  if (FIN) block_publish<4, BS>(acc, op.fin_part, op.fin_ticket, op.fin_out);
+  else store_block_partial<BS>(acc, part_buf(part, 0));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;
     s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
@@ -338,13 +340,23 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
     for (int c = 0; c < NB; ++c) in.V[k][c] = op.V[(c * 3 + k) * NL + l];
   in.code = op.code[l];
   in.partner = op.partner[l];
+  // Compact halo records: only lanes with an in-partition halo slot own one
+  // (12.7 % of the lanes at C2).  The wave's (mask, base) is one scalar load;
+  // lane i reads record base + #(mask lanes below i) — a lane without a halo
+  // reads its next neighbour's record (unused), so a wave touches exactly its
+  // own contiguous records and every load stays unconditional.
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)((l - lane) >> 6));
+  const uint64_t m = op.hmask[w];
+  const int64_t hi = (int64_t)op.hbase[w] + __popcll(m & ((1ull << lane) - 1ull));
+  const int64_t NR = op.NR;
   const double* __restrict__ h = v.h[par];
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int c = 0; c < ND; ++c) in.h[q * ND + c] = h[(q * 3 + c) * NL + l];
+    for (int c = 0; c < ND; ++c) in.h[q * ND + c] = h[(q * 3 + c) * NR + hi];
 #pragma unroll
-  for (int c = 0; c < NM; ++c) in.hM[c] = v.hM[c * NL + l];
+  for (int c = 0; c < NM; ++c) in.hM[c] = v.hM[c * NR + hi];
 }
 
 // DIST (multi-partition): α, β come from the gathered rank partial sums; a
@@ -379,10 +391,14 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
   const double tol2 = st->tol2, reg = st->reg;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
-  if (DIST)
+  if constexpr (DIST) {
     wave_gall(dv.gall[par], S);
-  else
+  } else if constexpr (PU == 0) {  // FIN: the previous launch's last block reduced them
+#pragma unroll
+    for (int c = 0; c < 4; ++c) S[c] = op.fin_out[4 * par + c];
+  } else {
     wave_partials<PU>(part_buf(part, par), S);
+  }
   trace_point<TRACE, BS>(trace, 1, S[0]);
 
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
@@ -437,7 +453,7 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
     for (int c = 0; c < NB; ++c) D[c] = in.D[c];
     D[0] += reg;
     D[ND == 3 ? 3 : 2] += reg;
-    if (ND == 3) D[5] += reg;
+    if constexpr (ND == 3) D[5] += reg;
     double y[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
@@ -509,11 +525,11 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
       for (int c = 0; c < 3 * ND; ++c) rsy[c] = lds_b[wv][ow][c];
     }
     if (go && in.partner >= 0) {
-      const int64_t pt = in.partner;
+      const int64_t pt = in.partner, NR = op.NR;
 #pragma unroll
       for (int q = 0; q < 3; ++q)
 #pragma unroll
-        for (int c = 0; c < ND; ++c) h_new[(q * 3 + c) * NL + pt] = rsy[q * ND + c];
+        for (int c = 0; c < ND; ++c) h_new[(q * 3 + c) * NR + pt] = rsy[q * ND + c];
     }
     if (DIST && go && in.partner <= -2) {
       double* __restrict__ rec = dv.xs[par ^ 1] + pair_of(in.partner) * RW;
@@ -531,7 +547,12 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
     lds_fence();
   }
   trace_point<TRACE, BS>(trace, 2, ylast);
-  if (go) store_block_partial<BS>(acc, part_buf(part, par ^ 1));
+  if (go) {
+    if (PU == 0 && !DIST)
+      block_publish<4, BS>(acc, op.fin_part, op.fin_ticket, op.fin_out + 4 * (par ^ 1));
+    else
+      store_block_partial<BS>(acc, part_buf(part, par ^ 1));
+  }
   if (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     trace_point<TRACE, BS>(trace, 3, acc[0]);
@@ -605,15 +626,13 @@ __global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restric
 // what a small system saturates (C2: 557 waves in 140 blocks of 256 left 116
 // CUs idle and loaded ≈ 68 KB per busy CU).  So: the largest block (256, 128
 // or 64 threads) whose grid still covers the CUs; block partials ≤ 512.
-// MFEA_ELL_BS=64|128|256 overrides (experiments).
+// MFEA_ELL_BS=64|128|256 overrides (experiments; fixed for a handle's life:
+// its captured graphs keep the geometry they were built with).
 // ---------------------------------------------------------------------------
 static int env_bs() {
-  static const int v = [] {
-    const char* e = std::getenv("MFEA_ELL_BS");
-    const int b = e ? std::atoi(e) : 0;
-    return (b == 64 || b == 128 || b == 256) ? b : 0;
-  }();
-  return v;
+  const char* e = std::getenv("MFEA_ELL_BS");
+  const int b = e ? std::atoi(e) : 0;
+  return (b == 64 || b == 128 || b == 256) ? b : 0;
 }
 int ell_block_size(int64_t NL) {
   if (const int b = env_bs()) return b;
@@ -621,12 +640,22 @@ int ell_block_size(int64_t NL) {
     if ((NL + b - 1) / b >= 256) return b;
   return 64;
 }
-int64_t ell_grid_size(int64_t NL) {
+// Past 512 blocks a capped grid makes every wave loop over several passes,
+// each a serialised load → compute → store round trip (C5, 15 M lanes: 116
+// passes, 2.2 ms per launch at a quarter of HBM bandwidth).  There the grid
+// covers the lanes once and the last block finishes the reduction instead.
+// MFEA_ELL_FIN=0|1 overrides.
+bool ell_fin(int64_t NL) {
+  if (const char* e = std::getenv("MFEA_ELL_FIN")) return std::atoi(e) != 0;
+  const int b = ell_block_size(NL);
+  return (NL + b - 1) / b > kCgMaxG;
+}
+int64_t ell_grid_size(int64_t NL, bool fin) {
   const int b = ell_block_size(NL);
   const int64_t g = (NL + b - 1) / b;
-  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
+  return g < 1 ? 1 : ((!fin && g > kCgMaxG) ? kCgMaxG : g);
 }
-// partial groups of 64 each wave loads: ≥ grid / 64
+// partial groups of 64 each wave loads: ≥ grid / 64 (0: FIN, none)
 static int pu_of(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : g <= 320 ? 5 : 8; }
 
 static dim3 ell_grid_ew(const EllOp& op) { return dim3((unsigned)grid_rows(op.NL > 0 ? op.NL : 1)); }
@@ -646,16 +675,22 @@ void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int prec
   else init_nd<3>(s, op, sop, precond, rv, v);
 }
 
+template <int ND, bool DIST, int BS, bool FIN>
+static void first_fin(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
+                      Slot* slots, double* part, const DistVecs& dv) {
+  const dim3 grid((unsigned)ell_grid_size(op.NL, FIN));
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS, FIN>), grid, dim3(BS), 0, s, op, reg, v,
+                       slots, part, dv);
+  else
+    hipLaunchKernelGGL((k_ell_first<ND, false, DIST, BS, FIN>), grid, dim3(BS), 0, s, op, reg, v,
+                       slots, part, dv);
+}
 template <int ND, bool DIST, int BS>
 static void first_bs(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                      Slot* slots, double* part, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL));
-  if (precond == 1)
-    hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
-                       part, dv);
-  else
-    hipLaunchKernelGGL((k_ell_first<ND, false, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
-                       part, dv);
+  if (!DIST && ell_fin(op.NL)) first_fin<ND, false, BS, true>(s, op, reg, precond, v, slots, part, dv);
+  else first_fin<ND, DIST, BS, false>(s, op, reg, precond, v, slots, part, dv);
 }
 template <int ND, bool DIST>
 static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
@@ -696,7 +731,7 @@ template <int ND, int PU, bool TRACE, bool DIST, int BS>
 static void iter_launch(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                         Slot* slots, const SolveState* st, double* part,
                         unsigned long long* trace, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  const dim3 grid((unsigned)ell_grid_size(op.NL, PU == 0 && !DIST));
   if (precond == 1)
     hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST, BS>), grid, dim3(BS), 0, s, j, op, v,
                        slots, st, part, trace, dv);
@@ -709,7 +744,11 @@ template <int ND, bool TRACE, int BS>
 static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                     const DistVecs& dv) {
-  switch (pu_of(ell_grid_size(op.NL))) {
+  if (ell_fin(op.NL)) {
+    iter_launch<ND, 0, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv);
+    return;
+  }
+  switch (pu_of(ell_grid_size(op.NL, false))) {
     case 1: iter_launch<ND, 1, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 2: iter_launch<ND, 2, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 4: iter_launch<ND, 4, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
@@ -759,7 +798,7 @@ void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const E
 }
 
 void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend) {
-  switch (pu_of(ell_grid_size(NL))) {
+  switch (pu_of(ell_grid_size(NL, false))) {  // the partitioned iteration's grid
     case 1: hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 2: hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 4: hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend); break;

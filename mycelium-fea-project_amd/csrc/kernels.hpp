@@ -158,13 +158,22 @@ struct EllOp {
   int64_t NL;                // lanes, multiple of 64
   int nd;                    // DOFs per node in the lanes: 2 (planar mesh) or 3
   const uint32_t* code;      // bytes 0..2: slot sources; byte 3: int8 group info
-  const int32_t* partner;    // halo push target of slot 0, -1
+  const int32_t* partner;    // slot-0 halo push: compact record index, -1 none,
+                             // -2 - pair for a cross-partition record
   const int32_t* lane_row;   // owner lane → free row, -1
   const int32_t* src_pos;    // [3][NL] SELL position of each slot, -1
   const int32_t* nbr_lane;   // [3][NL] neighbour owner lane (first iteration only)
   double* V;                 // [NB][3][NL] slot blocks (component c, slot k: (c·3+k)·NL)
   double* D;                 // [NB][NL] diagonal block (unregularised), 0 off owners
                              // NB = 6 (xx xy xz yy yz zz) or, nd = 2, 3 (xx xy yy)
+  // large systems (grid > 512 blocks, one pass per wave): the grid reduction
+  // is finished in-launch by the last block (device_util.hpp block_publish)
+  double* fin_part;          // [4][grid + 8] block / shard partials
+  unsigned* fin_ticket;      // one ticket set
+  double* fin_out;           // [2][4] reduced (γ, δ, ‖r‖², ‖u‖²) by parity
+  int64_t NR;                // compact halo records (+1 spare), stride of h / hM
+  const uint64_t* hmask;     // [NL/64] lanes of each wave owning a halo record
+  const int32_t* hbase;      // [NL/64] the wave's first record
 };
 struct EllVecs {  // component c of a lane vector at [c·NL + lane], c < nd
   double* x;      // [3][NL]
@@ -173,8 +182,8 @@ struct EllVecs {  // component c of a lane vector at [c·NL + lane], c < nd
   double* s[2];
   double* w[2];
   double* M;      // [3|6][NL] Jacobi / block-Jacobi inverse, 0 off owners
-  double* h[2];   // [9][NL] halo records by parity: r, s, w of the slot-0 neighbour at (q·3+c)·NL
-  double* hM;     // [3|6][NL] halo record of the slot-0 neighbour's M
+  double* h[2];   // [9][NR] halo records by parity: r, s, w of the slot-0 neighbour at (q·3+c)·NR
+  double* hM;     // [3|6][NR] halo record of the slot-0 neighbour's M
 };
 // ---- multi-partition CG (partition.hpp; one partition per GPU) -------------
 // Cross-partition halo records, pair k (partition.hpp) at rec[k·RW + q·nd + c]
@@ -203,9 +212,12 @@ void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, c
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                      Slot* slots, const SolveState* st, double* part,
                      unsigned long long* trace = nullptr, const DistVecs* dv = nullptr);
-// launch geometry of the lane CG kernels (block size 64/128/256, grid ≤ 512)
+// launch geometry of the lane CG kernels: block size 64/128/256; grid ≤ 512
+// with block partials re-reduced by every wave of the next launch, or, for
+// large systems (ell_fin), one pass per wave with the in-launch reduction
 int ell_block_size(int64_t NL);
-int64_t ell_grid_size(int64_t NL);
+bool ell_fin(int64_t NL);
+int64_t ell_grid_size(int64_t NL, bool fin);
 // x of the owner lanes → row-order x (free rows)
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
 // this partition's block partials of the iteration (parity buffer `p`, the

@@ -313,6 +313,22 @@ std::string build_ell(const Pattern& P, Ell& L, const std::vector<int32_t>* elem
     if (mirror < 0 || (L.code[mirror] & 0xFF) != kEllHalo) return "internal: halo mirror missing";
     L.partner[l] = mirror;
   }
+  const int64_t nw = n_lanes / kSlice;
+  L.hrec.assign(n_lanes, -1);
+  L.hmask.assign(nw, 0);
+  L.hbase.assign(nw, 0);
+  int64_t nr = 0;
+  for (int64_t w = 0; w < nw; ++w) {
+    L.hbase[w] = (int32_t)nr;
+    for (int t = 0; t < kSlice; ++t) {
+      const int64_t l = w * kSlice + t;
+      if ((L.code[l] & 0xFF) == kEllHalo && L.partner[l] >= 0) {
+        L.hmask[w] |= 1ull << t;
+        L.hrec[l] = (int32_t)nr++;
+      }
+    }
+  }
+  L.n_hrec = nr;
   return "";
 }
 

@@ -86,6 +86,11 @@ struct Ell {
   std::vector<int32_t> partner;   // push target lane of slot 0 (halo), -1
   std::vector<int32_t> src_pos;   // [k][n_lanes] SELL position of the slot, -1
   std::vector<int32_t> nbr_lane;  // [k][n_lanes] owner lane of the neighbour, -1
+  // compact halo records: the in-partition halo lanes, numbered in lane order
+  int64_t n_hrec = 0;
+  std::vector<int32_t> hrec;      // per lane: its record index, -1
+  std::vector<uint64_t> hmask;    // per wave: lanes owning a record
+  std::vector<int32_t> hbase;     // per wave: index of its first record
 };
 
 // Builds the lanes for P's free rows.  Returns "" on success.

@@ -415,3 +415,35 @@ def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
     assert st2.status == 0 and st3.status == 0 and st2.iters == st3.iters
     assert np.array_equal(U2, U3)
     assert np.all(U2[2::3] == 0.0)
+
+
+# ---------------------------------------------------------------------------
+# launch geometries of the lane kernel (ell.hip): block size 64/128/256 and the
+# in-launch reduction of large systems (FIN: one pass per wave, the last block
+# finishes the grid reduction) forced on a small system — same iterates up to
+# summation order, each geometry bitwise reproducible
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("bs,fin,precond", [(64, "1", 0), (128, "0", 0), (256, "1", 0), (128, "1", 1)])
+def test_lane_geometries_match_direct(monkeypatch, bs, fin, precond):
+    from mfea import Engine, make_opts
+    monkeypatch.setenv("MFEA_ELL_BS", str(bs))
+    monkeypatch.setenv("MFEA_ELL_FIN", fin)
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    eng = Engine(0)
+    try:
+        _sim181147(eng)
+        eng.assemble()
+        dy = float(sysz["dy"])
+        st = eng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=200000, precond=precond))
+        U = eng.displacement()
+        assert st.status == 0 and rel(U, sysz["U"]) <= 1e-10
+        eng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=200000, precond=precond))
+        assert np.array_equal(U, eng.displacement())
+        if precond == 0:
+            s8 = eng.solve(dy, -dy, make_opts(rtol=1e-8))
+            assert abs(s8.iters - int(sysz["pcg_iters_1e8"])) <= 3
+        # one full step with failures on the geometry: same records as the default
+        f, n, _ = eng.step(dy, -dy, make_opts(rtol=1e-13, max_it=200000, precond=precond), 0.018)
+        assert n == eng.active().sum()
+    finally:
+        eng.close()

@@ -63,9 +63,11 @@ def iteration_bytes(info, block):
                      M — NL_M = NB for block Jacobi, 0 for Jacobi, whose
                      M = 1/(D_ii + reg) is formed in registers — three slot
                      blocks, code + partner)
-      per halo lane  read 8·(3·nd + NM) (its compact record: r s w + M of the
-                     out-of-wave neighbour), written 8·3·nd (the record it fills)
-      per wave       read 16 (halo mask + record base)
+      halo records   read 8·(3·nd + NM) (r s w + M of the out-of-wave
+                     neighbour) by every lane (one record per lane, small
+                     systems) or by halo lanes only + 16 B per wave (mask and
+                     base; compact records, large systems); written 8·3·nd per
+                     halo lane (the record it fills)
       per free row   written 8·5·nd (p x s r w)
     SELL kernel (cg.hip): per free row 120 + minv + 120 + 48 + 4 B, per slot 52 B.
     """
@@ -74,8 +76,13 @@ def iteration_bytes(info, block):
         nb = 3 if nd == 2 else 6
         nm = nb if block else nd
         per_lane = 8 * (5 * nd + nb + (nb if block else 0) + 3 * nb) + 8
-        b = (info["n_lanes"] * per_lane + info["n_lanes"] // 64 * 16 + info["n_free_nodes"] * 40 * nd
-             + info["n_halo"] * (8 * (3 * nd + nm) + 24 * nd))
+        rec = 8 * (3 * nd + nm)  # a halo record r s w + M
+        if info["halo_compact"]:  # only halo lanes read one; + mask and base per wave
+            reads = info["n_halo"] * rec + info["n_lanes"] // 64 * 16
+        else:                     # one record per lane, read by every lane
+            reads = info["n_lanes"] * rec
+        b = (info["n_lanes"] * per_lane + reads + info["n_free_nodes"] * 40 * nd
+             + info["n_halo"] * 24 * nd)
         return b, f"k_ell_iter (lanes, {nd} DOF/node: update + SpMV + reduction)"
     minv = 48 if block else 24
     b = info["n_free_nodes"] * (120 + minv + 120 + 48 + 4) + info["free_incidences"] * 52
@@ -107,40 +114,62 @@ def main():
     from mfea.synth import CONFIGS
     import fea_solver as fs
 
-    nx, ny = CONFIGS[a.config]
+    nx0, ny = CONFIGS[a.config]
     mode = a.mode if world > 1 else ("parts" if a.parts > 1 else "1gpu")
     note = None
-    eng = Engine(local)
-    if mode == "partitioned":
-        nx *= world  # weak scaling: one tile column (≈ the 1-GPU network) per GPU
-        try:
-            uid = [dist_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            eng.dist_init(rank, world, uid[0])
-            eng.set_partition_axis(0)
-        except Exception as ex:  # noqa: BLE001  (reported in the JSON, then replicas)
-            note = f"partitioned init failed ({ex}); replicas instead"
-            mode, nx = "replicas", nx // world
-            eng.close()
-            eng = Engine(local)
-    elif mode == "parts":
-        eng.set_parts(a.parts, 0)
-    xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
-    top, bot = synth.grips(xyz)
-    n_dof = 3 * len(xyz)
-
-    eng.set_material(fs.E_mod, fs.A, fs.I)
-    eng.set_mesh(xyz, e2n)
-    eng.set_bc(top, bot)
-    eng.set_active(None)
-    info = eng.info()
     dy = fs.DISPLACEMENT_MAX * a.load_step / (fs.N_STEPS - 1)
     pc = PC_BLOCK_JACOBI if a.precond == "bjacobi" else PC_JACOBI
     opts = make_opts(rtol=a.rtol, max_it=200000, precond=pc)
 
-    def one_step():
+    def setup(mode):
+        """engine + resident mesh for one mode; returns (eng, nx, xyz, e2n, top, bot)"""
+        nx = nx0 * world if mode == "partitioned" else nx0  # weak scaling: a tile column per GPU
+        eng = Engine(local)
+        if mode == "partitioned":
+            uid = [dist_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            eng.dist_init(rank, world, uid[0])
+            eng.set_partition_axis(0)
+        elif mode == "parts":
+            eng.set_parts(a.parts, 0)
+        xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
+        top, bot = synth.grips(xyz)
+        eng.set_material(fs.E_mod, fs.A, fs.I)
+        eng.set_mesh(xyz, e2n)
+        eng.set_bc(top, bot)
+        eng.set_active(None)
+        return eng, nx, xyz, e2n, top, bot
+
+    def run_step(eng):
         eng.set_active(None)                       # every step starts from the intact mesh
         return eng.step(dy, -dy, opts, fs.MAX_STRAIN)
+
+    if mode == "partitioned":
+        # one probing step over RCCL; every rank must succeed, or all fall back
+        # to independent replicas (agreed over gloo) — the line reports which
+        ok, err = 1, ""
+        eng = None
+        try:
+            eng, nx, xyz, e2n, top, bot = setup(mode)
+            run_step(eng)
+        except Exception as ex:  # noqa: BLE001
+            ok, err = 0, str(ex)
+        import torch
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            note = f"partitioned solve failed on some rank ({err or 'peer'}); replicas instead"
+            if eng is not None:
+                eng.close()
+            mode = "replicas"
+            eng, nx, xyz, e2n, top, bot = setup(mode)
+    else:
+        eng, nx, xyz, e2n, top, bot = setup(mode)
+    n_dof = 3 * len(xyz)
+    info = eng.info()
+
+    def one_step():
+        return run_step(eng)
 
     def barrier_sync():
         if dist is not None:
@@ -214,6 +243,7 @@ def main():
             "n_dof": n_dof, "n_free_dof": st.n_free, "n_elems": len(e2n),
             "precond": a.precond, "rtol": a.rtol, "parallelism": parallelism,
             "cg_kernel": "lanes" if info["cg_lanes"] else "sell", "n_lanes": info["n_lanes"],
+            "lane_geometry": {"block": info["block_size"], "grid": info["grid"], "halo_records": "compact" if info["halo_compact"] else "per lane"},
             "rank0_part": {"free_dof": 3 * nf, "n_pairs": info["n_pairs"], "n_ghost": info["n_ghost"]},
         },
         "cg_iters": iters,

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 3
+#define MFEA_ABI_VERSION 4
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -159,6 +159,9 @@ typedef struct {
   int32_t part;             /* this handle's (first) partition                         */
   int64_t n_pairs;          /* cut free-free elements of that partition (records/iter)  */
   int64_t n_ghost;          /* its ghost rows (other partitions' nodes)                */
+  int32_t halo_compact;     /* lane operator: 1 compact halo records, 0 one per lane   */
+  int32_t block_size;       /* lane CG kernels: threads per block                      */
+  int64_t grid;             /* lane CG kernels: blocks per launch                      */
 } mfea_info;
 int mfea_get_info(mfea_handle* h, mfea_info* info);
 /* Launches the dominant kernel — the fused SpMV + single-reduction CG iteration —

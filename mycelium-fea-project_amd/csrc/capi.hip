@@ -92,11 +92,11 @@ struct Part {
   // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
   Ell L;
   bool ell_ok = false;
+  bool ell_hc = false;  // compact halo records (ell_op)
   DevBuf<uint32_t> e_code;
   DevBuf<int32_t> e_partner, e_lane_row, e_src_pos, e_nbr_lane, e_hbase;
   DevBuf<uint64_t> e_hmask;
   DevBuf<double> e_f;  // all lane-operator doubles, carved by ell_op / ell_vecs
-  DevBuf<double> e_fin;  // in-launch reduction of large systems: [2][4] out | partials
   DevBuf<Slot> slots;
   DevBuf<SolveState> state, state_mirror;
   SolveState* mirror = nullptr;  // where k_cg_advance publishes the final state
@@ -313,11 +313,19 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(pt.e_lane_row.alloc(NL));
     HIPC(pt.e_src_pos.alloc(3 * NL));
     HIPC(pt.e_nbr_lane.alloc(3 * NL));
-    HIPC(pt.e_f.alloc((kEllDoubles - 24) * NL + 24 * (L.n_hrec + 1)));
+    HIPC(pt.e_f.alloc((kEllDoubles - 24) * NL + 24 * std::max<int64_t>(NL, L.n_hrec + 1)));
     HIPC(up(pt.e_code.ptr, code.data(), NL * sizeof(uint32_t)));
-    // the device partner is the record the lane fills: its mirror's record
+    // Halo record layout (ell.hip load_lane): compact (measured on one box:
+    // C3 21.8 vs 23.7 µs per iteration, C2 41.6 vs 41.7 ms per step) or one
+    // per lane (MFEA_ELL_HC=0).  The device partner is the record the lane
+    // fills: its mirror lane's record.
+    {
+      const char* e = std::getenv("MFEA_ELL_HC");
+      pt.ell_hc = e ? std::atoi(e) != 0 : true;
+    }
     std::vector<int32_t> push(NL);
-    for (int64_t l = 0; l < NL; ++l) push[l] = L.partner[l] >= 0 ? L.hrec[L.partner[l]] : L.partner[l];
+    for (int64_t l = 0; l < NL; ++l)
+      push[l] = L.partner[l] >= 0 ? (pt.ell_hc ? L.hrec[L.partner[l]] : L.partner[l]) : L.partner[l];
     HIPC(up(pt.e_partner.ptr, push.data(), NL * sizeof(int32_t)));
     HIPC(pt.e_hmask.alloc(NL / 64));
     HIPC(pt.e_hbase.alloc(NL / 64));
@@ -328,8 +336,6 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(up(pt.e_nbr_lane.ptr, L.nbr_lane.data(), 3 * NL * sizeof(int32_t)));
     // zero records: a lane without a halo slot reads its neighbour's (unused)
     if (NL) HIPC(hipMemsetAsync(pt.e_f.ptr, 0, pt.e_f.n * sizeof(double), s));
-    HIPC(pt.e_fin.alloc(8 + 4 * (NL / 64 + 16)));
-    HIPC(hipMemsetAsync(pt.e_fin.ptr, 0, pt.e_fin.n * sizeof(double), s));
   }
   if (dm) {
     const PartPlan& pl = pt.plan;
@@ -413,10 +419,17 @@ int ensure_built(mfea_handle* h) {
   return 0;
 }
 
-// MFEA_CG_KERNEL=sell forces the SELL iteration kernel (comparison runs)
+// The lane operator pays off while most rows fit one lane.  Dense networks
+// (C5: mean degree 7.5 → 4.5 lanes per free row, most of them helpers that
+// move zeros) run the SELL kernel instead: measured 0.94 vs 2.16 ms per
+// iteration at 10 M DOF.  The partitioned path always runs lanes.
+// MFEA_CG_KERNEL=sell|lanes forces one (comparison runs).
 bool use_ell(const Part& pt) {
+  if (!pt.ell_ok) return false;
   const char* e = std::getenv("MFEA_CG_KERNEL");
-  return pt.ell_ok && !(e && std::strcmp(e, "sell") == 0);
+  if (e && std::strcmp(e, "sell") == 0) return false;
+  if (e && std::strcmp(e, "lanes") == 0) return true;
+  return pt.L.n_lanes <= 2 * std::max<int64_t>(pt.P.n_free, 1);
 }
 
 mfea_solve_opts default_opts() {
@@ -458,6 +471,9 @@ CgVecs cg_vecs(Part& pt) {
   return v;
 }
 
+// stride of the halo record arrays: compact records + a spare, or one per lane
+int64_t ell_nr(const Part& pt) { return pt.ell_hc ? pt.L.n_hrec + 1 : pt.L.n_lanes; }
+
 EllOp ell_op(const mfea_handle* h, Part& pt) {
   EllOp op;
   const int64_t NL = pt.L.n_lanes;
@@ -470,10 +486,8 @@ EllOp ell_op(const mfea_handle* h, Part& pt) {
   op.nbr_lane = pt.e_nbr_lane.ptr;
   op.V = pt.e_f.ptr;
   op.D = op.V + 18 * NL;
-  op.NR = pt.L.n_hrec + 1;  // + the spare record the last wave's non-halo lanes read
-  op.fin_out = pt.e_fin.ptr;
-  op.fin_part = pt.e_fin.ptr + 8;
-  op.fin_ticket = tix(pt, 8);
+  op.hc = pt.ell_hc ? 1 : 0;
+  op.NR = ell_nr(pt);
   op.hmask = pt.e_hmask.ptr;
   op.hbase = pt.e_hbase.ptr;
   return op;
@@ -496,7 +510,7 @@ EllVecs ell_vecs(Part& pt) {
     v.w[q] = take(3);
   }
   v.M = take(6);
-  const int64_t NR = pt.L.n_hrec + 1;  // compact halo records (ell_op)
+  const int64_t NR = ell_nr(pt);
   v.h[0] = f;
   v.h[1] = f + 9 * NR;
   v.hM = f + 18 * NR;
@@ -1369,6 +1383,11 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
   info->part = pt.rank;
   info->n_pairs = pt.plan.n_pairs;
   info->n_ghost = P.n_ghost;
+  if (pt.ell_ok) {
+    info->halo_compact = pt.ell_hc ? 1 : 0;
+    info->block_size = ell_block_size(pt.L.n_lanes);
+    info->grid = ell_grid_size(pt.L.n_lanes);
+  }
   return 0;
 }
 
@@ -1401,8 +1420,6 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   std::vector<double> pones(4 * kCgMaxPartials, 1.0);
   HIPC(hipMemcpyAsync(pt.cg_part.ptr, pones.data(), pones.size() * sizeof(double),
                       hipMemcpyHostToDevice, s));
-  if (pt.ell_ok) HIPC(hipMemcpyAsync(pt.e_fin.ptr, pones.data(), 4 * sizeof(double),
-                                     hipMemcpyHostToDevice, s));  // FIN: parity-0 sums
   Slot s0;
   std::memset(&s0, 0, sizeof(s0));
   s0.flag = kInit;
@@ -1427,7 +1444,7 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   hipStream_t s = h->stream;
   Part& pt = part0(h);
   const bool ell = use_ell(pt);
-  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes, ell_fin(pt.L.n_lanes)) : cg_grid(pt.P.n_free);
+  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes) : cg_grid(pt.P.n_free);
   const int64_t nw = g * ((ell ? ell_block_size(pt.L.n_lanes) : cg_block_size(0)) / 64);
   if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
   unsigned long long* d = nullptr;

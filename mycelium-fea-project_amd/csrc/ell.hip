@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kCgBS) void k_ell_pack0(EllOp op, EllVecs v, DistVe
 // records (its M is kept in dv.mr for the iterations), and the lane's own
 // parity-0 record goes to its pair's send slot.
 // ---------------------------------------------------------------------------
-template <int ND, bool BLOCK, bool DIST, int BS, bool FIN>
+template <int ND, bool BLOCK, bool DIST, int BS>
 __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs v, Slot* slots,
                                                   double* part, DistVecs dv) {
   constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>(), RW = 3 * ND;
@@ -286,8 +286,7 @@ __global__ __launch_bounds__(BS) void k_ell_first(EllOp op, double reg, EllVecs 
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  if (FIN) block_publish<4, BS>(acc, op.fin_part, op.fin_ticket, op.fin_out);
-  else store_block_partial<BS>(acc, part_buf(part, 0));
+  store_block_partial<BS>(acc, part_buf(part, 0));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;
     s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
@@ -318,7 +317,7 @@ struct LaneIn {
   int32_t partner;
 };
 
-template <int ND, bool BLOCK>
+template <int ND, bool BLOCK, bool HC>
 __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, const EllVecs& v,
                                           LaneIn<ND, BLOCK>& in) {
   constexpr int NB = Dof<ND>::NB, NM = n_minv<ND, BLOCK>();
@@ -340,15 +339,22 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
     for (int c = 0; c < NB; ++c) in.V[k][c] = op.V[(c * 3 + k) * NL + l];
   in.code = op.code[l];
   in.partner = op.partner[l];
-  // Compact halo records: only lanes with an in-partition halo slot own one
-  // (12.7 % of the lanes at C2).  The wave's (mask, base) is one scalar load;
-  // lane i reads record base + #(mask lanes below i) — a lane without a halo
-  // reads its next neighbour's record (unused), so a wave touches exactly its
-  // own contiguous records and every load stays unconditional.
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane((int)((l - lane) >> 6));
-  const uint64_t m = op.hmask[w];
-  const int64_t hi = (int64_t)op.hbase[w] + __popcll(m & ((1ull << lane) - 1ull));
+  // Halo records.  Compact (op.hc, large systems): only lanes with an
+  // in-partition halo slot own one (12.7 % of the lanes on the tiled meshes).
+  // The wave's (mask, base) is one scalar load; lane i reads record base +
+  // #(mask lanes below i) — a lane without a halo reads its next neighbour's
+  // record (unused), so a wave touches exactly its own contiguous records and
+  // every load stays unconditional.  The scalar hop overlaps the lane's other
+  // loads (C2 unchanged) and the bytes saved shorten a bandwidth-bound launch
+  // (C3 −8 %).  Per lane records (op.hc = 0, indexed by the lane) remain for
+  // comparison runs.
+  int64_t hi = l;
+  if constexpr (HC) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)((l - lane) >> 6));
+    const uint64_t m = op.hmask[w];
+    hi = (int64_t)op.hbase[w] + __popcll(m & ((1ull << lane) - 1ull));
+  }
   const int64_t NR = op.NR;
   const double* __restrict__ h = v.h[par];
 #pragma unroll
@@ -363,7 +369,7 @@ __device__ __forceinline__ void load_lane(int64_t l, int par, const EllOp& op, c
 // remote slot-0 neighbour's record is read from the received records of its
 // pair (an index-dependent load: only waves holding such lanes pay a second
 // round trip), and the lane's record for the peer goes to the send slot.
-template <int ND, bool BLOCK, int PU, bool TRACE, bool DIST, int BS>
+template <int ND, bool BLOCK, int PU, bool TRACE, bool DIST, int BS, bool HC>
 __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slot* slots,
                                                  const SolveState* st, double* part,
                                                  unsigned long long* trace, DistVecs dv) {
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
 
   int64_t l = (int64_t)blockIdx.x * BS + threadIdx.x;
   LaneIn<ND, BLOCK> in;
-  if (l - lane < NL) load_lane<ND, BLOCK>(l, par, op, v, in);
+  if (l - lane < NL) load_lane<ND, BLOCK, HC>(l, par, op, v, in);
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
   const double g0 = slots[j].v[0], a0 = slots[j].alpha;
   const double tol2 = st->tol2, reg = st->reg;
@@ -393,9 +399,6 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
   double S[4];
   if constexpr (DIST) {
     wave_gall(dv.gall[par], S);
-  } else if constexpr (PU == 0) {  // FIN: the previous launch's last block reduced them
-#pragma unroll
-    for (int c = 0; c < 4; ++c) S[c] = op.fin_out[4 * par + c];
   } else {
     wave_partials<PU>(part_buf(part, par), S);
   }
@@ -409,7 +412,7 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   double ylast = 0.0;
   for (bool first = true; l - lane < NL; l += stride, first = false) {  // wave-uniform
-    if (!first) load_lane<ND, BLOCK>(l, par, op, v, in);
+    if (!first) load_lane<ND, BLOCK, HC>(l, par, op, v, in);
     if (DIST && in.partner <= -2) {
       const int64_t k = pair_of(in.partner);
       const double* __restrict__ rec = dv.xr[par] + k * RW;
@@ -547,12 +550,7 @@ __global__ __launch_bounds__(BS) void k_ell_iter(int j, EllOp op, EllVecs v, Slo
     lds_fence();
   }
   trace_point<TRACE, BS>(trace, 2, ylast);
-  if (go) {
-    if (PU == 0 && !DIST)
-      block_publish<4, BS>(acc, op.fin_part, op.fin_ticket, op.fin_out + 4 * (par ^ 1));
-    else
-      store_block_partial<BS>(acc, part_buf(part, par ^ 1));
-  }
+  if (go) store_block_partial<BS>(acc, part_buf(part, par ^ 1));
   if (TRACE) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     trace_point<TRACE, BS>(trace, 3, acc[0]);
@@ -621,41 +619,26 @@ __global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restric
 
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
-// Launch geometry of the lane kernels.  A launch needs ≥ 256 blocks to put
-// work on every CU (256 CUs in 8 XCDs): the per-CU memory pipe, not HBM, is
-// what a small system saturates (C2: 557 waves in 140 blocks of 256 left 116
-// CUs idle and loaded ≈ 68 KB per busy CU).  So: the largest block (256, 128
-// or 64 threads) whose grid still covers the CUs; block partials ≤ 512.
-// MFEA_ELL_BS=64|128|256 overrides (experiments; fixed for a handle's life:
-// its captured graphs keep the geometry they were built with).
+// Launch geometry of the lane kernels: 256-thread blocks, at most 512 of them
+// (each wave of the next launch re-reads every block partial).  Measured on
+// one box (C2, per iteration of the real solve): 6.09 µs at 256 threads vs
+// 6.36 at 128 (grid over all 256 CUs) and 6.54 at 64.  An in-launch grid
+// reduction by the last block (no cap, one pass per wave) was slower at C3
+// (22.5 vs 20.2 µs: its tail costs more than the passes save) and was
+// dropped.  MFEA_ELL_BS=64|128|256 overrides the block size (experiments;
+// fixed for a handle's life: its captured graphs keep their geometry).
 // ---------------------------------------------------------------------------
-static int env_bs() {
+int ell_block_size(int64_t) {
   const char* e = std::getenv("MFEA_ELL_BS");
   const int b = e ? std::atoi(e) : 0;
-  return (b == 64 || b == 128 || b == 256) ? b : 0;
+  return (b == 64 || b == 128) ? b : 256;
 }
-int ell_block_size(int64_t NL) {
-  if (const int b = env_bs()) return b;
-  for (int b : {256, 128})
-    if ((NL + b - 1) / b >= 256) return b;
-  return 64;
-}
-// Past 512 blocks a capped grid makes every wave loop over several passes,
-// each a serialised load → compute → store round trip (C5, 15 M lanes: 116
-// passes, 2.2 ms per launch at a quarter of HBM bandwidth).  There the grid
-// covers the lanes once and the last block finishes the reduction instead.
-// MFEA_ELL_FIN=0|1 overrides.
-bool ell_fin(int64_t NL) {
-  if (const char* e = std::getenv("MFEA_ELL_FIN")) return std::atoi(e) != 0;
-  const int b = ell_block_size(NL);
-  return (NL + b - 1) / b > kCgMaxG;
-}
-int64_t ell_grid_size(int64_t NL, bool fin) {
+int64_t ell_grid_size(int64_t NL) {
   const int b = ell_block_size(NL);
   const int64_t g = (NL + b - 1) / b;
-  return g < 1 ? 1 : ((!fin && g > kCgMaxG) ? kCgMaxG : g);
+  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
 }
-// partial groups of 64 each wave loads: ≥ grid / 64 (0: FIN, none)
+// partial groups of 64 each wave loads: ≥ grid / 64
 static int pu_of(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : g <= 320 ? 5 : 8; }
 
 static dim3 ell_grid_ew(const EllOp& op) { return dim3((unsigned)grid_rows(op.NL > 0 ? op.NL : 1)); }
@@ -675,22 +658,16 @@ void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int prec
   else init_nd<3>(s, op, sop, precond, rv, v);
 }
 
-template <int ND, bool DIST, int BS, bool FIN>
-static void first_fin(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
-                      Slot* slots, double* part, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL, FIN));
-  if (precond == 1)
-    hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS, FIN>), grid, dim3(BS), 0, s, op, reg, v,
-                       slots, part, dv);
-  else
-    hipLaunchKernelGGL((k_ell_first<ND, false, DIST, BS, FIN>), grid, dim3(BS), 0, s, op, reg, v,
-                       slots, part, dv);
-}
 template <int ND, bool DIST, int BS>
 static void first_bs(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                      Slot* slots, double* part, const DistVecs& dv) {
-  if (!DIST && ell_fin(op.NL)) first_fin<ND, false, BS, true>(s, op, reg, precond, v, slots, part, dv);
-  else first_fin<ND, DIST, BS, false>(s, op, reg, precond, v, slots, part, dv);
+  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
+                       part, dv);
+  else
+    hipLaunchKernelGGL((k_ell_first<ND, false, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
+                       part, dv);
 }
 template <int ND, bool DIST>
 static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
@@ -727,28 +704,33 @@ void launch_ell_pack0(hipStream_t s, const EllOp& op, int precond, const EllVecs
   else pack0_nd<3>(s, op, precond, v, dv);
 }
 
+template <int ND, int PU, bool TRACE, bool DIST, int BS, bool HC>
+static void iter_launch_hc(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
+                           Slot* slots, const SolveState* st, double* part,
+                           unsigned long long* trace, const DistVecs& dv) {
+  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  if (precond == 1)
+    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST, BS, HC>), grid, dim3(BS), 0, s, j, op,
+                       v, slots, st, part, trace, dv);
+  else
+    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE, DIST, BS, HC>), grid, dim3(BS), 0, s, j, op,
+                       v, slots, st, part, trace, dv);
+}
 template <int ND, int PU, bool TRACE, bool DIST, int BS>
 static void iter_launch(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                         Slot* slots, const SolveState* st, double* part,
                         unsigned long long* trace, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL, PU == 0 && !DIST));
-  if (precond == 1)
-    hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST, BS>), grid, dim3(BS), 0, s, j, op, v,
-                       slots, st, part, trace, dv);
+  if (op.hc)
+    iter_launch_hc<ND, PU, TRACE, DIST, BS, true>(s, j, op, precond, v, slots, st, part, trace, dv);
   else
-    hipLaunchKernelGGL((k_ell_iter<ND, false, PU, TRACE, DIST, BS>), grid, dim3(BS), 0, s, j, op, v,
-                       slots, st, part, trace, dv);
+    iter_launch_hc<ND, PU, TRACE, DIST, BS, false>(s, j, op, precond, v, slots, st, part, trace, dv);
 }
 
 template <int ND, bool TRACE, int BS>
 static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                     const DistVecs& dv) {
-  if (ell_fin(op.NL)) {
-    iter_launch<ND, 0, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv);
-    return;
-  }
-  switch (pu_of(ell_grid_size(op.NL, false))) {
+  switch (pu_of(ell_grid_size(op.NL))) {
     case 1: iter_launch<ND, 1, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 2: iter_launch<ND, 2, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 4: iter_launch<ND, 4, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
@@ -798,7 +780,7 @@ void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const E
 }
 
 void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend) {
-  switch (pu_of(ell_grid_size(NL, false))) {  // the partitioned iteration's grid
+  switch (pu_of(ell_grid_size(NL))) {  // the partitioned iteration's grid
     case 1: hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 2: hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 4: hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend); break;

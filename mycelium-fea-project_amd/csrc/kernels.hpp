@@ -166,12 +166,8 @@ struct EllOp {
   double* V;                 // [NB][3][NL] slot blocks (component c, slot k: (c·3+k)·NL)
   double* D;                 // [NB][NL] diagonal block (unregularised), 0 off owners
                              // NB = 6 (xx xy xz yy yz zz) or, nd = 2, 3 (xx xy yy)
-  // large systems (grid > 512 blocks, one pass per wave): the grid reduction
-  // is finished in-launch by the last block (device_util.hpp block_publish)
-  double* fin_part;          // [4][grid + 8] block / shard partials
-  unsigned* fin_ticket;      // one ticket set
-  double* fin_out;           // [2][4] reduced (γ, δ, ‖r‖², ‖u‖²) by parity
-  int64_t NR;                // compact halo records (+1 spare), stride of h / hM
+  int hc;                    // 1: compact halo records, 0: one record per lane
+  int64_t NR;                // stride of h / hM: records (+1 spare) or NL
   const uint64_t* hmask;     // [NL/64] lanes of each wave owning a halo record
   const int32_t* hbase;      // [NL/64] the wave's first record
 };
@@ -212,12 +208,10 @@ void launch_ell_first(hipStream_t s, const EllOp& op, double reg, int precond, c
 void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                      Slot* slots, const SolveState* st, double* part,
                      unsigned long long* trace = nullptr, const DistVecs* dv = nullptr);
-// launch geometry of the lane CG kernels: block size 64/128/256; grid ≤ 512
-// with block partials re-reduced by every wave of the next launch, or, for
-// large systems (ell_fin), one pass per wave with the in-launch reduction
+// launch geometry of the lane CG kernels: threads per block; blocks (≤ 512,
+// their partials re-reduced by every wave of the next launch)
 int ell_block_size(int64_t NL);
-bool ell_fin(int64_t NL);
-int64_t ell_grid_size(int64_t NL, bool fin);
+int64_t ell_grid_size(int64_t NL);
 // x of the owner lanes → row-order x (free rows)
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
 // this partition's block partials of the iteration (parity buffer `p`, the

@@ -47,7 +47,8 @@ class Info(C.Structure):
                 ("n_slots", C.c_int64), ("free_incidences", C.c_int64), ("planar", C.c_int32),
                 ("cg_lanes", C.c_int32), ("n_lanes", C.c_int64), ("n_halo", C.c_int64),
                 ("n_parts", C.c_int32), ("part", C.c_int32), ("n_pairs", C.c_int64),
-                ("n_ghost", C.c_int64)]
+                ("n_ghost", C.c_int64), ("halo_compact", C.c_int32), ("block_size", C.c_int32),
+                ("grid", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -303,10 +303,7 @@ def test_c2_properties(engine):
 def _solve_with(engine, kernel, dy, opts):
     old = os.environ.get("MFEA_CG_KERNEL")
     try:
-        if kernel == "sell":
-            os.environ["MFEA_CG_KERNEL"] = "sell"
-        else:
-            os.environ.pop("MFEA_CG_KERNEL", None)
+        os.environ["MFEA_CG_KERNEL"] = kernel  # "lanes" | "sell" (else chosen by density)
         st = engine.solve(dy, -dy, opts)
         assert engine.info()["cg_lanes"] == (kernel == "lanes")
         return st, engine.displacement()
@@ -387,6 +384,7 @@ def test_lane_kernel_natural_order_many_halos(engine, monkeypatch):
     slots go through pushed halo records and groups grow helper lanes."""
     from mfea import make_opts, synth
     monkeypatch.setenv("MFEA_ORDER", "natural")
+    monkeypatch.setenv("MFEA_CG_KERNEL", "lanes")  # dense in lanes: default would pick SELL
     xyz, e2n = synth.tiled_mesh(1, 1)
     top, bot = synth.grips(xyz)
     engine.set_mesh(xyz, e2n)
@@ -419,15 +417,17 @@ def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
 
 # ---------------------------------------------------------------------------
 # launch geometries of the lane kernel (ell.hip): block size 64/128/256 and the
-# in-launch reduction of large systems (FIN: one pass per wave, the last block
-# finishes the grid reduction) forced on a small system — same iterates up to
-# summation order, each geometry bitwise reproducible
+# halo record layout (compact / per lane) forced on a small system — same
+# iterates up to summation order, each geometry bitwise reproducible
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("bs,fin,precond", [(64, "1", 0), (128, "0", 0), (256, "1", 0), (128, "1", 1)])
-def test_lane_geometries_match_direct(monkeypatch, bs, fin, precond):
+@pytest.mark.parametrize("bs,hc,precond", [(64, "1", 0), (128, "0", 0), (256, "1", 0), (128, "1", 1),
+                                          (256, "0", 1)])
+def test_lane_geometries_match_direct(monkeypatch, bs, hc, precond):
+    """hc: compact halo records (large systems) or one record per lane."""
     from mfea import Engine, make_opts
     monkeypatch.setenv("MFEA_ELL_BS", str(bs))
-    monkeypatch.setenv("MFEA_ELL_FIN", fin)
+    monkeypatch.setenv("MFEA_ELL_HC", hc)
+    monkeypatch.setenv("MFEA_CG_KERNEL", "lanes")
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     eng = Engine(0)
     try:
@@ -447,3 +447,21 @@ def test_lane_geometries_match_direct(monkeypatch, bs, fin, precond):
         assert n == eng.active().sum()
     finally:
         eng.close()
+
+
+def test_dense_network_runs_sell_kernel_and_matches_direct(engine, monkeypatch):
+    """Dense-filament networks (the C5 recipe: intra-tile chords, mean degree
+    ≈ 7.5) need > 2 lanes per free row; the engine then runs the SELL kernel."""
+    from mfea import make_opts, synth
+    monkeypatch.delenv("MFEA_CG_KERNEL", raising=False)
+    xyz, e2n = synth.tiled_mesh(1, 1, chords=True)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    info = engine.info()
+    assert info["n_lanes"] > 2 * info["n_free_nodes"] and info["cg_lanes"] == 0
+    st = engine.solve(0.01, -0.01, make_opts(rtol=1e-13, max_it=200000))
+    assert st.status == 0
+    assert rel(engine.displacement(), _direct(xyz, e2n, top, bot, 0.01)) <= 1e-10

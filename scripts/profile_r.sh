@@ -6,7 +6,8 @@ set -u
 TAG=$1; CFG=${2:-C2_100k}
 D=gpurun_out/prof_$TAG
 mkdir -p $D
-export MFEA_NO_GRAPH=1
+# rocprofv3 traces the hipGraph-replayed kernels too (no MFEA_NO_GRAPH: eager
+# launches under the profiler inflate a 6 µs kernel's duration by ≈ 1.5 µs)
 B="python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o t -- $B > $D/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o f -- $B > $D/fetch.log 2>&1 || exit $?

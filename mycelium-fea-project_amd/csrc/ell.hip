@@ -631,12 +631,17 @@ __global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restric
 int ell_block_size(int64_t) {
   const char* e = std::getenv("MFEA_ELL_BS");
   const int b = e ? std::atoi(e) : 0;
-  return (b == 64 || b == 128) ? b : 256;
+  return (b == 64 || b == 128 || b == 512) ? b : 256;
 }
+// MFEA_ELL_MAXG caps the grid below kCgMaxG (tests: several passes per wave
+// on small systems)
 int64_t ell_grid_size(int64_t NL) {
+  const char* e = std::getenv("MFEA_ELL_MAXG");  // read per call: tests vary it
+  const int64_t c = e ? std::atoll(e) : 0;
+  const int64_t cap = (c >= 1 && c < kCgMaxG) ? c : (int64_t)kCgMaxG;
   const int b = ell_block_size(NL);
   const int64_t g = (NL + b - 1) / b;
-  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
+  return g < 1 ? 1 : (g > cap ? cap : g);
 }
 // partial groups of 64 each wave loads: ≥ grid / 64
 static int pu_of(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : g <= 320 ? 5 : 8; }
@@ -675,6 +680,7 @@ static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, co
   switch (ell_block_size(op.NL)) {
     case 64: first_bs<ND, DIST, 64>(s, op, reg, precond, v, slots, part, dv); break;
     case 128: first_bs<ND, DIST, 128>(s, op, reg, precond, v, slots, part, dv); break;
+    case 512: first_bs<ND, DIST, 512>(s, op, reg, precond, v, slots, part, dv); break;
     default: first_bs<ND, DIST, 256>(s, op, reg, precond, v, slots, part, dv); break;
   }
 }
@@ -746,6 +752,7 @@ static void iter_bs(hipStream_t s, int j, const EllOp& op, int precond, const El
   switch (ell_block_size(op.NL)) {
     case 64: iter_pu<ND, TRACE, 64>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 128: iter_pu<ND, TRACE, 128>(s, j, op, precond, v, slots, st, part, trace, dv); break;
+    case 512: iter_pu<ND, TRACE, 512>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     default: iter_pu<ND, TRACE, 256>(s, j, op, precond, v, slots, st, part, trace, dv); break;
   }
 }
@@ -757,6 +764,7 @@ static void iter_dist(hipStream_t s, int j, const EllOp& op, int precond, const 
   switch (ell_block_size(op.NL)) {
     case 64: iter_launch<ND, 1, false, true, 64>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
     case 128: iter_launch<ND, 1, false, true, 128>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
+    case 512: iter_launch<ND, 1, false, true, 512>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
     default: iter_launch<ND, 1, false, true, 256>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
   }
 }

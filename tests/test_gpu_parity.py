@@ -420,13 +420,18 @@ def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
 # halo record layout (compact / per lane) forced on a small system — same
 # iterates up to summation order, each geometry bitwise reproducible
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("bs,hc,precond", [(64, "1", 0), (128, "0", 0), (256, "1", 0), (128, "1", 1),
-                                          (256, "0", 1)])
-def test_lane_geometries_match_direct(monkeypatch, bs, hc, precond):
-    """hc: compact halo records (large systems) or one record per lane."""
+@pytest.mark.parametrize("bs,hc,precond,maxg", [
+    (64, "1", 0, 0), (128, "0", 0, 0), (256, "1", 0, 0), (128, "1", 1, 0), (256, "0", 1, 0),
+    (512, "1", 0, 0), (512, "0", 1, 0),
+    # grid capped: every wave makes several passes (as at C3)
+    (64, "1", 0, 5), (256, "0", 1, 3), (128, "1", 1, 2), (512, "1", 0, 2)])
+def test_lane_geometries_match_direct(monkeypatch, bs, hc, precond, maxg):
+    """hc: compact halo records (large systems) or one record per lane; maxg
+    caps the grid so every wave makes several passes."""
     from mfea import Engine, make_opts
     monkeypatch.setenv("MFEA_ELL_BS", str(bs))
     monkeypatch.setenv("MFEA_ELL_HC", hc)
+    monkeypatch.setenv("MFEA_ELL_MAXG", str(maxg))
     monkeypatch.setenv("MFEA_CG_KERNEL", "lanes")
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     eng = Engine(0)

@@ -37,11 +37,11 @@ PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2_100k", choices=["C2_100k", "C3_1M", "C5_10M_dense"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3_1M", choices=["C2_100k", "C3_1M", "C5_10M_dense"])
     ap.add_argument("--rtol", type=float, default=1e-8)
-    ap.add_argument("--precond", default="jacobi", choices=["jacobi", "bjacobi"])
+    ap.add_argument("--precond", default="gamg", choices=["gamg", "jacobi", "bjacobi"])
     ap.add_argument("--load-step", type=int, default=20, help="load step index of 40 (dy)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-steps", type=int, default=1)
@@ -52,6 +52,33 @@ def parse():
     ap.add_argument("--parts", type=int, default=1,
                     help="1 GPU: run the partitioned solve with this many partitions on it")
     return ap.parse_args()
+
+
+def amg_iteration_bytes(ai):
+    """Algorithmic HBM bytes of one GAMG-PCG iteration: every
+    launch of the iteration, each array counted once per launch.  Per level l
+    (n rows, nb blocks of A_l, pb blocks of P_l, B = 8·ND² bytes per block,
+    V = 8·ND per row vector):
+      resid    nb·(B+4) + 3·V·n                 (A, b, x, t)
+      restrict pb·(B+8) + V·n + (2V + B)·n'     (Pᵀ, t; b', x', D⁻¹ of level l+1)
+      prolong  pb·(B+4) + 2·V·n + V·n'          (P, x in/out, e of level l+1)
+      post     nb·(B+4) + (3V + B)·n            (A, b, x, e, D⁻¹)
+    CG: update 10·V·n0 + (V + B)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀);
+        w      nb0·(B+4) + 3·V·n0.
+    """
+    nd = ai["nd"]
+    B, V = 8 * nd * nd, 8 * nd
+    rows, blocks, pbl = ai["rows"], ai["blocks"], ai["pblocks"]
+    b = 0
+    for l in range(ai["levels"] - 1):
+        n, nn = rows[l], rows[l + 1]
+        b += blocks[l] * (B + 4) + 3 * V * n
+        b += pbl[l] * (B + 8) + V * n + (2 * V + B) * nn
+        b += pbl[l] * (B + 4) + 2 * V * n + V * nn
+        b += blocks[l] * (B + 4) + (3 * V + B) * n
+    n0 = rows[0]
+    b += 10 * V * n0 + (V + B) * n0 + blocks[0] * (B + 4) + 3 * V * n0
+    return b
 
 
 def iteration_bytes(info, block):
@@ -110,7 +137,7 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
-    from mfea import Engine, make_opts, PC_BLOCK_JACOBI, PC_JACOBI, dist_unique_id, synth
+    from mfea import Engine, make_opts, PC_BLOCK_JACOBI, PC_GAMG, PC_JACOBI, dist_unique_id, synth
     from mfea.synth import CONFIGS
     import fea_solver as fs
 
@@ -118,7 +145,7 @@ def main():
     mode = a.mode if world > 1 else ("parts" if a.parts > 1 else "1gpu")
     note = None
     dy = fs.DISPLACEMENT_MAX * a.load_step / (fs.N_STEPS - 1)
-    pc = PC_BLOCK_JACOBI if a.precond == "bjacobi" else PC_JACOBI
+    pc = {"gamg": PC_GAMG, "jacobi": PC_JACOBI, "bjacobi": PC_BLOCK_JACOBI}[a.precond]
     opts = make_opts(rtol=a.rtol, max_it=200000, precond=pc)
 
     def setup(mode):
@@ -200,8 +227,14 @@ def main():
     # ---- roofline of the dominant kernel (one CG-CG iteration launch), live
     # HIP events on the engine's stream; algorithmic bytes per launch as in
     # DESIGN.md §Roofline (partitioned: rank 0's partition, without exchange)
-    iter_ms = eng.profile_iteration(pc, reps=200)
-    iter_bytes, kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
+    iter_ms = eng.profile_iteration(pc, reps=200 if pc != PC_GAMG else 50)
+    if pc == PC_GAMG:
+        ai = eng.amg_info()
+        iter_bytes = amg_iteration_bytes(ai)
+        kernel = (f"GAMG-PCG iteration ({4 * (ai['levels'] - 1) + 2} launches: update + "
+                  f"{ai['levels']}-level V-cycle + w = A u)")
+    else:
+        iter_bytes, kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
     nf = info["n_free_nodes"]
     achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
     traffic = None
@@ -249,7 +282,8 @@ def main():
         "cg_iters": iters,
         "relres": st.relres,
         "step_breakdown_ms": {"assemble": st.t_assemble_ms, "rhs": st.t_rhs_ms,
-                              "pcg": st.t_solve_ms, "post": st.t_post_ms},
+                              "pcg": st.t_solve_ms, "post": st.t_post_ms,
+                              "amg_setup (inside pcg)": st.t_setup_ms},
         "roofline": {
             "kernel": kernel,
             "bound": "hbm",
@@ -262,6 +296,9 @@ def main():
             "avg_launch_us": iter_ms * 1e3,
         },
     }
+    if pc == PC_GAMG:
+        out["amg"] = {"levels": ai["levels"], "rows": ai["rows"], "blocks": ai["blocks"],
+                      "setup_pair_items": ai["pair_items"]}
     if note:
         out["note"] = note
 

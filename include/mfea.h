@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 4
+#define MFEA_ABI_VERSION 5
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -45,6 +45,10 @@ extern "C" {
 /* solver selection (mfea_solve_opts.precond) */
 #define MFEA_PC_JACOBI 0        /* PCJACOBI — diagonal of K_ff + reg·I              */
 #define MFEA_PC_BLOCK_JACOBI 1  /* 3×3 node-block Jacobi (exact inverse per block)   */
+#define MFEA_PC_GAMG 2          /* smoothed-aggregation AMG V-cycle, the counterpart of
+                                   the reference sweep's `-pc_type gamg`
+                                   (src/fea_petsc_solverAndPC.cpp:330-391); single-
+                                   partition handles, unpreconditioned stopping norm */
 
 /* stopping norm (mfea_solve_opts.norm) */
 #define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
@@ -69,6 +73,9 @@ typedef struct {
   double bnorm;      /* ‖b_f‖₂                                                          */
   int64_t n_free;    /* free DOFs                                                       */
   double t_assemble_ms, t_rhs_ms, t_solve_ms, t_post_ms; /* device time (HIP events)   */
+  double t_setup_ms; /* MFEA_PC_GAMG: numeric hierarchy setup (inside t_solve_ms)     */
+  int32_t amg_levels; /* MFEA_PC_GAMG: levels of the hierarchy (0 otherwise)         */
+  int32_t amg_rebuilt; /* 1 if this solve rebuilt the symbolic hierarchy (new active set) */
 } mfea_stats;
 
 /* ---- lifecycle ------------------------------------------------------------ */

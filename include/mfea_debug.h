@@ -23,6 +23,14 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
  * multi-GPU path on one GPU).  axis as mfea_set_partition_axis. */
 int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
 
+/* The MFEA_PC_GAMG hierarchy for the current active set (built if needed):
+ * *n_levels levels; for level l < cap: rows[l] (nodes / aggregates),
+ * blocks[l] (stored ND×ND blocks of A_l, diagonal included) and pblocks[l]
+ * (blocks of the prolongator P_l; 0 on the coarsest level).  *pair_items =
+ * index-list entries of the numeric setup; *nd = DOFs per node. */
+int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,673 @@
+// amg.hip — SA-AMG preconditioned CG on device (amg.hpp, amg_kernels.hpp).
+//
+// Numeric setup per solve (after assembly), level by level:
+//   A_0      gather of the assembled SELL slots (multi-edges summed in slot order)
+//   D_l⁻¹    exact inverse of every diagonal block; Gershgorin bound g_l of
+//            ρ(D_l⁻¹ A_l); smoother weight ω_l = 4 / (3 ρ̂_l), ρ̂_l = max(2, g_l / 1.45)
+//   P_l      (I − ω_l D_l⁻¹ A_l) P_tent, P_tent = aggregate indicator ⊗ I
+//   A_{l+1}  P_lᵀ (A_l P_l), both products as fixed-order gathers
+// Why ρ̂ = max(2, g/1.45): on level 0, A = Σ_e A_e + reg·I with every element
+// matrix A_e = [[S,−S],[−S,S]] ≤ 2·blockdiag(A_e), so ρ(D⁻¹A) ≤ 2 exactly; on
+// the coarse levels the measured ρ stays ≈ 2 while the
+// Gershgorin bound is ≈ 2.7.  ω_l·λ ≤ (4/3)·g/ρ̂ ≤ (4/3)·1.45 < 2 for every
+// eigenvalue λ ≤ g, so the damped block-Jacobi smoother converges in the A
+// norm on every level and the V-cycle is symmetric positive definite — the
+// requirement for CG — while ω takes the sharp value 2/3 whenever g < 2.9.
+//
+// V-cycle (one per PCG iteration, pre- and post-smoothing by one damped
+// block-Jacobi sweep each, exact block-diagonal solve on the coarsest level):
+//   x_l = ω D⁻¹ b_l                      (fused into the kernel producing b_l)
+//   t_l = b_l − A_l x_l                  k_amg_resid
+//   b_{l+1} = P_lᵀ t_l, x_{l+1} = ω D⁻¹ b_{l+1}   k_amg_restrict
+//   ... recursion ...
+//   x_l += P_l e_{l+1}                   k_amg_prolong
+//   e_l = x_l + ω D⁻¹ (b_l − A_l x_l)    k_amg_post
+// CG: the single-reduction (Chronopoulos–Gear) recurrences of cg.hip with
+// u = M r the V-cycle output: per iteration one update kernel (reads the
+// previous partials, forms α, β, the stopping test), the V-cycle, and one
+// w = A_0 u kernel that writes the next partials (γ, δ, ‖r‖², ‖u‖²).
+#include "amg_kernels.hpp"
+#include "device_util.hpp"
+
+namespace mfea {
+
+template <int ND>
+__device__ __forceinline__ void bload(const double* __restrict__ v, int64_t npos, int64_t q, double* m) {
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) m[c] = v[c * npos + q];
+}
+template <int ND>
+__device__ __forceinline__ void bstore(double* __restrict__ v, int64_t npos, int64_t q, const double* m) {
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) v[c * npos + q] = m[c];
+}
+template <int ND>
+__device__ __forceinline__ void vload(const double* __restrict__ v, int64_t i, double* o) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a) o[a] = v[ND * i + a];
+}
+template <int ND>
+__device__ __forceinline__ void vstore(double* __restrict__ v, int64_t i, const double* o) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a) v[ND * i + a] = o[a];
+}
+// y += M x
+template <int ND>
+__device__ __forceinline__ void mv_acc(const double* m, const double* x, double* y) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) y[a] = fma(m[a * ND + b], x[b], y[a]);
+}
+// y += Mᵀ x
+template <int ND>
+__device__ __forceinline__ void mtv_acc(const double* m, const double* x, double* y) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) y[a] = fma(m[b * ND + a], x[b], y[a]);
+}
+// C += A B
+template <int ND>
+__device__ __forceinline__ void mm_acc(const double* A, const double* Bm, double* C) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) {
+      double s = C[a * ND + b];
+#pragma unroll
+      for (int k = 0; k < ND; ++k) s = fma(A[a * ND + k], Bm[k * ND + b], s);
+      C[a * ND + b] = s;
+    }
+}
+// C += Aᵀ B
+template <int ND>
+__device__ __forceinline__ void mtm_acc(const double* A, const double* Bm, double* C) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) {
+      double s = C[a * ND + b];
+#pragma unroll
+      for (int k = 0; k < ND; ++k) s = fma(A[k * ND + a], Bm[k * ND + b], s);
+      C[a * ND + b] = s;
+    }
+}
+// exact inverse (adjugate / determinant); a singular block (a free row with
+// no active element and reg = 0) gets 0, as PCJACOBI's guard does
+template <int ND>
+__device__ __forceinline__ void binv(const double* m, double* o) {
+  if constexpr (ND == 2) {
+    const double det = m[0] * m[3] - m[1] * m[2];
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    o[0] = m[3] * id;
+    o[1] = -m[1] * id;
+    o[2] = -m[2] * id;
+    o[3] = m[0] * id;
+  } else {
+    const double c00 = m[4] * m[8] - m[5] * m[7];
+    const double c01 = m[5] * m[6] - m[3] * m[8];
+    const double c02 = m[3] * m[7] - m[4] * m[6];
+    const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    o[0] = c00 * id;
+    o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+    o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+    o[3] = c01 * id;
+    o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+    o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+    o[6] = c02 * id;
+    o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+    o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+  }
+}
+// symmetric block of the assembled operator (xx xy xz yy yz zz) → ND×ND
+template <int ND>
+__device__ __forceinline__ void sym_to(const double* s6, double* m) {
+  if constexpr (ND == 2) {
+    m[0] = s6[0];
+    m[1] = s6[1];
+    m[2] = s6[1];
+    m[3] = s6[3];
+  } else {
+    m[0] = s6[0]; m[1] = s6[1]; m[2] = s6[2];
+    m[3] = s6[1]; m[4] = s6[3]; m[5] = s6[4];
+    m[6] = s6[2]; m[7] = s6[4]; m[8] = s6[5];
+  }
+}
+
+__device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gate != kRun; }
+
+// slot range of the wave's slice (scalar loads, wave-uniform)
+__device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
+  const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));
+  const int a = M.sptr[s], b = M.sptr[s + 1];
+  base = (int64_t)a * 64 + (row & 63);
+  width = b - a;
+}
+
+// y −= Σ_k A_ik x_col  (every slot, diagonal included)
+template <int ND>
+__device__ __forceinline__ void spmv_sub(const AmgMatD& A, int64_t i, const double* __restrict__ x,
+                                         double* y) {
+  int64_t base;
+  int w;
+  slice_of(A, i, base, w);
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    const int32_t c = A.col[q];
+    if (c < 0) continue;
+    double m[ND * ND], xc[ND];
+    bload<ND>(A.val, A.npos, q, m);
+    vload<ND>(x, c, xc);
+#pragma unroll
+    for (int a = 0; a < ND; ++a)
+#pragma unroll
+      for (int b = 0; b < ND; ++b) y[a] = fma(-m[a * ND + b], xc[b], y[a]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// numeric setup
+// ---------------------------------------------------------------------------
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
+                                                   const int32_t* __restrict__ lst, double reg) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= A.n) return;
+  int64_t base;
+  int w;
+  slice_of(A, i, base, w);
+  if (i >= A.n) return;
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    double m[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+    if (k == 0) {
+      double s6[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + i];
+      s6[0] += reg;
+      s6[3] += reg;
+      s6[5] += reg;
+      sym_to<ND>(s6, m);
+    } else if (A.col[q] >= 0) {
+      for (int t = ptr[q]; t < ptr[q + 1]; ++t) {
+        double s6[6], e[ND * ND];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s6[c] = sop.val[(int64_t)c * sop.G + lst[t]];
+        sym_to<ND>(s6, e);
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+      }
+    }
+    bstore<ND>(A.val, A.npos, q, m);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
+  __shared__ double red[kBlock / 64];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const AmgMatD& A = L.A;
+  double g = 0.0;
+  if (i - (threadIdx.x & 63) < A.n) {
+    int64_t base;
+    int w;
+    slice_of(A, i, base, w);
+    if (i < A.n) {
+      double D[ND * ND], Di[ND * ND];
+      bload<ND>(A.val, A.npos, base, D);
+      binv<ND>(D, Di);
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) L.dinv[(int64_t)c * A.n + i] = Di[c];
+      double rs[ND];
+#pragma unroll
+      for (int a = 0; a < ND; ++a) rs[a] = 0.0;
+      for (int k = 0; k < w; ++k) {
+        const int64_t q = base + (int64_t)k * 64;
+        if (A.col[q] < 0) continue;
+        double m[ND * ND], pm[ND * ND];
+        bload<ND>(A.val, A.npos, q, m);
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+        mm_acc<ND>(Di, m, pm);
+#pragma unroll
+        for (int a = 0; a < ND; ++a)
+#pragma unroll
+          for (int b = 0; b < ND; ++b) rs[a] += fabs(pm[a * ND + b]);
+      }
+#pragma unroll
+      for (int a = 0; a < ND; ++a) g = fmax(g, rs[a]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = red[0];
+    for (int k = 1; k < kBlock / 64; ++k) m = fmax(m, red[k]);
+    L.gpart[blockIdx.x] = m;
+  }
+}
+
+constexpr double kRhoFloor = 2.0;   // the exact level-0 bound (see the header)
+constexpr double kRhoSafety = 1.45; // ω·g ≤ (4/3)·1.45 < 2
+
+__global__ __launch_bounds__(kBlock) void k_amg_omega(const double* __restrict__ gpart, int64_t nb,
+                                                       double* omega) {
+  __shared__ double red[kBlock / 64];
+  double g = 0.0;
+  for (int64_t k = threadIdx.x; k < nb; k += kBlock) g = fmax(g, gpart[k]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = red[0];
+    for (int k = 1; k < kBlock / 64; ++k) m = fmax(m, red[k]);
+    const double rho = fmax(kRhoFloor, m / kRhoSafety);
+    omega[0] = (4.0 / 3.0) / rho;
+    omega[1] = m;
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const AmgMatD& P = L.P;
+  if (i - (threadIdx.x & 63) >= P.n) return;
+  int64_t base;
+  int w;
+  slice_of(P, i, base, w);
+  if (i >= P.n) return;
+  const double om = L.omega[0];
+  double Di[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[(int64_t)c * L.A.n + i];
+  const int32_t ai = L.agg[i];
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    const int32_t J = P.col[q];
+    if (J < 0) continue;
+    double S[ND * ND], pm[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) {
+      S[c] = 0.0;
+      pm[c] = 0.0;
+    }
+    for (int t = L.pv_ptr[q]; t < L.pv_ptr[q + 1]; ++t) {
+      double m[ND * ND];
+      bload<ND>(L.A.val, L.A.npos, L.pv_a[t], m);
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) S[c] += m[c];
+    }
+    mm_acc<ND>(Di, S, pm);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
+    if (J == ai) {
+#pragma unroll
+      for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
+    }
+    bstore<ND>(P.val, P.npos, q, pm);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const AmgMatD& M = L.AP;
+  if (i - (threadIdx.x & 63) >= M.n) return;
+  int64_t base;
+  int w;
+  slice_of(M, i, base, w);
+  if (i >= M.n) return;
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    if (M.col[q] < 0) continue;
+    double C[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
+    for (int t = L.ap_ptr[q]; t < L.ap_ptr[q + 1]; ++t) {
+      double a[ND * ND], p[ND * ND];
+      bload<ND>(L.A.val, L.A.npos, L.ap_a[t], a);
+      bload<ND>(L.P.val, L.P.npos, L.ap_b[t], p);
+      mm_acc<ND>(a, p, C);
+    }
+    bstore<ND>(L.apval, M.npos, q, C);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
+  const int64_t I = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (I - (threadIdx.x & 63) >= Ac.n) return;
+  int64_t base;
+  int w;
+  slice_of(Ac, I, base, w);
+  if (I >= Ac.n) return;
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    if (Ac.col[q] < 0) continue;
+    double C[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
+    for (int t = L.ac_ptr[q]; t < L.ac_ptr[q + 1]; ++t) {
+      double p[ND * ND], m[ND * ND];
+      bload<ND>(L.P.val, L.P.npos, L.ac_a[t], p);
+      bload<ND>(L.apval, L.AP.npos, L.ac_b[t], m);
+      mtm_acc<ND>(p, m, C);
+    }
+    bstore<ND>(Ac.val, Ac.npos, q, C);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// V-cycle
+// ---------------------------------------------------------------------------
+template <int ND>
+__device__ __forceinline__ void dinv_apply(const AmgLevD& L, int64_t i, double scale, const double* v,
+                                           double* o) {
+  double Di[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[(int64_t)c * L.A.n + i];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) o[a] = 0.0;
+  mv_acc<ND>(Di, v, o);
+#pragma unroll
+  for (int a = 0; a < ND; ++a) o[a] *= scale;
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const int32_t* gate) {
+  if (gated(gate)) return;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= L.A.n) return;
+  double y[ND];
+  if (i < L.A.n) vload<ND>(L.b, i, y);
+  spmv_sub<ND>(L.A, i < L.A.n ? i : L.A.n - 1, L.x, y);
+  if (i < L.A.n) vstore<ND>(L.te, i, y);
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, const int32_t* gate) {
+  if (gated(gate)) return;
+  const int64_t I = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const AmgMatD& R = L.R;
+  if (I - (threadIdx.x & 63) >= R.n) return;
+  int64_t base;
+  int w;
+  slice_of(R, I, base, w);
+  if (I >= R.n) return;
+  double bc[ND];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) bc[a] = 0.0;
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    const int32_t i = R.col[q];
+    if (i < 0) continue;
+    double p[ND * ND], t[ND];
+    bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
+    vload<ND>(L.te, i, t);
+    mtv_acc<ND>(p, t, bc);
+  }
+  vstore<ND>(N.b, I, bc);
+  double xn[ND];
+  dinv_apply<ND>(N, I, N.coarsest ? 1.0 : N.omega[0], bc, xn);
+  vstore<ND>(N.x, I, xn);
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, const int32_t* gate) {
+  if (gated(gate)) return;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const AmgMatD& P = L.P;
+  if (i - (threadIdx.x & 63) >= P.n) return;
+  int64_t base;
+  int w;
+  slice_of(P, i, base, w);
+  if (i >= P.n) return;
+  const double* __restrict__ e = N.coarsest ? N.x : N.te;
+  double x[ND];
+  vload<ND>(L.x, i, x);
+  for (int k = 0; k < w; ++k) {
+    const int64_t q = base + (int64_t)k * 64;
+    const int32_t J = P.col[q];
+    if (J < 0) continue;
+    double p[ND * ND], ec[ND];
+    bload<ND>(P.val, P.npos, q, p);
+    vload<ND>(e, J, ec);
+    mv_acc<ND>(p, ec, x);
+  }
+  vstore<ND>(L.x, i, x);
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const int32_t* gate) {
+  if (gated(gate)) return;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= L.A.n) return;
+  const int64_t ii = i < L.A.n ? i : L.A.n - 1;
+  double y[ND], x[ND];
+  vload<ND>(L.b, ii, y);
+  vload<ND>(L.x, ii, x);
+  spmv_sub<ND>(L.A, ii, L.x, y);
+  double d[ND];
+  dinv_apply<ND>(L, ii, L.omega[0], y, d);
+#pragma unroll
+  for (int a = 0; a < ND; ++a) x[a] += d[a];
+  if (i < L.A.n) vstore<ND>(L.te, i, x);
+}
+
+// ---------------------------------------------------------------------------
+// CG
+// ---------------------------------------------------------------------------
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, const double* __restrict__ b_row) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= cg.n) return;
+  double r[ND], z[ND], x0[ND];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) {
+    r[a] = b_row[3 * i + a];
+    z[a] = 0.0;
+  }
+  vstore<ND>(cg.r, i, r);
+  vstore<ND>(cg.x, i, z);
+  vstore<ND>(cg.p, i, z);
+  vstore<ND>(cg.s, i, z);
+  // a single-level hierarchy (no free-free coupling) is its own coarsest
+  // level: the V-cycle is then the exact block solve, written straight to u
+  dinv_apply<ND>(L0, i, L0.coarsest ? 1.0 : L0.omega[0], r, x0);
+  vstore<ND>(L0.coarsest ? L0.te : L0.x, i, x0);
+}
+
+template <int ND, bool FIRST>
+__global__ __launch_bounds__(kCgBS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part) {
+  if (!FIRST && slots[j + 1].flag != kRun) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  const int lane = threadIdx.x & 63;
+  for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i - lane < cg.n; i += stride) {
+    const int64_t ii = i < cg.n ? i : cg.n - 1;
+    double y[ND], u[ND], r[ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0;
+    spmv_sub<ND>(L0.A, ii, cg.u, y);  // y = −A u
+    if (i >= cg.n) continue;
+    vload<ND>(cg.u, i, u);
+    vload<ND>(cg.r, i, r);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = -y[a];
+    vstore<ND>(cg.w, i, y);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      acc[0] = fma(r[a], u[a], acc[0]);
+      acc[1] = fma(y[a], u[a], acc[1]);
+      acc[2] = fma(r[a], r[a], acc[2]);
+      acc[3] = fma(u[a], u[a], acc[3]);
+    }
+  }
+  store_block_partial(acc, part_buf(part, FIRST ? 0 : ((j & 1) ^ 1)));
+  if (FIRST && blockIdx.x == 0 && threadIdx.x == 0) {
+    Slot s0;
+    s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
+    s0.alpha = s0.beta = s0.res = 0.0;
+    s0.flag = kInit;
+    s0.pad = 0;
+    slots[0] = s0;
+  }
+}
+
+template <int ND, int PU>
+__global__ __launch_bounds__(kCgBS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg cg, Slot* slots,
+                                                         const SolveState* st, double* part) {
+  const int f0 = __builtin_nontemporal_load(&slots[j].flag);
+  const double g0 = slots[j].v[0], a0 = slots[j].alpha;
+  const double tol2 = st->tol2;
+  const int base_it = st->base, max_it = st->max_it, norm = st->norm;
+  double S[4];
+  wave_partials<PU>(part_buf(part, j & 1), S);
+  const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
+  cg_record(slots, j, S, cs);
+  if (cs.status != kRun) return;
+  const double alpha = cs.alpha, beta = cs.beta, om = L0.omega[0];
+  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i < cg.n; i += stride) {
+    double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND], x0[ND];
+    vload<ND>(cg.u, i, u);
+    vload<ND>(cg.w, i, w);
+    vload<ND>(cg.p, i, p);
+    vload<ND>(cg.s, i, s);
+    vload<ND>(cg.x, i, x);
+    vload<ND>(cg.r, i, r);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) {
+      p[a] = fma(beta, p[a], u[a]);
+      s[a] = fma(beta, s[a], w[a]);
+      x[a] = fma(alpha, p[a], x[a]);
+      r[a] = fma(-alpha, s[a], r[a]);
+    }
+    vstore<ND>(cg.p, i, p);
+    vstore<ND>(cg.s, i, s);
+    vstore<ND>(cg.x, i, x);
+    vstore<ND>(cg.r, i, r);
+    dinv_apply<ND>(L0, i, L0.coarsest ? 1.0 : om, r, x0);
+    vstore<ND>(L0.coarsest ? L0.te : L0.x, i, x0);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_finish(AmgCg cg, double* __restrict__ x_row) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= cg.n) return;
+#pragma unroll
+  for (int a = 0; a < ND; ++a) x_row[3 * i + a] = cg.x[ND * i + a];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock > 0 ? (n + kBlock - 1) / kBlock : 1)); }
+
+int64_t amg_w_grid(int64_t n) {
+  const int64_t g = (n + kCgBS - 1) / kCgBS;
+  return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
+}
+static int pu_of_grid(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : 8; }
+
+template <int ND>
+static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* p, const int32_t* a,
+                  double reg) {
+  if (L0.A.n > 0) hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.n), dim3(kBlock), 0, s, L0.A, sop, p, a, reg);
+}
+void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* a0_ptr,
+                   const int32_t* a0_a, double reg) {
+  if (nd == 2) a0_nd<2>(s, L0, sop, a0_ptr, a0_a, reg);
+  else a0_nd<3>(s, L0, sop, a0_ptr, a0_a, reg);
+}
+
+template <int ND>
+static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N) {
+  if (L.A.n <= 0) return;
+  const dim3 g = rows_grid(L.A.n);
+  hipLaunchKernelGGL(k_amg_dinv<ND>, g, dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
+  if (L.coarsest || !N) return;
+  hipLaunchKernelGGL(k_amg_pvals<ND>, rows_grid(L.P.n), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(L.AP.n), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.n), dim3(kBlock), 0, s, L, N->A);
+}
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next) {
+  if (nd == 2) setup_nd<2>(s, L, next);
+  else setup_nd<3>(s, L, next);
+}
+
+template <int ND>
+static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const int32_t* gate) {
+  for (int l = 0; l + 1 < nlev; ++l) {
+    hipLaunchKernelGGL(k_amg_resid<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], gate);
+    hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(lev[l + 1].A.n), dim3(kBlock), 0, s, lev[l],
+                       lev[l + 1], gate);
+  }
+  for (int l = nlev - 2; l >= 0; --l) {
+    hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], lev[l + 1],
+                       gate);
+    hipLaunchKernelGGL(k_amg_post<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], gate);
+  }
+}
+void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const int32_t* gate) {
+  if (nlev <= 0 || lev[0].A.n <= 0) return;
+  if (nlev == 1) {  // a single level is the coarsest: block-Jacobi solve, done by the producer
+    return;
+  }
+  if (nd == 2) vcycle_nd<2>(s, lev, nlev, gate);
+  else vcycle_nd<3>(s, lev, nlev, gate);
+}
+
+void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row) {
+  if (cg.n <= 0) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_cg_init<2>, rows_grid(cg.n), dim3(kBlock), 0, s, L0, cg, b_row);
+  else hipLaunchKernelGGL(k_amg_cg_init<3>, rows_grid(cg.n), dim3(kBlock), 0, s, L0, cg, b_row);
+}
+
+template <int ND>
+static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
+                 double* part) {
+  const dim3 g((unsigned)amg_w_grid(cg.n));
+  if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, part);
+  else hipLaunchKernelGGL((k_amg_cg_w<ND, false>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, part);
+}
+void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
+                     Slot* slots, double* part) {
+  if (nd == 2) w_nd<2>(s, j, first, L0, cg, slots, part);
+  else w_nd<3>(s, j, first, L0, cg, slots, part);
+}
+
+template <int ND>
+static void upd_nd(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
+                   const SolveState* st, double* part) {
+  const int64_t gw = amg_w_grid(cg.n);
+  const dim3 g((unsigned)gw);
+  switch (pu_of_grid(gw)) {
+    case 1: hipLaunchKernelGGL((k_amg_cg_update<ND, 1>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
+    case 2: hipLaunchKernelGGL((k_amg_cg_update<ND, 2>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
+    case 4: hipLaunchKernelGGL((k_amg_cg_update<ND, 4>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
+    default: hipLaunchKernelGGL((k_amg_cg_update<ND, 8>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
+  }
+}
+void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
+                          const SolveState* st, double* part) {
+  if (nd == 2) upd_nd<2>(s, j, L0, cg, slots, st, part);
+  else upd_nd<3>(s, j, L0, cg, slots, st, part);
+}
+
+void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row) {
+  if (cg.n <= 0) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_finish<2>, rows_grid(cg.n), dim3(kBlock), 0, s, cg, x_row);
+  else hipLaunchKernelGGL(k_amg_finish<3>, rows_grid(cg.n), dim3(kBlock), 0, s, cg, x_row);
+}
+
+}  // namespace mfea

@@ -1,0 +1,87 @@
+// amg_kernels.hpp — device views and launchers of the SA-AMG preconditioned CG
+// (amg.hip).  Layout of one level l in HBM (n rows = nodes or aggregates,
+// ND = 2 or 3 DOFs per row, NB2 = ND² doubles per block, row-major):
+//   A.val[NB2][npos]   SELL-64 blocks of A_l, slot 0 of a row = its diagonal
+//   dinv[NB2][n]       block-Jacobi inverse of the diagonal blocks
+//   b, x, te [n][ND]   V-cycle right-hand side, iterate, residual / output
+//   P.val[NB2][npos_P] smoothed prolongator (rows = level l, cols = level l+1)
+//   R (col, rp)        P transposed: coarse row → (fine row, P position)
+//   apval[NB2][npos_AP] A_l·P_l (setup only)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+
+namespace mfea {
+
+struct AmgMatD {
+  int64_t n = 0;     // rows
+  int64_t npos = 0;  // SELL positions (slot rows · 64)
+  const int32_t* sptr = nullptr;
+  const int32_t* col = nullptr;
+  double* val = nullptr;  // [NB2][npos]
+};
+
+struct AmgLevD {
+  AmgMatD A;
+  double* dinv = nullptr;
+  double* gpart = nullptr;  // per-block Gershgorin maxima (setup)
+  double* omega = nullptr;  // [2]: smoother weight ω_l, Gershgorin bound g_l
+  double* b = nullptr;
+  double* x = nullptr;
+  double* te = nullptr;
+  int coarsest = 0;
+  // transfer to level l+1 (not on the coarsest level)
+  AmgMatD P;
+  const int32_t* agg = nullptr;
+  const int32_t* pv_ptr = nullptr;
+  const int32_t* pv_a = nullptr;
+  AmgMatD R;  // val unused
+  const int32_t* rp = nullptr;
+  double* apval = nullptr;
+  AmgMatD AP;  // pattern only (sptr, col) + npos; values in apval
+  const int32_t* ap_ptr = nullptr;
+  const int32_t* ap_a = nullptr;
+  const int32_t* ap_b = nullptr;
+  const int32_t* ac_ptr = nullptr;  // into level l+1's A.val
+  const int32_t* ac_a = nullptr;
+  const int32_t* ac_b = nullptr;
+};
+
+// CG vectors of the AMG path: free rows in level-0 order, ND per row
+struct AmgCg {
+  int64_t n = 0;
+  double* x = nullptr;
+  double* p = nullptr;
+  double* s = nullptr;
+  double* r = nullptr;  // = level 0's b
+  double* w = nullptr;
+  double* u = nullptr;  // = level 0's te (the V-cycle output)
+};
+
+// ---- numeric setup (every solve) ------------------------------------------
+// A_0 from the assembled SELL operator: off-diagonal = Σ of the listed slots'
+// K_ij (= −S_e), diagonal = K_ii + reg·I.
+void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* a0_ptr,
+                   const int32_t* a0_a, double reg);
+// dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next);
+// ---- one V-cycle z = M r (level 0's b → level 0's te); gate = NULL: always,
+// else only while *gate == kRun
+void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const int32_t* gate);
+// ---- CG (single-reduction, as cg.hip) ---------------------------------------
+// r = b (row-order 3-comp RHS of k_cg_rhs), x = p = s = 0, level-0 x = ω D⁻¹ r
+void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row);
+// w = A_0 u, partials (γ, δ, ‖r‖², ‖u‖²) → parity; first: slots[0] = INIT, parity 0
+void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
+                     Slot* slots, double* part);
+// iteration j: α, β from the partials, p s x r update, level-0 x = ω D⁻¹ r
+void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg,
+                          Slot* slots, const SolveState* st, double* part);
+// x (level-0 order, ND per row) → row-order x[3·row + c]
+void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row);
+// grid of the w kernel (its partials are re-read by the update kernel)
+int64_t amg_w_grid(int64_t n);
+
+}  // namespace mfea

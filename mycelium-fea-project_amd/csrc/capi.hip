@@ -17,6 +17,8 @@
 #include <thread>
 #include <vector>
 
+#include "amg.hpp"
+#include "amg_kernels.hpp"
 #include "kernels.hpp"
 #include "mfea_debug.h"
 #include "mfea.h"
@@ -110,6 +112,17 @@ struct Part {
   double* gred = nullptr;  // [64][4] gathered scalars (RHS norms, reaction, #active)
   double* xh_send = nullptr;
   double* xh_recv = nullptr;
+  // SA-AMG preconditioner (amg.hpp): symbolic plan for the active set amg_key
+  AmgPlan amg;
+  bool amg_ok = false;
+  std::vector<uint8_t> amg_key;
+  int64_t amg_gen = 0;               // bumped on every rebuild (captured graphs hold its pointers)
+  DevBuf<int32_t> amg_i;             // every index array of the plan, carved
+  DevBuf<double> amg_d;              // every value / vector array, carved
+  std::vector<AmgLevD> amg_lev;      // device views
+  AmgCg amg_cg;
+  const int32_t* amg_a0_ptr = nullptr;
+  const int32_t* amg_a0_a = nullptr;
 };
 
 struct mfea_handle {
@@ -141,8 +154,15 @@ struct mfea_handle {
   hipGraphExec_t graph = nullptr;
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipEvent_t ev[6] = {};
+  hipEvent_t ev_setup = nullptr;
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
+  // host view of the element activity (single partition; keys the AMG plan):
+  // exact after set_active / a build, stale once a post kernel deactivated
+  // elements (then downloaded on demand)
+  std::vector<uint8_t> act_host;
+  bool act_host_ok = false;
+  int64_t act_count = 0;
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
   DevBuf<int32_t> c_indices;
@@ -413,6 +433,17 @@ int ensure_built(mfea_handle* h) {
     for (int64_t t : h->top) known[t] = 1;
     for (int64_t b : h->bot) known[b] = 1;
     h->n_free_global = h->N - (int64_t)std::count(known.begin(), known.end(), 1);
+  }
+  if (!dm) {  // the host view of the activity the device now holds
+    const int64_t E = part0(h).P.n_elems;
+    if (h->active_host.size() == (size_t)h->Ecount) {
+      h->act_host.resize(E);
+      for (int64_t e = 0; e < E; ++e) h->act_host[e] = h->active_host[e] ? 1 : 0;
+    } else {
+      h->act_host.assign(E, 1);
+    }
+    h->act_count = (int64_t)std::count(h->act_host.begin(), h->act_host.end(), (uint8_t)1);
+    h->act_host_ok = true;
   }
   h->active_host.clear();
   h->dirty = false;
@@ -790,6 +821,232 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   return finish_solve(h, fin, st);
 }
 
+// ---------------------------------------------------------------------------
+// SA-AMG preconditioned CG (amg.hpp / amg.hip), single partition.
+// ---------------------------------------------------------------------------
+constexpr size_t kAmgAlign = 64;  // elements: every carved array starts 256/512-B aligned
+size_t amg_al(size_t n) { return (n + kAmgAlign - 1) / kAmgAlign * kAmgAlign; }
+
+// Carves the plan's index arrays and the value / vector arrays out of two
+// device allocations and uploads the indices.  Pass 0 sizes, pass 1 carves.
+int upload_amg(mfea_handle* h, Part& pt) {
+  const AmgPlan& pl = pt.amg;
+  const int nd = pl.nd, nb2 = nd * nd;
+  const int nlev = (int)pl.lev.size();
+  hipStream_t s = h->stream;
+  size_t ni = 0, ndd = 0;
+  int32_t* ip = nullptr;
+  double* dp = nullptr;
+  int pass = 0;
+  hipError_t err = hipSuccess;
+  auto I = [&](const std::vector<int32_t>& v) -> const int32_t* {
+    if (pass == 0) {
+      ni += amg_al(v.size());
+      return nullptr;
+    }
+    int32_t* p = ip;
+    ip += amg_al(v.size());
+    if (!v.empty() && err == hipSuccess)
+      err = hipMemcpyAsync(p, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice, s);
+    return p;
+  };
+  auto D = [&](size_t n) -> double* {
+    if (pass == 0) {
+      ndd += amg_al(n);
+      return nullptr;
+    }
+    double* p = dp;
+    dp += amg_al(n);
+    return p;
+  };
+  auto mat = [&](const SellPat& S, bool vals) {
+    AmgMatD m;
+    m.n = S.n;
+    m.npos = S.n_pos();
+    m.sptr = I(S.sptr);
+    m.col = I(S.col);
+    m.val = vals ? D((size_t)nb2 * m.npos) : nullptr;
+    return m;
+  };
+  for (pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      HIPC(pt.amg_i.alloc(std::max<size_t>(ni, 1)));
+      HIPC(pt.amg_d.alloc(std::max<size_t>(ndd, 1)));
+      HIPC(hipMemsetAsync(pt.amg_d.ptr, 0, pt.amg_d.n * sizeof(double), s));
+      ip = pt.amg_i.ptr;
+      dp = pt.amg_d.ptr;
+    }
+    pt.amg_lev.assign(nlev, AmgLevD{});
+    for (int l = 0; l < nlev; ++l) {
+      const AmgLevel& L = pl.lev[l];
+      AmgLevD& d = pt.amg_lev[l];
+      const int64_t n = L.A.n;
+      d.A = mat(L.A, true);
+      d.dinv = D((size_t)nb2 * n);
+      d.gpart = D((size_t)(n + kBlock - 1) / kBlock + 1);
+      d.omega = D(2);
+      d.b = D((size_t)nd * n);
+      d.x = D((size_t)nd * n);
+      d.te = D((size_t)nd * n);
+      d.coarsest = L.coarsest ? 1 : 0;
+      if (!L.coarsest) {
+        d.agg = I(L.agg);
+        d.P = mat(L.P, true);
+        d.pv_ptr = I(L.pv.ptr);
+        d.pv_a = I(L.pv.a);
+        d.R = mat(L.R, false);
+        d.rp = I(L.rp);
+        d.AP = mat(L.AP, false);
+        d.apval = D((size_t)nb2 * d.AP.npos);
+        d.ap_ptr = I(L.ap.ptr);
+        d.ap_a = I(L.ap.a);
+        d.ap_b = I(L.ap.b);
+        d.ac_ptr = I(L.ac.ptr);
+        d.ac_a = I(L.ac.a);
+        d.ac_b = I(L.ac.b);
+      }
+    }
+    pt.amg_a0_ptr = I(pl.a0.ptr);
+    pt.amg_a0_a = I(pl.a0.a);
+    const int64_t nf = nlev ? pl.lev[0].A.n : 0;
+    pt.amg_cg.n = nf;
+    pt.amg_cg.x = D((size_t)nd * nf);
+    pt.amg_cg.p = D((size_t)nd * nf);
+    pt.amg_cg.s = D((size_t)nd * nf);
+    pt.amg_cg.w = D((size_t)nd * nf);
+    pt.amg_cg.r = nlev ? pt.amg_lev[0].b : nullptr;
+    pt.amg_cg.u = nlev ? pt.amg_lev[0].te : nullptr;
+  }
+  HIPC(err);
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// The element activity of the handle's single partition, on the host.
+int current_active(mfea_handle* h, Part& pt) {
+  if (h->act_host_ok && h->act_host.size() == (size_t)pt.P.n_elems) return 0;
+  h->act_host.resize(pt.P.n_elems);
+  if (pt.P.n_elems)
+    HIPC(hipMemcpy(h->act_host.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
+  h->act_count = (int64_t)std::count(h->act_host.begin(), h->act_host.end(), (uint8_t)1);
+  h->act_host_ok = true;
+  return 0;
+}
+
+// (Re)build the hierarchy when the active set differs from the plan's.
+int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
+  *rebuilt = false;
+  RC(current_active(h, pt));
+  if (pt.amg_ok && pt.amg_key == h->act_host) return 0;
+  pt.amg_ok = false;
+  const std::string err = build_amg(pt.P, h->act_host, lane_dofs(h), pt.amg);
+  if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+  destroy_graph(h);
+  RC(upload_amg(h, pt));
+  pt.amg_key = h->act_host;
+  pt.amg_ok = true;
+  ++pt.amg_gen;
+  *rebuilt = true;
+  return 0;
+}
+
+void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
+  hipStream_t s = h->stream;
+  const int nd = pt.amg.nd;
+  const AmgLevD& L0 = pt.amg_lev[0];
+  launch_amg_cg_update(s, nd, j, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), profile ? nullptr : &pt.slots.ptr[j + 1].flag);
+  launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+}
+
+void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
+  for (int j = 0; j < chunk; ++j) enqueue_amg_iteration(h, pt, j, false);
+  launch_cg_advance(h->stream, chunk, pt.slots.ptr, pt.state.ptr, pt.mirror);
+}
+
+// hierarchy values for the current K (the per-solve numeric setup)
+void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
+  hipStream_t s = h->stream;
+  const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
+  launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  for (int l = 0; l < nlev; ++l)
+    launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr);
+}
+
+int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
+              mfea_stats* st) {
+  Part& pt = part0(h);
+  hipStream_t s = h->stream;
+  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
+    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
+  bool rebuilt = false;
+  RC(ensure_amg(h, pt, &rebuilt));
+  const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 4;
+  const SellOp op = sell_op(pt);
+  const CgVecs v = cg_vecs(pt);
+  const int nd = pt.amg.nd;
+  HIPC(hipEventRecord(h->ev[1], s));
+  launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 0, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
+  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
+  HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  HIPC(hipEventRecord(h->ev[2], s));
+  enqueue_amg_setup(h, pt, o->reg);
+  HIPC(hipEventRecord(h->ev_setup, s));
+  const AmgLevD& L0 = pt.amg_lev[0];
+  launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), nullptr);
+  launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+  HIPC(hipGetLastError());
+  const int tag = -1000 - (int)(pt.amg_gen % 1000000);
+  static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  SolveState fin;
+  int rc;
+  if (no_graph) {
+    rc = drive_chunks(
+        h, chunk, o->max_it,
+        [&]() -> int {
+          enqueue_amg_chunk(h, pt, chunk);
+          HIPC(hipGetLastError());
+          return 0;
+        },
+        &fin, /*mirror=*/true);
+  } else {
+    if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG ||
+        h->graph_ell != tag) {
+      destroy_graph(h);
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      enqueue_amg_chunk(h, pt, chunk);
+      HIPC(hipStreamEndCapture(s, &g));
+      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_chunk = chunk;
+      h->graph_precond = MFEA_PC_GAMG;
+      h->graph_ell = tag;
+    }
+    rc = drive_chunks(
+        h, chunk, o->max_it,
+        [&]() -> int {
+          HIPC(hipGraphLaunch(h->graph, s));
+          return 0;
+        },
+        &fin, /*mirror=*/true);
+  }
+  if (rc) return rc;
+  launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
+  HIPC(hipGetLastError());
+  rc = finish_solve(h, fin, st);
+  if (st) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev_setup);
+    st->t_setup_ms = ms;
+    st->amg_levels = (int32_t)pt.amg_lev.size();
+    st->amg_rebuilt = rebuilt ? 1 : 0;
+  }
+  return rc;
+}
+
 // The partitioned solve: the same CG-CG iterations on every partition's lanes,
 // with the exchanges of partition.hpp between kernels.
 int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
@@ -928,6 +1185,8 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if (total_force) *total_force = h->h_red[0];
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
+  // elements only ever fail here: a changed count means a changed set
+  if (!dm && h->act_host_ok && h->n_active != h->act_count) h->act_host_ok = false;
   if (st) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[4], h->ev[5]);
@@ -938,6 +1197,12 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
 
 int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
+  if (o->precond == MFEA_PC_GAMG) {
+    if (partitioned(h)) return fail(MFEA_EINVAL, "MFEA_PC_GAMG: single-partition handles only");
+    return solve_amg(h, dy_top, dy_bot, o, st);
+  }
+  if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
+    return fail(MFEA_EINVAL, "unknown preconditioner");
   return partitioned(h) ? solve_dist(h, dy_top, dy_bot, o, st) : solve_impl(h, dy_top, dy_bot, o, st);
 }
 
@@ -982,6 +1247,7 @@ int mfea_create(int device, mfea_handle** out) {
   HIPC(hipSetDevice(device));
   HIPC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   for (auto& ev : h->ev) HIPC(hipEventCreate(&ev));
+  HIPC(hipEventCreate(&h->ev_setup));
   for (auto& ev : h->poll) HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIPC(hipHostMalloc(&h->h_state, 2 * sizeof(SolveState),
                      hipHostMallocMapped | hipHostMallocCoherent));
@@ -1009,6 +1275,7 @@ int mfea_destroy(mfea_handle* h) {
     if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : h->poll)
     if (ev) (void)hipEventDestroy(ev);
+  if (h->ev_setup) (void)hipEventDestroy(h->ev_setup);
   if (h->h_state) (void)hipHostFree(h->h_state);
   if (h->h_red) (void)hipHostFree(h->h_red);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1087,9 +1354,15 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
       for (int64_t le = 0; le < E; ++le)
         a[le] = active[partitioned(h) ? pt.plan.elem_g[le] : le] ? 1 : 0;
       HIPC(hipMemcpy(pt.active.ptr, a.data(), E, hipMemcpyHostToDevice));
+      if (!partitioned(h)) h->act_host = std::move(a);
     } else {
       HIPC(hipMemset(pt.active.ptr, 1, E));
+      if (!partitioned(h)) h->act_host.assign(E, 1);
     }
+  }
+  if (!partitioned(h)) {
+    h->act_count = (int64_t)std::count(h->act_host.begin(), h->act_host.end(), (uint8_t)1);
+    h->act_host_ok = true;
   }
   return 0;
 }
@@ -1409,6 +1682,25 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   RC(ensure_built(h));
   Part& pt = part0(h);
   hipStream_t s = h->stream;
+  if (precond == MFEA_PC_GAMG) {
+    if (!pt.amg_ok) return fail(MFEA_ESTATE, "profile GAMG after a GAMG solve");
+    // Running state: slots[0] = INIT and real partials from an ungated first
+    // w kernel; every rep is update + V-cycle + w(first) — the full work of
+    // one PCG iteration, all stores included.
+    const int nd = pt.amg.nd;
+    launch_amg_cg_w(s, nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+    launch_cg_init_finalize(s, pt.red.ptr + 8, 0.0, 0.0, 0, 1 << 30, 1e-12, pt.state.ptr);
+    enqueue_amg_iteration(h, pt, 0, true);  // warm
+    HIPC(hipEventRecord(h->ev[0], s));
+    for (int k = 0; k < reps; ++k) enqueue_amg_iteration(h, pt, 0, true);
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(h->ev[1], s));
+    HIPC(hipEventSynchronize(h->ev[1]));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    *avg_ms = ms / reps;
+    return 0;
+  }
   const int pc = precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
   // Running state with tol 0: slots[0] = INIT and parity-0 partials of 1, so
   // γ = δ = ‖r‖² = ‖u‖² = G > 0, α = 1, β = 0.  Every launch is iteration 0
@@ -1456,6 +1748,33 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   (void)hipFree(d);
   if (e != hipSuccess) return fail(MFEA_EDEVICE, hipGetErrorString(e));
   *n_waves = nw;
+  return 0;
+}
+
+int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd) {
+  if (!h || !n_levels || cap < 0 || (cap && (!rows || !blocks || !pblocks)))
+    return fail(MFEA_EINVAL, "bad argument");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  if (partitioned(h)) return fail(MFEA_ESTATE, "GAMG: single-partition handles only");
+  Part& pt = part0(h);
+  bool rebuilt = false;
+  RC(ensure_amg(h, pt, &rebuilt));
+  const AmgPlan& pl = pt.amg;
+  *n_levels = (int)pl.lev.size();
+  for (int l = 0; l < std::min(cap, *n_levels); ++l) {
+    const SellPat& A = pl.lev[l].A;
+    rows[l] = A.n;
+    int64_t nb = 0;
+    for (int64_t i = 0; i < A.n; ++i) nb += A.rlen[i];
+    blocks[l] = nb;
+    int64_t pb = 0;
+    for (int32_t r : pl.lev[l].P.rlen) pb += r;
+    pblocks[l] = pb;
+  }
+  if (pair_items) *pair_items = pl.pair_items;
+  if (nd) *nd = pl.nd;
   return 0;
 }
 

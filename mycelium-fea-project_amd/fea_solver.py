@@ -8,9 +8,11 @@ libmfea.so's HIP kernels.  Run it exactly like the reference:
     python mycelium-fea-project_amd/fea_solver.py <results_dir> [options]
 
 Differences by design: the direct SuperLU solve
-(src/fea_solver.py:128) is replaced by device Jacobi-PCG run to a tight
-relative residual (default 1e-13 → displacement within ~1e-10 relative L2 of the
-direct solution); PNG plotting (plot_network, py:137-181) is out of scope.
+(src/fea_solver.py:128) is replaced by device PCG preconditioned with a
+smoothed-aggregation AMG V-cycle (the reference sweep's `-pc_type gamg`; Jacobi
+and block Jacobi on request) run to a tight relative residual (default 1e-13 →
+displacement within ~1e-10 relative L2 of the direct solution); PNG plotting
+(plot_network, py:137-181) is out of scope.
 """
 from __future__ import annotations
 
@@ -43,7 +45,7 @@ GRIP_LENGTH = 1.5
 # solver settings of the device PCG (no counterpart in the direct-solve reference)
 RTOL = 1e-13
 MAX_IT = 200000
-PRECOND = _capi.PC_JACOBI
+PRECOND = _capi.PC_GAMG  # multi-partition runs use PC_JACOBI
 REG = 1e-12  # src/fea_solver.py:125
 
 _engine = None
@@ -106,7 +108,8 @@ def solve_system(K, known_dofs, known_vals):
     K_ff + 1e-12·I solved by device Jacobi-PCG (rtol RTOL); raises
     np.linalg.LinAlgError (a SolverFailure) if it does not converge."""
     K = sp.csr_matrix(K)
-    U, _ = get_engine().solve_csr(K.indptr, K.indices, K.data, known_dofs, known_vals, _opts())
+    U, _ = get_engine().solve_csr(K.indptr, K.indices, K.data, known_dofs, known_vals,
+                                  _opts(precond=_capi.PC_JACOBI))
     return U
 
 
@@ -153,6 +156,8 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     eng.set_mesh(coords, e2n)
     eng.set_bc(top, bot)
     eng.set_active(None)
+    if precond is None and nparts > 1 and PRECOND == _capi.PC_GAMG:
+        precond = _capi.PC_JACOBI  # the AMG hierarchy is single-partition
     opts = _opts(rtol, max_it, precond)
 
     stress_record, active_record, disp_record, force_disp_curve, solve_times = [], [], [], [], []
@@ -221,14 +226,15 @@ def main(argv=None):
     ap.add_argument("--rtol", type=float, default=RTOL)
     ap.add_argument("--max-it", type=int, default=MAX_IT)
     ap.add_argument("--reg", type=float, default=REG)
-    ap.add_argument("--pc", choices=["jacobi", "bjacobi"], default="jacobi")
+    ap.add_argument("--pc", choices=["gamg", "jacobi", "bjacobi"], default="gamg")
     ap.add_argument("--format", choices=["python", "petsc"], default="python")
     ap.add_argument("--parts", type=int, default=1,
                     help="partitions of the multi-GPU solve, all on this device")
     a = ap.parse_args(argv)
     N_STEPS, DISPLACEMENT_MAX, MAX_STRAIN, REG = a.n_steps, a.disp_max, a.max_strain, a.reg
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,
-               precond=_capi.PC_BLOCK_JACOBI if a.pc == "bjacobi" else _capi.PC_JACOBI,
+               precond={"gamg": None if a.parts > 1 else _capi.PC_GAMG, "jacobi": _capi.PC_JACOBI,
+                        "bjacobi": _capi.PC_BLOCK_JACOBI}[a.pc],
                out_format=a.format, nparts=a.parts)
 
 

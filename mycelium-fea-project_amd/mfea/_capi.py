@@ -21,7 +21,7 @@ _lib = C.CDLL(LIB_PATH)
 
 # error codes (mfea.h)
 OK, EINVAL, EDEVICE, ESTATE, EMAXIT, EBREAKDOWN, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5, -6, -7
-PC_JACOBI, PC_BLOCK_JACOBI = 0, 1
+PC_JACOBI, PC_BLOCK_JACOBI, PC_GAMG = 0, 1, 2
 NORM_UNPRECONDITIONED, NORM_PRECONDITIONED = 0, 1
 MESH_SKIP_INVALID = 1
 
@@ -35,7 +35,8 @@ class SolveOpts(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("iters", C.c_int32), ("status", C.c_int32), ("relres", C.c_double),
                 ("bnorm", C.c_double), ("n_free", C.c_int64), ("t_assemble_ms", C.c_double),
-                ("t_rhs_ms", C.c_double), ("t_solve_ms", C.c_double), ("t_post_ms", C.c_double)]
+                ("t_rhs_ms", C.c_double), ("t_solve_ms", C.c_double), ("t_post_ms", C.c_double),
+                ("t_setup_ms", C.c_double), ("amg_levels", C.c_int32), ("amg_rebuilt", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -87,6 +88,8 @@ _sig = {
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
+    "mfea_debug_amg_info": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P, C.c_int,
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(_lib, _name)
@@ -300,6 +303,22 @@ class Engine:
         _check(_lib.mfea_debug_trace_iteration(self._h, int(precond), out.ctypes.data, out.size,
                                                C.byref(nw)))
         return out[:4 * nw.value].reshape(-1, 4)
+
+    def amg_info(self) -> dict:
+        """The MFEA_PC_GAMG hierarchy for the current active set: rows and
+        stored blocks per level, index-list entries of the numeric setup."""
+        cap = 64
+        nl = C.c_int()
+        rows = np.zeros(cap, dtype=np.int64)
+        blocks = np.zeros(cap, dtype=np.int64)
+        pblocks = np.zeros(cap, dtype=np.int64)
+        items = C.c_int64()
+        nd = C.c_int()
+        _check(_lib.mfea_debug_amg_info(self._h, C.byref(nl), rows.ctypes.data, blocks.ctypes.data,
+                                        pblocks.ctypes.data, cap, C.byref(items), C.byref(nd)))
+        n = nl.value
+        return {"levels": n, "rows": rows[:n].tolist(), "blocks": blocks[:n].tolist(),
+                "pblocks": pblocks[:n].tolist(), "pair_items": items.value, "nd": nd.value}
 
     # ---- reference-API helpers ------------------------------------------------
     def element_stiffness(self, p1s, p2s, E, A, I):

@@ -1,0 +1,185 @@
+"""NumPy restatement of the SA-AMG numeric setup and V-cycle (TEST INFRASTRUCTURE).
+
+Executes the host symbolic plan of ``csrc/amg_symbolic.cpp`` (fetched through
+``tests/native/host_shim.cpp``) with the arithmetic of ``csrc/amg.hip``:
+A_0 from the assembled SELL slots, exact block-diagonal inverses, the
+Gershgorin-bounded smoother weight, the smoothed prolongator and the two
+Galerkin products, then the V-cycle and a textbook PCG.  The tests compare
+the plan's products against SciPy's ``Pᵀ A P`` and the resulting solve against
+the reference's direct solve (``spsolve``, src/fea_solver.py:128).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import scipy.sparse as sp
+
+RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
+
+_NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
+          "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b")
+
+
+def fetch_plan(shim, active, nd):
+    """build_amg on the shim's last pattern → list of per-level dicts of arrays."""
+    a = np.ascontiguousarray(active, dtype=np.uint8)
+    err = C.create_string_buffer(256)
+    nlev = shim.shim_amg(a.ctypes.data_as(C.c_void_p), int(nd), err, 256)
+    if nlev < 0:
+        raise RuntimeError(err.value.decode())
+
+    def arr(l, name):
+        n = shim.shim_amg_array(l, name.encode(), None)
+        out = np.zeros(max(n, 0), dtype=np.int32)
+        if n > 0:
+            shim.shim_amg_array(l, name.encode(), out.ctypes.data_as(C.c_void_p))
+        return out
+
+    levels = []
+    for l in range(nlev):
+        L = {"n": shim.shim_amg_array(l, b"n", None), "nc": shim.shim_amg_array(l, b"nc", None),
+             "coarsest": bool(shim.shim_amg_array(l, b"coarsest", None))}
+        for name in _NAMES:
+            if name in ("A.sptr", "A.col") or not L["coarsest"]:
+                L[name] = arr(l, name)
+        levels.append(L)
+    levels[0]["a0.ptr"] = arr(0, "a0.ptr")
+    levels[0]["a0.a"] = arr(0, "a0.a")
+    return levels
+
+
+def pos_rows(sptr, n):
+    """(row, slot k) of every SELL-64 position (−1 for positions past n)."""
+    npos = int(sptr[-1]) * 64
+    row = np.full(npos, -1, dtype=np.int64)
+    k = np.zeros(npos, dtype=np.int64)
+    for s in range(len(sptr) - 1):
+        for t in range(sptr[s], sptr[s + 1]):
+            r = 64 * s + np.arange(64)
+            ok = r < n
+            row[t * 64:(t + 1) * 64][ok] = r[ok]
+            k[t * 64:(t + 1) * 64] = t - sptr[s]
+    return row, k
+
+
+def seg_sum(vals, ptr):
+    """out[q] = Σ vals[ptr[q]:ptr[q+1]] in list order (zeros for empty lists)."""
+    npos = len(ptr) - 1
+    out = np.zeros((npos,) + vals.shape[1:])
+    lens = np.diff(ptr)
+    for q in np.flatnonzero(lens):
+        acc = np.zeros(vals.shape[1:])
+        for t in range(ptr[q], ptr[q + 1]):
+            acc = acc + vals[t]
+        out[q] = acc
+    return out
+
+
+def _sym(v6, nd):
+    if nd == 2:
+        return np.stack([np.stack([v6[..., 0], v6[..., 1]], -1), np.stack([v6[..., 1], v6[..., 3]], -1)], -2)
+    return np.stack([np.stack([v6[..., 0], v6[..., 1], v6[..., 2]], -1),
+                     np.stack([v6[..., 1], v6[..., 3], v6[..., 4]], -1),
+                     np.stack([v6[..., 2], v6[..., 4], v6[..., 5]], -1)], -2)
+
+
+def to_scipy(blocks, sptr, col, n_rows, n_cols, nd):
+    row, _ = pos_rows(sptr, n_rows)
+    ok = (col >= 0) & (row >= 0)
+    r, c, b = row[ok], col[ok], blocks[ok]
+    rr = (r[:, None, None] * nd + np.arange(nd)[None, :, None]) + 0 * np.arange(nd)[None, None, :]
+    cc = (c[:, None, None] * nd + np.arange(nd)[None, None, :]) + 0 * np.arange(nd)[None, :, None]
+    return sp.csr_matrix((b.ravel(), (rr.ravel(), cc.ravel())), shape=(n_rows * nd, n_cols * nd))
+
+
+def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
+    """The per-solve numeric setup of amg.hip on the plan: fills A (blocks),
+    dinv, omega, P, AP for every level.  val/diag: the assembled SELL values."""
+    L0 = levels[0]
+    n0 = L0["n"]
+    row, k = pos_rows(L0["A.sptr"], n0)
+    npos = len(row)
+    A = np.zeros((npos, nd, nd))
+    v6 = np.stack([val[c * G:(c + 1) * G] for c in range(6)], -1)        # [G][6]
+    offd = seg_sum(_sym(v6, nd)[L0["a0.a"]], L0["a0.ptr"])
+    d6 = np.stack([diag[c * N:(c + 1) * N] for c in range(6)], -1).copy()  # [N][6]
+    d6[:, [0, 3, 5]] += reg
+    isdiag = (k == 0) & (row >= 0)
+    A[isdiag] = _sym(d6[row[isdiag]], nd)
+    offm = (k > 0) & (L0["A.col"] >= 0)
+    A[offm] = offd[offm]
+    L0["Ab"] = A
+    for l, L in enumerate(levels):
+        n = L["n"]
+        row, k = pos_rows(L["A.sptr"], n)
+        Ab = L["Ab"]
+        D = Ab[(k == 0) & (row >= 0)]          # rows in order
+        Dinv = np.linalg.inv(D)
+        L["dinv"] = Dinv
+        ok = (L["A.col"] >= 0) & (row >= 0)
+        M = np.abs(np.einsum("pab,pbc->pac", Dinv[row[ok]], Ab[ok])).sum(axis=2)  # [p][a]
+        rs = np.zeros((n, nd))
+        np.add.at(rs, row[ok], M)
+        g = rs.max() if n else 0.0
+        rho = max(RHO_FLOOR, g / RHO_SAFETY)
+        L["omega"] = (4.0 / 3.0) / rho
+        L["g"] = g
+        L["A"] = to_scipy(Ab, L["A.sptr"], L["A.col"], n, n, nd)
+        if L["coarsest"]:
+            break
+        prow, _ = pos_rows(L["P.sptr"], n)
+        S = seg_sum(Ab[L["pv.a"]], L["pv.ptr"])
+        okp = (L["P.col"] >= 0) & (prow >= 0)
+        Pb = np.zeros_like(S)
+        Pb[okp] = -L["omega"] * np.einsum("pab,pbc->pac", Dinv[prow[okp]], S[okp])
+        ident = okp & (L["P.col"] == np.where(prow >= 0, L["agg"][np.maximum(prow, 0)], -9))
+        Pb[ident] += np.eye(nd)
+        L["Pb"] = Pb
+        L["P"] = to_scipy(Pb, L["P.sptr"], L["P.col"], n, L["nc"], nd)
+        APb = seg_sum(np.einsum("pab,pbc->pac", Ab[L["ap.a"]], Pb[L["ap.b"]]), L["ap.ptr"])
+        L["APb"] = APb
+        Acb = seg_sum(np.einsum("pba,pbc->pac", Pb[L["ac.a"]], APb[L["ac.b"]]), L["ac.ptr"])
+        levels[l + 1]["Ab"] = Acb
+    return levels
+
+
+def vcycle(levels, b, l=0):
+    L = levels[l]
+    nd = L["dinv"].shape[1]
+    Dinv = L["dinv"]
+
+    def dapply(v, s):
+        return s * np.einsum("iab,ib->ia", Dinv, v.reshape(-1, nd)).ravel()
+
+    if L["coarsest"]:
+        return dapply(b, 1.0)
+    A, P, w = L["A"], L["P"], L["omega"]
+    x = dapply(b, w)
+    t = b - A @ x
+    x = x + P @ vcycle(levels, P.T @ t, l + 1)
+    return x + dapply(b - A @ x, w)
+
+
+def pcg(A, b, M, rtol=1e-8, max_it=1000):
+    """Textbook PCG, x0 = 0, stop on ‖r‖ ≤ rtol‖b‖ (SciPy cg semantics)."""
+    x = np.zeros_like(b)
+    r = b.copy()
+    bn = np.linalg.norm(b)
+    if bn == 0:
+        return x, 0
+    z = M(r)
+    p = z.copy()
+    rho = r @ z
+    it = 0
+    while np.linalg.norm(r) > rtol * bn and it < max_it:
+        q = A @ p
+        al = rho / (p @ q)
+        x += al * p
+        r -= al * q
+        z = M(r)
+        rn = r @ z
+        p = z + (rn / rho) * p
+        rho = rn
+        it += 1
+    return x, it

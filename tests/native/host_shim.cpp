@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "amg.hpp"
 #include "partition.hpp"
 #include "symbolic.hpp"
 
@@ -89,6 +90,85 @@ int64_t shim_export(const uint8_t* active, double EA, double EI12, int64_t* indp
     std::memcpy(data, dv.data(), dv.size() * 8);
   }
   return (int64_t)ix.size();
+}
+
+// Host SELL values (val[6][G] = −S_e per slot, diag[6][N]) of the last built
+// pattern, the same formula as shim_export (test input only).
+void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val, double* diag) {
+  const Pattern& P = g_P;
+  const int64_t N = P.n_nodes, G = P.n_slots() * kSlice;
+  std::memset(val, 0, 6 * G * sizeof(double));
+  for (int64_t i = 0; i < N; ++i) {
+    const int64_t s = i / kSlice, lane = i % kSlice;
+    double d[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < P.row_len[i]; ++k) {
+      const int64_t idx = ((int64_t)P.slice_ptr[s] + k) * kSlice + lane;
+      const int32_t e = P.s_elem[idx], j = P.s_col[idx];
+      if (!active[e]) continue;
+      const double vx = P.xyz_perm[3 * j] - P.xyz_perm[3 * i];
+      const double vy = P.xyz_perm[3 * j + 1] - P.xyz_perm[3 * i + 1];
+      const double vz = P.xyz_perm[3 * j + 2] - P.xyz_perm[3 * i + 2];
+      double L = std::sqrt(vx * vx + vy * vy + vz * vz);
+      if (L < 1e-12) L = 1e-12;
+      const double n[3] = {vx / L, vy / L, vz / L};
+      const double kax = EA / L, kb = EI12 / (L * L * L);
+      const int ab[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+      for (int c = 0; c < 6; ++c) {
+        const double t = n[ab[c][0]] * n[ab[c][1]];
+        const double S = t * kax + ((ab[c][0] == ab[c][1] ? 1.0 : 0.0) - t) * kb;
+        d[c] += S;
+        val[c * G + idx] = -S;
+      }
+    }
+    for (int c = 0; c < 6; ++c) diag[c * N + i] = d[c];
+  }
+}
+
+// SA-AMG plan (amg_symbolic.cpp) of the last built pattern: returns the
+// number of levels (or -1, error in err).
+static AmgPlan g_amg;
+int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
+  std::vector<uint8_t> a(active, active + g_P.n_elems);
+  std::string e = build_amg(g_P, a, nd, g_amg);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return (int)g_amg.lev.size();
+}
+
+// one int32 array of level l by name; returns its length (out == NULL: size
+// only), -1 for an unknown name.  "n" / "nc" / "coarsest" return scalars.
+int64_t shim_amg_array(int l, const char* name, int32_t* out) {
+  const AmgLevel& L = g_amg.lev[l];
+  const std::string n(name);
+  const std::vector<int32_t>* v = nullptr;
+  if (n == "n") return L.A.n;
+  if (n == "nc") return L.nc;
+  if (n == "coarsest") return L.coarsest ? 1 : 0;
+  if (n == "A.sptr") v = &L.A.sptr;
+  else if (n == "A.col") v = &L.A.col;
+  else if (n == "agg") v = &L.agg;
+  else if (n == "P.sptr") v = &L.P.sptr;
+  else if (n == "P.col") v = &L.P.col;
+  else if (n == "pv.ptr") v = &L.pv.ptr;
+  else if (n == "pv.a") v = &L.pv.a;
+  else if (n == "R.sptr") v = &L.R.sptr;
+  else if (n == "R.col") v = &L.R.col;
+  else if (n == "rp") v = &L.rp;
+  else if (n == "AP.sptr") v = &L.AP.sptr;
+  else if (n == "AP.col") v = &L.AP.col;
+  else if (n == "ap.ptr") v = &L.ap.ptr;
+  else if (n == "ap.a") v = &L.ap.a;
+  else if (n == "ap.b") v = &L.ap.b;
+  else if (n == "ac.ptr") v = &L.ac.ptr;
+  else if (n == "ac.a") v = &L.ac.a;
+  else if (n == "ac.b") v = &L.ac.b;
+  else if (n == "a0.ptr") v = &g_amg.a0.ptr;
+  else if (n == "a0.a") v = &g_amg.a0.a;
+  else return -1;
+  if (out && !v->empty()) std::memcpy(out, v->data(), v->size() * 4);
+  return (int64_t)v->size();
 }
 
 // Wave-local lanes of the last built pattern: returns n_lanes (or -1, error in

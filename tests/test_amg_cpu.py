@@ -1,0 +1,171 @@
+"""SA-AMG symbolic plan (csrc/amg_symbolic.cpp), no GPU: the plan's index lists
+executed with the arithmetic of csrc/amg.hip (tests/amg_ref.py) must give
+A_0 = K_ff + reg·I of the reference (src/fea_solver.py:115-125) and
+A_{l+1} = P_lᵀ A_l P_l on every level; the resulting V-cycle must precondition
+CG to the direct solve (src/fea_solver.py:128); aggregates must never span two
+components of the active free-node graph."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+from scipy.sparse.csgraph import connected_components
+from scipy.sparse.linalg import spsolve
+
+import amg_ref
+import fea_oracle as fo
+from conftest import build_host_shim, load_mesh
+
+P = C.c_void_p
+EA = fo.E_MOD * fo.AREA
+EI12 = (12 * fo.E_MOD) * fo.INERTIA
+
+
+@pytest.fixture(scope="module")
+def shim():
+    lib = C.CDLL(build_host_shim())
+    lib.shim_build.restype = C.c_int
+    lib.shim_build.argtypes = [C.c_int64, P, C.c_int64, P, C.c_int, C.c_int64, P, C.c_int64, P,
+                               C.c_int, P, C.c_char_p, C.c_int]
+    lib.shim_arrays.argtypes = [P] * 6
+    lib.shim_sell_values.argtypes = [P, C.c_double, C.c_double, P, P]
+    lib.shim_amg.restype = C.c_int
+    lib.shim_amg.argtypes = [P, C.c_int, C.c_char_p, C.c_int]
+    lib.shim_amg_array.restype = C.c_int64
+    lib.shim_amg_array.argtypes = [C.c_int, C.c_char_p, P]
+    return lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(P)
+
+
+def setup_case(shim, xyz, e2n, top, bot, active, nd):
+    """pattern + plan + numeric setup; returns (levels, K_ff in level-0 order, b, perm)."""
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    e2n = np.ascontiguousarray(e2n, np.int64)
+    top = np.ascontiguousarray(top, np.int64)
+    bot = np.ascontiguousarray(bot, np.int64)
+    N, E = len(xyz), len(e2n)
+    sizes = np.zeros(5, np.int64)
+    err = C.create_string_buffer(256)
+    assert shim.shim_build(N, _ptr(xyz), E, _ptr(e2n), 0, len(top), _ptr(top), len(bot), _ptr(bot),
+                           -1, _ptr(sizes), err, 256) == 0, err.value
+    nf, G = int(sizes[0]), int(sizes[4])
+    perm = np.empty(N, np.int32)
+    junk = [np.empty(N, np.int32), np.empty(int(sizes[3]) + 1, np.int32), np.empty(G, np.int32),
+            np.empty(G, np.int32), np.empty(N, np.uint8)]
+    shim.shim_arrays(_ptr(perm), *[_ptr(j) for j in junk])
+    act = np.ascontiguousarray(active, np.uint8)
+    val = np.zeros(6 * G)
+    diag = np.zeros(6 * N)
+    shim.shim_sell_values(_ptr(act), EA, EI12, _ptr(val), _ptr(diag))
+    levels = amg_ref.fetch_plan(shim, act, nd)
+    amg_ref.numeric_setup(levels, val, diag, G, N, nd)
+    # the reference's system, reordered to the plan's rows (free rows = perm[:nf])
+    K = fo.assemble_global_stiffness(xyz, e2n, act.astype(bool))
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    A3, b3, free = fo.free_system(K, known, vals)
+    dofs = (perm[:nf, None].astype(np.int64) * 3 + np.arange(nd)).ravel()
+    pos = np.searchsorted(free, dofs)
+    assert np.array_equal(free[pos], dofs)
+    Kff = A3[pos][:, pos].tocsr()
+    return levels, Kff, b3[pos], perm[:nf]
+
+
+def _rel(a, b):
+    d = (a - b).tocoo() if sp.issparse(a) else a - b
+    na = sp.linalg.norm(b) if sp.issparse(b) else np.linalg.norm(b)
+    nd_ = sp.linalg.norm(d) if sp.issparse(d) else np.linalg.norm(d)
+    return nd_ / na
+
+
+def _golden22k():
+    nodes, elems = load_mesh("sim_20251117_181147")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, fo.GRIP_LENGTH)
+    return xyz, elems[["n1", "n2"]].values, top, bot
+
+
+def test_plan_products_match_scipy_galerkin(shim):
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    assert len(levels) >= 3
+    # A_0 = K_ff + reg·I exactly as the reference forms it (planar: x, y DOFs)
+    assert _rel(levels[0]["A"], Kff) <= 1e-15
+    for l in range(len(levels) - 1):
+        L, Nx = levels[l], levels[l + 1]
+        Ac = (L["P"].T @ L["A"] @ L["P"]).tocsr()
+        assert _rel(Nx["A"], Ac) <= 1e-13, l
+        assert Nx["n"] == L["nc"] < L["n"]
+    # the coarsest level is block diagonal: its block inverse is the exact solve
+    C_ = levels[-1]["A"].tocoo()
+    assert np.all(C_.row // 2 == C_.col // 2)
+
+
+def test_vcycle_pcg_reaches_direct_solve(shim):
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    ref = spsolve(Kff.tocsc(), b)
+    x, it = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13)
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10
+    _, it8 = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-8)
+    # Jacobi-PCG needs 1,644 iterations on this system (tests/golden, SciPy)
+    assert it8 <= 40, it8
+
+
+def test_vcycle_is_symmetric_positive_definite(shim):
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, _, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    rng = np.random.default_rng(7)
+    n = Kff.shape[0]
+    X = rng.standard_normal((n, 6))
+    MX = np.stack([amg_ref.vcycle(levels, X[:, k]) for k in range(6)], 1)
+    G = X.T @ MX
+    assert np.abs(G - G.T).max() <= 1e-9 * np.abs(G).max()
+    assert np.all(np.linalg.eigvalsh(0.5 * (G + G.T)) > 0)
+
+
+def test_3d_mesh_plan(shim):
+    nodes, elems = load_mesh("sim_20251115_135507")
+    xyz = nodes[["x", "y", "z"]].values
+    assert np.any(xyz[:, 2] != 0)
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 0.5)
+    e2n = elems[["n1", "n2"]].values
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 3)
+    assert _rel(levels[0]["A"], Kff) <= 1e-15
+    for l in range(len(levels) - 1):
+        L = levels[l]
+        assert _rel(levels[l + 1]["A"], (L["P"].T @ L["A"] @ L["P"]).tocsr()) <= 1e-13
+    ref = spsolve(Kff.tocsc(), b)
+    x, _ = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13)
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10
+
+
+def test_aggregates_respect_components_after_failures(shim):
+    """Deactivate a band of elements (as strain failures do): aggregates stay
+    inside components of the ACTIVE free graph, so an unloaded component keeps
+    exactly zero iterates (the direct solve's answer there)."""
+    xyz, e2n, top, bot = _golden22k()
+    mid = xyz[:, 1].mean()
+    y1, y2 = xyz[e2n[:, 0], 1], xyz[e2n[:, 1], 1]
+    active = ~(((y1 - mid) * (y2 - mid) <= 0) & (np.abs(xyz[e2n[:, 0], 0] - xyz[:, 0].mean()) < 0.8))
+    levels, Kff, b, perm = setup_case(shim, xyz, e2n, top, bot, active, 2)
+    L0 = levels[0]
+    n = L0["n"]
+    G = sp.csr_matrix((np.ones(Kff.nnz), (Kff.tocoo().row // 2, Kff.tocoo().col // 2)), shape=(n, n))
+    ncomp, lab = connected_components(G, directed=False)
+    agg = L0["agg"]
+    for a in np.unique(agg[agg >= 0]):
+        assert len(np.unique(lab[agg == a])) == 1
+    # a component with zero load stays exactly zero through the V-cycle
+    z = amg_ref.vcycle(levels, b)
+    bn = np.abs(b.reshape(-1, 2)).sum(1)
+    for c in range(ncomp):
+        m = lab == c
+        if not np.any(bn[m]):
+            assert not np.any(z.reshape(-1, 2)[m]), c
+    ref = spsolve(Kff.tocsc(), b)
+    x, _ = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13)
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10

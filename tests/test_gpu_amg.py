@@ -1,0 +1,119 @@
+"""GPU parity of the SA-AMG preconditioned CG (MFEA_PC_GAMG, csrc/amg.hip):
+displacements within 1e-10 relative L2 of the reference's direct solve
+(src/fea_solver.py:128) at rtol 1e-13, iteration counts equal to the NumPy
+restatement of the same hierarchy (tests/amg_ref.py) within ±2, bitwise
+reproducible solves, and the rebuild of the hierarchy when elements fail."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_mesh
+
+pytestmark = pytest.mark.gpu
+
+import fea_oracle as fo  # noqa: E402  (checker only)
+
+
+def rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / (nb if nb > 0 else 1.0)
+
+
+def _opts(rtol, **kw):
+    from mfea import PC_GAMG, make_opts
+    return make_opts(rtol=rtol, max_it=2000, precond=PC_GAMG, **kw)
+
+
+def _sim181147(engine):
+    nodes, elems = load_mesh("sim_20251117_181147")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    e2n = elems[["n1", "n2"]].values
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    return xyz, e2n, top, bot
+
+
+def test_gamg_matches_direct_and_restatement(engine):
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    _sim181147(engine)
+    engine.assemble()
+    dy = float(sysz["dy"])
+    st = engine.solve(dy, -dy, _opts(1e-13))
+    assert st.status == 0 and st.amg_levels >= 3
+    assert rel(engine.displacement(), sysz["U"]) <= 1e-10
+    st8 = engine.solve(dy, -dy, _opts(1e-8))
+    # the NumPy restatement of this hierarchy needs 17 (tests/test_amg_cpu.py);
+    # Jacobi-PCG needs 1,644 (SciPy cg, tests/golden)
+    assert abs(st8.iters - 17) <= 2, st8.iters
+    info = engine.amg_info()
+    assert info["rows"][0] == engine.info()["n_free_nodes"] and info["nd"] == 2
+
+
+def test_gamg_deterministic_and_no_rebuild(engine):
+    _sim181147(engine)
+    engine.assemble()
+    st1 = engine.solve(0.01, -0.01, _opts(1e-10))
+    U1 = engine.displacement()
+    engine.assemble()
+    st2 = engine.solve(0.01, -0.01, _opts(1e-10))
+    assert np.array_equal(U1, engine.displacement())
+    assert st1.iters == st2.iters and st2.amg_rebuilt == 0
+    engine.set_active(None)   # same (all-active) set: the plan is kept
+    engine.assemble()
+    assert engine.solve(0.01, -0.01, _opts(1e-10)).amg_rebuilt == 0
+
+
+def test_gamg_rebuilds_after_failures_and_matches_direct(engine):
+    """Steps with element failures: the hierarchy follows the active set, and
+    every step's U matches the direct solve of that step's K."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    active = np.ones(len(e2n), bool)
+    rebuilt = []
+    for step in (10, 25, 39):
+        dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+        engine.set_active(active)
+        f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
+        rebuilt.append(st.amg_rebuilt)
+        K = fo.assemble_global_stiffness(xyz, e2n, active)
+        known, vals = fo.known_dof_map(top, bot, dy, -dy)
+        Uref = fo.solve_system(K, known, vals)
+        assert rel(engine.displacement(), Uref) <= 1e-10, step
+        active = engine.active()
+    assert n_act < len(e2n)          # failures happened
+    assert sum(rebuilt[1:]) >= 1     # and a later step rebuilt the plan
+
+
+def test_gamg_3d_mesh_matches_direct(engine):
+    nodes, elems = load_mesh("sim_20251115_135507")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 0.5)
+    e2n = elems[["n1", "n2"]].values
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    st = engine.solve(0.01, -0.01, _opts(1e-13))
+    assert st.status == 0 and engine.amg_info()["nd"] == 3
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, 0.01, -0.01)
+    assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
+
+
+def test_gamg_rejects_preconditioned_norm(engine):
+    from mfea import MfeaError, NORM_PRECONDITIONED
+    _sim181147(engine)
+    engine.assemble()
+    with pytest.raises(MfeaError):
+        engine.solve(0.01, -0.01, _opts(1e-8, norm=NORM_PRECONDITIONED))
+
+
+def test_gamg_profile_iteration(engine):
+    from mfea import PC_GAMG
+    _sim181147(engine)
+    engine.assemble()
+    engine.solve(0.01, -0.01, _opts(1e-8))
+    ms = engine.profile_iteration(PC_GAMG, reps=20)
+    assert 0 < ms < 5.0

@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--precond", default="gamg", choices=["gamg", "jacobi", "bjacobi"])
     ap.add_argument("--load-step", type=int, default=20, help="load step index of 40 (dy)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu1-its", type=int, default=150,
+                    help="PCG iterations of the bounded 1-core CPU sample")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
@@ -125,6 +126,69 @@ def cpu_model():
     except OSError:
         pass
     return platform.processor()
+
+
+def host_threads():
+    """Threads the CPU legs may use: OMP_NUM_THREADS (the GPU box sets it to the
+    job's CPU share, 16), else the process's CPU affinity."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env or len(os.sched_getaffinity(0))
+
+
+def cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof):
+    """CPU baselines on this host (rank 0, N = 1, after the timed region):
+    (1) the "host PETSc CG" — oracle/cpu_fea.c, a C/OpenMP restatement of
+        fea_petsc.cpp assembly + KSPCG/PCJACOBI (same stopping rule) — one full
+        step on every thread the job may use;
+    (2) the same on 1 core, a bounded sample: assembly, RHS and post run in
+        full, PCG for --cpu1-its iterations, extrapolated to (1)'s count;
+    (3) the reference Python's own solver class: NumPy assembly + SciPy
+        spsolve (SuperLU, src/fea_solver.py:128) through oracle/fea_oracle.py."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import cpu_fea  # baseline legs only
+    import fea_oracle as fo
+    import fea_solver as fs
+    threads = host_threads()
+    host = f"{cpu_model()} ({os.cpu_count()} CPUs visible, {len(os.sched_getaffinity(0))} in affinity)"
+    c = cpu_fea.CpuFea(xyz, e2n, top, bot, fs.E_mod, fs.A, fs.I)
+    t = time.perf_counter()
+    r = c.step(dy, -dy, rtol=a.rtol, max_it=200000, threads=threads)
+    t_all = time.perf_counter() - t
+    its = r["iters"]
+    c.active[:] = 1
+    k = max(1, min(a.cpu1_its, its))
+    r1 = c.step(dy, -dy, rtol=a.rtol, max_it=k, threads=1)
+    tt = r1["times"]
+    t_one = tt[0] + tt[1] + tt[3] + tt[2] / k * its
+    c.close()
+    t = time.perf_counter()
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    t_asm = time.perf_counter() - t
+    t = time.perf_counter()
+    fo.solve_system(K, known, vals)
+    t_sol = time.perf_counter() - t
+    legs = {
+        "cg_jacobi_all_threads": {
+            "value": n_dof / t_all, "unit": "DOF/s", "cores": threads, "kind": "port",
+            "sample": f"1 full load step of the same {a.config} mesh: C/OpenMP restatement of "
+                      f"fea_petsc.cpp assembly + PETSc KSPCG/PCJACOBI to rtol {a.rtol} ({its} iters), "
+                      f"{t_all:.2f} s on {threads} threads of {host}"},
+        "cg_jacobi_1core": {
+            "value": n_dof / t_one, "unit": "DOF/s", "cores": 1, "kind": "port",
+            "sample": f"bounded: assembly + RHS + post in full, {k} of {its} PCG iterations "
+                      f"({tt[2]:.2f} s) extrapolated -> {t_one:.1f} s per step, 1 thread of {host}"},
+        "direct_spsolve": {
+            "value": n_dof / (t_asm + t_sol), "unit": "DOF/s", "cores": 1, "kind": "port",
+            "sample": f"1 step: NumPy csr assembly {t_asm:.2f} s + SciPy spsolve (SuperLU) "
+                      f"{t_sol:.2f} s — the reference Python's direct solve "
+                      f"(src/fea_solver.py:74-135); solve-only {n_dof / t_sol:.3g} DOF/s"},
+    }
+    out["cpu_baseline"] = legs["cg_jacobi_all_threads"]
+    out["cpu_baselines"] = legs
+    out["speedup_vs_cpu"] = out["value"] / legs["cg_jacobi_all_threads"]["value"]
+    out["speedup_vs_cpu_1core"] = out["value"] / legs["cg_jacobi_1core"]["value"]
+    out["speedup_vs_direct"] = out["value"] / legs["direct_spsolve"]["value"]
 
 
 def main():
@@ -303,25 +367,7 @@ def main():
         out["note"] = note
 
     if rank == 0 and not a.no_cpu and world == 1:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import cpu_fea  # baseline leg only
-        cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        c = cpu_fea.CpuFea(xyz, e2n, top, bot, fs.E_mod, fs.A, fs.I)
-        t = time.perf_counter()
-        its = []
-        for _ in range(a.cpu_steps):
-            c.active[:] = 1
-            r = c.step(dy, -dy, rtol=a.rtol, max_it=200000, threads=cores)
-            its.append(r["iters"])
-        tc = time.perf_counter() - t
-        c.close()
-        out["cpu_baseline"] = {
-            "value": n_dof * a.cpu_steps / tc, "unit": "DOF/s", "cores": cores, "kind": "port",
-            "sample": f"{a.cpu_steps} full load step(s) of the same {a.config} mesh, C/OpenMP "
-                      f"restatement of fea_petsc.cpp assembly + PETSc KSPCG/PCJACOBI to rtol {a.rtol} "
-                      f"({its[-1]} iters), {tc:.2f} s on {cpu_model()}",
-        }
-        out["speedup_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof)
 
     if rank == 0:
         print(json.dumps(out), flush=True)

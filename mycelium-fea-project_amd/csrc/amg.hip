@@ -146,25 +146,54 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
   width = b - a;
 }
 
-// y −= Σ_k A_ik x_col  (every slot, diagonal included)
+// y ±= Σ_k M_k x_{col_k} over every SELL slot of one row (the diagonal
+// included).  U slots per step with all their loads issued before the first
+// FMA: a row costs ⌈w/U⌉ dependent memory round trips instead of w (the
+// per-thread chain col → value, x is what bounds the small levels).  Slots
+// past the row's width or padded (col < 0) contribute exact zeros.
+template <int ND>
+constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
+
+template <int ND, bool SUB>
+__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const double* __restrict__ val,
+                                         int64_t npos, int64_t base, int w,
+                                         const double* __restrict__ x, double* y) {
+  constexpr int U = mac_unroll<ND>();
+  for (int k = 0; k < w; k += U) {
+    int32_t c[U];
+    int64_t q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q[u] = k + u < w ? base + (int64_t)(k + u) * 64 : base;
+      c[u] = k + u < w ? col[q[u]] : -1;
+    }
+    double m[U][ND * ND], xc[U][ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(val, npos, q[u], m[u]);
+      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : 0.0;
+#pragma unroll
+      for (int a = 0; a < ND; ++a)
+#pragma unroll
+        for (int b = 0; b < ND; ++b)
+          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
+    }
+  }
+}
+
+// y −= Σ_k A_ik x_col
 template <int ND>
 __device__ __forceinline__ void spmv_sub(const AmgMatD& A, int64_t i, const double* __restrict__ x,
                                          double* y) {
   int64_t base;
   int w;
   slice_of(A, i, base, w);
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    const int32_t c = A.col[q];
-    if (c < 0) continue;
-    double m[ND * ND], xc[ND];
-    bload<ND>(A.val, A.npos, q, m);
-    vload<ND>(x, c, xc);
-#pragma unroll
-    for (int a = 0; a < ND; ++a)
-#pragma unroll
-      for (int b = 0; b < ND; ++b) y[a] = fma(-m[a * ND + b], xc[b], y[a]);
-  }
+  sell_mac<ND, true>(A.col, A.val, A.npos, base, w, x, y);
 }
 
 // ---------------------------------------------------------------------------
@@ -315,53 +344,55 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   }
 }
 
+// R = Pᵀ values in R's own SELL layout (coalesced restriction loads)
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const AmgMatD& M = L.AP;
-  if (i - (threadIdx.x & 63) >= M.n) return;
-  int64_t base;
-  int w;
-  slice_of(M, i, base, w);
-  if (i >= M.n) return;
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    if (M.col[q] < 0) continue;
-    double C[ND * ND];
+__global__ __launch_bounds__(kBlock) void k_amg_rvals(AmgLevD L) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= L.R.npos || L.R.col[q] < 0) return;
+  double p[ND * ND], t[ND * ND];
+  bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-    for (int t = L.ap_ptr[q]; t < L.ap_ptr[q + 1]; ++t) {
-      double a[ND * ND], p[ND * ND];
-      bload<ND>(L.A.val, L.A.npos, L.ap_a[t], a);
-      bload<ND>(L.P.val, L.P.npos, L.ap_b[t], p);
-      mm_acc<ND>(a, p, C);
-    }
-    bstore<ND>(L.apval, M.npos, q, C);
-  }
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
+  bstore<ND>(L.R.val, L.R.npos, q, t);
 }
 
+// One output block per thread (every SELL position of the product; pads
+// have empty lists): AP(i, J) = Σ A[a]·P[b].
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= L.AP.npos || L.AP.col[q] < 0) return;
+  double C[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
+  const int t0 = L.ap_ptr[q], t1 = L.ap_ptr[q + 1];
+  for (int t = t0; t < t1; ++t) {
+    double a[ND * ND], p[ND * ND];
+    bload<ND>(L.A.val, L.A.npos, L.ap_a[t], a);
+    bload<ND>(L.P.val, L.P.npos, L.ap_b[t], p);
+    mm_acc<ND>(a, p, C);
+  }
+  bstore<ND>(L.apval, L.AP.npos, q, C);
+}
+
+// A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
-  const int64_t I = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (I - (threadIdx.x & 63) >= Ac.n) return;
-  int64_t base;
-  int w;
-  slice_of(Ac, I, base, w);
-  if (I >= Ac.n) return;
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    if (Ac.col[q] < 0) continue;
-    double C[ND * ND];
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= Ac.npos || Ac.col[q] < 0) return;
+  double C[ND * ND];
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-    for (int t = L.ac_ptr[q]; t < L.ac_ptr[q + 1]; ++t) {
-      double p[ND * ND], m[ND * ND];
-      bload<ND>(L.P.val, L.P.npos, L.ac_a[t], p);
-      bload<ND>(L.apval, L.AP.npos, L.ac_b[t], m);
-      mtm_acc<ND>(p, m, C);
-    }
-    bstore<ND>(Ac.val, Ac.npos, q, C);
+  for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
+  const int t0 = L.ac_ptr[q], t1 = L.ac_ptr[q + 1];
+  for (int t = t0; t < t1; ++t) {
+    double p[ND * ND], m[ND * ND];
+    bload<ND>(L.P.val, L.P.npos, L.ac_a[t], p);
+    bload<ND>(L.apval, L.AP.npos, L.ac_b[t], m);
+    mtm_acc<ND>(p, m, C);
   }
+  bstore<ND>(Ac.val, Ac.npos, q, C);
 }
 
 // ---------------------------------------------------------------------------
@@ -400,19 +431,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   int64_t base;
   int w;
   slice_of(R, I, base, w);
-  if (I >= R.n) return;
   double bc[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) bc[a] = 0.0;
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    const int32_t i = R.col[q];
-    if (i < 0) continue;
-    double p[ND * ND], t[ND];
-    bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
-    vload<ND>(L.te, i, t);
-    mtv_acc<ND>(p, t, bc);
-  }
+  sell_mac<ND, false>(R.col, R.val, R.npos, base, w, L.te, bc);  // R.val = Pᵀ blocks
+  if (I >= R.n) return;
   vstore<ND>(N.b, I, bc);
   double xn[ND];
   dinv_apply<ND>(N, I, N.coarsest ? 1.0 : N.omega[0], bc, xn);
@@ -428,20 +451,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, co
   int64_t base;
   int w;
   slice_of(P, i, base, w);
-  if (i >= P.n) return;
-  const double* __restrict__ e = N.coarsest ? N.x : N.te;
+  const int64_t ii = i < P.n ? i : P.n - 1;
   double x[ND];
-  vload<ND>(L.x, i, x);
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    const int32_t J = P.col[q];
-    if (J < 0) continue;
-    double p[ND * ND], ec[ND];
-    bload<ND>(P.val, P.npos, q, p);
-    vload<ND>(e, J, ec);
-    mv_acc<ND>(p, ec, x);
-  }
-  vstore<ND>(L.x, i, x);
+  vload<ND>(L.x, ii, x);
+  sell_mac<ND, false>(P.col, P.val, P.npos, base, w, N.coarsest ? N.x : N.te, x);
+  if (i < P.n) vstore<ND>(L.x, i, x);
 }
 
 template <int ND>
@@ -597,8 +611,9 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N) {
   hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
   if (L.coarsest || !N) return;
   hipLaunchKernelGGL(k_amg_pvals<ND>, rows_grid(L.P.n), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(L.AP.n), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.n), dim3(kBlock), 0, s, L, N->A);
+  hipLaunchKernelGGL(k_amg_rvals<ND>, rows_grid(L.R.npos), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(L.AP.npos), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next) {
   if (nd == 2) setup_nd<2>(s, L, next);

@@ -5,7 +5,7 @@
 //   dinv[NB2][n]       block-Jacobi inverse of the diagonal blocks
 //   b, x, te [n][ND]   V-cycle right-hand side, iterate, residual / output
 //   P.val[NB2][npos_P] smoothed prolongator (rows = level l, cols = level l+1)
-//   R (col, rp)        P transposed: coarse row → (fine row, P position)
+//   R.val[NB2][npos_R] P transposed: coarse row → fine rows (rp: the P position)
 //   apval[NB2][npos_AP] A_l·P_l (setup only)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -37,7 +37,7 @@ struct AmgLevD {
   const int32_t* agg = nullptr;
   const int32_t* pv_ptr = nullptr;
   const int32_t* pv_a = nullptr;
-  AmgMatD R;  // val unused
+  AmgMatD R;  // val = Pᵀ blocks in R's layout (setup)
   const int32_t* rp = nullptr;
   double* apval = nullptr;
   AmgMatD AP;  // pattern only (sptr, col) + npos; values in apval

@@ -894,7 +894,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
         d.P = mat(L.P, true);
         d.pv_ptr = I(L.pv.ptr);
         d.pv_a = I(L.pv.a);
-        d.R = mat(L.R, false);
+        d.R = mat(L.R, true);
         d.rp = I(L.rp);
         d.AP = mat(L.AP, false);
         d.apval = D((size_t)nb2 * d.AP.npos);

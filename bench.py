@@ -57,28 +57,31 @@ def parse():
 
 def amg_iteration_bytes(ai):
     """Algorithmic HBM bytes of one GAMG-PCG iteration: every
-    launch of the iteration, each array counted once per launch.  Per level l
-    (n rows, nb blocks of A_l, pb blocks of P_l, B = 8·ND² bytes per block,
-    V = 8·ND per row vector):
-      resid    nb·(B+4) + 3·V·n                 (A, b, x, t)
-      restrict pb·(B+8) + V·n + (2V + B)·n'     (Pᵀ, t; b', x', D⁻¹ of level l+1)
-      prolong  pb·(B+4) + 2·V·n + V·n'          (P, x in/out, e of level l+1)
-      post     nb·(B+4) + (3V + B)·n            (A, b, x, e, D⁻¹)
-    CG: update 10·V·n0 + (V + B)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀);
-        w      nb0·(B+4) + 3·V·n0.
+    launch of the iteration, each array counted once per launch.  The V-cycle
+    is f32 (B = 4·ND² bytes per block, V = 4·ND per row vector), the CG f64
+    (V8 = 8·ND; A_0 in f64 for w = A u, B8 = 8·ND²).  Per level l (n rows, nb
+    blocks of A_l, pb blocks of P_l = R_l; level 0's b and e are the CG's
+    f64 r and u, Vb = V8 there, V elsewhere):
+      resid    nb·(B+4) + (2V + Vb)·n              (A, x, b in; t out)
+      restrict pb·(B+4) + V·n + (2V + B)·n'        (Pᵀ, t in; b', x' out, D⁻¹')
+      prolong  pb·(B+4) + 2V·n + V·n'              (P, x in/out, e' in)
+      post     nb·(B+4) + (V + B + 2Vb)·n          (A, x, D⁻¹, b in; e out)
+    CG: update (10·V8 + B + V)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀ out);
+        w      nb0·(B8+4) + 3·V8·n0.
     """
     nd = ai["nd"]
-    B, V = 8 * nd * nd, 8 * nd
+    B, V, B8, V8 = 4 * nd * nd, 4 * nd, 8 * nd * nd, 8 * nd
     rows, blocks, pbl = ai["rows"], ai["blocks"], ai["pblocks"]
     b = 0
     for l in range(ai["levels"] - 1):
         n, nn = rows[l], rows[l + 1]
-        b += blocks[l] * (B + 4) + 3 * V * n
-        b += pbl[l] * (B + 8) + V * n + (2 * V + B) * nn
+        Vb = V8 if l == 0 else V
+        b += blocks[l] * (B + 4) + (2 * V + Vb) * n
+        b += pbl[l] * (B + 4) + V * n + (2 * V + B) * nn
         b += pbl[l] * (B + 4) + 2 * V * n + V * nn
-        b += blocks[l] * (B + 4) + (3 * V + B) * n
+        b += blocks[l] * (B + 4) + (V + B + 2 * Vb) * n
     n0 = rows[0]
-    b += 10 * V * n0 + (V + B) * n0 + blocks[0] * (B + 4) + 3 * V * n0
+    b += (10 * V8 + B + V) * n0 + blocks[0] * (B8 + 4) + 3 * V8 * n0
     return b
 
 
@@ -333,7 +336,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if pc != PC_GAMG else "f64 (CG; f32 AMG V-cycle)",
         "data": "synthetic (tiled copies of results/sim_20251117_181147; no RNG)",
         "config": {
             "workload": workload,

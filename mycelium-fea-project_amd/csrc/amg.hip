@@ -1,11 +1,14 @@
 // amg.hip — SA-AMG preconditioned CG on device (amg.hpp, amg_kernels.hpp).
 //
-// Numeric setup per solve (after assembly), level by level:
+// Numeric setup per solve (after assembly), level by level, in f64:
 //   A_0      gather of the assembled SELL slots (multi-edges summed in slot order)
 //   D_l⁻¹    exact inverse of every diagonal block; Gershgorin bound g_l of
 //            ρ(D_l⁻¹ A_l); smoother weight ω_l = 4 / (3 ρ̂_l), ρ̂_l = max(2, g_l / 1.45)
 //   P_l      (I − ω_l D_l⁻¹ A_l) P_tent, P_tent = aggregate indicator ⊗ I
 //   A_{l+1}  P_lᵀ (A_l P_l), both products as fixed-order gathers
+// Every producer also writes an f32 copy (A_l, D_l⁻¹, P_l, R_l = P_lᵀ) for
+// the V-cycle.
+//
 // Why ρ̂ = max(2, g/1.45): on level 0, A = Σ_e A_e + reg·I with every element
 // matrix A_e = [[S,−S],[−S,S]] ≤ 2·blockdiag(A_e), so ρ(D⁻¹A) ≤ 2 exactly; on
 // the coarse levels the measured ρ stays ≈ 2 while the
@@ -15,57 +18,46 @@
 // requirement for CG — while ω takes the sharp value 2/3 whenever g < 2.9.
 //
 // V-cycle (one per PCG iteration, pre- and post-smoothing by one damped
-// block-Jacobi sweep each, exact block-diagonal solve on the coarsest level):
+// block-Jacobi sweep each, exact block-diagonal solve on the coarsest level),
+// in f32 (values and vectors; the CG around it stays f64 — a preconditioner
+// only has to be a fixed SPD operator: measured, the f32 cycle gives the same
+// iteration counts to 1e-8 and to 1e-13 as the f64 one):
 //   x_l = ω D⁻¹ b_l                      (fused into the kernel producing b_l)
 //   t_l = b_l − A_l x_l                  k_amg_resid
 //   b_{l+1} = P_lᵀ t_l, x_{l+1} = ω D⁻¹ b_{l+1}   k_amg_restrict
 //   ... recursion ...
 //   x_l += P_l e_{l+1}                   k_amg_prolong
 //   e_l = x_l + ω D⁻¹ (b_l − A_l x_l)    k_amg_post
+// Level 0 reads the CG's f64 residual r as b_0 and writes the CG's f64 u as e_0.
 // CG: the single-reduction (Chronopoulos–Gear) recurrences of cg.hip with
 // u = M r the V-cycle output: per iteration one update kernel (reads the
 // previous partials, forms α, β, the stopping test), the V-cycle, and one
-// w = A_0 u kernel that writes the next partials (γ, δ, ‖r‖², ‖u‖²).
+// w = A_0 u kernel (f64 A_0) that writes the next partials (γ, δ, ‖r‖², ‖u‖²).
 #include "amg_kernels.hpp"
 #include "device_util.hpp"
 
 namespace mfea {
 
-template <int ND>
-__device__ __forceinline__ void bload(const double* __restrict__ v, int64_t npos, int64_t q, double* m) {
+// ---- block / vector helpers (T = storage type, C = compute type) -----------
+template <int ND, class T, class C>
+__device__ __forceinline__ void bload(const T* __restrict__ v, int64_t npos, int64_t q, C* m) {
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) m[c] = v[c * npos + q];
+  for (int c = 0; c < ND * ND; ++c) m[c] = (C)v[c * npos + q];
 }
-template <int ND>
-__device__ __forceinline__ void bstore(double* __restrict__ v, int64_t npos, int64_t q, const double* m) {
+template <int ND, class T, class C>
+__device__ __forceinline__ void bstore(T* __restrict__ v, int64_t npos, int64_t q, const C* m) {
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) v[c * npos + q] = m[c];
+  for (int c = 0; c < ND * ND; ++c) v[c * npos + q] = (T)m[c];
 }
-template <int ND>
-__device__ __forceinline__ void vload(const double* __restrict__ v, int64_t i, double* o) {
+template <int ND, class T, class C>
+__device__ __forceinline__ void vload(const T* __restrict__ v, int64_t i, C* o) {
 #pragma unroll
-  for (int a = 0; a < ND; ++a) o[a] = v[ND * i + a];
+  for (int a = 0; a < ND; ++a) o[a] = (C)v[ND * i + a];
 }
-template <int ND>
-__device__ __forceinline__ void vstore(double* __restrict__ v, int64_t i, const double* o) {
+template <int ND, class T, class C>
+__device__ __forceinline__ void vstore(T* __restrict__ v, int64_t i, const C* o) {
 #pragma unroll
-  for (int a = 0; a < ND; ++a) v[ND * i + a] = o[a];
-}
-// y += M x
-template <int ND>
-__device__ __forceinline__ void mv_acc(const double* m, const double* x, double* y) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a)
-#pragma unroll
-    for (int b = 0; b < ND; ++b) y[a] = fma(m[a * ND + b], x[b], y[a]);
-}
-// y += Mᵀ x
-template <int ND>
-__device__ __forceinline__ void mtv_acc(const double* m, const double* x, double* y) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a)
-#pragma unroll
-    for (int b = 0; b < ND; ++b) y[a] = fma(m[b * ND + a], x[b], y[a]);
+  for (int a = 0; a < ND; ++a) v[ND * i + a] = (T)o[a];
 }
 // C += A B
 template <int ND>
@@ -154,10 +146,10 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
 template <int ND>
 constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
 
-template <int ND, bool SUB>
-__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const double* __restrict__ val,
+template <int ND, bool SUB, class TV, class TX, class C>
+__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                          int64_t npos, int64_t base, int w,
-                                         const double* __restrict__ x, double* y) {
+                                         const TX* __restrict__ x, C* y) {
   constexpr int U = mac_unroll<ND>();
   for (int k = 0; k < w; k += U) {
     int32_t c[U];
@@ -167,7 +159,7 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
       q[u] = k + u < w ? base + (int64_t)(k + u) * 64 : base;
       c[u] = k + u < w ? col[q[u]] : -1;
     }
-    double m[U][ND * ND], xc[U][ND];
+    C m[U][ND * ND], xc[U][ND];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       bload<ND>(val, npos, q[u], m[u]);
@@ -176,7 +168,7 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : 0.0;
+      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
 #pragma unroll
       for (int a = 0; a < ND; ++a)
 #pragma unroll
@@ -186,21 +178,28 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
   }
 }
 
-// y −= Σ_k A_ik x_col
-template <int ND>
-__device__ __forceinline__ void spmv_sub(const AmgMatD& A, int64_t i, const double* __restrict__ x,
-                                         double* y) {
-  int64_t base;
-  int w;
-  slice_of(A, i, base, w);
-  sell_mac<ND, true>(A.col, A.val, A.npos, base, w, x, y);
+// o = s · D⁻¹ v  (D⁻¹ SoA [NB2][n], storage TD, compute C)
+template <int ND, class TD, class C>
+__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t n, int64_t i, C s,
+                                           const C* v, C* o) {
+  C Di[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) Di[c] = (C)dinv[(int64_t)c * n + i];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) {
+    C acc = 0;
+#pragma unroll
+    for (int b = 0; b < ND; ++b) acc = fma(Di[a * ND + b], v[b], acc);
+    o[a] = s * acc;
+  }
 }
 
 // ---------------------------------------------------------------------------
-// numeric setup
+// numeric setup (f64, with f32 copies for the V-cycle)
 // ---------------------------------------------------------------------------
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
+__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ row0,
+                                                   const int32_t* __restrict__ ptr,
                                                    const int32_t* __restrict__ lst, double reg) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i - (threadIdx.x & 63) >= A.n) return;
@@ -216,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const 
     if (k == 0) {
       double s6[6];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + i];
+      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
       s6[0] += reg;
       s6[3] += reg;
       s6[5] += reg;
@@ -232,6 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const 
       }
     }
     bstore<ND>(A.val, A.npos, q, m);
+    bstore<ND>(A.val32, A.npos, q, m);
   }
 }
 
@@ -250,7 +250,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
       bload<ND>(A.val, A.npos, base, D);
       binv<ND>(D, Di);
 #pragma unroll
-      for (int c = 0; c < ND * ND; ++c) L.dinv[(int64_t)c * A.n + i] = Di[c];
+      for (int c = 0; c < ND * ND; ++c) {
+        L.dinv[(int64_t)c * A.n + i] = Di[c];
+        L.dinv32[(int64_t)c * A.n + i] = (float)Di[c];
+      }
       double rs[ND];
 #pragma unroll
       for (int a = 0; a < ND; ++a) rs[a] = 0.0;
@@ -341,10 +344,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
       for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
     }
     bstore<ND>(P.val, P.npos, q, pm);
+    bstore<ND>(P.val32, P.npos, q, pm);
   }
 }
 
-// R = Pᵀ values in R's own SELL layout (coalesced restriction loads)
+// R = Pᵀ (f32) in R's own SELL layout: coalesced restriction loads
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_rvals(AmgLevD L) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_rvals(AmgLevD L) {
   for (int a = 0; a < ND; ++a)
 #pragma unroll
     for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
-  bstore<ND>(L.R.val, L.R.npos, q, t);
+  bstore<ND>(L.R.val32, L.R.npos, q, t);
 }
 
 // One output block per thread (every SELL position of the product; pads
@@ -393,33 +397,27 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
     mtm_acc<ND>(p, m, C);
   }
   bstore<ND>(Ac.val, Ac.npos, q, C);
+  bstore<ND>(Ac.val32, Ac.npos, q, C);
 }
 
 // ---------------------------------------------------------------------------
-// V-cycle
+// V-cycle (f32; level 0 reads r and writes u in f64)
 // ---------------------------------------------------------------------------
-template <int ND>
-__device__ __forceinline__ void dinv_apply(const AmgLevD& L, int64_t i, double scale, const double* v,
-                                           double* o) {
-  double Di[ND * ND];
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[(int64_t)c * L.A.n + i];
-#pragma unroll
-  for (int a = 0; a < ND; ++a) o[a] = 0.0;
-  mv_acc<ND>(Di, v, o);
-#pragma unroll
-  for (int a = 0; a < ND; ++a) o[a] *= scale;
-}
-
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const int32_t* gate) {
+template <int ND, class TB>
+__global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
+                                                      const int32_t* gate) {
   if (gated(gate)) return;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= L.A.n) return;
-  double y[ND];
-  if (i < L.A.n) vload<ND>(L.b, i, y);
-  spmv_sub<ND>(L.A, i < L.A.n ? i : L.A.n - 1, L.x, y);
-  if (i < L.A.n) vstore<ND>(L.te, i, y);
+  const int64_t n = L.A.n;
+  if (i - (threadIdx.x & 63) >= n) return;
+  const int64_t ii = i < n ? i : n - 1;
+  int64_t base;
+  int w;
+  slice_of(L.A, ii, base, w);
+  float y[ND];
+  vload<ND>(b, ii, y);
+  sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  if (i < n) vstore<ND>(L.t, i, y);
 }
 
 template <int ND>
@@ -431,14 +429,14 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   int64_t base;
   int w;
   slice_of(R, I, base, w);
-  double bc[ND];
+  float bc[ND];
 #pragma unroll
-  for (int a = 0; a < ND; ++a) bc[a] = 0.0;
-  sell_mac<ND, false>(R.col, R.val, R.npos, base, w, L.te, bc);  // R.val = Pᵀ blocks
+  for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
+  sell_mac<ND, false>(R.col, R.val32, R.npos, base, w, L.t, bc);  // R = Pᵀ blocks
   if (I >= R.n) return;
   vstore<ND>(N.b, I, bc);
-  double xn[ND];
-  dinv_apply<ND>(N, I, N.coarsest ? 1.0 : N.omega[0], bc, xn);
+  float xn[ND];
+  dinv_apply<ND>(N.dinv32, N.A.n, I, N.coarsest ? 1.0f : (float)N.omega[0], bc, xn);
   vstore<ND>(N.x, I, xn);
 }
 
@@ -452,50 +450,177 @@ __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, co
   int w;
   slice_of(P, i, base, w);
   const int64_t ii = i < P.n ? i : P.n - 1;
-  double x[ND];
+  float x[ND];
   vload<ND>(L.x, ii, x);
-  sell_mac<ND, false>(P.col, P.val, P.npos, base, w, N.coarsest ? N.x : N.te, x);
+  sell_mac<ND, false>(P.col, P.val32, P.npos, base, w, N.coarsest ? N.x : N.e, x);
   if (i < P.n) vstore<ND>(L.x, i, x);
 }
 
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const int32_t* gate) {
+template <int ND, class TB, class TE>
+__global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
+                                                     const int32_t* gate) {
   if (gated(gate)) return;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= L.A.n) return;
-  const int64_t ii = i < L.A.n ? i : L.A.n - 1;
-  double y[ND], x[ND];
-  vload<ND>(L.b, ii, y);
+  const int64_t n = L.A.n;
+  if (i - (threadIdx.x & 63) >= n) return;
+  const int64_t ii = i < n ? i : n - 1;
+  int64_t base;
+  int w;
+  slice_of(L.A, ii, base, w);
+  float y[ND], x[ND], d[ND];
+  vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
-  spmv_sub<ND>(L.A, ii, L.x, y);
-  double d[ND];
-  dinv_apply<ND>(L, ii, L.omega[0], y, d);
+  sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  dinv_apply<ND>(L.dinv32, n, ii, (float)L.omega[0], y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
-  if (i < L.A.n) vstore<ND>(L.te, i, x);
+  if (i < n) vstore<ND>(e, i, x);
 }
 
 // ---------------------------------------------------------------------------
-// CG
+// The V-cycle below level l0 in ONE workgroup: resid / restrict down to the
+// coarsest level, prolong / post back up to l0, the phases separated by
+// workgroup barriers instead of kernel boundaries.  The deep levels hold a
+// few thousand rows at most, so a full-grid launch per phase is ≈ 4.5 µs of
+// latency for ≈ 0.1 µs of work; here a phase costs its rows' dependent loads
+// (≈ rows/1024 × 3 hops) plus one barrier.  lev: device copy of the level
+// views; levels ≥ l0 use f32 b and e.
 // ---------------------------------------------------------------------------
+constexpr int kTailBS = 1024;
+
+template <int ND>
+__device__ __forceinline__ void tail_resid(const AmgLevD& L) {
+  const int64_t n = L.A.n;
+  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
+    const int64_t i = r0 + threadIdx.x;
+    if (r0 + (threadIdx.x & ~63) >= n) break;  // whole wave past the end
+    const int64_t ii = i < n ? i : n - 1;
+    int64_t base;
+    int w;
+    slice_of(L.A, ii, base, w);
+    float y[ND];
+    vload<ND>(L.b, ii, y);
+    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    if (i < n) vstore<ND>(L.t, i, y);
+  }
+}
+template <int ND>
+__device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N) {
+  const int64_t n = L.R.n;
+  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
+    const int64_t I = r0 + threadIdx.x;
+    if (r0 + (threadIdx.x & ~63) >= n) break;
+    int64_t base;
+    int w;
+    slice_of(L.R, I, base, w);
+    float bc[ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
+    sell_mac<ND, false>(L.R.col, L.R.val32, L.R.npos, base, w, L.t, bc);
+    if (I < n) {
+      vstore<ND>(N.b, I, bc);
+      float xn[ND];
+      dinv_apply<ND>(N.dinv32, N.A.n, I, sc, bc, xn);
+      vstore<ND>(N.x, I, xn);
+    }
+  }
+}
+template <int ND>
+__device__ __forceinline__ void tail_prolong(const AmgLevD& L, const AmgLevD& N) {
+  const int64_t n = L.P.n;
+  const float* e = N.coarsest ? N.x : N.e;
+  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
+    const int64_t i = r0 + threadIdx.x;
+    if (r0 + (threadIdx.x & ~63) >= n) break;
+    int64_t base;
+    int w;
+    slice_of(L.P, i, base, w);
+    const int64_t ii = i < n ? i : n - 1;
+    float x[ND];
+    vload<ND>(L.x, ii, x);
+    sell_mac<ND, false>(L.P.col, L.P.val32, L.P.npos, base, w, e, x);
+    if (i < n) vstore<ND>(L.x, i, x);
+  }
+}
+template <int ND>
+__device__ __forceinline__ void tail_post(const AmgLevD& L) {
+  const int64_t n = L.A.n;
+  const float om = (float)L.omega[0];
+  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
+    const int64_t i = r0 + threadIdx.x;
+    if (r0 + (threadIdx.x & ~63) >= n) break;
+    const int64_t ii = i < n ? i : n - 1;
+    int64_t base;
+    int w;
+    slice_of(L.A, ii, base, w);
+    float y[ND], x[ND], d[ND];
+    vload<ND>(L.b, ii, y);
+    vload<ND>(L.x, ii, x);
+    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    dinv_apply<ND>(L.dinv32, n, ii, om, y, d);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) x[a] += d[a];
+    if (i < n) vstore<ND>(L.e, i, x);
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kTailBS) void k_amg_tail(const AmgLevD* __restrict__ lev, int l0, int nlev,
+                                                      const int32_t* gate) {
+  if (gated(gate)) return;
+  for (int l = l0; l + 1 < nlev; ++l) {
+    const AmgLevD L = lev[l];
+    tail_resid<ND>(L);
+    __syncthreads();
+    tail_restrict<ND>(L, lev[l + 1]);
+    __syncthreads();
+  }
+  for (int l = nlev - 2; l >= l0; --l) {
+    const AmgLevD L = lev[l];
+    tail_prolong<ND>(L, lev[l + 1]);
+    __syncthreads();
+    tail_post<ND>(L);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CG (f64)
+// ---------------------------------------------------------------------------
+// the V-cycle's first smoothing step x_0 = ω D⁻¹ r (f32), or — a single-level
+// hierarchy (no free-free coupling) is its own coarsest level — the exact
+// block solve u = D⁻¹ r (f64) straight into the CG's u
+template <int ND>
+__device__ __forceinline__ void vcycle_entry(const AmgLevD& L0, const AmgCg& cg, int64_t i, const double* r) {
+  if (L0.coarsest) {
+    double u[ND];
+    dinv_apply<ND>(L0.dinv, L0.A.n, i, 1.0, r, u);
+    vstore<ND>(cg.u, i, u);
+  } else {
+    float rf[ND], x0[ND];
+#pragma unroll
+    for (int a = 0; a < ND; ++a) rf[a] = (float)r[a];
+    dinv_apply<ND>(L0.dinv32, L0.A.n, i, (float)L0.omega[0], rf, x0);
+    vstore<ND>(L0.x, i, x0);
+  }
+}
+
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, const double* __restrict__ b_row) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= cg.n) return;
-  double r[ND], z[ND], x0[ND];
+  double r[ND], z[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) {
-    r[a] = b_row[3 * i + a];
+    r[a] = b_row[3 * (int64_t)cg.row0[i] + a];
     z[a] = 0.0;
   }
   vstore<ND>(cg.r, i, r);
   vstore<ND>(cg.x, i, z);
   vstore<ND>(cg.p, i, z);
   vstore<ND>(cg.s, i, z);
-  // a single-level hierarchy (no free-free coupling) is its own coarsest
-  // level: the V-cycle is then the exact block solve, written straight to u
-  dinv_apply<ND>(L0, i, L0.coarsest ? 1.0 : L0.omega[0], r, x0);
-  vstore<ND>(L0.coarsest ? L0.te : L0.x, i, x0);
+  vcycle_entry<ND>(L0, cg, i, r);
 }
 
 template <int ND, bool FIRST>
@@ -506,15 +631,16 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg,
   const int lane = threadIdx.x & 63;
   for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i - lane < cg.n; i += stride) {
     const int64_t ii = i < cg.n ? i : cg.n - 1;
+    int64_t base;
+    int w;
+    slice_of(L0.A, ii, base, w);
     double y[ND], u[ND], r[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    spmv_sub<ND>(L0.A, ii, cg.u, y);  // y = −A u
+    sell_mac<ND, false>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
     if (i >= cg.n) continue;
     vload<ND>(cg.u, i, u);
     vload<ND>(cg.r, i, r);
-#pragma unroll
-    for (int a = 0; a < ND; ++a) y[a] = -y[a];
     vstore<ND>(cg.w, i, y);
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
@@ -547,10 +673,10 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_update(int j, AmgLevD L0, AmgC
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
   cg_record(slots, j, S, cs);
   if (cs.status != kRun) return;
-  const double alpha = cs.alpha, beta = cs.beta, om = L0.omega[0];
+  const double alpha = cs.alpha, beta = cs.beta;
   const int64_t stride = (int64_t)gridDim.x * kCgBS;
   for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i < cg.n; i += stride) {
-    double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND], x0[ND];
+    double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
     vload<ND>(cg.u, i, u);
     vload<ND>(cg.w, i, w);
     vload<ND>(cg.p, i, p);
@@ -568,8 +694,7 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_update(int j, AmgLevD L0, AmgC
     vstore<ND>(cg.s, i, s);
     vstore<ND>(cg.x, i, x);
     vstore<ND>(cg.r, i, r);
-    dinv_apply<ND>(L0, i, L0.coarsest ? 1.0 : om, r, x0);
-    vstore<ND>(L0.coarsest ? L0.te : L0.x, i, x0);
+    vcycle_entry<ND>(L0, cg, i, r);
   }
 }
 
@@ -578,7 +703,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_finish(AmgCg cg, double* __restr
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= cg.n) return;
 #pragma unroll
-  for (int a = 0; a < ND; ++a) x_row[3 * i + a] = cg.x[ND * i + a];
+  for (int a = 0; a < ND; ++a) x_row[3 * (int64_t)cg.row0[i] + a] = cg.x[ND * i + a];
 }
 
 // ---------------------------------------------------------------------------
@@ -593,14 +718,15 @@ int64_t amg_w_grid(int64_t n) {
 static int pu_of_grid(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : 8; }
 
 template <int ND>
-static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* p, const int32_t* a,
-                  double reg) {
-  if (L0.A.n > 0) hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.n), dim3(kBlock), 0, s, L0.A, sop, p, a, reg);
+static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
+                  const int32_t* a, double reg) {
+  if (L0.A.n > 0)
+    hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.n), dim3(kBlock), 0, s, L0.A, sop, row0, p, a, reg);
 }
-void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* a0_ptr,
-                   const int32_t* a0_a, double reg) {
-  if (nd == 2) a0_nd<2>(s, L0, sop, a0_ptr, a0_a, reg);
-  else a0_nd<3>(s, L0, sop, a0_ptr, a0_a, reg);
+void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
+                   const int32_t* a0_ptr, const int32_t* a0_a, double reg) {
+  if (nd == 2) a0_nd<2>(s, L0, sop, row0, a0_ptr, a0_a, reg);
+  else a0_nd<3>(s, L0, sop, row0, a0_ptr, a0_a, reg);
 }
 
 template <int ND>
@@ -621,25 +747,41 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 }
 
 template <int ND>
-static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const int32_t* gate) {
-  for (int l = 0; l + 1 < nlev; ++l) {
-    hipLaunchKernelGGL(k_amg_resid<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], gate);
-    hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(lev[l + 1].A.n), dim3(kBlock), 0, s, lev[l],
-                       lev[l + 1], gate);
+static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const AmgLevD* lev_dev,
+                      int tail, const int32_t* gate) {
+  const dim3 b(kBlock);
+  const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
+  for (int l = 0; l < top; ++l) {
+    if (l == 0)
+      hipLaunchKernelGGL((k_amg_resid<ND, double>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
+    else
+      hipLaunchKernelGGL((k_amg_resid<ND, float>), rows_grid(lev[l].A.n), b, 0, s, lev[l], (const float*)lev[l].b, gate);
+    hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(lev[l + 1].A.n), b, 0, s, lev[l], lev[l + 1], gate);
   }
-  for (int l = nlev - 2; l >= 0; --l) {
-    hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], lev[l + 1],
-                       gate);
-    hipLaunchKernelGGL(k_amg_post<ND>, rows_grid(lev[l].A.n), dim3(kBlock), 0, s, lev[l], gate);
+  if (tail > 0) hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, lev_dev, tail, nlev, gate);
+  for (int l = top - 1; l >= 0; --l) {
+    hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
+    if (l == 0)
+      hipLaunchKernelGGL((k_amg_post<ND, double, double>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
+                         (const double*)cg.r, cg.u, gate);
+    else
+      hipLaunchKernelGGL((k_amg_post<ND, float, float>), rows_grid(lev[l].A.n), b, 0, s, lev[l],
+                         (const float*)lev[l].b, lev[l].e, gate);
   }
 }
-void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const int32_t* gate) {
-  if (nlev <= 0 || lev[0].A.n <= 0) return;
-  if (nlev == 1) {  // a single level is the coarsest: block-Jacobi solve, done by the producer
-    return;
-  }
-  if (nd == 2) vcycle_nd<2>(s, lev, nlev, gate);
-  else vcycle_nd<3>(s, lev, nlev, gate);
+void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
+                       const AmgLevD* lev_dev, int tail, const int32_t* gate) {
+  // one level: the coarsest solve u = D⁻¹ r is done by the producer of r
+  if (nlev <= 1 || lev[0].A.n <= 0) return;
+  if (tail >= nlev - 1) tail = 0;  // nothing below the coarsest to fuse
+  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, lev_dev, tail, gate);
+  else vcycle_nd<3>(s, lev, nlev, cg, lev_dev, tail, gate);
+}
+
+int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows) {
+  for (int l = 1; l + 1 < nlev; ++l)
+    if (rows[l] <= max_rows) return l;
+  return 0;
 }
 
 void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row) {

@@ -75,6 +75,9 @@ struct AmgLevel {
 struct AmgPlan {
   int nd = 2;
   std::vector<AmgLevel> lev;  // lev[0] = the free-node system
+  // level-0 row i ↔ free row row0[i] of the Pattern (rows are relabelled per
+  // level so SELL slices hold rows of similar length; amg_symbolic.cpp)
+  std::vector<int32_t> row0;
   // level-0 values: A_0(i, j≠i) = Σ over the SELL slots of the assembled
   // operator (symbolic.hpp) joining i and j; the diagonal = diag[i] + reg·I
   PosList a0;                 // per A_0 position: SELL slot positions (diag: none)

@@ -2,10 +2,11 @@
 // (amg.hip).  Layout of one level l in HBM (n rows = nodes or aggregates,
 // ND = 2 or 3 DOFs per row, NB2 = ND² doubles per block, row-major):
 //   A.val[NB2][npos]   SELL-64 blocks of A_l, slot 0 of a row = its diagonal
-//   dinv[NB2][n]       block-Jacobi inverse of the diagonal blocks
-//   b, x, te [n][ND]   V-cycle right-hand side, iterate, residual / output
+//                      (f64 for the setup and the CG; val32: f32 V-cycle copy)
+//   dinv[NB2][n]       block-Jacobi inverse of the diagonal blocks (+ f32 copy)
+//   b, x, t, e [n][ND] f32 V-cycle right-hand side, iterate, residual, output
 //   P.val[NB2][npos_P] smoothed prolongator (rows = level l, cols = level l+1)
-//   R.val[NB2][npos_R] P transposed: coarse row → fine rows (rp: the P position)
+//   R.val32[NB2][npos_R] P transposed: coarse row → fine rows (rp: the P position)
 //   apval[NB2][npos_AP] A_l·P_l (setup only)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -20,24 +21,28 @@ struct AmgMatD {
   int64_t npos = 0;  // SELL positions (slot rows · 64)
   const int32_t* sptr = nullptr;
   const int32_t* col = nullptr;
-  double* val = nullptr;  // [NB2][npos]
+  double* val = nullptr;   // [NB2][npos] f64 (setup; A_0 also serves the CG's w = A u)
+  float* val32 = nullptr;  // [NB2][npos] f32 copy for the V-cycle
 };
 
 struct AmgLevD {
   AmgMatD A;
   double* dinv = nullptr;
+  float* dinv32 = nullptr;
   double* gpart = nullptr;  // per-block Gershgorin maxima (setup)
   double* omega = nullptr;  // [2]: smoother weight ω_l, Gershgorin bound g_l
-  double* b = nullptr;
-  double* x = nullptr;
-  double* te = nullptr;
+  // V-cycle vectors [n][ND], f32 (level 0: b = the CG's r, e = the CG's u, f64)
+  float* b = nullptr;
+  float* x = nullptr;
+  float* t = nullptr;
+  float* e = nullptr;
   int coarsest = 0;
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   const int32_t* agg = nullptr;
   const int32_t* pv_ptr = nullptr;
   const int32_t* pv_a = nullptr;
-  AmgMatD R;  // val = Pᵀ blocks in R's layout (setup)
+  AmgMatD R;  // val32 = Pᵀ blocks in R's layout (setup)
   const int32_t* rp = nullptr;
   double* apval = nullptr;
   AmgMatD AP;  // pattern only (sptr, col) + npos; values in apval
@@ -49,27 +54,32 @@ struct AmgLevD {
   const int32_t* ac_b = nullptr;
 };
 
-// CG vectors of the AMG path: free rows in level-0 order, ND per row
+// CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
 struct AmgCg {
   int64_t n = 0;
+  const int32_t* row0 = nullptr;  // level-0 row → Pattern (row-order) free row
   double* x = nullptr;
   double* p = nullptr;
   double* s = nullptr;
-  double* r = nullptr;  // = level 0's b
+  double* r = nullptr;  // level 0's V-cycle input
   double* w = nullptr;
-  double* u = nullptr;  // = level 0's te (the V-cycle output)
+  double* u = nullptr;  // level 0's V-cycle output
 };
 
 // ---- numeric setup (every solve) ------------------------------------------
 // A_0 from the assembled SELL operator: off-diagonal = Σ of the listed slots'
 // K_ij (= −S_e), diagonal = K_ii + reg·I.
-void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* a0_ptr,
-                   const int32_t* a0_a, double reg);
+void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
+                   const int32_t* a0_ptr, const int32_t* a0_a, double reg);
 // dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next);
-// ---- one V-cycle z = M r (level 0's b → level 0's te); gate = NULL: always,
-// else only while *gate == kRun
-void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const int32_t* gate);
+// ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
+// else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
+// single-workgroup launch (k_amg_tail) reading the level views at lev_dev.
+void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
+                       const AmgLevD* lev_dev, int tail, const int32_t* gate);
+// first level l ≥ 1 (above the coarsest) with at most max_rows rows, or 0
+int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------
 // r = b (row-order 3-comp RHS of k_cg_rhs), x = p = s = 0, level-0 x = ω D⁻¹ r
 void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row);

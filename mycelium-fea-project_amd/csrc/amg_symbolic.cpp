@@ -1,5 +1,18 @@
 // amg_symbolic.cpp — host symbolic phase of the SA-AMG preconditioner (amg.hpp).
-// Pure host C++ (no HIP), unit-tested on CPU through the debug C ABI.
+// Pure host C++ (no HIP), unit-tested on CPU through tests/native/host_shim.cpp.
+//
+// Two stages:
+//   1. the hierarchy in natural numbering, as row-major (CSR) patterns whose
+//      index lists reference CSR entries: aggregation, P, R = Pᵀ, A·P and
+//      A_{l+1} = Pᵀ A P (Gustavson, fixed order);
+//   2. the device layout: every level's rows are relabelled so that, inside
+//      windows of kSortWindow consecutive rows, longer rows come first
+//      (SELL-C-σ, C = 64): the 64 rows of a slice then have nearly equal
+//      lengths and a slice's width (its longest row) stops padding the
+//      others.  Natural (DFS / aggregate) order is kept across windows, so
+//      gathers stay local.  Measured on the C3 network: valid positions of
+//      the level-0 A / R layouts 52 % / 28 % in natural order, 97 % / 81 %
+//      with 4096-row windows.
 #include <algorithm>
 #include <numeric>
 
@@ -9,43 +22,30 @@ namespace mfea {
 
 namespace {
 
-// SELL-64 pattern from per-row column lists (storage order as given)
-std::string make_sell(int64_t n, const std::vector<int64_t>& rowptr, const std::vector<int32_t>& cols,
-                      SellPat& S) {
-  S = SellPat();
-  S.n = n;
-  const int64_t ns = (n + 63) / 64;
-  S.sptr.assign(ns + 1, 0);
-  S.rlen.assign(n, 0);
-  int64_t slots = 0;
-  for (int64_t s = 0; s < ns; ++s) {
-    int64_t w = 0;
-    for (int64_t r = 64 * s; r < std::min<int64_t>(n, 64 * s + 64); ++r) {
-      const int64_t len = rowptr[r + 1] - rowptr[r];
-      S.rlen[r] = (int32_t)len;
-      w = std::max(w, len);
-    }
-    slots += w;
-    if (slots * 64 > INT32_MAX) return "AMG level too large for int32 positions";
-    S.sptr[s + 1] = (int32_t)slots;
-  }
-  S.col.assign(slots * 64, -1);
-  for (int64_t r = 0; r < n; ++r)
-    for (int64_t k = rowptr[r]; k < rowptr[r + 1]; ++k) S.col[S.pos(r, (int)(k - rowptr[r]))] = cols[k];
-  return "";
-}
+constexpr int64_t kSortWindow = 4096;  // rows per SELL-C-σ sorting window (64 slices)
 
-// list sizes → CSR pointer over positions (checks int32)
-std::string finish_ptr(PosList& L, int64_t& items) {
-  int64_t run = 0;
-  for (size_t q = 0; q + 1 < L.ptr.size(); ++q) {
-    const int64_t c = L.ptr[q + 1];
-    L.ptr[q + 1] = (int32_t)(run += c);
-    if (run > INT32_MAX) return "AMG index lists too large for int32";
-  }
-  items += run;
-  return "";
-}
+struct Csr {
+  int64_t n = 0;
+  std::vector<int64_t> ptr{0};
+  std::vector<int32_t> col;
+  int64_t len(int64_t r) const { return ptr[r + 1] - ptr[r]; }
+};
+// index lists per entry of an output matrix (CSR over its entries)
+struct Lists {
+  std::vector<int64_t> ptr{0};
+  std::vector<int32_t> a, b;
+};
+
+struct LevelCsr {
+  Csr A;
+  int64_t nc = 0;
+  std::vector<int32_t> agg;
+  Csr P, R, AP;
+  Lists pv;                // per P entry: A entries
+  std::vector<int32_t> rp;  // per R entry: P entry
+  Lists ap;                // per AP entry: (A entry, P entry)
+  Lists ac;                // per A_{l+1} entry: (P entry, AP entry)
+};
 
 // Standard SA aggregation (PyAMG standard_aggregation) with every coupling
 // strong: (1) a node whose neighbours are all unaggregated roots a new
@@ -53,16 +53,17 @@ std::string finish_ptr(PosList& L, int64_t& items) {
 // neighbour from pass 1; (3) a node still left roots an aggregate with its
 // unaggregated neighbours.  Isolated rows (no off-diagonal) stay out (-1):
 // they are decoupled, so the smoother alone solves them up to a scalar.
-int64_t aggregate(const SellPat& A, std::vector<int32_t>& agg) {
+// A's rows hold their diagonal first.
+int64_t aggregate(const Csr& A, std::vector<int32_t>& agg) {
   const int64_t n = A.n;
   agg.assign(n, -1);
   std::vector<int8_t> pass(n, 0);
   int64_t na = 0;
   auto nbrs = [&](int64_t i, auto&& f) {
-    for (int k = 1; k < A.rlen[i]; ++k) f((int64_t)A.col[A.pos(i, k)]);
+    for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k) f((int64_t)A.col[k]);
   };
   for (int64_t i = 0; i < n; ++i) {
-    if (agg[i] >= 0 || A.rlen[i] <= 1) continue;
+    if (agg[i] >= 0 || A.len(i) <= 1) continue;
     bool ok = true;
     nbrs(i, [&](int64_t j) { ok = ok && agg[j] < 0; });
     if (!ok) continue;
@@ -72,7 +73,7 @@ int64_t aggregate(const SellPat& A, std::vector<int32_t>& agg) {
     ++na;
   }
   for (int64_t i = 0; i < n; ++i) {
-    if (agg[i] >= 0 || A.rlen[i] <= 1) continue;
+    if (agg[i] >= 0 || A.len(i) <= 1) continue;
     int32_t a = -1;
     nbrs(i, [&](int64_t j) { if (a < 0 && pass[j] == 1) a = agg[j]; });
     if (a >= 0) {
@@ -81,7 +82,7 @@ int64_t aggregate(const SellPat& A, std::vector<int32_t>& agg) {
     }
   }
   for (int64_t i = 0; i < n; ++i) {
-    if (agg[i] >= 0 || A.rlen[i] <= 1) continue;
+    if (agg[i] >= 0 || A.len(i) <= 1) continue;
     agg[i] = (int32_t)na;
     pass[i] = 3;
     nbrs(i, [&](int64_t j) {
@@ -95,178 +96,187 @@ int64_t aggregate(const SellPat& A, std::vector<int32_t>& agg) {
   return na;
 }
 
-// One level's P, R, AP and the next level's A pattern with the index lists.
-std::string coarsen(AmgLevel& L, SellPat& Anext, int64_t& items) {
-  const SellPat& A = L.A;
+std::string check32(int64_t v, const char* what) {
+  return v > INT32_MAX ? std::string("AMG ") + what + " too large for int32 indices" : std::string();
+}
+
+// One level's P, R, AP and the next level's A (natural numbering).
+std::string coarsen(LevelCsr& L, Csr& An) {
+  const Csr& A = L.A;
   const int64_t n = A.n, nc = L.nc;
+  // ---- P: row i → the aggregates of {i} ∪ nbrs(i), ascending; value lists
+  {
+    std::vector<std::pair<int32_t, int32_t>> t;  // (aggregate, A entry)
+    for (int64_t i = 0; i < n; ++i) {
+      t.clear();
+      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
+        const int32_t a = L.agg[A.col[k]];
+        if (a >= 0) t.emplace_back(a, (int32_t)k);
+      }
+      std::stable_sort(t.begin(), t.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      for (size_t k = 0; k < t.size(); ++k) {
+        if (k == 0 || t[k].first != t[k - 1].first) {
+          L.P.col.push_back(t[k].first);
+          L.pv.ptr.push_back(L.pv.ptr.back());
+        }
+        L.pv.a.push_back(t[k].second);
+        ++L.pv.ptr.back();
+      }
+      L.P.ptr.push_back((int64_t)L.P.col.size());
+    }
+    L.P.n = n;
+  }
   std::string err;
-  // ---- P: row i → the aggregates of {i} ∪ nbrs(i), sorted; value lists
-  std::vector<int64_t> prow(n + 1, 0);
-  std::vector<int32_t> pcol;
-  std::vector<std::vector<int32_t>> plist;  // per P entry (CSR order): A positions
+  if (!(err = check32((int64_t)L.P.col.size(), "prolongator")).empty()) return err;
+  // ---- R = Pᵀ: coarse row J → (fine row i ascending, P entry)
   {
-    std::vector<int32_t> cols;
-    for (int64_t i = 0; i < n; ++i) {
-      cols.clear();
-      for (int k = 0; k < A.rlen[i]; ++k) {
-        const int32_t a = L.agg[A.col[A.pos(i, k)]];
-        if (a >= 0) cols.push_back(a);
-      }
-      std::sort(cols.begin(), cols.end());
-      cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
-      for (int32_t c : cols) {
-        pcol.push_back(c);
-        std::vector<int32_t> li;
-        for (int k = 0; k < A.rlen[i]; ++k)
-          if (L.agg[A.col[A.pos(i, k)]] == c) li.push_back((int32_t)A.pos(i, k));
-        plist.push_back(std::move(li));
-      }
-      prow[i + 1] = (int64_t)pcol.size();
-    }
-  }
-  if (!(err = make_sell(n, prow, pcol, L.P)).empty()) return err;
-  L.pv.ptr.assign(L.P.n_pos() + 1, 0);
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = prow[i]; k < prow[i + 1]; ++k)
-      L.pv.ptr[L.P.pos(i, (int)(k - prow[i])) + 1] = (int32_t)plist[k].size();
-  if (!(err = finish_ptr(L.pv, items)).empty()) return err;
-  L.pv.a.resize(L.pv.ptr.back());
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = prow[i]; k < prow[i + 1]; ++k) {
-      const int64_t q = L.P.pos(i, (int)(k - prow[i]));
-      std::copy(plist[k].begin(), plist[k].end(), L.pv.a.begin() + L.pv.ptr[q]);
-    }
-  plist.clear();
-  plist.shrink_to_fit();
-
-  // ---- R = Pᵀ: coarse row J → (fine row i, P position), i ascending
-  std::vector<int64_t> rrow(nc + 1, 0);
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = prow[i]; k < prow[i + 1]; ++k) rrow[pcol[k] + 1]++;
-  for (int64_t J = 0; J < nc; ++J) rrow[J + 1] += rrow[J];
-  std::vector<int32_t> rcol(rrow[nc]), rpp(rrow[nc]);
-  {
-    std::vector<int64_t> fill(rrow.begin(), rrow.end() - 1);
+    L.R.n = nc;
+    L.R.ptr.assign(nc + 1, 0);
+    for (int32_t J : L.P.col) L.R.ptr[J + 1]++;
+    for (int64_t J = 0; J < nc; ++J) L.R.ptr[J + 1] += L.R.ptr[J];
+    L.R.col.resize(L.P.col.size());
+    L.rp.resize(L.P.col.size());
+    std::vector<int64_t> fill(L.R.ptr.begin(), L.R.ptr.end() - 1);
     for (int64_t i = 0; i < n; ++i)
-      for (int64_t k = prow[i]; k < prow[i + 1]; ++k) {
-        const int64_t t = fill[pcol[k]]++;
-        rcol[t] = (int32_t)i;
-        rpp[t] = (int32_t)L.P.pos(i, (int)(k - prow[i]));
+      for (int64_t k = L.P.ptr[i]; k < L.P.ptr[i + 1]; ++k) {
+        const int64_t t = fill[L.P.col[k]]++;
+        L.R.col[t] = (int32_t)i;
+        L.rp[t] = (int32_t)k;
       }
   }
-  if (!(err = make_sell(nc, rrow, rcol, L.R)).empty()) return err;
-  L.rp.assign(L.R.n_pos(), -1);
-  for (int64_t J = 0; J < nc; ++J)
-    for (int64_t t = rrow[J]; t < rrow[J + 1]; ++t) L.rp[L.R.pos(J, (int)(t - rrow[J]))] = rpp[t];
-
-  // ---- AP = A·P (Gustavson, outputs sorted by column)
-  std::vector<int64_t> aprow(n + 1, 0);
-  std::vector<int32_t> apcol;
-  std::vector<int32_t> mark(nc, -1);
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> appairs;  // per AP entry (CSR order)
+  // ---- AP = A·P: per row, (J, A entry, P entry) triples, stable-sorted by J
   {
-    std::vector<int32_t> cols;
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> acc;
+    struct T3 { int32_t J, a, p; };
+    std::vector<T3> t;
+    L.AP.n = n;
     for (int64_t i = 0; i < n; ++i) {
-      cols.clear();
-      acc.clear();
-      for (int k = 0; k < A.rlen[i]; ++k) {
-        const int64_t apos = A.pos(i, k);
-        const int64_t kk = A.col[apos];
-        for (int64_t t = prow[kk]; t < prow[kk + 1]; ++t) {
-          const int32_t J = pcol[t];
-          if (mark[J] < 0) {
-            mark[J] = (int32_t)cols.size();
-            cols.push_back(J);
-            acc.emplace_back();
-          }
-          acc[mark[J]].emplace_back((int32_t)apos, (int32_t)L.P.pos(kk, (int)(t - prow[kk])));
+      t.clear();
+      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
+        const int64_t kk = A.col[k];
+        for (int64_t q = L.P.ptr[kk]; q < L.P.ptr[kk + 1]; ++q) t.push_back({L.P.col[q], (int32_t)k, (int32_t)q});
+      }
+      std::stable_sort(t.begin(), t.end(), [](const T3& x, const T3& y) { return x.J < y.J; });
+      for (size_t k = 0; k < t.size(); ++k) {
+        if (k == 0 || t[k].J != t[k - 1].J) {
+          L.AP.col.push_back(t[k].J);
+          L.ap.ptr.push_back(L.ap.ptr.back());
         }
+        L.ap.a.push_back(t[k].a);
+        L.ap.b.push_back(t[k].p);
+        ++L.ap.ptr.back();
       }
-      std::vector<int32_t> order(cols.size());
-      std::iota(order.begin(), order.end(), 0);
-      std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return cols[x] < cols[y]; });
-      for (int32_t o : order) {
-        apcol.push_back(cols[o]);
-        appairs.push_back(std::move(acc[o]));
-        mark[cols[o]] = -1;
-      }
-      aprow[i + 1] = (int64_t)apcol.size();
+      L.AP.ptr.push_back((int64_t)L.AP.col.size());
     }
   }
-  if (!(err = make_sell(n, aprow, apcol, L.AP)).empty()) return err;
-  L.ap.ptr.assign(L.AP.n_pos() + 1, 0);
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = aprow[i]; k < aprow[i + 1]; ++k)
-      L.ap.ptr[L.AP.pos(i, (int)(k - aprow[i])) + 1] = (int32_t)appairs[k].size();
-  if (!(err = finish_ptr(L.ap, items)).empty()) return err;
-  L.ap.a.resize(L.ap.ptr.back());
-  L.ap.b.resize(L.ap.ptr.back());
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t k = aprow[i]; k < aprow[i + 1]; ++k) {
-      int64_t q = L.ap.ptr[L.AP.pos(i, (int)(k - aprow[i]))];
-      for (auto& pr : appairs[k]) {
-        L.ap.a[q] = pr.first;
-        L.ap.b[q] = pr.second;
-        ++q;
-      }
-    }
-  appairs.clear();
-  appairs.shrink_to_fit();
-
-  // ---- A_{l+1} = Pᵀ (AP): coarse row I over R row I; diagonal first
-  std::vector<int64_t> crow(nc + 1, 0);
-  std::vector<int32_t> ccol;
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> cpairs;
+  if (!(err = check32((int64_t)L.AP.col.size(), "A·P")).empty()) return err;
+  // ---- A_{l+1} = Pᵀ (AP): coarse row I over R row I, diagonal first
   {
-    std::vector<int32_t> cols;
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> acc;
+    struct T3 { int32_t J, p, m; };
+    std::vector<T3> t;
+    An = Csr();
+    An.n = nc;
     for (int64_t I = 0; I < nc; ++I) {
-      cols.clear();
-      acc.clear();
-      mark[I] = 0;
-      cols.push_back((int32_t)I);
-      acc.emplace_back();
-      for (int64_t t = rrow[I]; t < rrow[I + 1]; ++t) {
-        const int64_t i = rcol[t];
-        for (int64_t k = aprow[i]; k < aprow[i + 1]; ++k) {
-          const int32_t J = apcol[k];
-          if (mark[J] < 0) {
-            mark[J] = (int32_t)cols.size();
-            cols.push_back(J);
-            acc.emplace_back();
-          }
-          acc[mark[J]].emplace_back(rpp[t], (int32_t)L.AP.pos(i, (int)(k - aprow[i])));
+      t.clear();
+      for (int64_t r = L.R.ptr[I]; r < L.R.ptr[I + 1]; ++r) {
+        const int64_t i = L.R.col[r];
+        for (int64_t k = L.AP.ptr[i]; k < L.AP.ptr[i + 1]; ++k) t.push_back({L.AP.col[k], L.rp[r], (int32_t)k});
+      }
+      std::stable_sort(t.begin(), t.end(), [I](const T3& x, const T3& y) {
+        const bool dx = x.J == I, dy = y.J == I;  // the diagonal block first, then ascending
+        return dx != dy ? dx : x.J < y.J;
+      });
+      for (size_t k = 0; k < t.size(); ++k) {
+        if (k == 0 || t[k].J != t[k - 1].J) {
+          An.col.push_back(t[k].J);
+          L.ac.ptr.push_back(L.ac.ptr.back());
         }
+        L.ac.a.push_back(t[k].p);
+        L.ac.b.push_back(t[k].m);
+        ++L.ac.ptr.back();
       }
-      std::vector<int32_t> order(cols.size());
-      std::iota(order.begin(), order.end(), 0);
-      std::sort(order.begin() + 1, order.end(), [&](int32_t x, int32_t y) { return cols[x] < cols[y]; });
-      for (int32_t o : order) {
-        ccol.push_back(cols[o]);
-        cpairs.push_back(std::move(acc[o]));
-        mark[cols[o]] = -1;
-      }
-      crow[I + 1] = (int64_t)ccol.size();
+      An.ptr.push_back((int64_t)An.col.size());
     }
   }
-  if (!(err = make_sell(nc, crow, ccol, Anext)).empty()) return err;
-  L.ac.ptr.assign(Anext.n_pos() + 1, 0);
-  for (int64_t I = 0; I < nc; ++I)
-    for (int64_t k = crow[I]; k < crow[I + 1]; ++k)
-      L.ac.ptr[Anext.pos(I, (int)(k - crow[I])) + 1] = (int32_t)cpairs[k].size();
-  if (!(err = finish_ptr(L.ac, items)).empty()) return err;
-  L.ac.a.resize(L.ac.ptr.back());
-  L.ac.b.resize(L.ac.ptr.back());
-  for (int64_t I = 0; I < nc; ++I)
-    for (int64_t k = crow[I]; k < crow[I + 1]; ++k) {
-      int64_t q = L.ac.ptr[Anext.pos(I, (int)(k - crow[I]))];
-      for (auto& pr : cpairs[k]) {
-        L.ac.a[q] = pr.first;
-        L.ac.b[q] = pr.second;
-        ++q;
-      }
+  return check32((int64_t)An.col.size(), "coarse operator");
+}
+
+// ---- stage 2: relabelled SELL layouts -----------------------------------------
+// new = perm[old]: inside windows of kSortWindow rows, rows by descending key
+// (stable: ties keep natural order)
+std::vector<int32_t> sort_perm(const std::vector<int64_t>& key) {
+  const int64_t n = (int64_t)key.size();
+  std::vector<int32_t> order(n), perm(n);
+  std::iota(order.begin(), order.end(), 0);
+  for (int64_t w0 = 0; w0 < n; w0 += kSortWindow) {
+    const int64_t w1 = std::min(n, w0 + kSortWindow);
+    std::stable_sort(order.begin() + w0, order.begin() + w1,
+                     [&](int32_t x, int32_t y) { return key[x] > key[y]; });
+  }
+  for (int64_t k = 0; k < n; ++k) perm[order[k]] = (int32_t)k;
+  return perm;
+}
+
+// SELL-64 of M with rows relabelled by rperm and columns by cperm; epos[e] =
+// position of CSR entry e
+std::string layout(const Csr& M, const std::vector<int32_t>& rperm, const std::vector<int32_t>* cperm,
+                   SellPat& S, std::vector<int32_t>& epos) {
+  const int64_t n = M.n;
+  std::vector<int32_t> inv(n);
+  for (int64_t r = 0; r < n; ++r) inv[rperm[r]] = (int32_t)r;
+  S = SellPat();
+  S.n = n;
+  const int64_t ns = (n + 63) / 64;
+  S.sptr.assign(ns + 1, 0);
+  S.rlen.assign(n, 0);
+  int64_t slots = 0;
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t r = 64 * s; r < std::min<int64_t>(n, 64 * s + 64); ++r) {
+      const int64_t len = M.len(inv[r]);
+      S.rlen[r] = (int32_t)len;
+      w = std::max(w, len);
     }
+    slots += w;
+    if (slots * 64 > INT32_MAX) return "AMG level too large for int32 positions";
+    S.sptr[s + 1] = (int32_t)slots;
+  }
+  S.col.assign(slots * 64, -1);
+  epos.assign(M.col.size(), -1);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t o = inv[r];
+    for (int64_t k = M.ptr[o]; k < M.ptr[o + 1]; ++k) {
+      const int64_t q = S.pos(r, (int)(k - M.ptr[o]));
+      S.col[q] = cperm ? (*cperm)[M.col[k]] : M.col[k];
+      epos[k] = (int32_t)q;
+    }
+  }
+  return "";
+}
+
+// per-entry lists → per-position lists (items translated by ta / tb)
+std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npos,
+                   const std::vector<int32_t>* ta, const std::vector<int32_t>* tb, bool pair,
+                   PosList& out, int64_t& items) {
+  out = PosList();
+  out.ptr.assign(npos + 1, 0);
+  const int64_t ne = (int64_t)L.ptr.size() - 1;
+  for (int64_t e = 0; e < ne; ++e) out.ptr[epos[e] + 1] = (int32_t)(L.ptr[e + 1] - L.ptr[e]);
+  int64_t run = 0;
+  for (int64_t q = 0; q < npos; ++q) {
+    run += out.ptr[q + 1];
+    if (run > INT32_MAX) return "AMG index lists too large for int32";
+    out.ptr[q + 1] = (int32_t)run;
+  }
+  items += run;
+  out.a.resize(run);
+  if (pair) out.b.resize(run);
+  for (int64_t e = 0; e < ne; ++e) {
+    int64_t d = out.ptr[epos[e]];
+    for (int64_t t = L.ptr[e]; t < L.ptr[e + 1]; ++t, ++d) {
+      out.a[d] = ta ? (*ta)[L.a[t]] : L.a[t];
+      if (pair) out.b[d] = tb ? (*tb)[L.b[t]] : L.b[t];
+    }
+  }
   return "";
 }
 
@@ -278,11 +288,12 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   if ((int64_t)active.size() != P.n_elems) return "internal: active size mismatch";
   const int64_t nf = P.n_free;
   std::string err;
-  // ---- level 0: free rows, neighbours through active free-free elements
-  std::vector<int64_t> rowptr(nf + 1, 0);
-  std::vector<int32_t> cols;
-  std::vector<std::vector<int32_t>> slots;  // per A_0 entry (CSR order): SELL positions
+  // ---- stage 1, level 0: free rows, neighbours through active free-free elements
+  std::vector<LevelCsr> lv(1);
+  Lists a0;  // per A_0 entry: SELL slot positions of the assembled operator
   {
+    Csr& A = lv[0].A;
+    A.n = nf;
     std::vector<std::pair<int32_t, int32_t>> nb;  // (neighbour, SELL position)
     for (int64_t i = 0; i < nf; ++i) {
       nb.clear();
@@ -293,53 +304,76 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
         if (j < 0 || j >= nf || e < 0 || !active[e]) continue;
         nb.emplace_back(j, (int32_t)pos);
       }
-      std::stable_sort(nb.begin(), nb.end(),
-                       [](const auto& x, const auto& y) { return x.first < y.first; });
-      cols.push_back((int32_t)i);
-      slots.emplace_back();
+      std::stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      A.col.push_back((int32_t)i);
+      a0.ptr.push_back(a0.ptr.back());
       for (size_t k = 0; k < nb.size(); ++k) {
         if (k == 0 || nb[k].first != nb[k - 1].first) {
-          cols.push_back(nb[k].first);
-          slots.emplace_back();
+          A.col.push_back(nb[k].first);
+          a0.ptr.push_back(a0.ptr.back());
         }
-        slots.back().push_back(nb[k].second);
+        a0.a.push_back(nb[k].second);
+        ++a0.ptr.back();
       }
-      rowptr[i + 1] = (int64_t)cols.size();
+      A.ptr.push_back((int64_t)A.col.size());
     }
   }
-  plan.lev.emplace_back();
-  if (!(err = make_sell(nf, rowptr, cols, plan.lev[0].A)).empty()) return err;
-  {
-    const SellPat& A = plan.lev[0].A;
-    plan.a0.ptr.assign(A.n_pos() + 1, 0);
-    for (int64_t i = 0; i < nf; ++i)
-      for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        plan.a0.ptr[A.pos(i, (int)(k - rowptr[i])) + 1] = (int32_t)slots[k].size();
-    if (!(err = finish_ptr(plan.a0, plan.pair_items)).empty()) return err;
-    plan.a0.a.resize(plan.a0.ptr.back());
-    for (int64_t i = 0; i < nf; ++i)
-      for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k)
-        std::copy(slots[k].begin(), slots[k].end(),
-                  plan.a0.a.begin() + plan.a0.ptr[A.pos(i, (int)(k - rowptr[i]))]);
-  }
-  slots.clear();
   // ---- coarsen until every row is isolated (the coarsest level is then
   // block diagonal and its block-Jacobi inverse is exact)
   for (int l = 0;; ++l) {
-    AmgLevel& L = plan.lev[l];
+    LevelCsr& L = lv[l];
     const int64_t na = aggregate(L.A, L.agg);
     if (na == 0 || l + 1 == kAmgMaxLevels) {
-      L.coarsest = true;
       plan.capped = na > 0;  // couplings left: the coarsest block Jacobi is then inexact
-      L.nc = 0;
       L.agg.clear();
       break;
     }
     L.nc = na;
-    SellPat Anext;
-    if (!(err = coarsen(L, Anext, plan.pair_items)).empty()) return err;
-    plan.lev.emplace_back();
-    plan.lev.back().A = std::move(Anext);
+    Csr An;
+    if (!(err = coarsen(L, An)).empty()) return err;
+    lv.emplace_back();
+    lv.back().A = std::move(An);
+  }
+  // ---- stage 2: row labels per level (sort key: the level's A row plus, for
+  // a coarse level, its R row — the two SELL matrices its rows index)
+  const int nlev = (int)lv.size();
+  std::vector<std::vector<int32_t>> perm(nlev);
+  for (int l = 0; l < nlev; ++l) {
+    const int64_t n = lv[l].A.n;
+    std::vector<int64_t> key(n);
+    for (int64_t i = 0; i < n; ++i) key[i] = lv[l].A.len(i) + (l ? lv[l - 1].R.len(i) : 0);
+    perm[l] = sort_perm(key);
+  }
+  plan.row0.assign(nf, 0);
+  for (int64_t i = 0; i < nf; ++i) plan.row0[perm[0][i]] = (int32_t)i;
+  plan.lev.resize(nlev);
+  std::vector<std::vector<int32_t>> eA(nlev);
+  for (int l = 0; l < nlev; ++l)
+    if (!(err = layout(lv[l].A, perm[l], &perm[l], plan.lev[l].A, eA[l])).empty()) return err;
+  if (!(err = to_pos(a0, eA[0], plan.lev[0].A.n_pos(), nullptr, nullptr, false, plan.a0, plan.pair_items)).empty())
+    return err;
+  for (int l = 0; l < nlev; ++l) {
+    AmgLevel& out = plan.lev[l];
+    LevelCsr& L = lv[l];
+    out.coarsest = l + 1 == nlev;
+    if (out.coarsest) continue;
+    out.nc = L.nc;
+    out.agg.assign(L.A.n, -1);
+    for (int64_t i = 0; i < L.A.n; ++i)
+      out.agg[perm[l][i]] = L.agg[i] >= 0 ? perm[l + 1][L.agg[i]] : -1;
+    std::vector<int32_t> eP, eR, eAP;
+    if (!(err = layout(L.P, perm[l], &perm[l + 1], out.P, eP)).empty()) return err;
+    if (!(err = layout(L.R, perm[l + 1], &perm[l], out.R, eR)).empty()) return err;
+    if (!(err = layout(L.AP, perm[l], &perm[l + 1], out.AP, eAP)).empty()) return err;
+    if (!(err = to_pos(L.pv, eP, out.P.n_pos(), &eA[l], nullptr, false, out.pv, plan.pair_items)).empty())
+      return err;
+    out.rp.assign(out.R.n_pos(), -1);
+    for (size_t e = 0; e < L.rp.size(); ++e) out.rp[eR[e]] = eP[L.rp[e]];
+    if (!(err = to_pos(L.ap, eAP, out.AP.n_pos(), &eA[l], &eP, true, out.ap, plan.pair_items)).empty())
+      return err;
+    if (!(err = to_pos(L.ac, eA[l + 1], plan.lev[l + 1].A.n_pos(), &eP, &eAP, true, out.ac, plan.pair_items))
+             .empty())
+      return err;
   }
   return "";
 }

@@ -117,9 +117,13 @@ struct Part {
   bool amg_ok = false;
   std::vector<uint8_t> amg_key;
   int64_t amg_gen = 0;               // bumped on every rebuild (captured graphs hold its pointers)
+  int amg_last_iters = 0;            // iterations of the last converged GAMG solve (chunk plan)
   DevBuf<int32_t> amg_i;             // every index array of the plan, carved
-  DevBuf<double> amg_d;              // every value / vector array, carved
+  DevBuf<double> amg_d;              // every f64 value / vector array, carved
+  DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
+  DevBuf<AmgLevD> amg_lev_d;         // the same, on the device (k_amg_tail)
+  int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
   AmgCg amg_cg;
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
@@ -728,6 +732,39 @@ int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, Solve
   return 0;
 }
 
+// Replays planned from the expected iteration count (the AMG solves of one
+// handle converge in a near-constant number of iterations): enough chunks
+// for `expected` iterations are queued back to back with no host wait, then
+// one chunk at a time until the device reports done.  A wrong guess costs a
+// chunk of early-exiting launches (too high) or one host round trip per
+// extra chunk (too low) — never correctness.
+template <class Enqueue>
+int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&& enqueue,
+                  SolveState* out) {
+  hipStream_t s = h->stream;
+  const int64_t max_chunks = (int64_t)max_it / chunk + 3;
+  volatile SolveState* hs = h->h_state;
+  hs[0].done = 0;
+  int64_t k = 0;
+  const int64_t first = std::min<int64_t>(max_chunks, std::max(1, (expected + 1 + chunk - 1) / chunk));
+  for (; k < first; ++k) RC(enqueue());
+  HIPC(hipEventRecord(h->poll[0], s));
+  RC(wait_event(h, h->poll[0]));
+  while (!hs[0].done && k < max_chunks) {
+    RC(enqueue());
+    HIPC(hipEventRecord(h->poll[0], s));
+    RC(wait_event(h, h->poll[0]));
+    ++k;
+  }
+  RC(sync_stream(h));
+  *out = h->h_state[0];
+  if (!out->done) {
+    out->status = MFEA_EMAXIT;
+    out->iters = max_it;
+  }
+  return 0;
+}
+
 int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
   HIPC(hipEventRecord(h->ev[3], h->stream));
   RC(wait_event(h, h->ev[3]));
@@ -824,6 +861,9 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
 // ---------------------------------------------------------------------------
 // SA-AMG preconditioned CG (amg.hpp / amg.hip), single partition.
 // ---------------------------------------------------------------------------
+// levels of at most this many rows run inside the single-workgroup tail
+// (MFEA_AMG_TAIL_ROWS overrides; 0 disables)
+constexpr int64_t kAmgTailRows = 2048;
 constexpr size_t kAmgAlign = 64;  // elements: every carved array starts 256/512-B aligned
 size_t amg_al(size_t n) { return (n + kAmgAlign - 1) / kAmgAlign * kAmgAlign; }
 
@@ -834,9 +874,10 @@ int upload_amg(mfea_handle* h, Part& pt) {
   const int nd = pl.nd, nb2 = nd * nd;
   const int nlev = (int)pl.lev.size();
   hipStream_t s = h->stream;
-  size_t ni = 0, ndd = 0;
+  size_t ni = 0, ndd = 0, nff = 0;
   int32_t* ip = nullptr;
   double* dp = nullptr;
+  float* fp = nullptr;
   int pass = 0;
   hipError_t err = hipSuccess;
   auto I = [&](const std::vector<int32_t>& v) -> const int32_t* {
@@ -859,44 +900,60 @@ int upload_amg(mfea_handle* h, Part& pt) {
     dp += amg_al(n);
     return p;
   };
-  auto mat = [&](const SellPat& S, bool vals) {
+  auto F = [&](size_t n) -> float* {
+    if (pass == 0) {
+      nff += amg_al(n);
+      return nullptr;
+    }
+    float* p = fp;
+    fp += amg_al(n);
+    return p;
+  };
+  // vals64: f64 values (setup / CG), vals32: the f32 V-cycle copy
+  auto mat = [&](const SellPat& S, bool vals64, bool vals32) {
     AmgMatD m;
     m.n = S.n;
     m.npos = S.n_pos();
     m.sptr = I(S.sptr);
     m.col = I(S.col);
-    m.val = vals ? D((size_t)nb2 * m.npos) : nullptr;
+    m.val = vals64 ? D((size_t)nb2 * m.npos) : nullptr;
+    m.val32 = vals32 ? F((size_t)nb2 * m.npos) : nullptr;
     return m;
   };
   for (pass = 0; pass < 2; ++pass) {
     if (pass == 1) {
       HIPC(pt.amg_i.alloc(std::max<size_t>(ni, 1)));
       HIPC(pt.amg_d.alloc(std::max<size_t>(ndd, 1)));
+      HIPC(pt.amg_f.alloc(std::max<size_t>(nff, 1)));
       HIPC(hipMemsetAsync(pt.amg_d.ptr, 0, pt.amg_d.n * sizeof(double), s));
+      HIPC(hipMemsetAsync(pt.amg_f.ptr, 0, pt.amg_f.n * sizeof(float), s));
       ip = pt.amg_i.ptr;
       dp = pt.amg_d.ptr;
+      fp = pt.amg_f.ptr;
     }
     pt.amg_lev.assign(nlev, AmgLevD{});
     for (int l = 0; l < nlev; ++l) {
       const AmgLevel& L = pl.lev[l];
       AmgLevD& d = pt.amg_lev[l];
       const int64_t n = L.A.n;
-      d.A = mat(L.A, true);
+      d.A = mat(L.A, true, true);
       d.dinv = D((size_t)nb2 * n);
+      d.dinv32 = F((size_t)nb2 * n);
       d.gpart = D((size_t)(n + kBlock - 1) / kBlock + 1);
       d.omega = D(2);
-      d.b = D((size_t)nd * n);
-      d.x = D((size_t)nd * n);
-      d.te = D((size_t)nd * n);
+      d.b = l ? F((size_t)nd * n) : nullptr;  // level 0 reads the CG's r
+      d.x = F((size_t)nd * n);
+      d.t = F((size_t)nd * n);
+      d.e = l ? F((size_t)nd * n) : nullptr;  // level 0 writes the CG's u
       d.coarsest = L.coarsest ? 1 : 0;
       if (!L.coarsest) {
         d.agg = I(L.agg);
-        d.P = mat(L.P, true);
+        d.P = mat(L.P, true, true);
         d.pv_ptr = I(L.pv.ptr);
         d.pv_a = I(L.pv.a);
-        d.R = mat(L.R, true);
+        d.R = mat(L.R, false, true);
         d.rp = I(L.rp);
-        d.AP = mat(L.AP, false);
+        d.AP = mat(L.AP, false, false);
         d.apval = D((size_t)nb2 * d.AP.npos);
         d.ap_ptr = I(L.ap.ptr);
         d.ap_a = I(L.ap.a);
@@ -910,14 +967,24 @@ int upload_amg(mfea_handle* h, Part& pt) {
     pt.amg_a0_a = I(pl.a0.a);
     const int64_t nf = nlev ? pl.lev[0].A.n : 0;
     pt.amg_cg.n = nf;
+    pt.amg_cg.row0 = I(pl.row0);
     pt.amg_cg.x = D((size_t)nd * nf);
     pt.amg_cg.p = D((size_t)nd * nf);
     pt.amg_cg.s = D((size_t)nd * nf);
     pt.amg_cg.w = D((size_t)nd * nf);
-    pt.amg_cg.r = nlev ? pt.amg_lev[0].b : nullptr;
-    pt.amg_cg.u = nlev ? pt.amg_lev[0].te : nullptr;
+    pt.amg_cg.r = D((size_t)nd * nf);
+    pt.amg_cg.u = D((size_t)nd * nf);
   }
   HIPC(err);
+  HIPC(pt.amg_lev_d.alloc(std::max(nlev, 1)));
+  if (nlev)
+    HIPC(hipMemcpyAsync(pt.amg_lev_d.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
+  {
+    std::vector<int64_t> rows(nlev);
+    for (int l = 0; l < nlev; ++l) rows[l] = pl.lev[l].A.n;
+    const char* e = std::getenv("MFEA_AMG_TAIL_ROWS");
+    pt.amg_tail = amg_tail_level(rows.data(), nlev, e ? std::atoll(e) : kAmgTailRows);
+  }
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -955,7 +1022,8 @@ void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_update(s, nd, j, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), profile ? nullptr : &pt.slots.ptr[j + 1].flag);
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+                    pt.amg_tail, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
   launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
 }
 
@@ -968,7 +1036,7 @@ void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
 void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   hipStream_t s = h->stream;
   const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
-  launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   for (int l = 0; l < nlev; ++l)
     launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr);
 }
@@ -981,7 +1049,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
   bool rebuilt = false;
   RC(ensure_amg(h, pt, &rebuilt));
-  const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 4;
+  const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
   const int nd = pt.amg.nd;
@@ -994,22 +1062,23 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   HIPC(hipEventRecord(h->ev_setup, s));
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), nullptr);
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+                    pt.amg_tail, nullptr);
   launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
   HIPC(hipGetLastError());
   const int tag = -1000 - (int)(pt.amg_gen % 1000000);
   static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  const int expected = std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16);
   SolveState fin;
   int rc;
   if (no_graph) {
-    rc = drive_chunks(
-        h, chunk, o->max_it,
-        [&]() -> int {
-          enqueue_amg_chunk(h, pt, chunk);
-          HIPC(hipGetLastError());
-          return 0;
-        },
-        &fin, /*mirror=*/true);
+    rc = drive_planned(h, chunk, o->max_it, expected,
+                       [&]() -> int {
+                         enqueue_amg_chunk(h, pt, chunk);
+                         HIPC(hipGetLastError());
+                         return 0;
+                       },
+                       &fin);
   } else {
     if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG ||
         h->graph_ell != tag) {
@@ -1025,15 +1094,15 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
       h->graph_precond = MFEA_PC_GAMG;
       h->graph_ell = tag;
     }
-    rc = drive_chunks(
-        h, chunk, o->max_it,
-        [&]() -> int {
-          HIPC(hipGraphLaunch(h->graph, s));
-          return 0;
-        },
-        &fin, /*mirror=*/true);
+    rc = drive_planned(h, chunk, o->max_it, expected,
+                       [&]() -> int {
+                         HIPC(hipGraphLaunch(h->graph, s));
+                         return 0;
+                       },
+                       &fin);
   }
   if (rc) return rc;
+  if (fin.status == 0) pt.amg_last_iters = fin.iters;
   launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
   HIPC(hipGetLastError());
   rc = finish_solve(h, fin, st);

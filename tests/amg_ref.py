@@ -44,6 +44,7 @@ def fetch_plan(shim, active, nd):
             if name in ("A.sptr", "A.col") or not L["coarsest"]:
                 L[name] = arr(l, name)
         levels.append(L)
+    levels[0]["row0"] = arr(0, "row0")
     levels[0]["a0.ptr"] = arr(0, "a0.ptr")
     levels[0]["a0.a"] = arr(0, "a0.a")
     return levels
@@ -106,7 +107,7 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
     d6 = np.stack([diag[c * N:(c + 1) * N] for c in range(6)], -1).copy()  # [N][6]
     d6[:, [0, 3, 5]] += reg
     isdiag = (k == 0) & (row >= 0)
-    A[isdiag] = _sym(d6[row[isdiag]], nd)
+    A[isdiag] = _sym(d6[L0["row0"][row[isdiag]]], nd)
     offm = (k > 0) & (L0["A.col"] >= 0)
     A[offm] = offd[offm]
     L0["Ab"] = A

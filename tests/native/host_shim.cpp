@@ -164,6 +164,7 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   else if (n == "ac.ptr") v = &L.ac.ptr;
   else if (n == "ac.a") v = &L.ac.a;
   else if (n == "ac.b") v = &L.ac.b;
+  else if (n == "row0") v = &g_amg.row0;
   else if (n == "a0.ptr") v = &g_amg.a0.ptr;
   else if (n == "a0.a") v = &g_amg.a0.a;
   else return -1;

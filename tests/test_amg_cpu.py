@@ -62,16 +62,18 @@ def setup_case(shim, xyz, e2n, top, bot, active, nd):
     shim.shim_sell_values(_ptr(act), EA, EI12, _ptr(val), _ptr(diag))
     levels = amg_ref.fetch_plan(shim, act, nd)
     amg_ref.numeric_setup(levels, val, diag, G, N, nd)
-    # the reference's system, reordered to the plan's rows (free rows = perm[:nf])
+    # the reference's system, reordered to the plan's rows: level-0 row i is
+    # the Pattern's free row row0[i], i.e. original node perm[row0[i]]
     K = fo.assemble_global_stiffness(xyz, e2n, act.astype(bool))
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     known, vals = fo.known_dof_map(top, bot, dy, -dy)
     A3, b3, free = fo.free_system(K, known, vals)
-    dofs = (perm[:nf, None].astype(np.int64) * 3 + np.arange(nd)).ravel()
+    nodes0 = perm[:nf][levels[0]["row0"]]
+    dofs = (nodes0[:, None].astype(np.int64) * 3 + np.arange(nd)).ravel()
     pos = np.searchsorted(free, dofs)
     assert np.array_equal(free[pos], dofs)
     Kff = A3[pos][:, pos].tocsr()
-    return levels, Kff, b3[pos], perm[:nf]
+    return levels, Kff, b3[pos], nodes0
 
 
 def _rel(a, b):

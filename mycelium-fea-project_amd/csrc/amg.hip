@@ -39,15 +39,20 @@
 namespace mfea {
 
 // ---- block / vector helpers (T = storage type, C = compute type) -----------
+// Blocks are stored block-major ([position][NB2]): a SELL slot's 64 lanes read
+// 64 consecutive blocks (one contiguous run, 16/32-B vector loads per lane),
+// and the setup's index-list gathers fetch one contiguous block per item
+// instead of NB2 separate cache lines (the component-major layout made the
+// Galerkin products ≈ 0.7 TB/s effective).
 template <int ND, class T, class C>
-__device__ __forceinline__ void bload(const T* __restrict__ v, int64_t npos, int64_t q, C* m) {
+__device__ __forceinline__ void bload(const T* __restrict__ v, int64_t /*npos*/, int64_t q, C* m) {
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) m[c] = (C)v[c * npos + q];
+  for (int c = 0; c < ND * ND; ++c) m[c] = (C)v[q * (ND * ND) + c];
 }
 template <int ND, class T, class C>
-__device__ __forceinline__ void bstore(T* __restrict__ v, int64_t npos, int64_t q, const C* m) {
+__device__ __forceinline__ void bstore(T* __restrict__ v, int64_t /*npos*/, int64_t q, const C* m) {
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) v[c * npos + q] = (T)m[c];
+  for (int c = 0; c < ND * ND; ++c) v[q * (ND * ND) + c] = (T)m[c];
 }
 template <int ND, class T, class C>
 __device__ __forceinline__ void vload(const T* __restrict__ v, int64_t i, C* o) {
@@ -178,13 +183,13 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
   }
 }
 
-// o = s · D⁻¹ v  (D⁻¹ SoA [NB2][n], storage TD, compute C)
+// o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C)
 template <int ND, class TD, class C>
-__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t n, int64_t i, C s,
+__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t /*n*/, int64_t i, C s,
                                            const C* v, C* o) {
   C Di[ND * ND];
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Di[c] = (C)dinv[(int64_t)c * n + i];
+  for (int c = 0; c < ND * ND; ++c) Di[c] = (C)dinv[i * (ND * ND) + c];
 #pragma unroll
   for (int a = 0; a < ND; ++a) {
     C acc = 0;
@@ -194,49 +199,90 @@ __device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t 
   }
 }
 
-// ---------------------------------------------------------------------------
-// numeric setup (f64, with f32 copies for the V-cycle)
-// ---------------------------------------------------------------------------
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ row0,
-                                                   const int32_t* __restrict__ ptr,
-                                                   const int32_t* __restrict__ lst, double reg) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= A.n) return;
-  int64_t base;
-  int w;
-  slice_of(A, i, base, w);
-  if (i >= A.n) return;
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    double m[ND * ND];
+// C += Σ_t X[a_t]·Y[b_t] (TX: X[a_t]ᵀ·Y[b_t]) over one index list, in list
+// order, kPairU pairs' loads in flight per step (the lists are short, ≈ 2–10
+// pairs, and every pair is two dependent hops: index, then blocks)
+constexpr int kPairU = 4;
+template <int ND, bool TX>
+__device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
+                                         const int32_t* __restrict__ lb, const double* __restrict__ X,
+                                         int64_t nx, const double* __restrict__ Y, int64_t ny, double* C) {
+  for (int t = t0; t < t1; t += kPairU) {
+    int32_t ia[kPairU], ib[kPairU];
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
-    if (k == 0) {
-      double s6[6];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
-      s6[0] += reg;
-      s6[3] += reg;
-      s6[5] += reg;
-      sym_to<ND>(s6, m);
-    } else if (A.col[q] >= 0) {
-      for (int t = ptr[q]; t < ptr[q + 1]; ++t) {
-        double s6[6], e[ND * ND];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) s6[c] = sop.val[(int64_t)c * sop.G + lst[t]];
-        sym_to<ND>(s6, e);
-#pragma unroll
-        for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
-      }
+    for (int u = 0; u < kPairU; ++u) {
+      const int tt = t + u < t1 ? t + u : t0;
+      ia[u] = la[tt];
+      ib[u] = lb[tt];
     }
-    bstore<ND>(A.val, A.npos, q, m);
-    bstore<ND>(A.val32, A.npos, q, m);
+    double x[kPairU][ND * ND], y[kPairU][ND * ND];
+#pragma unroll
+    for (int u = 0; u < kPairU; ++u) {
+      bload<ND>(X, nx, ia[u], x[u]);
+      bload<ND>(Y, ny, ib[u], y[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kPairU; ++u) {
+      if (t + u >= t1) break;
+      if (TX) mtm_acc<ND>(x[u], y[u], C);
+      else mm_acc<ND>(x[u], y[u], C);
+    }
+  }
+}
+// S += Σ_t X[a_t] over one index list, in list order
+template <int ND>
+__device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
+                                         const double* __restrict__ X, int64_t nx, double* S) {
+  for (int t = t0; t < t1; t += kPairU) {
+    int32_t ia[kPairU];
+#pragma unroll
+    for (int u = 0; u < kPairU; ++u) ia[u] = la[t + u < t1 ? t + u : t0];
+    double x[kPairU][ND * ND];
+#pragma unroll
+    for (int u = 0; u < kPairU; ++u) bload<ND>(X, nx, ia[u], x[u]);
+#pragma unroll
+    for (int u = 0; u < kPairU; ++u) {
+      if (t + u >= t1) break;
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) S[c] += x[u][c];
+    }
   }
 }
 
+// ---------------------------------------------------------------------------
+// numeric setup (f64, with f32 copies for the V-cycle)
+// ---------------------------------------------------------------------------
+// A_0 off-diagonal blocks, one position per thread: Σ of the listed SELL
+// slots' K_ij (= −S_e) in slot order.  Diagonal and padding positions have
+// empty lists; the diagonal block is written by k_amg_dinv<ND, true>.
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
+__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
+                                                   const int32_t* __restrict__ lst) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= A.npos) return;
+  const int t0 = ptr[q], t1 = ptr[q + 1];
+  if (t0 == t1) return;
+  double m[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+  for (int t = t0; t < t1; ++t) {
+    double s6[6], e[ND * ND];
+    const int64_t g = lst[t];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s6[c] = sop.val[(int64_t)c * sop.G + g];
+    sym_to<ND>(s6, e);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+  }
+  bstore<ND>(A.val, A.npos, q, m);
+  bstore<ND>(A.val32, A.npos, q, m);
+}
+
+// Block-Jacobi inverse, Gershgorin bound per block.  L0: level 0, whose
+// diagonal block K_ii + reg·I (Pattern row row0[i]) is formed and stored here.
+template <int ND, bool L0>
+__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
+                                                     double reg) {
   __shared__ double red[kBlock / 64];
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const AmgMatD& A = L.A;
@@ -247,12 +293,24 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
     slice_of(A, i, base, w);
     if (i < A.n) {
       double D[ND * ND], Di[ND * ND];
-      bload<ND>(A.val, A.npos, base, D);
+      if (L0) {
+        double s6[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
+        s6[0] += reg;
+        s6[3] += reg;
+        s6[5] += reg;
+        sym_to<ND>(s6, D);
+        bstore<ND>(A.val, A.npos, base, D);
+        bstore<ND>(A.val32, A.npos, base, D);
+      } else {
+        bload<ND>(A.val, A.npos, base, D);
+      }
       binv<ND>(D, Di);
 #pragma unroll
       for (int c = 0; c < ND * ND; ++c) {
-        L.dinv[(int64_t)c * A.n + i] = Di[c];
-        L.dinv32[(int64_t)c * A.n + i] = (float)Di[c];
+        L.dinv[i * (ND * ND) + c] = Di[c];
+        L.dinv32[i * (ND * ND) + c] = (float)Di[c];
       }
       double rs[ND];
 #pragma unroll
@@ -261,7 +319,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
         const int64_t q = base + (int64_t)k * 64;
         if (A.col[q] < 0) continue;
         double m[ND * ND], pm[ND * ND];
-        bload<ND>(A.val, A.npos, q, m);
+        if (k == 0) {
+#pragma unroll
+          for (int c = 0; c < ND * ND; ++c) m[c] = D[c];
+        } else {
+          bload<ND>(A.val, A.npos, q, m);
+        }
 #pragma unroll
         for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
         mm_acc<ND>(Di, m, pm);
@@ -318,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   const double om = L.omega[0];
   double Di[ND * ND];
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[(int64_t)c * L.A.n + i];
+  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[i * (ND * ND) + c];
   const int32_t ai = L.agg[i];
   for (int k = 0; k < w; ++k) {
     const int64_t q = base + (int64_t)k * 64;
@@ -330,12 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
       S[c] = 0.0;
       pm[c] = 0.0;
     }
-    for (int t = L.pv_ptr[q]; t < L.pv_ptr[q + 1]; ++t) {
-      double m[ND * ND];
-      bload<ND>(L.A.val, L.A.npos, L.pv_a[t], m);
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) S[c] += m[c];
-    }
+    list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val, L.A.npos, S);
     mm_acc<ND>(Di, S, pm);
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
@@ -371,13 +429,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-  const int t0 = L.ap_ptr[q], t1 = L.ap_ptr[q + 1];
-  for (int t = t0; t < t1; ++t) {
-    double a[ND * ND], p[ND * ND];
-    bload<ND>(L.A.val, L.A.npos, L.ap_a[t], a);
-    bload<ND>(L.P.val, L.P.npos, L.ap_b[t], p);
-    mm_acc<ND>(a, p, C);
-  }
+  pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val, L.A.npos, L.P.val, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
 }
 
@@ -389,13 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-  const int t0 = L.ac_ptr[q], t1 = L.ac_ptr[q + 1];
-  for (int t = t0; t < t1; ++t) {
-    double p[ND * ND], m[ND * ND];
-    bload<ND>(L.P.val, L.P.npos, L.ac_a[t], p);
-    bload<ND>(L.apval, L.AP.npos, L.ac_b[t], m);
-    mtm_acc<ND>(p, m, C);
-  }
+  pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val, L.P.npos, L.apval, L.AP.npos, C);
   bstore<ND>(Ac.val, Ac.npos, q, C);
   bstore<ND>(Ac.val32, Ac.npos, q, C);
 }
@@ -623,13 +669,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, co
   vcycle_entry<ND>(L0, cg, i, r);
 }
 
-template <int ND, bool FIRST>
-__global__ __launch_bounds__(kCgBS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part) {
+template <int ND, bool FIRST, int BS>
+__global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part) {
   if (!FIRST && slots[j + 1].flag != kRun) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const int64_t stride = (int64_t)gridDim.x * kCgBS;
+  const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
-  for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i - lane < cg.n; i += stride) {
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i - lane < cg.n; i += stride) {
     const int64_t ii = i < cg.n ? i : cg.n - 1;
     int64_t base;
     int w;
@@ -650,7 +696,7 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg,
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  store_block_partial(acc, part_buf(part, FIRST ? 0 : ((j & 1) ^ 1)));
+  store_block_partial<BS>(acc, part_buf(part, FIRST ? 0 : ((j & 1) ^ 1)));
   if (FIRST && blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;
     s0.v[0] = s0.v[1] = s0.v[2] = s0.v[3] = 0.0;
@@ -661,8 +707,8 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg,
   }
 }
 
-template <int ND, int PU>
-__global__ __launch_bounds__(kCgBS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg cg, Slot* slots,
+template <int ND, int PU, int BS>
+__global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg cg, Slot* slots,
                                                          const SolveState* st, double* part) {
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
   const double g0 = slots[j].v[0], a0 = slots[j].alpha;
@@ -674,8 +720,8 @@ __global__ __launch_bounds__(kCgBS) void k_amg_cg_update(int j, AmgLevD L0, AmgC
   cg_record(slots, j, S, cs);
   if (cs.status != kRun) return;
   const double alpha = cs.alpha, beta = cs.beta;
-  const int64_t stride = (int64_t)gridDim.x * kCgBS;
-  for (int64_t i = (int64_t)blockIdx.x * kCgBS + threadIdx.x; i < cg.n; i += stride) {
+  const int64_t stride = (int64_t)gridDim.x * BS;
+  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < cg.n; i += stride) {
     double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
     vload<ND>(cg.u, i, u);
     vload<ND>(cg.w, i, w);
@@ -711,8 +757,17 @@ __global__ __launch_bounds__(kBlock) void k_amg_finish(AmgCg cg, double* __restr
 // ---------------------------------------------------------------------------
 static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock > 0 ? (n + kBlock - 1) / kBlock : 1)); }
 
+// The w kernel writes one partial per block and every wave of the next
+// update kernel re-reads them all (≤ kCgMaxG = 512 blocks).  Measured at C3
+// (336k rows): w 16.3 µs at 256 threads × 512 blocks (2.6 grid-stride
+// passes, 8 waves per CU), 14.9 at 1024 × 329 (but 329 blocks leave 73 CUs
+// with twice the work — the streaming update kernel went 10.7 → 15.3 µs);
+// so the update keeps 256-thread blocks and w takes 512 × 512 (16 waves per
+// CU, 1.3 passes).  Both read the w kernel's partial count, amg_w_grid.
+int amg_w_block(int64_t n) { return n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS; }
 int64_t amg_w_grid(int64_t n) {
-  const int64_t g = (n + kCgBS - 1) / kCgBS;
+  const int bs = amg_w_block(n);
+  const int64_t g = (n + bs - 1) / bs;
   return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
 }
 static int pu_of_grid(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 ? 4 : 8; }
@@ -720,8 +775,9 @@ static int pu_of_grid(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 
 template <int ND>
 static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
                   const int32_t* a, double reg) {
-  if (L0.A.n > 0)
-    hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.n), dim3(kBlock), 0, s, L0.A, sop, row0, p, a, reg);
+  if (L0.A.n <= 0) return;
+  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.npos), dim3(kBlock), 0, s, L0.A, sop, p, a);
+  hipLaunchKernelGGL((k_amg_dinv<ND, true>), rows_grid(L0.A.n), dim3(kBlock), 0, s, L0, sop, row0, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
                    const int32_t* a0_ptr, const int32_t* a0_a, double reg) {
@@ -730,10 +786,11 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 }
 
 template <int ND>
-static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N) {
+static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool level0) {
   if (L.A.n <= 0) return;
   const dim3 g = rows_grid(L.A.n);
-  hipLaunchKernelGGL(k_amg_dinv<ND>, g, dim3(kBlock), 0, s, L);
+  // level 0's k_amg_dinv ran in launch_amg_a0 (it also forms the diagonal)
+  if (!level0) hipLaunchKernelGGL((k_amg_dinv<ND, false>), g, dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
   if (L.coarsest || !N) return;
   hipLaunchKernelGGL(k_amg_pvals<ND>, rows_grid(L.P.n), dim3(kBlock), 0, s, L);
@@ -741,9 +798,9 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N) {
   hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(L.AP.npos), dim3(kBlock), 0, s, L);
   hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A);
 }
-void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next) {
-  if (nd == 2) setup_nd<2>(s, L, next);
-  else setup_nd<3>(s, L, next);
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0) {
+  if (nd == 2) setup_nd<2>(s, L, next, level0);
+  else setup_nd<3>(s, L, next, level0);
 }
 
 template <int ND>
@@ -790,12 +847,18 @@ void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& c
   else hipLaunchKernelGGL(k_amg_cg_init<3>, rows_grid(cg.n), dim3(kBlock), 0, s, L0, cg, b_row);
 }
 
+template <int ND, int BS>
+static void w_bs(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
+                 double* part) {
+  const dim3 g((unsigned)amg_w_grid(cg.n));
+  if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, part);
+  else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, part);
+}
 template <int ND>
 static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                  double* part) {
-  const dim3 g((unsigned)amg_w_grid(cg.n));
-  if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, part);
-  else hipLaunchKernelGGL((k_amg_cg_w<ND, false>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, part);
+  if (amg_w_block(cg.n) == 512) w_bs<ND, 512>(s, j, first, L0, cg, slots, part);
+  else w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part);
 }
 void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
                      Slot* slots, double* part) {
@@ -803,17 +866,24 @@ void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0
   else w_nd<3>(s, j, first, L0, cg, slots, part);
 }
 
+template <int ND, int BS>
+static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
+                   const SolveState* st, double* part) {
+  const int64_t gw = amg_w_grid(cg.n);  // partials to reduce = the w kernel's blocks
+  int64_t gu = (cg.n + BS - 1) / BS;
+  gu = gu < 1 ? 1 : (gu > kCgMaxG ? kCgMaxG : gu);
+  const dim3 g((unsigned)gu);
+  switch (pu_of_grid(gw)) {
+    case 1: hipLaunchKernelGGL((k_amg_cg_update<ND, 1, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
+    case 2: hipLaunchKernelGGL((k_amg_cg_update<ND, 2, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
+    case 4: hipLaunchKernelGGL((k_amg_cg_update<ND, 4, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
+    default: hipLaunchKernelGGL((k_amg_cg_update<ND, 8, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
+  }
+}
 template <int ND>
 static void upd_nd(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                    const SolveState* st, double* part) {
-  const int64_t gw = amg_w_grid(cg.n);
-  const dim3 g((unsigned)gw);
-  switch (pu_of_grid(gw)) {
-    case 1: hipLaunchKernelGGL((k_amg_cg_update<ND, 1>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
-    case 2: hipLaunchKernelGGL((k_amg_cg_update<ND, 2>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
-    case 4: hipLaunchKernelGGL((k_amg_cg_update<ND, 4>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
-    default: hipLaunchKernelGGL((k_amg_cg_update<ND, 8>), g, dim3(kCgBS), 0, s, j, L0, cg, slots, st, part); break;
-  }
+  upd_bs<ND, kCgBS>(s, j, L0, cg, slots, st, part);
 }
 void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                           const SolveState* st, double* part) {

@@ -1,13 +1,13 @@
 // amg_kernels.hpp — device views and launchers of the SA-AMG preconditioned CG
 // (amg.hip).  Layout of one level l in HBM (n rows = nodes or aggregates,
 // ND = 2 or 3 DOFs per row, NB2 = ND² doubles per block, row-major):
-//   A.val[NB2][npos]   SELL-64 blocks of A_l, slot 0 of a row = its diagonal
+//   A.val[npos][NB2]   SELL-64 blocks of A_l, slot 0 of a row = its diagonal
 //                      (f64 for the setup and the CG; val32: f32 V-cycle copy)
-//   dinv[NB2][n]       block-Jacobi inverse of the diagonal blocks (+ f32 copy)
+//   dinv[n][NB2]       block-Jacobi inverse of the diagonal blocks (+ f32 copy)
 //   b, x, t, e [n][ND] f32 V-cycle right-hand side, iterate, residual, output
-//   P.val[NB2][npos_P] smoothed prolongator (rows = level l, cols = level l+1)
-//   R.val32[NB2][npos_R] P transposed: coarse row → fine rows (rp: the P position)
-//   apval[NB2][npos_AP] A_l·P_l (setup only)
+//   P.val[npos_P][NB2] smoothed prolongator (rows = level l, cols = level l+1)
+//   R.val32[npos_R][NB2] P transposed: coarse row → fine rows (rp: the P position)
+//   apval[npos_AP][NB2] A_l·P_l (setup only)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,8 +21,8 @@ struct AmgMatD {
   int64_t npos = 0;  // SELL positions (slot rows · 64)
   const int32_t* sptr = nullptr;
   const int32_t* col = nullptr;
-  double* val = nullptr;   // [NB2][npos] f64 (setup; A_0 also serves the CG's w = A u)
-  float* val32 = nullptr;  // [NB2][npos] f32 copy for the V-cycle
+  double* val = nullptr;   // [npos][NB2] f64 (setup; A_0 also serves the CG's w = A u)
+  float* val32 = nullptr;  // [npos][NB2] f32 copy for the V-cycle
 };
 
 struct AmgLevD {
@@ -68,11 +68,12 @@ struct AmgCg {
 
 // ---- numeric setup (every solve) ------------------------------------------
 // A_0 from the assembled SELL operator: off-diagonal = Σ of the listed slots'
-// K_ij (= −S_e), diagonal = K_ii + reg·I.
+// K_ij (= −S_e), diagonal = K_ii + reg·I; then level 0's D⁻¹ and bound.
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
                    const int32_t* a0_ptr, const int32_t* a0_a, double reg);
 // dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
-void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next);
+// (level0: its D⁻¹ was formed by launch_amg_a0)
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail) reading the level views at lev_dev.

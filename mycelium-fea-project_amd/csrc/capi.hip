@@ -1038,7 +1038,7 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   for (int l = 0; l < nlev; ++l)
-    launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr);
+    launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
 }
 
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,

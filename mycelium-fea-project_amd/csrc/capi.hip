@@ -1759,14 +1759,25 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
     const int nd = pt.amg.nd;
     launch_amg_cg_w(s, nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
     launch_cg_init_finalize(s, pt.red.ptr + 8, 0.0, 0.0, 0, 1 << 30, 1e-12, pt.state.ptr);
-    enqueue_amg_iteration(h, pt, 0, true);  // warm
-    HIPC(hipEventRecord(h->ev[0], s));
+    // the reps iterations replay as one captured graph, as in the solve
+    // (eager launches of ≈ 20 short kernels per iteration are host-bound)
+    hipGraph_t g;
+    hipGraphExec_t ge = nullptr;
+    HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < reps; ++k) enqueue_amg_iteration(h, pt, 0, true);
-    HIPC(hipGetLastError());
-    HIPC(hipEventRecord(h->ev[1], s));
-    HIPC(hipEventSynchronize(h->ev[1]));
+    HIPC(hipStreamEndCapture(s, &g));
+    hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPC(e);
+    e = hipGraphLaunch(ge, s);  // warm
+    if (e == hipSuccess) e = hipEventRecord(h->ev[0], s);
+    if (e == hipSuccess) e = hipGraphLaunch(ge, s);
+    if (e == hipSuccess) e = hipEventRecord(h->ev[1], s);
+    if (e == hipSuccess) e = hipEventSynchronize(h->ev[1]);
     float ms = 0;
-    HIPC(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+    (void)hipGraphExecDestroy(ge);
+    HIPC(e);
     *avg_ms = ms / reps;
     return 0;
   }

@@ -117,3 +117,38 @@ def test_gamg_profile_iteration(engine):
     engine.solve(0.01, -0.01, _opts(1e-8))
     ms = engine.profile_iteration(PC_GAMG, reps=20)
     assert 0 < ms < 5.0
+
+
+# ---------------------------------------------------------------------------
+# benchmark sizes: C3 = 6×8 tiles (1.06 M DOF), the C5 chord recipe
+# on 2×2 tiles; U against the oracle's direct solve of the same system
+# ---------------------------------------------------------------------------
+def _big_case(engine, nx, ny, chords):
+    from mfea import synth
+    xyz, e2n = synth.tiled_mesh(nx, ny, chords=chords)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    A, b, free = fo.free_system(K, known, vals)
+    Uref = fo.solve_system(K, known, vals)
+    return dy, A, b, free, Uref
+
+
+@pytest.mark.parametrize("nx,ny,chords", [(6, 8, False), (2, 2, True)])
+def test_benchmark_sizes_match_direct(engine, nx, ny, chords):
+    from mfea import PC_JACOBI, make_opts
+    dy, A, b, free, Uref = _big_case(engine, nx, ny, chords)
+    for pc in ("gamg", "jacobi"):
+        opts = _opts(1e-13) if pc == "gamg" else make_opts(rtol=1e-13, max_it=200000, precond=PC_JACOBI)
+        st = engine.solve(dy, -dy, opts)
+        U = engine.displacement()
+        assert st.status == 0, pc
+        assert rel(U, Uref) <= 1e-10, (pc, rel(U, Uref))
+        assert np.linalg.norm(A @ U[free] - b) <= 1e-12 * np.linalg.norm(b), pc
+        if chords is False:
+            assert np.all(U[2::3] == 0.0)  # planar: z decouples exactly

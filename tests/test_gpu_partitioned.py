@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, load_gen, load_mesh, read_rt
-from test_gpu_parity import STRESS_RTOL, force_close, rel
+from test_gpu_parity import check_stress_records, force_close, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -125,9 +125,9 @@ def test_partitioned_dropin_matches_reference_vectors(tmp_path, gen, mesh, npart
     U = read_rt(res / "node_displacements.csv").values[:, :-1]
     for k, s in enumerate(g["U_steps"]):
         assert rel(U[s], g["U"][k]) <= 1e-10
+    nodes, elems = load_mesh(mesh)
     S = read_rt(res / "stress_record.csv").values[:, :-1]
-    for s in range(S.shape[0]):
-        assert rel(S[s], g["stress"][s]) <= STRESS_RTOL
+    check_stress_records(nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values, U, S, A)
 
 
 def test_partitioned_failures_match_committed_golden(tmp_path):

@@ -1,19 +1,22 @@
 """Benchmark: DOF solved/s of one full FEA load step on MI355X.
 
 A "step" = one pass of the hot path over the synthetic mesh: device assembly
-(all elements active) → Dirichlet elimination/RHS → Jacobi-PCG to ‖r‖ ≤ 1e-8‖b‖
-(x0 = 0) → reaction + stress/failure update.  Inputs are resident in HBM before
-the timed region; no CSV IO.  Workload (BASELINE.json configs[1]): the 100k-DOF
-synthetic network = 1×5 tiles of results/sim_20251117_181147 (110,625 DOF).
+(all elements active) → Dirichlet elimination/RHS → PCG (SA-AMG "gamg" V-cycle
+by default, as the reference's -pc_type gamg sweep) to ‖r‖ ≤ 1e-8‖b‖ (x0 = 0)
+→ reaction + stress/failure update.  Inputs are resident in HBM before the
+timed region; no CSV IO.  Workload (BASELINE.json configs[2]): C3_1M = 6×8
+tiles of results/sim_20251117_181147 (1.06 M DOF).
 
 N > 1 (one process per GPU, launched by torch.distributed.run): the
-partitioned solve over RCCL with weak scaling — the network is
-N×5 tiles (≈ 110k DOF per GPU) cut into N strips along x, one per GPU;
+partitioned solve over RCCL, one strip of the network per GPU
+(partition.hpp: x-strips whose boundaries follow the gaps between tiles).
+  --scaling weak   (default) the network is (6N)×8 tiles — C3 per GPU;
+  --scaling strong the C3 network itself is cut into N strips.
 `value` is the whole network's DOF/s.  `--mode replicas` runs N independent
 copies of the 1-GPU step instead.  torch.distributed (gloo) only carries the
 RCCL unique id, the barriers and the max-over-ranks time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2_100k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3_1M] [--scaling weak|strong]
 
 Prints ONE JSON line on rank 0.
 """
@@ -50,6 +53,8 @@ def parse():
                     help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
                     help="N > 1: one network cut over the GPUs, or N independent copies")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1 partitioned: C3 per GPU (weak) or C3 cut N ways (strong)")
     ap.add_argument("--parts", type=int, default=1,
                     help="1 GPU: run the partitioned solve with this many partitions on it")
     return ap.parse_args()
@@ -217,7 +222,8 @@ def main():
 
     def setup(mode):
         """engine + resident mesh for one mode; returns (eng, nx, xyz, e2n, top, bot)"""
-        nx = nx0 * world if mode == "partitioned" else nx0  # weak scaling: a tile column per GPU
+        # weak scaling: the config's tiles per GPU, side by side along x
+        nx = nx0 * world if mode == "partitioned" and a.scaling == "weak" else nx0
         eng = Engine(local)
         if mode == "partitioned":
             uid = [dist_unique_id() if rank == 0 else None]
@@ -239,22 +245,36 @@ def main():
         return eng.step(dy, -dy, opts, fs.MAX_STRAIN)
 
     if mode == "partitioned":
-        # one probing step over RCCL; every rank must succeed, or all fall back
-        # to independent replicas (agreed over gloo) — the line reports which
-        ok, err = 1, ""
-        eng = None
-        try:
-            eng, nx, xyz, e2n, top, bot = setup(mode)
-            run_step(eng)
-        except Exception as ex:  # noqa: BLE001
-            ok, err = 0, str(ex)
+        # one probing step over RCCL with the chunks as hipGraph replays (RCCL
+        # ops captured); every rank must succeed, else all retry with eager
+        # launches, else fall back to independent replicas (agreed over gloo)
+        # — the line reports which
         import torch
-        flag = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 0:
-            note = f"partitioned solve failed on some rank ({err or 'peer'}); replicas instead"
+
+        def agree(ok):
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            return int(flag.item()) == 1
+
+        eng, errs = None, []
+        for graph in (1, 0):
+            ok = 1
+            try:
+                eng, nx, xyz, e2n, top, bot = setup(mode)
+                eng.set_option("dist_graph", graph)
+                run_step(eng)
+            except Exception as ex:  # noqa: BLE001
+                ok = 0
+                errs.append(str(ex))
+            if agree(ok):
+                if graph == 0:
+                    note = f"graph-captured partitioned chunks failed ({errs[0] if errs else 'peer'}); eager launches"
+                break
             if eng is not None:
                 eng.close()
+                eng = None
+        if eng is None:
+            note = f"partitioned solve failed on some rank ({errs[-1] if errs else 'peer'}); replicas instead"
             mode = "replicas"
             eng, nx, xyz, e2n, top, bot = setup(mode)
     else:
@@ -320,7 +340,7 @@ def main():
     workload = (f"{a.config}: {nx}x{ny} tiles, {n_dof} DOF, {st.n_free} free DOF, {len(e2n)} elements, "
                 f"load step {a.load_step}/40")
     if mode == "partitioned":
-        workload += f", cut into {world} x-strips (one per GPU)"
+        workload += f", cut into {world} x-strips (one per GPU; {a.scaling} scaling)"
     elif mode == "parts":
         workload += f", {a.parts} partitions on 1 GPU"
     elif mode == "replicas":
@@ -334,7 +354,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling if mode == "partitioned" else "weak",
         "vs_baseline": None,
         "dtype": "f64" if pc != PC_GAMG else "f64 (CG; f32 AMG V-cycle)",
         "data": "synthetic (tiled copies of results/sim_20251117_181147; no RNG)",

@@ -23,6 +23,23 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
  * multi-GPU path on one GPU).  axis as mfea_set_partition_axis. */
 int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
 
+/* Tuning options of a handle (experiments and tests; the defaults are the
+ * measured best; the library reads no environment variables).  Names:
+ *   "graph" 0|1          single-partition CG chunks as hipGraph replays (1)
+ *   "dist_graph" 0|1     partitioned chunks, exchanges included, likewise (1)
+ *   "order" -1|0|k       free-row order: DFS (-1), natural (0), degree sort in windows of k
+ *   "lane_dof" 0|3       planar meshes on 2 DOFs per node (0) or 3
+ *   "cg_kernel" 0|1|2    Jacobi CG kernel: by density (0), lanes (1), SELL (2)
+ *   "ell_block" 64..512  lane kernels: threads per block (256)
+ *   "ell_maxg" n         lane kernels: grid cap (0 = 512)
+ *   "ell_compact" 0|1    lane kernels: compact halo records (1)
+ *   "amg_tail_rows" n    GAMG: deep levels of ≤ n rows in one workgroup (2048; 0 off)
+ *   "dist_timeout_ms" n  RCCL waits: give up after n ms
+ *   "part_slack_pct" n   partition boundaries move ≤ n % of a strip to the
+ *                        fewest crossing elements (35; 0 = equal free-node counts)
+ * Options that change the symbolic layout rebuild it at the next call. */
+int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
+
 /* The MFEA_PC_GAMG hierarchy for the current active set (built if needed):
  * *n_levels levels; for level l < cap: rows[l] (nodes / aggregates),
  * blocks[l] (stored ND×ND blocks of A_l, diagonal included) and pblocks[l]

@@ -669,8 +669,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, co
   vcycle_entry<ND>(L0, cg, i, r);
 }
 
-template <int ND, bool FIRST, int BS>
-__global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part) {
+template <int ND, bool FIRST, int BS, bool DIST>
+__global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part,
+                                                 AmgDist d) {
   if (!FIRST && slots[j + 1].flag != kRun) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
@@ -685,6 +686,20 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
     sell_mac<ND, false>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
     if (i >= cg.n) continue;
+    if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
+      for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
+        const int64_t q = d.gslot[t];
+        double s6[6], m[ND * ND], ug[ND];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s6[c] = d.sval[(int64_t)c * d.G + q];
+        sym_to<ND>(s6, m);
+        vload<ND>(d.urecv, d.grecv[t], ug);
+#pragma unroll
+        for (int a = 0; a < ND; ++a)
+#pragma unroll
+          for (int b = 0; b < ND; ++b) y[a] = fma(m[a * ND + b], ug[b], y[a]);
+      }
+    }
     vload<ND>(cg.u, i, u);
     vload<ND>(cg.r, i, r);
     vstore<ND>(cg.w, i, y);
@@ -707,15 +722,48 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
   }
 }
 
-template <int ND, int PU, int BS>
+// Partitioned: this rank's sums (its w kernel's block partials in block
+// order, as wave_partials does) → its row of gall[q] and gsend.  Every rank
+// then adds the gathered rows in rank order (k_amg_cg_update<DIST>): the same
+// bits everywhere, so α, β and the stopping test agree across ranks.
+template <int PU>
+__global__ __launch_bounds__(64) void k_amg_gsum(const double* __restrict__ p, double* row, double* gsend) {
+  double S[4];
+  wave_partials<PU>(p, S);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      row[c] = S[c];
+      gsend[c] = S[c];
+    }
+  }
+}
+
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_pack_u(AmgCg cg, AmgDist d) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= d.n_send) return;
+  const int64_t i = d.send_rows[k];  // -1: a fixed node (zeros)
+#pragma unroll
+  for (int a = 0; a < ND; ++a) d.usend[ND * k + a] = i >= 0 ? cg.u[ND * i + a] : 0.0;
+}
+
+template <int ND, int PU, int BS, bool DIST>
 __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg cg, Slot* slots,
-                                                         const SolveState* st, double* part) {
+                                                      const SolveState* st, double* part, AmgDist d) {
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
   const double g0 = slots[j].v[0], a0 = slots[j].alpha;
   const double tol2 = st->tol2;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
-  wave_partials<PU>(part_buf(part, j & 1), S);
+  if constexpr (DIST) {  // the gathered rank sums, rank order (rows ≥ world are 0)
+    const int lane = threadIdx.x & 63;
+    const double* g = d.gall[j & 1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) S[c] = wave_allsum(g[lane * 4 + c]);
+  } else {
+    wave_partials<PU>(part_buf(part, j & 1), S);
+  }
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
   cg_record(slots, j, S, cs);
   if (cs.status != kRun) return;
@@ -849,46 +897,69 @@ void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& c
 
 template <int ND, int BS>
 static void w_bs(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                 double* part) {
+                 double* part, const AmgDist* d) {
   const dim3 g((unsigned)amg_w_grid(cg.n));
-  if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, part);
-  else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, part);
+  const AmgDist dd = d ? *d : AmgDist{};
+  if (d) {
+    if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, true>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+    else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS, true>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+  } else {
+    if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, false>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+    else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS, false>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+  }
 }
 template <int ND>
 static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                 double* part) {
-  if (amg_w_block(cg.n) == 512) w_bs<ND, 512>(s, j, first, L0, cg, slots, part);
-  else w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part);
+                 double* part, const AmgDist* d) {
+  if (amg_w_block(cg.n) == 512) w_bs<ND, 512>(s, j, first, L0, cg, slots, part, d);
+  else w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part, d);
 }
 void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
-                     Slot* slots, double* part) {
-  if (nd == 2) w_nd<2>(s, j, first, L0, cg, slots, part);
-  else w_nd<3>(s, j, first, L0, cg, slots, part);
+                     Slot* slots, double* part, const AmgDist* d) {
+  if (nd == 2) w_nd<2>(s, j, first, L0, cg, slots, part, d);
+  else w_nd<3>(s, j, first, L0, cg, slots, part, d);
 }
 
-template <int ND, int BS>
+void launch_amg_gsum(hipStream_t s, int64_t n, const double* part_q, const AmgDist& d, int q) {
+  double* row = d.gall[q] + 4 * d.rank;
+  switch (pu_of_grid(amg_w_grid(n))) {  // the w kernel's grid = its partial count
+    case 1: hipLaunchKernelGGL(k_amg_gsum<1>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
+    case 2: hipLaunchKernelGGL(k_amg_gsum<2>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
+    case 4: hipLaunchKernelGGL(k_amg_gsum<4>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
+    default: hipLaunchKernelGGL(k_amg_gsum<8>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
+  }
+}
+
+void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d) {
+  if (d.n_send <= 0) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_pack_u<2>, rows_grid(d.n_send), dim3(kBlock), 0, s, cg, d);
+  else hipLaunchKernelGGL(k_amg_pack_u<3>, rows_grid(d.n_send), dim3(kBlock), 0, s, cg, d);
+}
+
+template <int ND, int BS, bool DIST>
 static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                   const SolveState* st, double* part) {
+                   const SolveState* st, double* part, const AmgDist& d) {
   const int64_t gw = amg_w_grid(cg.n);  // partials to reduce = the w kernel's blocks
   int64_t gu = (cg.n + BS - 1) / BS;
   gu = gu < 1 ? 1 : (gu > kCgMaxG ? kCgMaxG : gu);
   const dim3 g((unsigned)gu);
-  switch (pu_of_grid(gw)) {
-    case 1: hipLaunchKernelGGL((k_amg_cg_update<ND, 1, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
-    case 2: hipLaunchKernelGGL((k_amg_cg_update<ND, 2, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
-    case 4: hipLaunchKernelGGL((k_amg_cg_update<ND, 4, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
-    default: hipLaunchKernelGGL((k_amg_cg_update<ND, 8, BS>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part); break;
+  switch (DIST ? 1 : pu_of_grid(gw)) {
+    case 1: hipLaunchKernelGGL((k_amg_cg_update<ND, 1, BS, DIST>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part, d); break;
+    case 2: hipLaunchKernelGGL((k_amg_cg_update<ND, 2, BS, DIST>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part, d); break;
+    case 4: hipLaunchKernelGGL((k_amg_cg_update<ND, 4, BS, DIST>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part, d); break;
+    default: hipLaunchKernelGGL((k_amg_cg_update<ND, 8, BS, DIST>), g, dim3(BS), 0, s, j, L0, cg, slots, st, part, d); break;
   }
 }
 template <int ND>
 static void upd_nd(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                   const SolveState* st, double* part) {
-  upd_bs<ND, kCgBS>(s, j, L0, cg, slots, st, part);
+                   const SolveState* st, double* part, const AmgDist* d) {
+  if (d) upd_bs<ND, kCgBS, true>(s, j, L0, cg, slots, st, part, *d);
+  else upd_bs<ND, kCgBS, false>(s, j, L0, cg, slots, st, part, AmgDist{});
 }
 void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                          const SolveState* st, double* part) {
-  if (nd == 2) upd_nd<2>(s, j, L0, cg, slots, st, part);
-  else upd_nd<3>(s, j, L0, cg, slots, st, part);
+                          const SolveState* st, double* part, const AmgDist* d) {
+  if (nd == 2) upd_nd<2>(s, j, L0, cg, slots, st, part, d);
+  else upd_nd<3>(s, j, L0, cg, slots, st, part, d);
 }
 
 void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row) {

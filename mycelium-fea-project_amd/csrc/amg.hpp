@@ -89,4 +89,22 @@ struct AmgPlan {
 // activity `active` (P's element order).  Returns "" on success.
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan);
 
+// Partitioned solve (partition.hpp): the V-cycle is block Jacobi over the
+// partitions (each partition's hierarchy couples its own free rows only —
+// the strips are grip-to-grip, so the cut couplings are weak: 19 iterations
+// for 1, 2 and 4 strips of a 4×5-tile network) while the CG
+// operator w = A u is global: every owned row adds its couplings to the free
+// ghost rows, whose u arrives through the displacement-halo plan (xsend /
+// xrecv nodes, the same order on both sides).
+struct AmgHalo {
+  std::vector<int32_t> send_rows;  // level-0 rows of the xsend nodes, plan order
+  std::vector<int32_t> gptr;       // per level-0 row: its ghost couplings [gptr[i], gptr[i+1])
+  std::vector<int32_t> gslot;      // SELL slot position of the assembled operator (K_ig = −S_e)
+  std::vector<int32_t> grecv;      // index of the ghost's u in the received halo (xrecv order)
+};
+// xsend_rows / xrecv_rows: Pattern rows of the plan's xsend / xrecv nodes
+std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
+                           const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,
+                           AmgHalo& halo);
+
 }  // namespace mfea

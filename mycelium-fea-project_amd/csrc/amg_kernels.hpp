@@ -66,6 +66,23 @@ struct AmgCg {
   double* u = nullptr;  // level 0's V-cycle output
 };
 
+// Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered
+// per-rank partial sums, its ghost couplings and the u halo buffers.
+struct AmgDist {
+  int rank = 0;
+  double* gall[2] = {nullptr, nullptr};  // [64][4] per-rank partial sums by parity
+  double* gsend = nullptr;               // [4] this rank's, sent to every rank
+  const int32_t* gptr = nullptr;         // per level-0 row: ghost couplings
+  const int32_t* gslot = nullptr;        //   SELL slot of K_ig in the assembled operator
+  const int32_t* grecv = nullptr;        //   the ghost's index in urecv
+  const double* sval = nullptr;          // assembled SELL values val[6][G]
+  int64_t G = 0;
+  const int32_t* send_rows = nullptr;    // level-0 rows whose u the peers hold as ghosts
+  int64_t n_send = 0;
+  double* usend = nullptr;               // [n_send][ND]
+  const double* urecv = nullptr;         // [n_recv][ND]
+};
+
 // ---- numeric setup (every solve) ------------------------------------------
 // A_0 from the assembled SELL operator: off-diagonal = Σ of the listed slots'
 // K_ij (= −S_e), diagonal = K_ii + reg·I; then level 0's D⁻¹ and bound.
@@ -84,12 +101,19 @@ int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------
 // r = b (row-order 3-comp RHS of k_cg_rhs), x = p = s = 0, level-0 x = ω D⁻¹ r
 void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row);
-// w = A_0 u, partials (γ, δ, ‖r‖², ‖u‖²) → parity; first: slots[0] = INIT, parity 0
+// w = A_0 u (+ the ghost couplings when d), partials (γ, δ, ‖r‖², ‖u‖²) →
+// parity; first: slots[0] = INIT, parity 0
 void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
-                     Slot* slots, double* part);
-// iteration j: α, β from the partials, p s x r update, level-0 x = ω D⁻¹ r
+                     Slot* slots, double* part, const AmgDist* d = nullptr);
+// partitioned: this rank's block partials of parity q → gall[q] row rank, gsend
+void launch_amg_gsum(hipStream_t s, int64_t n, const double* part_q, const AmgDist& d, int q);
+// partitioned: u of the send rows → usend
+void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d);
+// iteration j: α, β from the partials (d: from the gathered rank sums), p s x
+// r update, level-0 x = ω D⁻¹ r
 void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg,
-                          Slot* slots, const SolveState* st, double* part);
+                          Slot* slots, const SolveState* st, double* part,
+                          const AmgDist* d = nullptr);
 // x (level-0 order, ND per row) → row-order x[3·row + c]
 void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row);
 // grid of the w kernel (its partials are re-read by the update kernel)

@@ -378,4 +378,34 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   return "";
 }
 
+std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
+                           const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,
+                           AmgHalo& halo) {
+  halo = AmgHalo();
+  const int64_t nf = P.n_free;
+  if ((int64_t)plan.row0.size() != nf) return "internal: AMG plan / pattern mismatch";
+  std::vector<int32_t> lev0(P.n_nodes, -1), recv(P.n_nodes, -1);
+  for (int64_t i = 0; i < nf; ++i) lev0[plan.row0[i]] = (int32_t)i;
+  for (size_t k = 0; k < xrecv_rows.size(); ++k) recv[xrecv_rows[k]] = (int32_t)k;
+  for (int32_t r : xsend_rows) {  // a grip (fixed) node travels as zeros: -1
+    if (r < 0 || r >= P.n_nodes) return "internal: halo send node out of range";
+    halo.send_rows.push_back(r < nf ? lev0[r] : -1);
+  }
+  halo.gptr.assign(nf + 1, 0);
+  for (int64_t i = 0; i < nf; ++i) {  // level-0 row i = Pattern row row0[i]
+    const int64_t r = plan.row0[i];
+    const int64_t base = (int64_t)P.slice_ptr[r >> 6] * 64 + (r & 63);
+    for (int t = 0; t < P.row_len[r]; ++t) {
+      const int64_t pos = base + (int64_t)t * 64;
+      const int32_t j = P.s_col[pos], e = P.s_elem[pos];
+      if (j < nf || e < 0 || !active[e] || P.code[j] != kGhost) continue;
+      if (recv[j] < 0) return "internal: a ghost free neighbour is missing from the halo plan";
+      halo.gslot.push_back((int32_t)pos);
+      halo.grecv.push_back(recv[j]);
+    }
+    halo.gptr[i + 1] = (int32_t)halo.gslot.size();
+  }
+  return "";
+}
+
 }  // namespace mfea

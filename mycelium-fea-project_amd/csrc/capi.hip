@@ -127,6 +127,11 @@ struct Part {
   AmgCg amg_cg;
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
+  // partitioned GAMG (amg.hpp AmgHalo): ghost couplings and the u halo
+  AmgHalo amg_halo;
+  AmgDist amg_dist;
+  DevBuf<int32_t> amg_hi;  // send_rows | gptr | gslot | grecv
+  DevBuf<double> amg_hd;   // usend | urecv
 };
 
 struct mfea_handle {
@@ -150,7 +155,7 @@ struct mfea_handle {
   int nparts = 1, axis = -1;
   int world = 1, rank = 0;
   ncclComm_t comm = nullptr;
-  double dist_timeout_s = 60.0;  // per wait; MFEA_DIST_TIMEOUT_S
+  double dist_timeout_s = 60.0;  // per wait; option "dist_timeout_ms"
   SolveState* h_state = nullptr;       // pinned, 2 entries
   SolveState* d_host_state = nullptr;  // device view of h_state (mapped)
   double* h_red = nullptr;             // pinned
@@ -167,6 +172,17 @@ struct mfea_handle {
   std::vector<uint8_t> act_host;
   bool act_host_ok = false;
   int64_t act_count = 0;
+  // tuning options (mfea_set_option; defaults from the environment at create)
+  bool opt_graph = true;       // single-partition chunks replay as hipGraphs
+  bool opt_dist_graph = true;  // partitioned chunks too
+  int opt_order = kOrderDFS;   // free-row order (symbolic.hpp)
+  int opt_lane_dof = 0;        // 0: 2 DOFs per node on planar meshes, 3: always 3
+  int opt_cg_kernel = 0;       // Jacobi CG: 0 by density, 1 lanes, 2 SELL
+  int opt_ell_block = 256;     // lane kernels: threads per block
+  int64_t opt_ell_maxg = 0;    // lane kernels: grid cap (0: kCgMaxG)
+  bool opt_ell_compact = true; // lane kernels: compact halo records
+  int64_t opt_amg_tail_rows = 2048;  // GAMG: levels of at most this many rows run in one workgroup
+  double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
   DevBuf<int32_t> c_indices;
@@ -206,21 +222,13 @@ int set_device(mfea_handle* h) {
   return 0;
 }
 
-// Row ordering of the free nodes: DFS by default; MFEA_ORDER=natural|<window>
-// for experiments (original order / degree sort inside windows).
-int order_mode() {
-  const char* e = std::getenv("MFEA_ORDER");
-  if (!e || !*e || std::strcmp(e, "dfs") == 0) return kOrderDFS;
-  if (std::strcmp(e, "natural") == 0) return 0;
-  return std::atoi(e);
-}
+// Row ordering of the free nodes: DFS by default (option "order": -1 DFS,
+// 0 natural, > 1 degree sort inside windows of that many rows).
+int order_mode(const mfea_handle* h) { return h->opt_order; }
 
-// planar meshes run the lanes with 2 DOFs per node (MFEA_LANE_DOF=3 forces 3);
+// planar meshes run with 2 DOFs per node (option "lane_dof" 3 forces 3);
 // decided on the whole mesh so every partition exchanges records of one width
-int lane_dofs(const mfea_handle* h) {
-  const char* e = std::getenv("MFEA_LANE_DOF");
-  return (h->planar && !(e && std::strcmp(e, "3") == 0)) ? 2 : 3;
-}
+int lane_dofs(const mfea_handle* h) { return (h->planar && h->opt_lane_dof != 3) ? 2 : 3; }
 
 // Waits for an event.  Partitioned over RCCL: polls with a deadline and the
 // communicator's error state, so a lost peer ends the call instead of hanging.
@@ -341,12 +349,9 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(up(pt.e_code.ptr, code.data(), NL * sizeof(uint32_t)));
     // Halo record layout (ell.hip load_lane): compact (measured on one box:
     // C3 21.8 vs 23.7 µs per iteration, C2 41.6 vs 41.7 ms per step) or one
-    // per lane (MFEA_ELL_HC=0).  The device partner is the record the lane
+    // per lane (option "ell_compact" 0).  The device partner is the record the lane
     // fills: its mirror lane's record.
-    {
-      const char* e = std::getenv("MFEA_ELL_HC");
-      pt.ell_hc = e ? std::atoi(e) != 0 : true;
-    }
+    pt.ell_hc = h->opt_ell_compact;
     std::vector<int32_t> push(NL);
     for (int64_t l = 0; l < NL; ++l)
       push[l] = L.partner[l] >= 0 ? (pt.ell_hc ? L.hrec[L.partner[l]] : L.partner[l]) : L.partner[l];
@@ -411,14 +416,14 @@ int ensure_built(mfea_handle* h) {
     std::string err;
     if (!dm) {
       err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(), skip, h->top, h->bot,
-                          order_mode(), pt.P);
+                          order_mode(h), pt.P);
     } else {
       err = build_partition(h->N, h->xyz.data(), h->Ecount, h->e2n.data(), skip, h->top, h->bot,
-                            h->world > 1 ? h->world : np, pt.rank, h->axis, pt.plan);
+                            h->world > 1 ? h->world : np, pt.rank, h->axis, h->opt_part_slack, pt.plan);
       if (err.empty())
         err = build_pattern((int64_t)pt.plan.node_g.size(), pt.plan.xyz.data(),
                             (int64_t)pt.plan.elem_g.size(), pt.plan.e2n.data(), false, pt.plan.top,
-                            pt.plan.bot, order_mode(), pt.P, &pt.plan.ghost);
+                            pt.plan.bot, order_mode(h), pt.P, &pt.plan.ghost);
     }
     if (!err.empty()) {
       h->parts.resize(1);
@@ -458,12 +463,11 @@ int ensure_built(mfea_handle* h) {
 // (C5: mean degree 7.5 → 4.5 lanes per free row, most of them helpers that
 // move zeros) run the SELL kernel instead: measured 0.94 vs 2.16 ms per
 // iteration at 10 M DOF.  The partitioned path always runs lanes.
-// MFEA_CG_KERNEL=sell|lanes forces one (comparison runs).
-bool use_ell(const Part& pt) {
+// Option "cg_kernel" 1 (lanes) / 2 (SELL) forces one (comparison runs).
+bool use_ell(const mfea_handle* h, const Part& pt) {
   if (!pt.ell_ok) return false;
-  const char* e = std::getenv("MFEA_CG_KERNEL");
-  if (e && std::strcmp(e, "sell") == 0) return false;
-  if (e && std::strcmp(e, "lanes") == 0) return true;
+  if (h->opt_cg_kernel == 2) return false;
+  if (h->opt_cg_kernel == 1) return true;
   return pt.L.n_lanes <= 2 * std::max<int64_t>(pt.P.n_free, 1);
 }
 
@@ -525,6 +529,8 @@ EllOp ell_op(const mfea_handle* h, Part& pt) {
   op.NR = ell_nr(pt);
   op.hmask = pt.e_hmask.ptr;
   op.hbase = pt.e_hbase.ptr;
+  op.bs = h->opt_ell_block;
+  op.maxg = h->opt_ell_maxg;
   return op;
 }
 
@@ -683,7 +689,7 @@ int enqueue_chunk_dist(mfea_handle* h, int chunk, int precond) {
     }
     for (auto& pp : h->parts) {
       Part& pt = *pp;
-      launch_psum(s, pt.L.n_lanes, cg_part_buf(pt, q), pt.dv.gall[q] + 4 * pt.rank, pt.dv.gsend);
+      launch_psum(s, ell_op(h, pt), cg_part_buf(pt, q), pt.dv.gall[q] + 4 * pt.rank, pt.dv.gsend);
     }
     HIPC(hipGetLastError());
     RC(xchg_records(h, q, true));
@@ -804,7 +810,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
                           pt.state.ptr);
   HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
-  const bool ell = use_ell(pt);
+  const bool ell = use_ell(h, pt);
   if (ell) {
     launch_ell_init(s, ell_op(h, pt), op, precond, v, ell_vecs(pt));
     launch_ell_first(s, ell_op(h, pt), o->reg, precond, ell_vecs(pt), pt.slots.ptr, pt.cg_part.ptr);
@@ -813,9 +819,9 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   }
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
-  // MFEA_NO_GRAPH=1: launch the chunk kernels eagerly (profilers that do not
+  // option "graph" 0: launch the chunk kernels eagerly (profilers that do not
   // follow hipGraph replays; same kernels, same order)
-  static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  const bool no_graph = !h->opt_graph;
   SolveState fin;
   int rc;
   if (no_graph) {
@@ -861,9 +867,6 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
 // ---------------------------------------------------------------------------
 // SA-AMG preconditioned CG (amg.hpp / amg.hip), single partition.
 // ---------------------------------------------------------------------------
-// levels of at most this many rows run inside the single-workgroup tail
-// (MFEA_AMG_TAIL_ROWS overrides; 0 disables)
-constexpr int64_t kAmgTailRows = 2048;
 constexpr size_t kAmgAlign = 64;  // elements: every carved array starts 256/512-B aligned
 size_t amg_al(size_t n) { return (n + kAmgAlign - 1) / kAmgAlign * kAmgAlign; }
 
@@ -982,8 +985,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
   {
     std::vector<int64_t> rows(nlev);
     for (int l = 0; l < nlev; ++l) rows[l] = pl.lev[l].A.n;
-    const char* e = std::getenv("MFEA_AMG_TAIL_ROWS");
-    pt.amg_tail = amg_tail_level(rows.data(), nlev, e ? std::atoll(e) : kAmgTailRows);
+    pt.amg_tail = amg_tail_level(rows.data(), nlev, h->opt_amg_tail_rows);
   }
   HIPC(hipStreamSynchronize(s));
   return 0;
@@ -1000,17 +1002,72 @@ int current_active(mfea_handle* h, Part& pt) {
   return 0;
 }
 
-// (Re)build the hierarchy when the active set differs from the plan's.
+// Partitioned GAMG: the halo plan (ghost couplings, u send rows) for the
+// plan's active set, uploaded next to the hierarchy.
+int upload_amg_halo(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
+  const PartPlan& pl = pt.plan;
+  const Pattern& P = pt.P;
+  std::vector<int32_t> xs(pl.xsend_node.size()), xr(pl.xrecv_node.size());
+  for (size_t i = 0; i < xs.size(); ++i) xs[i] = P.iperm[pl.xsend_node[i]];
+  for (size_t i = 0; i < xr.size(); ++i) xr[i] = P.iperm[pl.xrecv_node[i]];
+  const std::string err = build_amg_halo(P, key, pt.amg, xs, xr, pt.amg_halo);
+  if (!err.empty()) return fail(MFEA_EINVAL, "AMG halo: " + err);
+  const AmgHalo& hl = pt.amg_halo;
+  const int nd = pt.amg.nd;
+  const size_t a = hl.send_rows.size(), b = hl.gptr.size(), c = hl.gslot.size();
+  HIPC(pt.amg_hi.alloc(a + b + 2 * c + 1));
+  HIPC(pt.amg_hd.alloc(nd * (xs.size() + xr.size()) + 1));
+  hipStream_t s = h->stream;
+  auto up = [&](int32_t* d, const std::vector<int32_t>& v) {
+    return v.empty() ? hipSuccess : hipMemcpyAsync(d, v.data(), v.size() * 4, hipMemcpyHostToDevice, s);
+  };
+  int32_t* ib = pt.amg_hi.ptr;
+  HIPC(up(ib, hl.send_rows));
+  HIPC(up(ib + a, hl.gptr));
+  HIPC(up(ib + a + b, hl.gslot));
+  HIPC(up(ib + a + b + c, hl.grecv));
+  HIPC(hipMemsetAsync(pt.amg_hd.ptr, 0, pt.amg_hd.n * sizeof(double), s));
+  AmgDist& d = pt.amg_dist;
+  d = AmgDist{};
+  d.rank = pt.rank;
+  d.gall[0] = pt.dv.gall[0];
+  d.gall[1] = pt.dv.gall[1];
+  d.gsend = pt.dv.gsend;
+  d.send_rows = ib;
+  d.n_send = (int64_t)a;
+  d.gptr = ib + a;
+  d.gslot = ib + a + b;
+  d.grecv = ib + a + b + c;
+  d.sval = pt.val.ptr;
+  d.G = pt.G;
+  d.usend = pt.amg_hd.ptr;
+  d.urecv = pt.amg_hd.ptr + nd * xs.size();
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// (Re)build the hierarchy when the active set differs from the plan's.  One
+// partition: the host view of the activity (downloaded only when a post
+// kernel changed it); partitioned: each partition's own elements, read back.
 int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
   *rebuilt = false;
-  RC(current_active(h, pt));
-  if (pt.amg_ok && pt.amg_key == h->act_host) return 0;
+  const bool dm = partitioned(h);
+  std::vector<uint8_t> local;
+  if (dm) {
+    local.resize(pt.P.n_elems);
+    if (pt.P.n_elems) HIPC(hipMemcpy(local.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
+  } else {
+    RC(current_active(h, pt));
+  }
+  const std::vector<uint8_t>& key = dm ? local : h->act_host;
+  if (pt.amg_ok && pt.amg_key == key) return 0;
   pt.amg_ok = false;
-  const std::string err = build_amg(pt.P, h->act_host, lane_dofs(h), pt.amg);
+  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   RC(upload_amg(h, pt));
-  pt.amg_key = h->act_host;
+  if (dm) RC(upload_amg_halo(h, pt, key));
+  pt.amg_key = key;
   pt.amg_ok = true;
   ++pt.amg_gen;
   *rebuilt = true;
@@ -1025,6 +1082,97 @@ void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
   launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
                     pt.amg_tail, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
   launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+}
+
+// ---- partitioned GAMG exchanges -------------------------------------------
+// u of the send rows → the peers' urecv (the displacement-halo plan, ND
+// doubles per node)
+int xchg_u(mfea_handle* h) {
+  hipStream_t s = h->stream;
+  const int64_t nd = part0(h).amg.nd;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    const PartPlan& pl = pt.plan;
+    if (pl.xpeers.empty()) return 0;
+    NCCLC(ncclGroupStart());
+    for (size_t i = 0; i < pl.xpeers.size(); ++i) {
+      if (pl.xsend_cnt[i])
+        NCCLC(ncclSend(pt.amg_dist.usend + nd * pl.xsend_off[i], (size_t)(nd * pl.xsend_cnt[i]), ncclFloat64,
+                       pl.xpeers[i], h->comm, s));
+      if (pl.xrecv_cnt[i])
+        NCCLC(ncclRecv(const_cast<double*>(pt.amg_dist.urecv) + nd * pl.xrecv_off[i],
+                       (size_t)(nd * pl.xrecv_cnt[i]), ncclFloat64, pl.xpeers[i], h->comm, s));
+    }
+    NCCLC(ncclGroupEnd());
+    return 0;
+  }
+  for (auto& a : h->parts) {
+    const PartPlan& pa = a->plan;
+    for (size_t i = 0; i < pa.xpeers.size(); ++i) {
+      if (!pa.xsend_cnt[i]) continue;
+      Part& b = *h->parts[pa.xpeers[i]];
+      const PartPlan& pb = b.plan;
+      const auto it = std::lower_bound(pb.xpeers.begin(), pb.xpeers.end(), a->rank);
+      const size_t jb = (size_t)(it - pb.xpeers.begin());
+      if (it == pb.xpeers.end() || *it != a->rank || pb.xrecv_cnt[jb] != pa.xsend_cnt[i])
+        return fail(MFEA_EINVAL, "internal: asymmetric u halo");
+      HIPC(hipMemcpyAsync(const_cast<double*>(b.amg_dist.urecv) + nd * pb.xrecv_off[jb],
+                          a->amg_dist.usend + nd * pa.xsend_off[i], nd * pa.xsend_cnt[i] * sizeof(double),
+                          hipMemcpyDeviceToDevice, s));
+    }
+  }
+  return 0;
+}
+
+// every rank's 4 partial sums (gsend) → row `rank` of every rank's gall[q]
+int xchg_sums(mfea_handle* h, int q) {
+  hipStream_t s = h->stream;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    NCCLC(ncclAllGather(pt.dv.gsend, pt.dv.gall[q], 4, ncclFloat64, h->comm, s));
+    return 0;
+  }
+  for (auto& a : h->parts)
+    for (auto& b : h->parts)
+      if (b != a)
+        HIPC(hipMemcpyAsync(b->dv.gall[q] + 4 * a->rank, a->dv.gsend, 4 * sizeof(double),
+                            hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// one partitioned GAMG iteration j on every partition: update (gathered sums)
+// → local V-cycle → u halo → w = A u with the ghost couplings → this rank's
+// sums → all-gather.  Two exchanges per iteration (the V-cycle output is not
+// computable from a neighbour's state, unlike the Jacobi lanes' records).
+int enqueue_amg_dist_iteration(mfea_handle* h, int j) {
+  hipStream_t s = h->stream;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int nd = pt.amg.nd;
+    launch_amg_cg_update(s, nd, j, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr,
+                         &pt.amg_dist);
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+                      pt.amg_tail, &pt.slots.ptr[j + 1].flag);
+    launch_amg_pack_u(s, nd, pt.amg_cg, pt.amg_dist);
+  }
+  HIPC(hipGetLastError());
+  RC(xchg_u(h));
+  const int q = (j & 1) ^ 1;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_w(s, pt.amg.nd, j, false, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr,
+                    &pt.amg_dist);
+    launch_amg_gsum(s, pt.amg_cg.n, cg_part_buf(pt, q), pt.amg_dist, q);
+  }
+  HIPC(hipGetLastError());
+  return xchg_sums(h, q);
+}
+
+int enqueue_amg_dist_chunk(mfea_handle* h, int chunk) {
+  for (int j = 0; j < chunk; ++j) RC(enqueue_amg_dist_iteration(h, j));
+  for (auto& pp : h->parts) launch_cg_advance(h->stream, chunk, pp->slots.ptr, pp->state.ptr, pp->mirror);
+  HIPC(hipGetLastError());
+  return 0;
 }
 
 void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
@@ -1067,7 +1215,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
   HIPC(hipGetLastError());
   const int tag = -1000 - (int)(pt.amg_gen % 1000000);
-  static const bool no_graph = std::getenv("MFEA_NO_GRAPH") != nullptr;
+  const bool no_graph = !h->opt_graph;
   const int expected = std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16);
   SolveState fin;
   int rc;
@@ -1116,6 +1264,111 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   return rc;
 }
 
+// The partitioned GAMG solve: block-Jacobi-over-partitions AMG V-cycles inside
+// a global CG (amg.hpp AmgHalo), the exchanges of enqueue_amg_dist_iteration.
+int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
+                   mfea_stats* st) {
+  hipStream_t s = h->stream;
+  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
+    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
+  bool rebuilt = false;
+  for (auto& pp : h->parts) {
+    bool rb = false;
+    RC(ensure_amg(h, *pp, &rb));
+    rebuilt = rebuilt || rb;
+  }
+  const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
+  const int W = nranks(h);
+  HIPC(hipEventRecord(h->ev[1], s));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 0, cg_vecs(pt), pt.partials.ptr,
+                  tix(pt, 0), pt.red.ptr);
+  }
+  RC(gather4(h, 0));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
+    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
+    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  }
+  HIPC(hipEventRecord(h->ev[2], s));
+  for (auto& pp : h->parts) enqueue_amg_setup(h, *pp, o->reg);
+  HIPC(hipEventRecord(h->ev_setup, s));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int nd = pt.amg.nd;
+    launch_amg_cg_init(s, nd, pt.amg_lev[0], pt.amg_cg, cg_vecs(pt).r[0]);
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+                      pt.amg_tail, nullptr);
+    launch_amg_pack_u(s, nd, pt.amg_cg, pt.amg_dist);
+  }
+  RC(xchg_u(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_w(s, pt.amg.nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr,
+                    &pt.amg_dist);
+    launch_amg_gsum(s, pt.amg_cg.n, cg_part_buf(pt, 0), pt.amg_dist, 0);
+  }
+  RC(xchg_sums(h, 0));
+  HIPC(hipGetLastError());
+  int64_t gen = 0;
+  for (auto& pp : h->parts) gen = gen * 1000003 + pp->amg_gen;
+  const int tag = -2000000 - (int)(gen % 1000000);
+  Part& p0 = part0(h);
+  const int expected = std::min(o->max_it, p0.amg_last_iters > 0 ? p0.amg_last_iters : 16);
+  SolveState fin;
+  if (!h->opt_dist_graph) {
+    RC(drive_planned(h, chunk, o->max_it, expected, [&]() -> int { return enqueue_amg_dist_chunk(h, chunk); },
+                     &fin));
+  } else {
+    if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG ||
+        h->graph_ell != tag) {
+      destroy_graph(h);
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int rc = enqueue_amg_dist_chunk(h, chunk);
+      const hipError_t ce = hipStreamEndCapture(s, &g);
+      if (rc) return rc;
+      HIPC(ce);
+      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_chunk = chunk;
+      h->graph_precond = MFEA_PC_GAMG;
+      h->graph_ell = tag;
+    }
+    RC(drive_planned(h, chunk, o->max_it, expected,
+                     [&]() -> int {
+                       HIPC(hipGraphLaunch(h->graph, s));
+                       return 0;
+                     },
+                     &fin));
+  }
+  if (fin.status == 0) p0.amg_last_iters = fin.iters;
+  // x to row order, then the displacement halo (ghost rows of the post kernels)
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_finish(s, pt.amg.nd, pt.amg_cg, pt.x.ptr);
+    launch_rows_pack(s, pt.xsend_rows.ptr, (int64_t)pt.plan.xsend_node.size(), pt.x.ptr, pt.xh_send);
+  }
+  RC(xchg_xhalo(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rows_unpack(s, pt.xrecv_rows.ptr, (int64_t)pt.plan.xrecv_node.size(), pt.xh_recv, pt.x.ptr);
+  }
+  HIPC(hipGetLastError());
+  const int rc = finish_solve(h, fin, st);
+  if (st) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev_setup);
+    st->t_setup_ms = ms;
+    st->amg_levels = (int32_t)p0.amg_lev.size();
+    st->amg_rebuilt = rebuilt ? 1 : 0;
+  }
+  return rc;
+}
+
 // The partitioned solve: the same CG-CG iterations on every partition's lanes,
 // with the exchanges of partition.hpp between kernels.
 int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
@@ -1146,16 +1399,14 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
     Part& pt = *pp;
     launch_ell_first(s, ell_op(h, pt), o->reg, precond, ell_vecs(pt), pt.slots.ptr, pt.cg_part.ptr,
                      &pt.dv);
-    launch_psum(s, pt.L.n_lanes, cg_part_buf(pt, 0), pt.dv.gall[0] + 4 * pt.rank, pt.dv.gsend);
+    launch_psum(s, ell_op(h, pt), cg_part_buf(pt, 0), pt.dv.gall[0] + 4 * pt.rank, pt.dv.gsend);
   }
   RC(xchg_records(h, 0, true));
   HIPC(hipGetLastError());
   HIPC(hipEventRecord(h->ev[2], s));
-  // MFEA_DIST_GRAPH=1: replay each chunk (kernels + exchanges) as one hipGraph
-  static const bool dist_graph = [] {
-    const char* e = std::getenv("MFEA_DIST_GRAPH");
-    return e && *e == '1';
-  }();
+  // each chunk (kernels + exchanges) replays as one hipGraph (option
+  // "dist_graph" 0: eager launches)
+  const bool dist_graph = h->opt_dist_graph;
   SolveState fin;
   if (dist_graph) {
     const int tag = -10 - lane_dofs(h);  // graph_ell key of the partitioned chunk
@@ -1266,10 +1517,8 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
 
 int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
-  if (o->precond == MFEA_PC_GAMG) {
-    if (partitioned(h)) return fail(MFEA_EINVAL, "MFEA_PC_GAMG: single-partition handles only");
-    return solve_amg(h, dy_top, dy_bot, o, st);
-  }
+  if (o->precond == MFEA_PC_GAMG)
+    return partitioned(h) ? solve_amg_dist(h, dy_top, dy_bot, o, st) : solve_amg(h, dy_top, dy_bot, o, st);
   if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
     return fail(MFEA_EINVAL, "unknown preconditioner");
   return partitioned(h) ? solve_dist(h, dy_top, dy_bot, o, st) : solve_impl(h, dy_top, dy_bot, o, st);
@@ -1715,7 +1964,7 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
   for (int64_t i = 0; i < P.n_free; ++i) inc += P.row_len[i];
   info->free_incidences = inc;
   info->planar = h->planar ? 1 : 0;
-  info->cg_lanes = use_ell(pt) ? 1 : 0;
+  info->cg_lanes = use_ell(h, pt) ? 1 : 0;
   info->n_lanes = pt.ell_ok ? pt.L.n_lanes : 0;
   int64_t halo = 0;
   if (pt.ell_ok)
@@ -1727,8 +1976,8 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
   info->n_ghost = P.n_ghost;
   if (pt.ell_ok) {
     info->halo_compact = pt.ell_hc ? 1 : 0;
-    info->block_size = ell_block_size(pt.L.n_lanes);
-    info->grid = ell_grid_size(pt.L.n_lanes);
+    info->block_size = ell_block_size(ell_op(h, pt));
+    info->grid = ell_grid_size(ell_op(h, pt));
   }
   return 0;
 }
@@ -1737,7 +1986,7 @@ int mfea_get_info(mfea_handle* h, mfea_info* info) {
 // partitioned handles: the per-GPU kernel without its exchange)
 static void launch_iter0(mfea_handle* h, int pc, unsigned long long* trace) {
   Part& pt = part0(h);
-  if (use_ell(pt))
+  if (use_ell(h, pt))
     launch_ell_iter(h->stream, 0, ell_op(h, pt), pc, ell_vecs(pt), pt.slots.ptr, pt.state.ptr,
                     pt.cg_part.ptr, trace);
   else
@@ -1815,9 +2064,9 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
   RC(mfea_profile_iteration(h, precond, 20, &ms));  // same running state
   hipStream_t s = h->stream;
   Part& pt = part0(h);
-  const bool ell = use_ell(pt);
-  const int64_t g = ell ? ell_grid_size(pt.L.n_lanes) : cg_grid(pt.P.n_free);
-  const int64_t nw = g * ((ell ? ell_block_size(pt.L.n_lanes) : cg_block_size(0)) / 64);
+  const bool ell = use_ell(h, pt);
+  const int64_t g = ell ? ell_grid_size(ell_op(h, pt)) : cg_grid(pt.P.n_free);
+  const int64_t nw = g * ((ell ? ell_block_size(ell_op(h, pt)) : cg_block_size(0)) / 64);
   if (cap < nw * 4) return fail(MFEA_EINVAL, "trace buffer too small");
   unsigned long long* d = nullptr;
   HIPC(hipMalloc(&d, nw * 4 * sizeof(unsigned long long)));
@@ -1855,6 +2104,42 @@ int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* b
   }
   if (pair_items) *pair_items = pl.pair_items;
   if (nd) *nd = pl.nd;
+  return 0;
+}
+
+int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
+  if (!h || !name) return fail(MFEA_EINVAL, "NULL argument");
+  const std::string n(name);
+  bool rebuild = false;  // options baked into the symbolic layout
+  if (n == "graph") h->opt_graph = value != 0;
+  else if (n == "dist_graph") h->opt_dist_graph = value != 0;
+  else if (n == "order") { h->opt_order = (int)value; rebuild = true; }
+  else if (n == "lane_dof") { h->opt_lane_dof = (int)value; rebuild = true; }
+  else if (n == "cg_kernel") {
+    if (value < 0 || value > 2) return fail(MFEA_EINVAL, "cg_kernel: 0 auto, 1 lanes, 2 sell");
+    h->opt_cg_kernel = (int)value;
+  } else if (n == "ell_block") {
+    if (value != 64 && value != 128 && value != 256 && value != 512)
+      return fail(MFEA_EINVAL, "ell_block: 64, 128, 256 or 512");
+    h->opt_ell_block = (int)value;
+  } else if (n == "ell_maxg") h->opt_ell_maxg = value;
+  else if (n == "ell_compact") { h->opt_ell_compact = value != 0; rebuild = true; }
+  else if (n == "amg_tail_rows") { h->opt_amg_tail_rows = value; rebuild = true; }
+  else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
+  else if (n == "part_slack_pct") {
+    if (value < 0 || value > 45) return fail(MFEA_EINVAL, "part_slack_pct: 0..45");
+    h->opt_part_slack = value / 100.0;
+    rebuild = true;
+  }
+  else return fail(MFEA_EINVAL, "unknown option " + n);
+  destroy_graph(h);  // captured graphs hold the old geometry
+  if (rebuild) {
+    if (!h->dirty && h->Ecount) {  // keep the current activity across the rebuild
+      RC(set_device(h));
+      RC(gather_active(h, h->active_host));
+    }
+    h->dirty = true;
+  }
   return 0;
 }
 
@@ -1900,7 +2185,6 @@ int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id
   if (h->comm) return fail(MFEA_ESTATE, "handle already joined an RCCL world");
   if (h->nparts > 1) return fail(MFEA_ESTATE, "handle holds several partitions");
   RC(set_device(h));
-  if (const char* t = std::getenv("MFEA_DIST_TIMEOUT_S")) h->dist_timeout_s = std::atof(t);
   if (world > 1) {
     ncclUniqueId u;
     std::memcpy(&u, unique_id, sizeof(u));

@@ -625,22 +625,21 @@ __global__ __launch_bounds__(kBlock) void k_rows_unpack(const int32_t* __restric
 // 6.36 at 128 (grid over all 256 CUs) and 6.54 at 64.  An in-launch grid
 // reduction by the last block (no cap, one pass per wave) was slower at C3
 // (22.5 vs 20.2 µs: its tail costs more than the passes save) and was
-// dropped.  MFEA_ELL_BS=64|128|256 overrides the block size (experiments;
-// fixed for a handle's life: its captured graphs keep their geometry).
+// dropped.  The handle's options (mfea_set_option "ell_block" 64|128|256|512,
+// "ell_maxg" — fixed for a handle's life once graphs are captured) reach the
+// launchers through EllOp.bs / EllOp.maxg.
 // ---------------------------------------------------------------------------
-int ell_block_size(int64_t) {
-  const char* e = std::getenv("MFEA_ELL_BS");
-  const int b = e ? std::atoi(e) : 0;
+int ell_block_size(const EllOp& op) {
+  const int b = op.bs;
   return (b == 64 || b == 128 || b == 512) ? b : 256;
 }
-// MFEA_ELL_MAXG caps the grid below kCgMaxG (tests: several passes per wave
-// on small systems)
-int64_t ell_grid_size(int64_t NL) {
-  const char* e = std::getenv("MFEA_ELL_MAXG");  // read per call: tests vary it
-  const int64_t c = e ? std::atoll(e) : 0;
+// op.maxg caps the grid below kCgMaxG (tests: several passes per wave on
+// small systems)
+int64_t ell_grid_size(const EllOp& op) {
+  const int64_t c = op.maxg;
   const int64_t cap = (c >= 1 && c < kCgMaxG) ? c : (int64_t)kCgMaxG;
-  const int b = ell_block_size(NL);
-  const int64_t g = (NL + b - 1) / b;
+  const int b = ell_block_size(op);
+  const int64_t g = (op.NL + b - 1) / b;
   return g < 1 ? 1 : (g > cap ? cap : g);
 }
 // partial groups of 64 each wave loads: ≥ grid / 64
@@ -666,7 +665,7 @@ void launch_ell_init(hipStream_t s, const EllOp& op, const SellOp& sop, int prec
 template <int ND, bool DIST, int BS>
 static void first_bs(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                      Slot* slots, double* part, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  const dim3 grid((unsigned)ell_grid_size(op));
   if (precond == 1)
     hipLaunchKernelGGL((k_ell_first<ND, true, DIST, BS>), grid, dim3(BS), 0, s, op, reg, v, slots,
                        part, dv);
@@ -677,7 +676,7 @@ static void first_bs(hipStream_t s, const EllOp& op, double reg, int precond, co
 template <int ND, bool DIST>
 static void first_nd(hipStream_t s, const EllOp& op, double reg, int precond, const EllVecs& v,
                      Slot* slots, double* part, const DistVecs& dv) {
-  switch (ell_block_size(op.NL)) {
+  switch (ell_block_size(op)) {
     case 64: first_bs<ND, DIST, 64>(s, op, reg, precond, v, slots, part, dv); break;
     case 128: first_bs<ND, DIST, 128>(s, op, reg, precond, v, slots, part, dv); break;
     case 512: first_bs<ND, DIST, 512>(s, op, reg, precond, v, slots, part, dv); break;
@@ -714,7 +713,7 @@ template <int ND, int PU, bool TRACE, bool DIST, int BS, bool HC>
 static void iter_launch_hc(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                            Slot* slots, const SolveState* st, double* part,
                            unsigned long long* trace, const DistVecs& dv) {
-  const dim3 grid((unsigned)ell_grid_size(op.NL));
+  const dim3 grid((unsigned)ell_grid_size(op));
   if (precond == 1)
     hipLaunchKernelGGL((k_ell_iter<ND, true, PU, TRACE, DIST, BS, HC>), grid, dim3(BS), 0, s, j, op,
                        v, slots, st, part, trace, dv);
@@ -736,7 +735,7 @@ template <int ND, bool TRACE, int BS>
 static void iter_pu(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                     const DistVecs& dv) {
-  switch (pu_of(ell_grid_size(op.NL))) {
+  switch (pu_of(ell_grid_size(op))) {
     case 1: iter_launch<ND, 1, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 2: iter_launch<ND, 2, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 4: iter_launch<ND, 4, TRACE, false, BS>(s, j, op, precond, v, slots, st, part, trace, dv); break;
@@ -749,7 +748,7 @@ template <int ND, bool TRACE>
 static void iter_bs(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                     Slot* slots, const SolveState* st, double* part, unsigned long long* trace,
                     const DistVecs& dv) {
-  switch (ell_block_size(op.NL)) {
+  switch (ell_block_size(op)) {
     case 64: iter_pu<ND, TRACE, 64>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 128: iter_pu<ND, TRACE, 128>(s, j, op, precond, v, slots, st, part, trace, dv); break;
     case 512: iter_pu<ND, TRACE, 512>(s, j, op, precond, v, slots, st, part, trace, dv); break;
@@ -761,7 +760,7 @@ template <int ND>
 static void iter_dist(hipStream_t s, int j, const EllOp& op, int precond, const EllVecs& v,
                       Slot* slots, const SolveState* st, double* part, const DistVecs& dv) {
   // the rank partial sums replace the block partials: PU unused
-  switch (ell_block_size(op.NL)) {
+  switch (ell_block_size(op)) {
     case 64: iter_launch<ND, 1, false, true, 64>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
     case 128: iter_launch<ND, 1, false, true, 128>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
     case 512: iter_launch<ND, 1, false, true, 512>(s, j, op, precond, v, slots, st, part, nullptr, dv); break;
@@ -787,8 +786,8 @@ void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const E
   }
 }
 
-void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend) {
-  switch (pu_of(ell_grid_size(NL))) {  // the partitioned iteration's grid
+void launch_psum(hipStream_t s, const EllOp& op, const double* p, double* row, double* gsend) {
+  switch (pu_of(ell_grid_size(op))) {  // the partitioned iteration's grid
     case 1: hipLaunchKernelGGL(k_psum<1>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 2: hipLaunchKernelGGL(k_psum<2>, dim3(1), dim3(64), 0, s, p, row, gsend); break;
     case 4: hipLaunchKernelGGL(k_psum<4>, dim3(1), dim3(64), 0, s, p, row, gsend); break;

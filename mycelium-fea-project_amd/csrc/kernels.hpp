@@ -170,6 +170,8 @@ struct EllOp {
   int64_t NR;                // stride of h / hM: records (+1 spare) or NL
   const uint64_t* hmask;     // [NL/64] lanes of each wave owning a halo record
   const int32_t* hbase;      // [NL/64] the wave's first record
+  int bs = 256;              // launch geometry (handle options): threads per block
+  int64_t maxg = 0;          // grid cap below kCgMaxG (0: none)
 };
 struct EllVecs {  // component c of a lane vector at [c·NL + lane], c < nd
   double* x;      // [3][NL]
@@ -210,13 +212,13 @@ void launch_ell_iter(hipStream_t s, int j, const EllOp& op, int precond, const E
                      unsigned long long* trace = nullptr, const DistVecs* dv = nullptr);
 // launch geometry of the lane CG kernels: threads per block; blocks (≤ 512,
 // their partials re-reduced by every wave of the next launch)
-int ell_block_size(int64_t NL);
-int64_t ell_grid_size(int64_t NL);
+int ell_block_size(const EllOp& op);
+int64_t ell_grid_size(const EllOp& op);
 // x of the owner lanes → row-order x (free rows)
 void launch_ell_finish(hipStream_t s, const EllOp& op, const EllVecs& v, double* x_row);
 // this partition's block partials of the iteration (parity buffer `p`, the
 // iteration kernel's grid for NL lanes) → row[0..3] and gsend[0..3]
-void launch_psum(hipStream_t s, int64_t NL, const double* p, double* row, double* gsend);
+void launch_psum(hipStream_t s, const EllOp& op, const double* p, double* row, double* gsend);
 // out[c] = Σ_{r < world} g[4r + c] in rank order
 void launch_rank_sum(hipStream_t s, const double* g, int world, double* out);
 // out[3i + c] = x[3 rows[i] + c] / x[3 rows[i] + c] = in[3i + c]

@@ -3,8 +3,9 @@
 // distribution of src/fea_petsc_parallel.cpp:169-171, 234-268.
 //
 // Nodes are cut into `world` contiguous strips along one coordinate axis
-// (1-D coordinate bisection) with equal FREE-node counts; known (grip) nodes
-// follow the strip they lie in.  Rank r owns its strip's nodes and every
+// (1-D coordinate bisection) with equal FREE-node counts, each boundary then
+// moved (by at most `slack` × the strip size) to the position crossed by the
+// fewest elements; known (grip) nodes follow the strip they lie in.  Rank r owns its strip's nodes and every
 // element with an owned endpoint (owner-computes: a cut element is assembled by
 // both sides, identically), so assembly needs no communication.  Its local
 // mesh = owned nodes + ghost nodes (the far endpoints of cut elements).
@@ -49,16 +50,18 @@ struct PartPlan {
 };
 
 // Owner rank of every node.  axis: 0 = x, 1 = y, -1 = the longer bounding-box
-// extent of x and y.  Known nodes are those in top ∪ bot.
-std::vector<int32_t> node_owner(int64_t N, const double* xyz, const std::vector<int64_t>& top,
-                                const std::vector<int64_t>& bot, int world, int axis,
-                                int* axis_used);
+// extent of x and y.  Known nodes are those in top ∪ bot.  slack: 0 = equal
+// free-node counts; s > 0 = boundaries at the fewest crossing elements within
+// ±s × nfree / world free nodes of the equal cut (clamped to 0.45).
+std::vector<int32_t> node_owner(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
+                                const std::vector<int64_t>& top, const std::vector<int64_t>& bot,
+                                int world, int axis, double slack, int* axis_used);
 
 // Builds rank `rank`'s plan.  Elements with out-of-range endpoints are
 // rejected (skip_invalid = false) or left out of every rank (true).
 std::string build_partition(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
                             bool skip_invalid, const std::vector<int64_t>& top,
                             const std::vector<int64_t>& bot, int world, int rank, int axis,
-                            PartPlan& plan);
+                            double slack, PartPlan& plan);
 
 }  // namespace mfea

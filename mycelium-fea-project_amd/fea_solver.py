@@ -45,7 +45,7 @@ GRIP_LENGTH = 1.5
 # solver settings of the device PCG (no counterpart in the direct-solve reference)
 RTOL = 1e-13
 MAX_IT = 200000
-PRECOND = _capi.PC_GAMG  # multi-partition runs use PC_JACOBI
+PRECOND = _capi.PC_GAMG  # partitioned runs: one hierarchy per partition (amg.hpp AmgHalo)
 REG = 1e-12  # src/fea_solver.py:125
 
 _engine = None
@@ -156,8 +156,6 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     eng.set_mesh(coords, e2n)
     eng.set_bc(top, bot)
     eng.set_active(None)
-    if precond is None and nparts > 1 and PRECOND == _capi.PC_GAMG:
-        precond = _capi.PC_JACOBI  # the AMG hierarchy is single-partition
     opts = _opts(rtol, max_it, precond)
 
     stress_record, active_record, disp_record, force_disp_curve, solve_times = [], [], [], [], []
@@ -233,7 +231,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     N_STEPS, DISPLACEMENT_MAX, MAX_STRAIN, REG = a.n_steps, a.disp_max, a.max_strain, a.reg
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,
-               precond={"gamg": None if a.parts > 1 else _capi.PC_GAMG, "jacobi": _capi.PC_JACOBI,
+               precond={"gamg": _capi.PC_GAMG, "jacobi": _capi.PC_JACOBI,
                         "bjacobi": _capi.PC_BLOCK_JACOBI}[a.pc],
                out_format=a.format, nparts=a.parts)
 

@@ -5,12 +5,19 @@ ImportError at import time — there is no CPU fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# mfea_set_option defaults (include/mfea_debug.h)
+DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
+                   "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
+                   "dist_timeout_ms": 60000, "part_slack_pct": 35}
+CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
+
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
 
 if not os.path.exists(LIB_PATH):
@@ -88,6 +95,7 @@ _sig = {
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
+    "mfea_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "mfea_debug_amg_info": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P, C.c_int,
                                       C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
 }
@@ -214,6 +222,21 @@ class Engine:
         """nparts partitions of the multi-GPU solve held by this handle on one
         device (mfea_debug_set_parts: the partitioned path, testable on one GPU)."""
         _check(_lib.mfea_debug_set_parts(self._h, int(nparts), int(axis)))
+
+    def set_option(self, name: str, value: int):
+        """mfea_set_option (include/mfea_debug.h): tuning / comparison knobs."""
+        _check(_lib.mfea_set_option(self._h, name.encode(), int(value)))
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Set options for a block, then restore their defaults."""
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k in kw:
+                self.set_option(k, DEFAULT_OPTIONS[k])
 
     # ---- setup --------------------------------------------------------------
     def set_material(self, E, A, I):

@@ -202,9 +202,9 @@ int64_t shim_ell(int32_t* lane_row, int32_t* row_lane, int32_t* info, uint32_t* 
 static PartPlan g_plan;
 int shim_part(int64_t N, const double* xyz, int64_t E, const int64_t* e2n, int64_t ntop,
               const int64_t* top, int64_t nbot, const int64_t* bot, int world, int rank, int axis,
-              int64_t* sizes, char* err, int errn) {
+              int64_t* sizes, char* err, int errn, double slack) {
   std::vector<int64_t> t(top, top + ntop), b(bot, bot + nbot);
-  std::string e = build_partition(N, xyz, E, e2n, false, t, b, world, rank, axis, g_plan);
+  std::string e = build_partition(N, xyz, E, e2n, false, t, b, world, rank, axis, slack, g_plan);
   if (!e.empty()) {
     std::snprintf(err, errn, "%s", e.c_str());
     return -1;

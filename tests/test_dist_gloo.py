@@ -41,7 +41,7 @@ def _shim():
     lib = C.CDLL(build_host_shim())
     lib.shim_part.restype = C.c_int
     lib.shim_part.argtypes = [C.c_int64, P, C.c_int64, P, C.c_int64, P, C.c_int64, P, C.c_int,
-                              C.c_int, C.c_int, P, C.c_char_p, C.c_int]
+                              C.c_int, C.c_int, P, C.c_char_p, C.c_int, C.c_double]
     lib.shim_part_arrays.argtypes = [P] * 12
     return lib
 
@@ -50,7 +50,7 @@ def _ptr(a):
     return a.ctypes.data_as(P)
 
 
-def build_plan(xyz, e2n, top, bot, world, rank, axis=-1):
+def build_plan(xyz, e2n, top, bot, world, rank, axis=-1, slack=0.2):
     lib = _shim()
     xyz = np.ascontiguousarray(xyz, np.float64)
     e2n = np.ascontiguousarray(e2n, np.int64)
@@ -59,7 +59,7 @@ def build_plan(xyz, e2n, top, bot, world, rank, axis=-1):
     sz = np.zeros(8, np.int64)
     err = C.create_string_buffer(256)
     rc = lib.shim_part(len(xyz), _ptr(xyz), len(e2n), _ptr(e2n), len(top), _ptr(top), len(bot),
-                       _ptr(bot), world, rank, axis, _ptr(sz), err, 256)
+                       _ptr(bot), world, rank, axis, _ptr(sz), err, 256, slack)
     assert rc == 0, err.value
     nl, el, npair, npeer, nx, nxs, nxr, _ = (int(v) for v in sz)
     p = {"node_g": np.empty(nl, np.int64), "ghost": np.empty(nl, np.uint8),
@@ -72,7 +72,37 @@ def build_plan(xyz, e2n, top, bot, world, rank, axis=-1):
                                                  "peers", "peer_cnt", "xpeers", "xsend_cnt",
                                                  "xrecv_cnt", "xsend_node", "xrecv_node")))
     p["n_pairs"] = npair
+    p["axis"] = int(sz[7])
     return p
+
+
+def test_partition_boundaries_follow_sparse_gaps():
+    """Strip boundaries move (≤ 20 % of a strip) to the fewest crossing
+    elements: on a tiled network they land in the gaps between tiles."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mycelium-fea-project_amd"))
+    from mfea import synth
+    xyz, e2n = synth.tiled_mesh(6, 2)
+    top, bot = synth.grips(xyz)
+    known = np.zeros(len(xyz), bool)
+    known[top] = known[bot] = True
+    for world, sl in ((3, 0.2), (6, 0.2), (4, 0.4)):
+        cuts = {}
+        for slack in (0.0, sl):
+            owned = [build_plan(xyz, e2n, top, bot, world, r, axis=0, slack=slack) for r in range(world)]
+            own = np.full(len(xyz), -1)
+            for r, p in enumerate(owned):
+                own[p["node_g"][p["ghost"] == 0]] = r
+            assert np.all(own >= 0)
+            nfree = np.bincount(own[~known], minlength=world)
+            if slack == 0:
+                assert nfree.max() - nfree.min() <= 1
+            else:
+                assert np.all(np.abs(nfree - (~known).sum() / world) <= slack * (~known).sum() / world + 1)
+            cuts[slack] = int(np.sum(own[e2n[:, 0]] != own[e2n[:, 1]]))
+        print(world, cuts)
+        assert cuts[sl] < cuts[0.0] / 3, (world, cuts)
 
 
 def _split(arr, cnts):

@@ -351,17 +351,11 @@ def test_c2_properties(engine):
 # layout); same algorithm, so same iterates up to summation order
 # ---------------------------------------------------------------------------
 def _solve_with(engine, kernel, dy, opts):
-    old = os.environ.get("MFEA_CG_KERNEL")
-    try:
-        os.environ["MFEA_CG_KERNEL"] = kernel  # "lanes" | "sell" (else chosen by density)
+    from mfea._capi import CG_KERNEL
+    with engine.options(cg_kernel=CG_KERNEL[kernel]):  # "lanes" | "sell" (else chosen by density)
         st = engine.solve(dy, -dy, opts)
         assert engine.info()["cg_lanes"] == (kernel == "lanes")
         return st, engine.displacement()
-    finally:
-        if old is None:
-            os.environ.pop("MFEA_CG_KERNEL", None)
-        else:
-            os.environ["MFEA_CG_KERNEL"] = old
 
 
 @pytest.mark.parametrize("precond", [0, 1])
@@ -429,28 +423,32 @@ def test_lane_kernel_high_degree_and_multiedges(engine):
     assert abs(st_l.iters - st_s.iters) <= 3
 
 
-def test_lane_kernel_natural_order_many_halos(engine, monkeypatch):
+def test_lane_kernel_natural_order_many_halos():
     """Natural (export) row order: most neighbours are out of wave, so most
     slots go through pushed halo records and groups grow helper lanes."""
-    from mfea import make_opts, synth
-    monkeypatch.setenv("MFEA_ORDER", "natural")
-    monkeypatch.setenv("MFEA_CG_KERNEL", "lanes")  # dense in lanes: default would pick SELL
+    from mfea import Engine, make_opts, synth
     xyz, e2n = synth.tiled_mesh(1, 1)
     top, bot = synth.grips(xyz)
-    engine.set_mesh(xyz, e2n)
-    engine.set_bc(top, bot)
-    engine.set_active(None)
-    engine.assemble()
-    info = engine.info()
-    assert info["cg_lanes"] == 1 and info["n_halo"] > info["n_free_nodes"] // 4
-    Uref = _direct(xyz, e2n, top, bot, 0.01)
-    st, U = _solve_with(engine, "lanes", 0.01, make_opts(rtol=1e-13, max_it=200000))
-    assert st.status == 0
-    assert rel(U, Uref) <= 1e-10
+    engine = Engine(0)
+    try:
+        engine.set_option("order", 0)
+        engine.set_option("cg_kernel", 1)  # dense in lanes: default would pick SELL
+        engine.set_mesh(xyz, e2n)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        engine.assemble()
+        info = engine.info()
+        assert info["cg_lanes"] == 1 and info["n_halo"] > info["n_free_nodes"] // 4
+        Uref = _direct(xyz, e2n, top, bot, 0.01)
+        st, U = _solve_with(engine, "lanes", 0.01, make_opts(rtol=1e-13, max_it=200000))
+        assert st.status == 0
+        assert rel(U, Uref) <= 1e-10
+    finally:
+        engine.close()
 
 
 @pytest.mark.parametrize("precond", [0, 1])
-def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
+def test_planar_lanes_bitwise_equal_3dof_lanes(engine, precond):
     """On a planar mesh the 2-DOF lanes drop z components that are exactly 0
     in every iterate: U must equal the 3-DOF lanes' U bit for bit."""
     from mfea import make_opts
@@ -458,8 +456,10 @@ def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
     engine.assemble()
     opts = make_opts(rtol=1e-10, max_it=200000, precond=precond)
     st2, U2 = _solve_with(engine, "lanes", 0.01, opts)
-    monkeypatch.setenv("MFEA_LANE_DOF", "3")
-    st3, U3 = _solve_with(engine, "lanes", 0.01, opts)
+    with engine.options(lane_dof=3):   # rebuilds the layout with 3 DOFs per node
+        engine.assemble()
+        st3, U3 = _solve_with(engine, "lanes", 0.01, opts)
+    engine.assemble()
     assert st2.status == 0 and st3.status == 0 and st2.iters == st3.iters
     assert np.array_equal(U2, U3)
     assert np.all(U2[2::3] == 0.0)
@@ -475,17 +475,17 @@ def test_planar_lanes_bitwise_equal_3dof_lanes(engine, monkeypatch, precond):
     (512, "1", 0, 0), (512, "0", 1, 0),
     # grid capped: every wave makes several passes (as at C3)
     (64, "1", 0, 5), (256, "0", 1, 3), (128, "1", 1, 2), (512, "1", 0, 2)])
-def test_lane_geometries_match_direct(monkeypatch, bs, hc, precond, maxg):
+def test_lane_geometries_match_direct(bs, hc, precond, maxg):
     """hc: compact halo records (large systems) or one record per lane; maxg
     caps the grid so every wave makes several passes."""
     from mfea import Engine, make_opts
-    monkeypatch.setenv("MFEA_ELL_BS", str(bs))
-    monkeypatch.setenv("MFEA_ELL_HC", hc)
-    monkeypatch.setenv("MFEA_ELL_MAXG", str(maxg))
-    monkeypatch.setenv("MFEA_CG_KERNEL", "lanes")
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     eng = Engine(0)
     try:
+        eng.set_option("ell_block", bs)
+        eng.set_option("ell_compact", int(hc))
+        eng.set_option("ell_maxg", maxg)
+        eng.set_option("cg_kernel", 1)
         _sim181147(eng)
         eng.assemble()
         dy = float(sysz["dy"])
@@ -504,11 +504,10 @@ def test_lane_geometries_match_direct(monkeypatch, bs, hc, precond, maxg):
         eng.close()
 
 
-def test_dense_network_runs_sell_kernel_and_matches_direct(engine, monkeypatch):
+def test_dense_network_runs_sell_kernel_and_matches_direct(engine):
     """Dense-filament networks (the C5 recipe: intra-tile chords, mean degree
     ≈ 7.5) need > 2 lanes per free row; the engine then runs the SELL kernel."""
     from mfea import make_opts, synth
-    monkeypatch.delenv("MFEA_CG_KERNEL", raising=False)
     xyz, e2n = synth.tiled_mesh(1, 1, chords=True)
     top, bot = synth.grips(xyz)
     engine.set_mesh(xyz, e2n)

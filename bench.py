@@ -229,9 +229,9 @@ def main():
             uid = [dist_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             eng.dist_init(rank, world, uid[0])
-            eng.set_partition_axis(0)
+            eng.set_partition_axis(-1)  # the min-cut px × py grid (partition.hpp)
         elif mode == "parts":
-            eng.set_parts(a.parts, 0)
+            eng.set_parts(a.parts, -1)
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
         top, bot = synth.grips(xyz)
         eng.set_material(fs.E_mod, fs.A, fs.I)
@@ -340,7 +340,7 @@ def main():
     workload = (f"{a.config}: {nx}x{ny} tiles, {n_dof} DOF, {st.n_free} free DOF, {len(e2n)} elements, "
                 f"load step {a.load_step}/40")
     if mode == "partitioned":
-        workload += f", cut into {world} x-strips (one per GPU; {a.scaling} scaling)"
+        workload += f", cut into {world} strips (min-cut grid, one per GPU; {a.scaling} scaling)"
     elif mode == "parts":
         workload += f", {a.parts} partitions on 1 GPU"
     elif mode == "replicas":

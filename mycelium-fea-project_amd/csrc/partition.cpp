@@ -8,78 +8,117 @@
 
 namespace mfea {
 
-std::vector<int32_t> node_owner(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
-                                const std::vector<int64_t>& top, const std::vector<int64_t>& bot,
-                                int world, int axis, double slack, int* axis_used) {
-  std::vector<uint8_t> known(N, 0);
-  for (int64_t t : top) known[t] = 1;
-  for (int64_t b : bot) known[b] = 1;
-  if (axis < 0) {
-    double lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
-    for (int64_t n = 0; n < N; ++n)
-      for (int c = 0; c < 2; ++c) {
-        lo[c] = std::min(lo[c], xyz[3 * n + c]);
-        hi[c] = std::max(hi[c], xyz[3 * n + c]);
-      }
-    axis = (N > 0 && hi[1] - lo[1] > hi[0] - lo[0]) ? 1 : 0;
-  }
-  if (axis_used) *axis_used = axis;
-  std::vector<int64_t> ord(N);
+namespace {
+
+// Splits the nodes `ids` into k strips along `axis`: equal FREE-node counts,
+// each boundary then moved (by at most slack × the strip size) to the sorted
+// position crossed by the fewest elements with both ends in `ids`, so cuts
+// fall in the sparse gaps of a network (between tiles) rather than through
+// its dense parts — a 1-D min-cut in the spirit of graph partitioners.
+// Block-Jacobi-type preconditioners over the strips (partitioned GAMG) need
+// this: a boundary through a dense tile costs 10-30x the CG iterations
+// (DESIGN.md §5).  Known nodes join the strip around them.  pos: scratch of
+// size N, all -1 on entry and on return.  Returns the strip of each ids[i].
+std::vector<int32_t> split_strips(const std::vector<int64_t>& ids, const double* xyz, int64_t E,
+                                  const int64_t* e2n, int64_t N, const std::vector<uint8_t>& known,
+                                  int axis, int k, double slack, std::vector<int64_t>& pos) {
+  const int64_t n = (int64_t)ids.size();
+  std::vector<int64_t> ord(n);
   std::iota(ord.begin(), ord.end(), (int64_t)0);
   std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-    const double xa = xyz[3 * a + axis], xb = xyz[3 * b + axis];
-    return xa < xb || (xa == xb && a < b);
+    const double xa = xyz[3 * ids[a] + axis], xb = xyz[3 * ids[b] + axis];
+    return xa < xb || (xa == xb && ids[a] < ids[b]);
   });
-  // free nodes in axis order: fpos[s] = sorted position of the s-th free node
-  std::vector<int64_t> fpos;
-  for (int64_t q = 0; q < N; ++q)
-    if (!known[ord[q]]) fpos.push_back(q);
+  std::vector<int32_t> strip(n, 0);
+  std::vector<int64_t> fpos;  // sorted position of the s-th free node
+  for (int64_t q = 0; q < n; ++q)
+    if (!known[ids[ord[q]]]) fpos.push_back(q);
   const int64_t nfree = (int64_t)fpos.size();
-  std::vector<int32_t> own(N, 0);
-  if (world <= 1 || nfree == 0) return own;
-  // cut[q]: elements crossing a cut between sorted positions q and q + 1
-  std::vector<int64_t> pos(N), cut(N + 1, 0);
-  for (int64_t q = 0; q < N; ++q) pos[ord[q]] = q;
+  if (k <= 1 || nfree == 0) return strip;
+  for (int64_t q = 0; q < n; ++q) pos[ids[ord[q]]] = q;
+  std::vector<int64_t> cut(n + 1, 0);  // elements crossing between q and q + 1
   for (int64_t e = 0; e < E; ++e) {
     const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    if (a < 0 || a >= N || b < 0 || b >= N || a == b) continue;
-    const int64_t lo = std::min(pos[a], pos[b]), hi = std::max(pos[a], pos[b]);
-    ++cut[lo];
-    --cut[hi];
+    if (a < 0 || a >= N || b < 0 || b >= N || a == b || pos[a] < 0 || pos[b] < 0) continue;
+    ++cut[std::min(pos[a], pos[b])];
+    --cut[std::max(pos[a], pos[b])];
   }
-  for (int64_t q = 1; q <= N; ++q) cut[q] += cut[q - 1];
-  // Strip k starts at free node s_k = ⌈k·nfree/world⌉ (equal free counts).
-  // With slack > 0 each boundary may move by up to slack × the strip size to
-  // the sorted position (between two free nodes) crossed by the fewest
-  // elements: cuts then fall in the sparse gaps of a network (between tiles)
-  // rather than through its dense parts — a 1-D min-cut in the spirit of
-  // graph partitioners.  Block-Jacobi-type preconditioners over the strips
-  // (partitioned GAMG) need this: a strip boundary through a dense tile costs
-  // 20-30x the CG iterations.
-  const double strip = (double)nfree / world;
-  const int64_t d = (int64_t)std::floor(std::min(std::max(slack, 0.0), 0.45) * strip);
-  std::vector<int64_t> qcut(world, -1);  // last sorted position of strip k-1
-  for (int k = 1; k < world; ++k) {
-    const int64_t sk = (k * nfree + world - 1) / world;
-    const int64_t q0 = fpos[std::max<int64_t>(sk - 1, 0)];  // the equal-count cut
-    int64_t best = q0;
+  for (int64_t q = 1; q <= n; ++q) cut[q] += cut[q - 1];
+  for (int64_t i : ids) pos[i] = -1;
+  const int64_t d = (int64_t)std::floor(std::min(std::max(slack, 0.0), 0.45) * ((double)nfree / k));
+  std::vector<int64_t> qcut(k, -1);  // last sorted position of strip j-1
+  for (int j = 1; j < k; ++j) {
+    const int64_t sj = (j * nfree + k - 1) / k;  // strip j starts at free node ⌈j·nfree/k⌉
+    const int64_t q0 = fpos[std::max<int64_t>(sj - 1, 0)];  // the equal-count cut
+    int64_t best = std::max(q0, qcut[j - 1] + 1);
     if (d > 0) {
-      const int64_t slo = std::max<int64_t>(sk - d, 1), shi = std::min<int64_t>(sk + d, nfree - 1);
-      const int64_t qa = std::max(fpos[slo - 1], qcut[k - 1] + 1), qb = fpos[shi] - 1;
+      const int64_t slo = std::max<int64_t>(sj - d, 1), shi = std::min<int64_t>(sj + d, nfree - 1);
+      const int64_t qa = std::max(fpos[slo - 1], qcut[j - 1] + 1), qb = fpos[shi] - 1;
       for (int64_t q = qa; q <= qb; ++q) {
         const bool fewer = cut[q] < cut[best];
         const bool tie_closer = cut[q] == cut[best] && std::llabs(q - q0) < std::llabs(best - q0);
         if (fewer || tie_closer) best = q;
       }
     }
-    qcut[k] = std::max(best, qcut[k - 1] + 1);
+    qcut[j] = best;
   }
   int32_t r = 0;
-  for (int64_t q = 0; q < N; ++q) {
-    while (r + 1 < world && q > qcut[r + 1]) ++r;
-    own[ord[q]] = r;
+  for (int64_t q = 0; q < n; ++q) {
+    while (r + 1 < k && q > qcut[r + 1]) ++r;
+    strip[ord[q]] = r;
   }
-  return own;
+  return strip;
+}
+
+int64_t cut_elements(const std::vector<int32_t>& own, int64_t E, const int64_t* e2n, int64_t N) {
+  int64_t c = 0;
+  for (int64_t e = 0; e < E; ++e) {
+    const int64_t a = e2n[2 * e], b = e2n[2 * e + 1];
+    if (a >= 0 && a < N && b >= 0 && b < N && own[a] != own[b]) ++c;
+  }
+  return c;
+}
+
+}  // namespace
+
+std::vector<int32_t> node_owner(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,
+                                const std::vector<int64_t>& top, const std::vector<int64_t>& bot,
+                                int world, int axis, double slack, int* axis_used) {
+  std::vector<uint8_t> known(N, 0);
+  for (int64_t t : top) known[t] = 1;
+  for (int64_t b : bot) known[b] = 1;
+  std::vector<int64_t> all(N), pos(N, -1);
+  std::iota(all.begin(), all.end(), (int64_t)0);
+  if (axis == 0 || axis == 1 || world <= 1) {  // strips along one axis
+    if (axis_used) *axis_used = axis < 0 ? 0 : axis;
+    return split_strips(all, xyz, E, e2n, N, known, axis < 0 ? 0 : axis, world, slack, pos);
+  }
+  // axis -1: a px × py grid (px strips along x, each cut into py along y) for
+  // every factorisation of world; the one with the fewest cut elements wins
+  // (ties: fewer x strips)
+  std::vector<int32_t> best;
+  int64_t best_cut = -1;
+  int best_px = 1;
+  for (int px = 1; px <= world; ++px) {
+    if (world % px) continue;
+    const int py = world / px;
+    const std::vector<int32_t> sx = split_strips(all, xyz, E, e2n, N, known, 0, px, slack, pos);
+    std::vector<std::vector<int64_t>> col(px);
+    for (int64_t n = 0; n < N; ++n) col[sx[n]].push_back(n);
+    std::vector<int32_t> own(N, 0);
+    for (int c = 0; c < px; ++c) {
+      const std::vector<int32_t> sy = split_strips(col[c], xyz, E, e2n, N, known, 1, py, slack, pos);
+      for (size_t i = 0; i < col[c].size(); ++i) own[col[c][i]] = c * py + sy[i];
+    }
+    const int64_t cut = cut_elements(own, E, e2n, N);
+    if (best_cut < 0 || cut < best_cut) {
+      best_cut = cut;
+      best = std::move(own);
+      best_px = px;
+    }
+  }
+  if (axis_used) *axis_used = best_px == world ? 0 : (best_px == 1 ? 1 : 2);
+  return best;
 }
 
 std::string build_partition(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,

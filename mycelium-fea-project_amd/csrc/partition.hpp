@@ -2,8 +2,9 @@
 // per mesh / BC set).  SURVEY.md §8(e); stands in for the PETSc row-block
 // distribution of src/fea_petsc_parallel.cpp:169-171, 234-268.
 //
-// Nodes are cut into `world` contiguous strips along one coordinate axis
-// (1-D coordinate bisection) with equal FREE-node counts, each boundary then
+// Nodes are cut into a px × py grid of strips (px along x, each cut into py
+// along y; the factorisation of `world` with the fewest cut elements, or 1-D
+// strips along a given axis) with equal FREE-node counts, each boundary then
 // moved (by at most `slack` × the strip size) to the position crossed by the
 // fewest elements; known (grip) nodes follow the strip they lie in.  Rank r owns its strip's nodes and every
 // element with an owned endpoint (owner-computes: a cut element is assembled by
@@ -49,8 +50,9 @@ struct PartPlan {
   std::vector<int64_t> xsend_node, xrecv_node;  // local node ids, concatenated per peer
 };
 
-// Owner rank of every node.  axis: 0 = x, 1 = y, -1 = the longer bounding-box
-// extent of x and y.  Known nodes are those in top ∪ bot.  slack: 0 = equal
+// Owner rank of every node.  axis: 0 = strips along x, 1 = along y, -1 = the
+// px × py grid with the fewest cut elements (axis_used: 0, 1, or 2 = a 2-D
+// grid).  Known nodes are those in top ∪ bot.  slack: 0 = equal
 // free-node counts; s > 0 = boundaries at the fewest crossing elements within
 // ±s × nfree / world free nodes of the equal cut (clamped to 0.45).
 std::vector<int32_t> node_owner(int64_t N, const double* xyz, int64_t E, const int64_t* e2n,

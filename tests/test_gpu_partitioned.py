@@ -79,14 +79,13 @@ def test_partitioned_gamg_matches_direct(peng, nparts, axis):
     assert st8.iters <= int(sysz["pcg_iters_1e8"]) // 4, st8.iters
 
 
-@pytest.mark.parametrize("nparts,axis", [(2, 0), (4, 0), (2, 1)])
+@pytest.mark.parametrize("nparts,axis", [(2, 0), (4, 0), (2, 1), (4, -1), (8, -1)])
 def test_partitioned_gamg_iterations_on_tiled_network(peng, engine, nparts, axis):
     """A tiled network (4×4 tiles, 340k DOF): the strip boundaries fall in the
-    gaps between tiles (partition.hpp min-cut placement) and the partitioned
-    hierarchy converges in the one-partition iteration count (±2).  (Strips
-    without a grip — 4 strips along y here — float on their stitches: the
-    block-Jacobi preconditioner has no coarse space for their rigid modes and
-    needs ≈ 200 iterations)"""
+    gaps between tiles (partition.hpp min-cut placement; axis -1 = the px × py
+    grid with the fewest cut elements) and the partitioned hierarchy converges
+    in the one-partition iteration count (±2).  (Forced 1-D strips one tile
+    row tall — 4 along y here — need ≈ 200: DESIGN.md §5.)"""
     from mfea import PC_GAMG, make_opts, synth
     xyz, e2n = synth.tiled_mesh(4, 4)
     top, bot = synth.grips(xyz)

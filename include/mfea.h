@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 5
+#define MFEA_ABI_VERSION 6
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -195,6 +195,39 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
 #define MFEA_REC_FORCE 3  /* force_displacement.csv  */
 int mfea_write_record_csv(const char* path, int style, int kind, int64_t n_rows, int64_t n_cols,
                           const double* values, const uint8_t* flags, int n_threads);
+
+/* ---- network producer (host only) ------------------------------------------- */
+/* The hyphal growth model of src/mycelium_sim_2D.cpp (main :529-588, process
+ * functions :236-414), native and multi-threaded, for networks of millions of
+ * nodes.  With mfea_grow_default_params (the reference's
+ * constants :17-33, 5×5 inoculum, 150 steps, seed 42) and snapshot_every = 1
+ * it writes byte-identical nodes.csv / elements.csv (export_geometry :477-515),
+ * mycelium_growth_stats.csv and snapshots/step_NNNN.csv to the reference
+ * binary's.  Larger networks: more inoculation sites / a larger dish / more
+ * steps (substrate_E and omega0 are totals: scale them with the area). */
+typedef struct {
+  uint64_t seed;                     /* mt19937_64 seed (:17, argv[1])              */
+  double h0, dt, lambda_angle, P_branch, c_g, D, M_cap, omega0;
+  int32_t t_steps, h0_per_point;     /* growth steps; hyphae per inoculation site   */
+  double anastomosis_tol, wall_thickness, dish_size, substrate_width, substrate_E;
+  int32_t inoc_nx, inoc_ny;          /* inoculum grid (:143-159), centred           */
+  double inoc_dist;                  /* its spacing, mm                             */
+  double voxel_size;                 /* spatial hash voxel (:553, 0.1 mm)           */
+  int32_t snapshot_every;            /* 0: none; k: step_%04d.csv every k steps      */
+  const char* snapshot_dir;          /* where the snapshots go (must exist)          */
+  int32_t verbose;                   /* 1: the reference's stderr progress lines     */
+  int32_t threads;                   /* 0: all hardware threads; results identical   */
+} mfea_grow_params;
+typedef struct mfea_grow_net mfea_grow_net;
+void mfea_grow_default_params(mfea_grow_params* p);
+int mfea_grow(const mfea_grow_params* p, mfea_grow_net** out);
+int mfea_grow_info(const mfea_grow_net* g, int64_t* n_nodes, int64_t* n_elems, int64_t* n_hyphae);
+/* xyz (3·n_nodes) as nodes.csv carries them (6 significant digits, read back);
+ * e2n (2·n_elems) 0-based node rows as elements.csv.  Either may be NULL. */
+int mfea_grow_mesh(const mfea_grow_net* g, double* xyz, int32_t* e2n);
+/* nodes.csv, elements.csv and mycelium_growth_stats.csv into dir (must exist) */
+int mfea_grow_write(const mfea_grow_net* g, const char* dir);
+void mfea_grow_free(mfea_grow_net* g);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------- */
 /* Replaces the PETSC_COMM_WORLD row-block distribution of

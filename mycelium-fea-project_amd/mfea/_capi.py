@@ -62,6 +62,20 @@ class Info(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class GrowParams(C.Structure):
+    """mfea_grow_params (include/mfea.h) — src/mycelium_sim_2D.cpp:17-33."""
+    _fields_ = [("seed", C.c_uint64),
+                ("h0", C.c_double), ("dt", C.c_double), ("lambda_angle", C.c_double),
+                ("P_branch", C.c_double), ("c_g", C.c_double), ("D", C.c_double),
+                ("M_cap", C.c_double), ("omega0", C.c_double),
+                ("t_steps", C.c_int32), ("h0_per_point", C.c_int32),
+                ("anastomosis_tol", C.c_double), ("wall_thickness", C.c_double),
+                ("dish_size", C.c_double), ("substrate_width", C.c_double), ("substrate_E", C.c_double),
+                ("inoc_nx", C.c_int32), ("inoc_ny", C.c_int32), ("inoc_dist", C.c_double),
+                ("voxel_size", C.c_double), ("snapshot_every", C.c_int32), ("snapshot_dir", C.c_char_p),
+                ("verbose", C.c_int32), ("threads", C.c_int32)]
+
+
 _P = C.c_void_p
 _sig = {
     "mfea_get_info": (C.c_int, [_P, C.POINTER(Info)]),
@@ -92,6 +106,12 @@ _sig = {
     "mfea_set_partition_axis": (C.c_int, [_P, C.c_int]),
     "mfea_write_record_csv": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _P, _P,
                                         C.c_int]),
+    "mfea_grow_default_params": (None, [C.POINTER(GrowParams)]),
+    "mfea_grow": (C.c_int, [C.POINTER(GrowParams), C.POINTER(_P)]),
+    "mfea_grow_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "mfea_grow_mesh": (C.c_int, [_P, _P, _P]),
+    "mfea_grow_write": (C.c_int, [_P, C.c_char_p]),
+    "mfea_grow_free": (None, [_P]),
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
@@ -173,6 +193,56 @@ def write_record_csv(path, style, kind, records, n_cols=None, threads=None):
     p = a.ctypes.data_as(_P) if a.size else None
     _check(_lib.mfea_write_record_csv(os.fsencode(path), int(style), int(kind), nr, nc,
                                       None if flags else p, p if flags else None, int(threads)))
+
+
+def grow_params(**kw) -> GrowParams:
+    """The reference simulator's parameters (mfea_grow_default_params), with
+    fields overridden by keyword."""
+    p = GrowParams()
+    _lib.mfea_grow_default_params(C.byref(p))
+    for k, v in kw.items():
+        if k not in dict(GrowParams._fields_):
+            raise TypeError(f"unknown growth parameter {k!r}")
+        setattr(p, k, os.fsencode(v) if k == "snapshot_dir" and v is not None else v)
+    return p
+
+
+def scaled_grow_params(scale=1.0, **kw) -> GrowParams:
+    """A scale-times larger dish (host/mfea_grow.cpp --scale): inoculum grid
+    5·scale × 5·scale at the reference's spacing, substrate and Omega0 scaled
+    by the area, everything else the reference's."""
+    p = grow_params()
+    if scale != 1.0:
+        p.dish_size *= scale
+        p.substrate_width *= scale
+        p.substrate_E *= scale * scale
+        p.omega0 *= scale * scale
+        p.inoc_nx = p.inoc_ny = int(5 * scale + 0.5)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def grow_network(params: GrowParams | None = None, out_dir=None):
+    """Run the native producer (mfea_grow).  Returns (xyz, e2n) as the
+    reference's nodes.csv / elements.csv would read back (6 significant
+    digits), and writes those files (+ mycelium_growth_stats.csv) to out_dir
+    if given."""
+    p = params if params is not None else grow_params()
+    g = _P()
+    _check(_lib.mfea_grow(C.byref(p), C.byref(g)))
+    try:
+        nn, ne, nh = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(_lib.mfea_grow_info(g, C.byref(nn), C.byref(ne), C.byref(nh)))
+        xyz = np.empty((nn.value, 3), np.float64)
+        e2n = np.empty((ne.value, 2), np.int32)
+        _check(_lib.mfea_grow_mesh(g, _ptr(xyz), _ptr(e2n)))
+        if out_dir is not None:
+            os.makedirs(out_dir, exist_ok=True)
+            _check(_lib.mfea_grow_write(g, os.fsencode(out_dir)))
+    finally:
+        _lib.mfea_grow_free(g)
+    return xyz, e2n.astype(np.int64)
 
 
 def make_opts(rtol=1e-8, atol=0.0, max_it=100000, precond=PC_JACOBI, norm=NORM_UNPRECONDITIONED,

@@ -5,8 +5,8 @@ committed as data under tests/golden/meshes/.  ``tiled_mesh(nx, ny)`` copies it
 on an nx × ny grid with 0.04 mm gaps and stitches nodes of *different* tiles
 closer than 0.1 mm with extra bar elements (KD-tree pairs, sorted), so the
 network stays one connected, grip-to-grip load path.  ``chords`` adds
-intra-tile chords between nodes 0.04–0.06 mm apart (the "dense-filament" C5
-variant).  Deterministic: no RNG anywhere.
+intra-tile chords between not-yet-joined nodes 0.04–0.053 mm apart (the
+"dense-filament" C5 variant, mean degree ≈ 4).  Deterministic: no RNG anywhere.
 """
 from __future__ import annotations
 
@@ -25,6 +25,9 @@ def load_mesh(d):
     nodes = pd.read_csv(os.path.join(d, "nodes.csv"))
     elems = pd.read_csv(os.path.join(d, "elements.csv"))
     return nodes[["x", "y", "z"]].values.astype(np.float64), elems[["n1", "n2"]].values.astype(np.int64)
+
+
+CHORD_MIN, CHORD_MAX = 0.04, 0.053  # mm, the C5 "dense-filament" chord window
 
 
 def tiled_mesh(nx=1, ny=1, gap=0.04, stitch=0.1, chords=False, base=BASE_TILE):
@@ -50,11 +53,19 @@ def tiled_mesh(nx=1, ny=1, gap=0.04, stitch=0.1, chords=False, base=BASE_TILE):
         pairs = pairs[tile[pairs[:, 0]] != tile[pairs[:, 1]]]
         extra.append(pairs)
     if chords:
+        # intra-tile chords between nodes CHORD_MIN..CHORD_MAX apart that no
+        # element joins yet (the base tile's segments are 0.05 mm long, so a
+        # plain distance window would mostly double existing elements);
+        # mean degree ≈ 4.1 ("about 4"; the base tile is 2.0)
         tr = cKDTree(xyz[:, :2])
-        pairs = tr.query_pairs(0.06, output_type="ndarray")
+        pairs = tr.query_pairs(CHORD_MAX, output_type="ndarray")
         dd = np.linalg.norm(xyz[pairs[:, 0]] - xyz[pairs[:, 1]], axis=1)
-        pairs = pairs[(dd >= 0.04) & (tile[pairs[:, 0]] == tile[pairs[:, 1]])]
-        extra.append(pairs)
+        pairs = pairs[(dd >= CHORD_MIN) & (tile[pairs[:, 0]] == tile[pairs[:, 1]])]
+        pairs = np.sort(pairs, axis=1)
+        ek = np.sort(e2n, axis=1)
+        n_all = np.int64(len(xyz))
+        joined = np.isin(pairs[:, 0] * n_all + pairs[:, 1], ek[:, 0] * n_all + ek[:, 1])
+        extra.append(pairs[~joined])
     if extra:
         ex = np.concatenate(extra)
         ex = np.sort(ex, axis=1)

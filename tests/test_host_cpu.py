@@ -164,14 +164,14 @@ def test_self_loop_elements_are_excluded():
 # ---------------------------------------------------------------------------
 def test_library_exports_every_declared_symbol():
     header = "".join(open(f).read() for f in glob.glob(os.path.join(REPO, "include", "*.h")))
-    declared = set(re.findall(r"^\s*int\s+(mfea_\w+)\s*\(", header, re.M))
+    declared = set(re.findall(r"^\s*(?:int|void)\s+(mfea_\w+)\s*\(", header, re.M))
     assert len(declared) >= 20
     lib = C.CDLL(os.path.join(PKG, "libmfea.so"))
     for name in declared:
         assert hasattr(lib, name), name
     from mfea import _capi
     assert declared == set(_capi.EXPORTED)
-    assert _capi.abi_version() == 5
+    assert _capi.abi_version() == 6
 
 
 def test_create_without_gpu_fails_cleanly():

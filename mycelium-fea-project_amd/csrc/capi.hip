@@ -559,31 +559,43 @@ EllVecs ell_vecs(Part& pt) {
 }
 
 // ---------------------------------------------------------------------------
-// Exchanges of the partitioned solve.  Over RCCL: one group of point-to-point
-// transfers on the handle's stream (the partial-sum all-gather is done with
-// send/recv pairs too, so one group per iteration carries everything).
+// Exchanges of the partitioned solve.  Over RCCL: ONE group of point-to-point
+// transfers per exchange point on the handle's stream — the neighbour
+// payloads and the 4 partial sums to every other rank (send/recv pairs, not a
+// ring all-gather: over xGMI every rank pair has its own link, so the sums
+// cost one hop instead of world − 1 ring steps).  The sums travel as copies:
+// every rank then adds the same bits in the same (rank) order — never an
+// all-reduce, whose summation order may differ per rank.  The producer of
+// gsend also writes the rank's own row of gall[q].
 // Partitions on one device: device copies on the same stream.
 // ---------------------------------------------------------------------------
+// inside an open group: gsend → row `rank` of every other rank's gall
+int sums_p2p(mfea_handle* h, const double* gsend, double* gall) {
+  for (int r = 0; r < h->world; ++r) {
+    if (r == h->rank) continue;
+    NCCLC(ncclSend(gsend, 4, ncclFloat64, r, h->comm, h->stream));
+    NCCLC(ncclRecv(gall + 4 * r, 4, ncclFloat64, r, h->comm, h->stream));
+  }
+  return 0;
+}
+
 // CG records of parity q (xs[q] → the peers' xr[q]); gather: this rank's
-// partial sums (gsend) → row `rank` of every rank's gall[q].  The sums travel
-// by all-gather (a pure copy: every rank then adds the same bits in the same
-// order), never by an all-reduce whose summation order may differ per rank.
+// partial sums (gsend) → row `rank` of every rank's gall[q]
 int xchg_records(mfea_handle* h, int q, bool gather) {
   const int64_t RW = 3 * lane_dofs(h);
   hipStream_t s = h->stream;
   if (h->world > 1) {
     Part& pt = part0(h);
     const PartPlan& pl = pt.plan;
-    if (!pl.peers.empty()) {
-      NCCLC(ncclGroupStart());
-      for (size_t i = 0; i < pl.peers.size(); ++i) {
-        const size_t n = (size_t)(pl.peer_cnt[i] * RW);
-        NCCLC(ncclSend(pt.dv.xs[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
-        NCCLC(ncclRecv(pt.dv.xr[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
-      }
-      NCCLC(ncclGroupEnd());
+    if (pl.peers.empty() && !gather) return 0;
+    NCCLC(ncclGroupStart());
+    for (size_t i = 0; i < pl.peers.size(); ++i) {
+      const size_t n = (size_t)(pl.peer_cnt[i] * RW);
+      NCCLC(ncclSend(pt.dv.xs[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
+      NCCLC(ncclRecv(pt.dv.xr[q] + pl.peer_off[i] * RW, n, ncclFloat64, pl.peers[i], h->comm, s));
     }
-    if (gather) NCCLC(ncclAllGather(pt.dv.gsend, pt.dv.gall[q], 4, ncclFloat64, h->comm, s));
+    if (gather) RC(sums_p2p(h, pt.dv.gsend, pt.dv.gall[q]));
+    NCCLC(ncclGroupEnd());
     return 0;
   }
   for (auto& a : h->parts) {
@@ -1129,7 +1141,9 @@ int xchg_sums(mfea_handle* h, int q) {
   hipStream_t s = h->stream;
   if (h->world > 1) {
     Part& pt = part0(h);
-    NCCLC(ncclAllGather(pt.dv.gsend, pt.dv.gall[q], 4, ncclFloat64, h->comm, s));
+    NCCLC(ncclGroupStart());
+    RC(sums_p2p(h, pt.dv.gsend, pt.dv.gall[q]));
+    NCCLC(ncclGroupEnd());
     return 0;
   }
   for (auto& a : h->parts)

@@ -311,29 +311,41 @@ def main():
 
     force, n_active, st = stats[-1]
     iters = st.iters
-    # ---- roofline of the dominant kernel (one CG-CG iteration launch), live
-    # HIP events on the engine's stream; algorithmic bytes per launch as in
-    # DESIGN.md §Roofline (partitioned: rank 0's partition, without exchange)
-    iter_ms = eng.profile_iteration(pc, reps=200 if pc != PC_GAMG else 50)
-    if pc == PC_GAMG:
-        ai = eng.amg_info()
-        iter_bytes = amg_iteration_bytes(ai)
-        kernel = (f"GAMG-PCG iteration ({4 * (ai['levels'] - 1) + 2} launches: update + "
-                  f"{ai['levels']}-level V-cycle + w = A u)")
-    else:
-        iter_bytes, kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
+    # ---- roofline, live HIP events on the engine's stream, algorithmic bytes
+    # per launch as in DESIGN.md §4 (partitioned: rank 0's partition, without
+    # exchange).  GAMG: `roofline` = the SpMV kernel w = A_0 u (f64, with the
+    # CG's four partial sums — the metric's SpMV and the iteration's longest
+    # launch), `roofline_iteration` = one whole PCG iteration (every launch).
+    # Jacobi: the one fused iteration kernel.
     nf = info["n_free_nodes"]
-    achieved = iter_bytes / (iter_ms * 1e-3) / 1e9
-    traffic = None
+    tj = {}
     a.traffic = a.traffic or os.path.join(REPO, "profiles", f"traffic_{a.config}.json")
     if os.path.exists(a.traffic) and mode == "1gpu":
         try:
             tj = json.load(open(a.traffic))
-            # only a profile of the same config AND the same iteration kernel
-            if tj.get("config") == a.config and kernel.split()[0] in tj.get("iter_kernel", ""):
-                traffic = tj.get("bytes_per_launch")
+            if tj.get("config") != a.config:  # only a profile of the same config
+                tj = {}
         except Exception:
-            traffic = None
+            tj = {}
+    iter_ms = eng.profile_iteration(pc, reps=200 if pc != PC_GAMG else 50)
+    if pc == PC_GAMG:
+        ai = eng.amg_info()
+        iter_bytes = amg_iteration_bytes(ai)
+        iter_kernel = (f"GAMG-PCG iteration ({4 * (ai['levels'] - 1) + 2} launches: update + "
+                       f"{ai['levels']}-level V-cycle + w = A u)")
+        spmv_ms = eng.profile_spmv(reps=100)
+        nd = ai["nd"]
+        spmv_bytes = ai["blocks"][0] * (8 * nd * nd + 4) + 3 * 8 * nd * ai["rows"][0]
+        kernel = f"k_amg_cg_w (SpMV w = A_0 u, f64 {nd}x{nd} blocks, + CG partial sums)"
+        kernel_ms, kernel_bytes = spmv_ms, spmv_bytes
+        traffic = tj.get("spmv_bytes_per_launch") if tj.get("spmv_kernel") == "k_amg_cg_w" else None
+        iter_traffic = tj.get("iteration_bytes") if tj.get("iter_kernel", "").startswith("GAMG") else None
+    else:
+        iter_bytes, iter_kernel = iteration_bytes(info, pc == PC_BLOCK_JACOBI)
+        kernel, kernel_ms, kernel_bytes = iter_kernel, iter_ms, iter_bytes
+        traffic = tj.get("bytes_per_launch") if iter_kernel.split()[0] in tj.get("iter_kernel", "") else None
+        iter_traffic = None
+    achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9
 
     parallelism = {"1gpu": "1gpu", "parts": f"parts{a.parts}@1gpu",
                    "partitioned": f"partitioned{world} (RCCL)", "replicas": f"replicas{world}"}[mode]
@@ -379,11 +391,16 @@ def main():
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBPS,
             "traffic": traffic,
-            "alg_bytes_per_launch": iter_bytes,
-            "avg_launch_us": iter_ms * 1e3,
+            "alg_bytes_per_launch": kernel_bytes,
+            "avg_launch_us": kernel_ms * 1e3,
         },
     }
     if pc == PC_GAMG:
+        ia = iter_bytes / (iter_ms * 1e-3) / 1e9
+        out["roofline_iteration"] = {
+            "kernel": iter_kernel, "bound": "hbm", "achieved": ia, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": ia / PEAK_HBM_GBPS, "traffic": iter_traffic, "alg_bytes_per_iteration": iter_bytes,
+            "avg_iteration_us": iter_ms * 1e3}
         out["amg"] = {"levels": ai["levels"], "rows": ai["rows"], "blocks": ai["blocks"],
                       "setup_pair_items": ai["pair_items"]}
     if note:

@@ -176,6 +176,10 @@ int mfea_get_info(mfea_handle* h, mfea_info* info);
  * vectors, identical work each launch) and returns the average launch duration.
  * Call after mfea_solve (it overwrites the solver state). */
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms);
+/* MFEA_PC_GAMG: the SpMV kernel alone — w = A_0 u (f64 blocks) with the CG's
+ * four partial sums — replayed `reps` times back to back as one captured
+ * graph between two HIP events; average launch duration.  After a GAMG solve. */
+int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms);
 
 /* ---- record writer (host only: needs no device, no handle) ------------------ */
 /* Writes one of the driver's end-of-run CSV records, byte-identical to the

@@ -135,6 +135,18 @@ __device__ __forceinline__ void sym_to(const double* s6, double* m) {
 
 __device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gate != kRun; }
 
+// XCD-aware block order for the gathering kernels.  Blocks are dealt
+// round-robin over the 8 XCDs (b and b + 8 share one; MI355X_MICROARCH.md),
+// each with its own L2: numbering the blocks so that every XCD's share is one
+// contiguous row range keeps the neighbour rows a wave gathers in ITS L2
+// instead of fetching the same lines into several.  A bijection on
+// [0, gridDim.x); used for speed only, nothing depends on the placement.
+__device__ __forceinline__ int64_t xcd_block() {
+  const int64_t g = gridDim.x, b = blockIdx.x;
+  const int64_t q = g >> 3, r = g & 7, x = b & 7, i = b >> 3;
+  return x * q + (x < r ? x : r) + i;
+}
+
 // slot range of the wave's slice (scalar loads, wave-uniform)
 __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
   const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));
@@ -151,11 +163,10 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
 template <int ND>
 constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
 
-template <int ND, bool SUB, class TV, class TX, class C>
-__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                         int64_t npos, int64_t base, int w,
-                                         const TX* __restrict__ x, C* y) {
-  constexpr int U = mac_unroll<ND>();
+template <int ND, int U, bool SUB, class TV, class TX, class C>
+__device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                           int64_t npos, int64_t base, int w,
+                                           const TX* __restrict__ x, C* y) {
   for (int k = 0; k < w; k += U) {
     int32_t c[U];
     int64_t q[U];
@@ -181,6 +192,17 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
           y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
     }
   }
+}
+// Slices wider than U (the restriction's rows hold ≈ 6 blocks, the coarse
+// A rows 4–9) take one step of 2U loads instead of two dependent steps of U:
+// the width is slice-uniform, so the branch is too.
+template <int ND, bool SUB, class TV, class TX, class C>
+__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                         int64_t npos, int64_t base, int w,
+                                         const TX* __restrict__ x, C* y) {
+  constexpr int U = mac_unroll<ND>();
+  if (w > U) sell_mac_u<ND, 2 * U, SUB>(col, val, npos, base, w, x, y);
+  else sell_mac_u<ND, U, SUB>(col, val, npos, base, w, x, y);
 }
 
 // o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C)
@@ -453,7 +475,7 @@ template <int ND, class TB>
 __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
                                                       const int32_t* gate) {
   if (gated(gate)) return;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const int64_t n = L.A.n;
   if (i - (threadIdx.x & 63) >= n) return;
   const int64_t ii = i < n ? i : n - 1;
@@ -469,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, const int32_t* gate) {
   if (gated(gate)) return;
-  const int64_t I = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t I = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& R = L.R;
   if (I - (threadIdx.x & 63) >= R.n) return;
   int64_t base;
@@ -489,7 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, const int32_t* gate) {
   if (gated(gate)) return;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& P = L.P;
   if (i - (threadIdx.x & 63) >= P.n) return;
   int64_t base;
@@ -506,7 +528,7 @@ template <int ND, class TB, class TE>
 __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
                                                      const int32_t* gate) {
   if (gated(gate)) return;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const int64_t n = L.A.n;
   if (i - (threadIdx.x & 63) >= n) return;
   const int64_t ii = i < n ? i : n - 1;
@@ -676,7 +698,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
-  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i - lane < cg.n; i += stride) {
+  for (int64_t i = xcd_block() * BS + threadIdx.x; i - lane < cg.n; i += stride) {
     const int64_t ii = i < cg.n ? i : cg.n - 1;
     int64_t base;
     int w;
@@ -810,11 +832,18 @@ static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBl
 // (336k rows): w 16.3 µs at 256 threads × 512 blocks (2.6 grid-stride
 // passes, 8 waves per CU), 14.9 at 1024 × 329 (but 329 blocks leave 73 CUs
 // with twice the work — the streaming update kernel went 10.7 → 15.3 µs);
-// so the update keeps 256-thread blocks and w takes 512 × 512 (16 waves per
-// CU, 1.3 passes).  Both read the w kernel's partial count, amg_w_grid.
-int amg_w_block(int64_t n) { return n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS; }
-int64_t amg_w_grid(int64_t n) {
-  const int bs = amg_w_block(n);
+// so the update keeps 256-thread blocks.  w: 768-thread blocks above 512·512
+// rows (C3: 438 blocks, one pass; same-box A/B of the whole iteration 166.6
+// vs 170.0 µs at 512 and 169.5 at 1024; C5 1786 vs 1831 vs 1784), 512 / 256
+// below.  Both read the w kernel's partial count, amg_w_grid.  cg.w_block > 0
+// overrides the choice (mfea_set_option "amg_w_block").
+int amg_w_block(const AmgCg& cg) {
+  if (cg.w_block > 0) return cg.w_block;
+  return cg.n > (int64_t)kCgMaxG * 512 ? 768 : cg.n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS;
+}
+int64_t amg_w_grid(const AmgCg& cg) {
+  const int64_t n = cg.n;
+  const int bs = amg_w_block(cg);
   const int64_t g = (n + bs - 1) / bs;
   return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
 }
@@ -898,7 +927,7 @@ void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& c
 template <int ND, int BS>
 static void w_bs(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                  double* part, const AmgDist* d) {
-  const dim3 g((unsigned)amg_w_grid(cg.n));
+  const dim3 g((unsigned)amg_w_grid(cg));
   const AmgDist dd = d ? *d : AmgDist{};
   if (d) {
     if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, true>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
@@ -911,8 +940,12 @@ static void w_bs(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgC
 template <int ND>
 static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                  double* part, const AmgDist* d) {
-  if (amg_w_block(cg.n) == 512) w_bs<ND, 512>(s, j, first, L0, cg, slots, part, d);
-  else w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part, d);
+  switch (amg_w_block(cg)) {
+    case 512: w_bs<ND, 512>(s, j, first, L0, cg, slots, part, d); break;
+    case 768: w_bs<ND, 768>(s, j, first, L0, cg, slots, part, d); break;
+    case 1024: w_bs<ND, 1024>(s, j, first, L0, cg, slots, part, d); break;
+    default: w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part, d); break;
+  }
 }
 void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
                      Slot* slots, double* part, const AmgDist* d) {
@@ -920,9 +953,9 @@ void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0
   else w_nd<3>(s, j, first, L0, cg, slots, part, d);
 }
 
-void launch_amg_gsum(hipStream_t s, int64_t n, const double* part_q, const AmgDist& d, int q) {
+void launch_amg_gsum(hipStream_t s, const AmgCg& cg, const double* part_q, const AmgDist& d, int q) {
   double* row = d.gall[q] + 4 * d.rank;
-  switch (pu_of_grid(amg_w_grid(n))) {  // the w kernel's grid = its partial count
+  switch (pu_of_grid(amg_w_grid(cg))) {  // the w kernel's grid = its partial count
     case 1: hipLaunchKernelGGL(k_amg_gsum<1>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
     case 2: hipLaunchKernelGGL(k_amg_gsum<2>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
     case 4: hipLaunchKernelGGL(k_amg_gsum<4>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
@@ -939,7 +972,7 @@ void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d)
 template <int ND, int BS, bool DIST>
 static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                    const SolveState* st, double* part, const AmgDist& d) {
-  const int64_t gw = amg_w_grid(cg.n);  // partials to reduce = the w kernel's blocks
+  const int64_t gw = amg_w_grid(cg);  // partials to reduce = the w kernel's blocks
   int64_t gu = (cg.n + BS - 1) / BS;
   gu = gu < 1 ? 1 : (gu > kCgMaxG ? kCgMaxG : gu);
   const dim3 g((unsigned)gu);

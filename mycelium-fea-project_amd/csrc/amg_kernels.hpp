@@ -57,6 +57,7 @@ struct AmgLevD {
 // CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
 struct AmgCg {
   int64_t n = 0;
+  int w_block = 0;  // w = A u kernel threads per block (0: by size)
   const int32_t* row0 = nullptr;  // level-0 row → Pattern (row-order) free row
   double* x = nullptr;
   double* p = nullptr;
@@ -106,7 +107,7 @@ void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& c
 void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0, const AmgCg& cg,
                      Slot* slots, double* part, const AmgDist* d = nullptr);
 // partitioned: this rank's block partials of parity q → gall[q] row rank, gsend
-void launch_amg_gsum(hipStream_t s, int64_t n, const double* part_q, const AmgDist& d, int q);
+void launch_amg_gsum(hipStream_t s, const AmgCg& cg, const double* part_q, const AmgDist& d, int q);
 // partitioned: u of the send rows → usend
 void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d);
 // iteration j: α, β from the partials (d: from the gathered rank sums), p s x
@@ -117,6 +118,6 @@ void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const
 // x (level-0 order, ND per row) → row-order x[3·row + c]
 void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row);
 // grid of the w kernel (its partials are re-read by the update kernel)
-int64_t amg_w_grid(int64_t n);
+int64_t amg_w_grid(const AmgCg& cg);
 
 }  // namespace mfea

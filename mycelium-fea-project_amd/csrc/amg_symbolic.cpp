@@ -282,7 +282,9 @@ std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npo
 
 }  // namespace
 
-std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan) {
+std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
+                      int max_levels) {
+  max_levels = std::max(1, std::min(max_levels, kAmgMaxLevels));
   plan = AmgPlan();
   plan.nd = nd;
   if ((int64_t)active.size() != P.n_elems) return "internal: active size mismatch";
@@ -291,6 +293,9 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   // ---- stage 1, level 0: free rows, neighbours through active free-free elements
   std::vector<LevelCsr> lv(1);
   Lists a0;  // per A_0 entry: SELL slot positions of the assembled operator
+  // level-0 natural order = the Pattern's (depth-first: hyphal chains
+  // contiguous, so a slice's gathers hit few cache lines — measured on C3,
+  // 18 B per 16-B entry vs 36 B in a Hilbert-curve order of the nodes)
   {
     Csr& A = lv[0].A;
     A.n = nf;
@@ -307,12 +312,12 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       std::stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       A.col.push_back((int32_t)i);
       a0.ptr.push_back(a0.ptr.back());
-      for (size_t k = 0; k < nb.size(); ++k) {
-        if (k == 0 || nb[k].first != nb[k - 1].first) {
-          A.col.push_back(nb[k].first);
+      for (size_t t = 0; t < nb.size(); ++t) {
+        if (t == 0 || nb[t].first != nb[t - 1].first) {
+          A.col.push_back(nb[t].first);
           a0.ptr.push_back(a0.ptr.back());
         }
-        a0.a.push_back(nb[k].second);
+        a0.a.push_back(nb[t].second);
         ++a0.ptr.back();
       }
       A.ptr.push_back((int64_t)A.col.size());
@@ -323,7 +328,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   for (int l = 0;; ++l) {
     LevelCsr& L = lv[l];
     const int64_t na = aggregate(L.A, L.agg);
-    if (na == 0 || l + 1 == kAmgMaxLevels) {
+    if (na == 0 || l + 1 == max_levels) {
       plan.capped = na > 0;  // couplings left: the coarsest block Jacobi is then inexact
       L.agg.clear();
       break;
@@ -334,14 +339,19 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     lv.emplace_back();
     lv.back().A = std::move(An);
   }
-  // ---- stage 2: row labels per level (sort key: the level's A row plus, for
-  // a coarse level, its R row — the two SELL matrices its rows index)
+  // ---- stage 2: row labels per level.  Sort key: the lengths of the level's
+  // rows in the V-cycle's SELL matrices its rows index — A plus, for a coarse
+  // level, R — then, among equal keys, the AP row (the setup's A·P product):
+  // measured on C3, level-0 P / R / AP positions 704k / 652k / 1.69M → 666k /
+  // 631k / 918k, A's unchanged.
   const int nlev = (int)lv.size();
   std::vector<std::vector<int32_t>> perm(nlev);
   for (int l = 0; l < nlev; ++l) {
     const int64_t n = lv[l].A.n;
     std::vector<int64_t> key(n);
-    for (int64_t i = 0; i < n; ++i) key[i] = lv[l].A.len(i) + (l ? lv[l - 1].R.len(i) : 0);
+    for (int64_t i = 0; i < n; ++i)
+      key[i] = 64 * (lv[l].A.len(i) + (l ? lv[l - 1].R.len(i) : 0)) +
+               (l + 1 < nlev ? lv[l].AP.len(i) : 0);
     perm[l] = sort_perm(key);
   }
   plan.row0.assign(nf, 0);

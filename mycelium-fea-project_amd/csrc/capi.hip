@@ -182,6 +182,8 @@ struct mfea_handle {
   int64_t opt_ell_maxg = 0;    // lane kernels: grid cap (0: kCgMaxG)
   bool opt_ell_compact = true; // lane kernels: compact halo records
   int64_t opt_amg_tail_rows = 2048;  // GAMG: levels of at most this many rows run in one workgroup
+  int opt_amg_max_levels = kAmgMaxLevels;  // GAMG: hierarchy depth cap
+  int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
@@ -982,6 +984,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
     pt.amg_a0_a = I(pl.a0.a);
     const int64_t nf = nlev ? pl.lev[0].A.n : 0;
     pt.amg_cg.n = nf;
+    pt.amg_cg.w_block = h->opt_amg_w_block;
     pt.amg_cg.row0 = I(pl.row0);
     pt.amg_cg.x = D((size_t)nd * nf);
     pt.amg_cg.p = D((size_t)nd * nf);
@@ -1074,7 +1077,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
   const std::vector<uint8_t>& key = dm ? local : h->act_host;
   if (pt.amg_ok && pt.amg_key == key) return 0;
   pt.amg_ok = false;
-  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg);
+  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   RC(upload_amg(h, pt));
@@ -1176,7 +1179,7 @@ int enqueue_amg_dist_iteration(mfea_handle* h, int j) {
     Part& pt = *pp;
     launch_amg_cg_w(s, pt.amg.nd, j, false, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr,
                     &pt.amg_dist);
-    launch_amg_gsum(s, pt.amg_cg.n, cg_part_buf(pt, q), pt.amg_dist, q);
+    launch_amg_gsum(s, pt.amg_cg, cg_part_buf(pt, q), pt.amg_dist, q);
   }
   HIPC(hipGetLastError());
   return xchg_sums(h, q);
@@ -1322,7 +1325,7 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
     Part& pt = *pp;
     launch_amg_cg_w(s, pt.amg.nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr,
                     &pt.amg_dist);
-    launch_amg_gsum(s, pt.amg_cg.n, cg_part_buf(pt, 0), pt.amg_dist, 0);
+    launch_amg_gsum(s, pt.amg_cg, cg_part_buf(pt, 0), pt.amg_dist, 0);
   }
   RC(xchg_sums(h, 0));
   HIPC(hipGetLastError());
@@ -2008,6 +2011,35 @@ static void launch_iter0(mfea_handle* h, int pc, unsigned long long* trace) {
                    pt.cg_part.ptr, trace);
 }
 
+int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms) {
+  if (!h || !avg_ms || reps <= 0) return fail(MFEA_EINVAL, "bad argument");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  Part& pt = part0(h);
+  if (partitioned(h) || !pt.amg_ok) return fail(MFEA_ESTATE, "profile the SpMV after a single-partition GAMG solve");
+  hipStream_t s = h->stream;
+  const int nd = pt.amg.nd;
+  hipGraph_t g;
+  hipGraphExec_t ge = nullptr;
+  HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  for (int k = 0; k < reps; ++k) launch_amg_cg_w(s, nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+  HIPC(hipStreamEndCapture(s, &g));
+  hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  HIPC(e);
+  e = hipGraphLaunch(ge, s);  // warm
+  if (e == hipSuccess) e = hipEventRecord(h->ev[0], s);
+  if (e == hipSuccess) e = hipGraphLaunch(ge, s);
+  if (e == hipSuccess) e = hipEventRecord(h->ev[1], s);
+  if (e == hipSuccess) e = hipEventSynchronize(h->ev[1]);
+  float ms = 0;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+  (void)hipGraphExecDestroy(ge);
+  HIPC(e);
+  *avg_ms = ms / reps;
+  return 0;
+}
+
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms) {
   if (!h || !avg_ms || reps <= 0) return fail(MFEA_EINVAL, "bad argument");
   RC(set_device(h));
@@ -2139,6 +2171,17 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   } else if (n == "ell_maxg") h->opt_ell_maxg = value;
   else if (n == "ell_compact") { h->opt_ell_compact = value != 0; rebuild = true; }
   else if (n == "amg_tail_rows") { h->opt_amg_tail_rows = value; rebuild = true; }
+  else if (n == "amg_max_levels") {
+    if (value < 1 || value > kAmgMaxLevels) return fail(MFEA_EINVAL, "amg_max_levels: 1..32");
+    h->opt_amg_max_levels = (int)value;
+    rebuild = true;
+  }
+  else if (n == "amg_w_block") {
+    if (value != 0 && value != 256 && value != 512 && value != 768 && value != 1024)
+      return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 768 or 1024");
+    h->opt_amg_w_block = (int)value;
+    for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
+  }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "part_slack_pct") {
     if (value < 0 || value > 45) return fail(MFEA_EINVAL, "part_slack_pct: 0..45");

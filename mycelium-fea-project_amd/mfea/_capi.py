@@ -80,6 +80,7 @@ _P = C.c_void_p
 _sig = {
     "mfea_get_info": (C.c_int, [_P, C.POINTER(Info)]),
     "mfea_profile_iteration": (C.c_int, [_P, C.c_int, C.c_int, C.POINTER(C.c_double)]),
+    "mfea_profile_spmv": (C.c_int, [_P, C.c_int, C.POINTER(C.c_double)]),
     "mfea_abi_version": (C.c_int, []),
     "mfea_last_error": (C.c_int, [C.c_char_p, C.c_size_t]),
     "mfea_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
@@ -386,6 +387,12 @@ class Engine:
         """Average duration (ms) of the fused SpMV + CG iteration kernel."""
         ms = C.c_double()
         _check(_lib.mfea_profile_iteration(self._h, int(precond), int(reps), C.byref(ms)))
+        return ms.value
+
+    def profile_spmv(self, reps=100) -> float:
+        """GAMG: average duration (ms) of the w = A_0 u kernel (mfea_profile_spmv)."""
+        ms = C.c_double()
+        _check(_lib.mfea_profile_spmv(self._h, int(reps), C.byref(ms)))
         return ms.value
 
     def trace_iteration(self, precond=PC_JACOBI, cap=1 << 16):

@@ -1,0 +1,75 @@
+"""Same-box A/B of GAMG engine options on the benchmark networks.
+
+For each config and each value of one handle option (mfea_set_option), one
+process builds the mesh once, then per option value: a warm step, `--steps`
+timed steps (HIP-event device times from mfea_stats plus host wall time), the
+iteration count, the relative residual, the V-cycle iteration time
+(mfea_profile_iteration) and U's distance to the first value's U — values are
+interleaved per round so box drift hits all of them alike.
+
+    python tools/amg_ab.py --configs C3_1M C5_10M_dense --option amg_fused --values 1 0
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "mycelium-fea-project_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", nargs="+", default=["C3_1M"])
+    ap.add_argument("--option", default="amg_fused")
+    ap.add_argument("--values", nargs="+", type=int, default=[1, 0])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=2)
+    a = ap.parse_args()
+    import fea_solver as fs
+    from mfea import PC_GAMG, Engine, make_opts, synth
+    from mfea.synth import CONFIGS
+    dy = fs.DISPLACEMENT_MAX * 20 / (fs.N_STEPS - 1)
+    opts = make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG)
+    for cfg in a.configs:
+        nx, ny = CONFIGS[cfg]
+        xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
+        top, bot = synth.grips(xyz)
+        eng = Engine(0)
+        eng.set_material(fs.E_mod, fs.A, fs.I)
+        eng.set_mesh(xyz, e2n)
+        eng.set_bc(top, bot)
+        res = {v: {"ms_step": [], "wall_ms": [], "iter_us": []} for v in a.values}
+        U0 = None
+        for rnd in range(a.rounds):
+            for v in a.values:
+                eng.set_option(a.option, v)
+                eng.set_active(None)
+                eng.step(dy, -dy, opts, fs.MAX_STRAIN)  # warm (graph capture)
+                for _ in range(a.steps):
+                    eng.set_active(None)
+                    t = time.perf_counter()
+                    _, _, st = eng.step(dy, -dy, opts, fs.MAX_STRAIN)
+                    res[v]["wall_ms"].append(1e3 * (time.perf_counter() - t))
+                    res[v]["ms_step"].append(st.t_assemble_ms + st.t_rhs_ms + st.t_solve_ms + st.t_post_ms)
+                res[v]["iter_us"].append(1e3 * eng.profile_iteration(PC_GAMG, reps=30))
+                U = eng.displacement()
+                if U0 is None:
+                    U0 = U
+                res[v].update(iters=st.iters, relres=st.relres, setup_ms=st.t_setup_ms,
+                              dU=float(np.linalg.norm(U - U0) / np.linalg.norm(U0)))
+        for v in a.values:
+            r = res[v]
+            print(json.dumps({"config": cfg, a.option: v, "iters": r["iters"], "relres": r["relres"],
+                              "dU_vs_first": r["dU"], "setup_ms": r["setup_ms"],
+                              "wall_ms_med": float(np.median(r["wall_ms"])),
+                              "dev_ms_med": float(np.median(r["ms_step"])),
+                              "iter_us": [round(x, 2) for x in r["iter_us"]]}), flush=True)
+        eng.close()
+
+
+if __name__ == "__main__":
+    main()

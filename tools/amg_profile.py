@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3_1M")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--set", nargs="*", default=[], help="engine options name=value (mfea_set_option)")
     a = ap.parse_args()
     import fea_solver as fs
     from mfea import PC_GAMG, Engine, make_opts, synth
@@ -28,6 +29,9 @@ def main():
     xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
     top, bot = synth.grips(xyz)
     eng = Engine(0)
+    for kv in a.set:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     eng.set_material(fs.E_mod, fs.A, fs.I)
     eng.set_mesh(xyz, e2n)
     eng.set_bc(top, bot)

@@ -5,7 +5,7 @@
 // the MI355X through libmfea.so (include/mfea.h).  Host C++ only: it reads the
 // CSVs, makes the C-ABI calls and writes the records.
 //
-//   mfea_petsc <results_dir> [-ksp_type cg] [-pc_type jacobi|bjacobi]
+//   mfea_petsc <results_dir> [-ksp_type cg] [-pc_type jacobi|bjacobi|gamg]
 //              [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it N]
 //              [-ksp_norm_type preconditioned|unpreconditioned]
 //              [-n_steps N] [-disp_max D] [-grip_length G] [-max_strain S]
@@ -18,8 +18,11 @@
 // (src/fea_petsc_parallel.cpp:339); here -pc_type bjacobi (the default) is the
 // exact inverse of each node's 3×3 diagonal block and jacobi is PCJACOBI.
 // Documented differences: prescribed DOFs hold exactly their value (PETSc adds
-// the 1e-12 shift to those rows too and returns x/(1+1e-12)); -pc_type
-// icc/ilu/sor/gamg and other -ksp_type are rejected.
+// the 1e-12 shift to those rows too and returns x/(1+1e-12)); -pc_type gamg
+// (the reference sweep's GAMG, src/fea_petsc_solverAndPC.cpp:330-391) is the
+// engine's SA-AMG V-cycle and stops on the unpreconditioned residual (the
+// default norm under gamg; asking for the preconditioned one is an error);
+// -pc_type icc/ilu/sor and other -ksp_type are rejected.
 #include <sys/stat.h>
 #include <sys/types.h>
 
@@ -45,6 +48,7 @@ struct Options {
   int max_it = 10000;
   int precond = MFEA_PC_BLOCK_JACOBI;
   int norm = MFEA_NORM_PRECONDITIONED;
+  bool norm_given = false;
   int n_steps = 40;              // src/fea_petsc.cpp:28
   double disp_max = 0.02;        // :29
   double max_strain = 0.018;     // :30
@@ -80,8 +84,10 @@ Options parse(int argc, char** argv) {
     } else if (a == "-pc_type") {
       if (!std::strcmp(v, "jacobi")) o.precond = MFEA_PC_JACOBI;
       else if (!std::strcmp(v, "bjacobi")) o.precond = MFEA_PC_BLOCK_JACOBI;
-      else die(std::string("-pc_type ") + v + " not supported (jacobi, bjacobi)");
+      else if (!std::strcmp(v, "gamg")) o.precond = MFEA_PC_GAMG;
+      else die(std::string("-pc_type ") + v + " not supported (jacobi, bjacobi, gamg)");
     } else if (a == "-ksp_norm_type") {
+      o.norm_given = true;
       if (!std::strcmp(v, "preconditioned")) o.norm = MFEA_NORM_PRECONDITIONED;
       else if (!std::strcmp(v, "unpreconditioned")) o.norm = MFEA_NORM_UNPRECONDITIONED;
       else die(std::string("-ksp_norm_type ") + v + " not supported");
@@ -106,6 +112,11 @@ Options parse(int argc, char** argv) {
     } else {
       die("unknown option " + a);
     }
+  }
+  if (o.precond == MFEA_PC_GAMG) {
+    if (o.norm_given && o.norm == MFEA_NORM_PRECONDITIONED)
+      die("-pc_type gamg stops on the unpreconditioned residual (-ksp_norm_type unpreconditioned)");
+    o.norm = MFEA_NORM_UNPRECONDITIONED;
   }
   if (o.n_steps < 2) die("-n_steps must be at least 2");
   return o;

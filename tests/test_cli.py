@@ -31,6 +31,8 @@ def test_cli_usage_and_bad_options():
     assert r.returncode == 1 and "cg only" in r.stderr
     r = run("x", "-bogus", "1")
     assert r.returncode == 1 and "unknown option" in r.stderr
+    r = run("x", "-pc_type", "gamg", "-ksp_norm_type", "preconditioned")
+    assert r.returncode == 1 and "unpreconditioned" in r.stderr
 
 
 def test_cli_unreadable_input(tmp_path):
@@ -75,10 +77,11 @@ def test_cli_reproduces_petsc_golden(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cli_sim181147_force_matches_python_golden(tmp_path):
+@pytest.mark.parametrize("pc", ["jacobi", "gamg"])
+def test_cli_sim181147_force_matches_python_golden(tmp_path, pc):
     d = tmp_path / "sim"
     shutil.copytree(os.path.join(GOLDEN, "meshes", "sim_20251117_181147"), d)
-    r = run(d, "-ksp_rtol", 1e-13, "-ksp_norm_type", "unpreconditioned", "-pc_type", "jacobi",
+    r = run(d, "-ksp_rtol", 1e-13, "-ksp_norm_type", "unpreconditioned", "-pc_type", pc,
             "-ksp_max_it", 200000)
     assert r.returncode == 0, r.stderr
     F = read_rt(d / "fea_results" / "force_displacement.csv").values

@@ -1192,9 +1192,22 @@ int enqueue_amg_dist_chunk(mfea_handle* h, int chunk) {
   return 0;
 }
 
+// One replayed chunk = `chunk` groups of (V-cycle j, w_j, update j+1): the
+// chunk ENDS with an update, so the last planned chunk leaves the device
+// knowing whether the solve converged and no chunk of early-exiting launches
+// is queued after the converging update (each gated launch still costs
+// ≈ 4 µs).  update 0 runs before the first chunk (solve_amg).
 void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
-  for (int j = 0; j < chunk; ++j) enqueue_amg_iteration(h, pt, j, false);
-  launch_cg_advance(h->stream, chunk, pt.slots.ptr, pt.state.ptr, pt.mirror);
+  hipStream_t s = h->stream;
+  const int nd = pt.amg.nd;
+  const AmgLevD& L0 = pt.amg_lev[0];
+  for (int j = 0; j < chunk; ++j) {
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+                      pt.amg_tail, &pt.slots.ptr[j + 1].flag);
+    launch_amg_cg_w(s, nd, j, false, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+    launch_amg_cg_update(s, nd, j + 1, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
+  }
+  launch_cg_advance(s, chunk, pt.slots.ptr, pt.state.ptr, pt.mirror, 1);
 }
 
 // hierarchy values for the current K (the per-solve numeric setup)
@@ -1230,10 +1243,14 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
                     pt.amg_tail, nullptr);
   launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+  launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
   HIPC(hipGetLastError());
   const int tag = -1000 - (int)(pt.amg_gen % 1000000);
   const bool no_graph = !h->opt_graph;
-  const int expected = std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16);
+  // the converging update is iteration `iters`; update 0 ran above, so
+  // `expected` more updates = expected / chunk chunks (drive_planned adds one
+  // for the update it assumes the chunk starts with: pass expected − 1)
+  const int expected = std::max(0, std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16) - 1);
   SolveState fin;
   int rc;
   if (no_graph) {

@@ -396,14 +396,20 @@ __global__ __launch_bounds__(kCgBS) void k_cg_iter(int j, SellOp op, CgVecs v, S
 // final state is mirrored into mapped pinned host memory (`host`), so the host
 // polls without a copy kernel; slot 0 is then poisoned so already-queued
 // chunks do nothing.
-__global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st, SolveState* host) {
+// shift 0: the chunk's updates wrote slots[1..chunk]; slots[0] = slots[chunk]
+// rolls over.  shift 1 (chunks that END with an update, amg.hip): slots[1]
+// holds the state entering the chunk and its updates wrote slots[2..chunk+1];
+// slots[1] = slots[chunk+1] rolls over.  Either way the first stopped state
+// slots[1 + j] was written by iteration base + j.
+__global__ void k_cg_advance(int chunk, int shift, Slot* slots, SolveState* st, SolveState* host) {
   if (blockIdx.x != 0) return;
   const int lane = threadIdx.x;
   if (st->done) return;
+  const int n = chunk + shift;
   int first = -1;
-  for (int j0 = 0; j0 < chunk && first < 0; j0 += 64) {
+  for (int j0 = 0; j0 < n && first < 0; j0 += 64) {
     const int j = j0 + lane;
-    const bool stop = j < chunk && slots[j + 1].flag != kRun;
+    const bool stop = j < n && slots[j + 1].flag != kRun;
     const unsigned long long m = __ballot(stop);
     if (m) first = j0 + __ffsll((long long)m) - 1;
   }
@@ -418,7 +424,7 @@ __global__ void k_cg_advance(int chunk, Slot* slots, SolveState* st, SolveState*
     *host = *st;
     return;
   }
-  slots[0] = slots[chunk];
+  slots[shift] = slots[chunk + shift];
   st->base += chunk;
 }
 
@@ -479,8 +485,8 @@ void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const C
   else iter_dispatch<false>(s, j, op, precond, v, slots, st, part, nullptr);
 }
 
-void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host) {
-  hipLaunchKernelGGL(k_cg_advance, dim3(1), dim3(64), 0, s, chunk, slots, st, host);
+void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host, int shift) {
+  hipLaunchKernelGGL(k_cg_advance, dim3(1), dim3(64), 0, s, chunk, shift, slots, st, host);
 }
 
 }  // namespace mfea

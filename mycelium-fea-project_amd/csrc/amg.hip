@@ -222,53 +222,66 @@ __device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t 
 }
 
 // C += Σ_t X[a_t]·Y[b_t] (TX: X[a_t]ᵀ·Y[b_t]) over one index list, in list
-// order, kPairU pairs' loads in flight per step (the lists are short, ≈ 2–10
-// pairs, and every pair is two dependent hops: index, then blocks)
-constexpr int kPairU = 4;
-template <int ND, bool TX>
-__device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const int32_t* __restrict__ lb, const double* __restrict__ X,
-                                         int64_t nx, const double* __restrict__ Y, int64_t ny, double* C) {
-  for (int t = t0; t < t1; t += kPairU) {
-    int32_t ia[kPairU], ib[kPairU];
+// order, U pairs' loads in flight per step (every pair is two dependent hops:
+// index, then blocks).  Lists longer than 4 take steps of 8 (the Galerkin
+// product's lists run ≈ 2–30 pairs).
+template <int ND, bool TX, int U>
+__device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __restrict__ la,
+                                           const int32_t* __restrict__ lb, const double* __restrict__ X,
+                                           const double* __restrict__ Y, double* C) {
+  for (int t = t0; t < t1; t += U) {
+    int32_t ia[U], ib[U];
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int tt = t + u < t1 ? t + u : t0;
       ia[u] = la[tt];
       ib[u] = lb[tt];
     }
-    double x[kPairU][ND * ND], y[kPairU][ND * ND];
+    double x[U][ND * ND], y[U][ND * ND];
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) {
-      bload<ND>(X, nx, ia[u], x[u]);
-      bload<ND>(Y, ny, ib[u], y[u]);
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(X, 0, ia[u], x[u]);
+      bload<ND>(Y, 0, ib[u], y[u]);
     }
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (t + u >= t1) break;
       if (TX) mtm_acc<ND>(x[u], y[u], C);
       else mm_acc<ND>(x[u], y[u], C);
     }
   }
 }
+template <int ND, bool TX>
+__device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
+                                         const int32_t* __restrict__ lb, const double* __restrict__ X,
+                                         int64_t /*nx*/, const double* __restrict__ Y, int64_t /*ny*/, double* C) {
+  if (t1 - t0 > 4) pair_sum_u<ND, TX, 8>(t0, t1, la, lb, X, Y, C);
+  else pair_sum_u<ND, TX, 4>(t0, t1, la, lb, X, Y, C);
+}
 // S += Σ_t X[a_t] over one index list, in list order
-template <int ND>
-__device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const double* __restrict__ X, int64_t nx, double* S) {
-  for (int t = t0; t < t1; t += kPairU) {
-    int32_t ia[kPairU];
+template <int ND, int U>
+__device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __restrict__ la,
+                                           const double* __restrict__ X, double* S) {
+  for (int t = t0; t < t1; t += U) {
+    int32_t ia[U];
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) ia[u] = la[t + u < t1 ? t + u : t0];
-    double x[kPairU][ND * ND];
+    for (int u = 0; u < U; ++u) ia[u] = la[t + u < t1 ? t + u : t0];
+    double x[U][ND * ND];
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) bload<ND>(X, nx, ia[u], x[u]);
+    for (int u = 0; u < U; ++u) bload<ND>(X, 0, ia[u], x[u]);
 #pragma unroll
-    for (int u = 0; u < kPairU; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (t + u >= t1) break;
 #pragma unroll
       for (int c = 0; c < ND * ND; ++c) S[c] += x[u][c];
     }
   }
+}
+template <int ND>
+__device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
+                                         const double* __restrict__ X, int64_t /*nx*/, double* S) {
+  if (t1 - t0 > 4) list_sum_u<ND, 8>(t0, t1, la, X, S);
+  else list_sum_u<ND, 4>(t0, t1, la, X, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -391,62 +404,55 @@ __global__ __launch_bounds__(kBlock) void k_amg_omega(const double* __restrict__
   }
 }
 
+// P values, one thread per (row, slot k = blockIdx.y): every slot of a row
+// in flight at once instead of one after another
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int k = blockIdx.y;
   const AmgMatD& P = L.P;
   if (i - (threadIdx.x & 63) >= P.n) return;
   int64_t base;
   int w;
   slice_of(P, i, base, w);
-  if (i >= P.n) return;
-  const double om = L.omega[0];
-  double Di[ND * ND];
+  if (i >= P.n || k >= w) return;
+  const int64_t q = base + (int64_t)k * 64;
+  const int32_t J = P.col[q];
+  if (J < 0) return;
+  double S[ND * ND], pm[ND * ND], Di[ND * ND];
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Di[c] = L.dinv[i * (ND * ND) + c];
-  const int32_t ai = L.agg[i];
-  for (int k = 0; k < w; ++k) {
-    const int64_t q = base + (int64_t)k * 64;
-    const int32_t J = P.col[q];
-    if (J < 0) continue;
-    double S[ND * ND], pm[ND * ND];
-#pragma unroll
-    for (int c = 0; c < ND * ND; ++c) {
-      S[c] = 0.0;
-      pm[c] = 0.0;
-    }
-    list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val, L.A.npos, S);
-    mm_acc<ND>(Di, S, pm);
-#pragma unroll
-    for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
-    if (J == ai) {
-#pragma unroll
-      for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
-    }
-    bstore<ND>(P.val, P.npos, q, pm);
-    bstore<ND>(P.val32, P.npos, q, pm);
+  for (int c = 0; c < ND * ND; ++c) {
+    S[c] = 0.0;
+    pm[c] = 0.0;
+    Di[c] = L.dinv[i * (ND * ND) + c];
   }
-}
-
-// R = Pᵀ (f32) in R's own SELL layout: coalesced restriction loads
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_rvals(AmgLevD L) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q >= L.R.npos || L.R.col[q] < 0) return;
-  double p[ND * ND], t[ND * ND];
-  bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
+  list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val, L.A.npos, S);
+  mm_acc<ND>(Di, S, pm);
+  const double om = L.omega[0];
 #pragma unroll
-  for (int a = 0; a < ND; ++a)
+  for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
+  if (J == L.agg[i]) {
 #pragma unroll
-    for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
-  bstore<ND>(L.R.val32, L.R.npos, q, t);
+    for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
+  }
+  bstore<ND>(P.val, P.npos, q, pm);
+  bstore<ND>(P.val32, P.npos, q, pm);
 }
 
 // One output block per thread (every SELL position of the product; pads
-// have empty lists): AP(i, J) = Σ A[a]·P[b].
+// have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q < L.R.npos && L.R.col[q] >= 0) {  // R = Pᵀ (f32) in R's own SELL layout
+    double p[ND * ND], t[ND * ND];
+    bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
+#pragma unroll
+    for (int a = 0; a < ND; ++a)
+#pragma unroll
+      for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
+    bstore<ND>(L.R.val32, L.R.npos, q, t);
+  }
   if (q >= L.AP.npos || L.AP.col[q] < 0) return;
   double C[ND * ND];
 #pragma unroll
@@ -870,9 +876,8 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
   if (!level0) hipLaunchKernelGGL((k_amg_dinv<ND, false>), g, dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
   if (L.coarsest || !N) return;
-  hipLaunchKernelGGL(k_amg_pvals<ND>, rows_grid(L.P.n), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_rvals<ND>, rows_grid(L.R.npos), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(L.AP.npos), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.n).x, (unsigned)std::max(1, L.P.wmax)), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.npos, L.R.npos)), dim3(kBlock), 0, s, L);
   hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0) {

@@ -19,6 +19,7 @@ namespace mfea {
 struct AmgMatD {
   int64_t n = 0;     // rows
   int64_t npos = 0;  // SELL positions (slot rows · 64)
+  int32_t wmax = 0;  // widest slice (host side: launch geometry)
   const int32_t* sptr = nullptr;
   const int32_t* col = nullptr;
   double* val = nullptr;   // [npos][NB2] f64 (setup; A_0 also serves the CG's w = A u)

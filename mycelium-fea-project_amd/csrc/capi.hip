@@ -931,6 +931,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
     AmgMatD m;
     m.n = S.n;
     m.npos = S.n_pos();
+    for (size_t k = 0; k + 1 < S.sptr.size(); ++k) m.wmax = std::max(m.wmax, S.sptr[k + 1] - S.sptr[k]);
     m.sptr = I(S.sptr);
     m.col = I(S.col);
     m.val = vals64 ? D((size_t)nb2 * m.npos) : nullptr;

@@ -29,12 +29,14 @@
 #include <algorithm>
 #include <array>
 #include <charconv>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <random>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "mfea.h"
@@ -120,8 +122,17 @@ struct GrowNet {
   double vs = 0.1;
   int64_t gx0 = 0, gy0 = 0, gz0 = 0, gnx = 0, gny = 0, gnz = 0;
   std::vector<int64_t> vstart, ventry;  // CSR: voxel → entries (segment ids, insertion order)
-  std::vector<std::vector<int64_t>> vextra;  // entries appended by the anastomosis pass
+  struct Geo {
+    double sx, sy, sz, ex, ey, ez;
+  };
+  std::vector<Geo> vgeo;  // each CSR entry's geometry at the rebuild, contiguous per voxel
+  double reject2 = 0;     // squared midpoint distance beyond which no entry can be within tol
+  double reject2_cur = 0; // the same for the current geometry (tips may have grown by tol)
+  std::unordered_map<int64_t, std::vector<int64_t>> vextra;  // entries appended by the anastomosis pass
   std::vector<uint8_t> vdirty;
+  std::vector<int32_t> vk, cntbuf;  // rebuild scratch: voxel per entry, per-chunk counts
+  std::vector<int64_t> hoff;        // per hypha: first position in ord (build_order)
+  std::vector<double> lenbuf;       // stats scratch
   // exported geometry
   std::vector<int64_t> node_of;  // 2 per segment in hypha-major order
   std::vector<double> nxyz;      // first-appearance coordinates
@@ -150,7 +161,8 @@ struct GrowNet {
 
   void build_order() {
     const int64_t H = (int64_t)first.size();
-    std::vector<int64_t> off(H + 1, 0);
+    std::vector<int64_t>& off = hoff;
+    off.assign(H + 1, 0);
     for (int64_t h = 0; h < H; ++h) off[h + 1] = off[h] + count[h];
     ord.resize(off[H]);
     parallel_for(H, threads, [&](int64_t lo, int64_t hi, int) {
@@ -197,11 +209,15 @@ struct GrowNet {
       if (v > cap) v = cap;
       return v;
     };
+    if ((int64_t)hoff.size() != H + 1) build_order();
     parallel_for(H, threads, [&](int64_t lo, int64_t hi, int) {
       for (int64_t h = lo; h < hi; ++h) {
-        int64_t pr = first[h];
+        const int64_t* o = ord.data() + hoff[h];
+        const int64_t cnt_h = hoff[h + 1] - hoff[h];
+        int64_t pr = o[0];
         double pr_old = I[pr], pr_len = len(pr);
-        for (int64_t s = next[pr]; s >= 0; pr = s, s = next[s]) {
+        for (int64_t k = 1; k < cnt_h; ++k) {
+          const int64_t s = o[k];
           const double s_old = I[s], s_len = len(s);
           const double denom = (s_len + pr_len) / 2.0;
           if (denom > 0.0) {
@@ -216,6 +232,7 @@ struct GrowNet {
             I[pr] = clampI(I[pr] + -adj);  // ... then (pred, −adj)
           }
           pr_old = s_old, pr_len = s_len;
+          pr = s;
         }
       }
     });
@@ -276,15 +293,15 @@ struct GrowNet {
   // :209-217 — every segment at its midpoint voxel, hypha-major order
   void rebuild_hash() {
     const int64_t n = (int64_t)ord.size();
-    std::vector<int64_t> vx(n), vy(n), vz(n);
     const int T = std::max(1, threads);
     std::vector<std::array<int64_t, 6>> ext(T, {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MIN, INT64_MIN, INT64_MIN});
     parallel_for(n, threads, [&](int64_t lo, int64_t hi, int t) {
       auto& e = ext[t];
       for (int64_t k = lo; k < hi; ++k) {
-        vox(mid(ord[k]), vx[k], vy[k], vz[k]);
-        e[0] = std::min(e[0], vx[k]), e[1] = std::min(e[1], vy[k]), e[2] = std::min(e[2], vz[k]);
-        e[3] = std::max(e[3], vx[k]), e[4] = std::max(e[4], vy[k]), e[5] = std::max(e[5], vz[k]);
+        int64_t x, y, z;
+        vox(mid(ord[k]), x, y, z);
+        e[0] = std::min(e[0], x), e[1] = std::min(e[1], y), e[2] = std::min(e[2], z);
+        e[3] = std::max(e[3], x), e[4] = std::max(e[4], y), e[5] = std::max(e[5], z);
       }
     });
     std::array<int64_t, 6> g = ext[0];
@@ -294,35 +311,79 @@ struct GrowNet {
     gnx = g[3] - g[0] + 1, gny = g[4] - g[1] + 1, gnz = g[5] - g[2] + 1;
     const int64_t NV = gnx * gny * gnz;
     // stable counting sort, chunk-parallel: chunk t's entries of voxel v go
-    // after chunks < t's entries of v
+    // after chunks < t's entries of v (chunks as parallel_for cuts them)
     const int TT = (int)std::max<int64_t>(1, std::min<int64_t>(threads, (n + 4095) / 4096));
-    std::vector<std::vector<int64_t>> cnt(TT, std::vector<int64_t>(NV, 0));
-    std::vector<int64_t> vk(n);
+    vk.resize(n);
+    cntbuf.resize((size_t)TT * NV);
+    parallel_for((int64_t)cntbuf.size(), threads, [&](int64_t lo, int64_t hi, int) {
+      std::memset(cntbuf.data() + lo, 0, (size_t)(hi - lo) * sizeof(int32_t));
+    });
     parallel_for(n, threads, [&](int64_t lo, int64_t hi, int t) {
-      auto& c = cnt[t];
+      int32_t* c = cntbuf.data() + (size_t)t * NV;
       for (int64_t k = lo; k < hi; ++k) {
-        vk[k] = vid(vx[k], vy[k], vz[k]);
+        int64_t x, y, z;
+        vox(mid(ord[k]), x, y, z);
+        vk[k] = (int32_t)vid(x, y, z);
         ++c[vk[k]];
       }
     });
-    vstart.assign(NV + 1, 0);
-    int64_t run = 0;
-    for (int64_t v = 0; v < NV; ++v) {
-      vstart[v] = run;
-      for (int t = 0; t < TT; ++t) {
-        const int64_t c = cnt[t][v];
-        cnt[t][v] = run;
-        run += c;
+    // voxel totals → starts (parallel over voxel ranges, serial scan of the
+    // range sums), then each chunk's offset inside its voxel
+    vstart.resize(NV + 1);
+    const int VT = (int)std::max<int64_t>(1, std::min<int64_t>(threads, (NV + 4095) / 4096));
+    std::vector<int64_t> rsum(VT + 1, 0);
+    parallel_for(NV, threads, [&](int64_t lo, int64_t hi, int t) {
+      int64_t acc = 0;
+      for (int64_t v = lo; v < hi; ++v) {
+        int64_t tot = 0;
+        for (int c = 0; c < TT; ++c) tot += cntbuf[(size_t)c * NV + v];
+        vstart[v] = tot;
+        acc += tot;
       }
-    }
-    vstart[NV] = run;
-    ventry.resize(n);
-    parallel_for(n, threads, [&](int64_t lo, int64_t hi, int t) {
-      auto& c = cnt[t];
-      for (int64_t k = lo; k < hi; ++k) ventry[c[vk[k]]++] = ord[k];
+      rsum[t + 1] = acc;
     });
-    vextra.assign(NV, {});
-    vdirty.assign(NV, 0);
+    for (int t = 0; t < VT; ++t) rsum[t + 1] += rsum[t];
+    parallel_for(NV, threads, [&](int64_t lo, int64_t hi, int t) {
+      int64_t run = rsum[t];
+      for (int64_t v = lo; v < hi; ++v) {
+        const int64_t tot = vstart[v];
+        vstart[v] = run;
+        for (int c = 0; c < TT; ++c) {
+          int32_t& cc = cntbuf[(size_t)c * NV + v];
+          const int32_t x = cc;
+          cc = (int32_t)(run - vstart[v]);  // offset inside the voxel
+          run += x;
+        }
+        (void)tot;
+      }
+    });
+    vstart[NV] = n;
+    ventry.resize(n);
+    vgeo.resize(n);
+    std::vector<double> lmax(T, 0.0);
+    parallel_for(n, threads, [&](int64_t lo, int64_t hi, int t) {
+      int32_t* c = cntbuf.data() + (size_t)t * NV;
+      for (int64_t k = lo; k < hi; ++k) {
+        const int64_t sgm = ord[k], at = vstart[vk[k]] + c[vk[k]]++;
+        ventry[at] = sgm;
+        vgeo[at] = Geo{sx[sgm], sy[sgm], sz[sgm], ex[sgm], ey[sgm], ez[sgm]};
+        lmax[t] = std::max(lmax[t], len(sgm));
+      }
+    });
+    // a point within tol of a segment is within L/2 + tol of its midpoint;
+    // the bound is padded far above rounding so the exact test decides
+    // every case it could accept
+    double L = 0;
+    for (double v : lmax) L = std::max(L, v);
+    const double R = 0.5 * L + p.anastomosis_tol;
+    reject2 = R * R * (1.0 + 1e-6) + 1e-18;
+    const double Rc = 0.5 * (L + 2 * p.anastomosis_tol) + p.anastomosis_tol;
+    reject2_cur = Rc * Rc * (1.0 + 1e-6) + 1e-18;
+    vextra.clear();
+    vdirty.resize(NV);
+    parallel_for(NV, threads, [&](int64_t lo, int64_t hi, int) {
+      std::memset(vdirty.data() + lo, 0, (size_t)(hi - lo));
+    });
   }
 
   // :72-82
@@ -343,7 +404,11 @@ struct GrowNet {
   // first entry of the 27 voxels around q (reference order :221-229) within
   // tol of q, skipping segment `self`; -1 if none.  extra: include the
   // entries appended during this pass.
-  int64_t search(int64_t self, V3 q, bool extra, V3* proj) const {
+  // current = false: the pre-pass state (the entries' geometry as rebuilt,
+  // contiguous); true: the segments' current geometry (after anastomoses of
+  // this pass) and the appended entries.
+  int64_t search(int64_t self, V3 q, bool current, V3* proj) const {
+    const bool extra = current;
     int64_t ix0, iy0, iz0;
     vox(q, ix0, iy0, iz0);
     for (int dx = -1; dx <= 1; ++dx)
@@ -354,13 +419,27 @@ struct GrowNet {
           for (int64_t k = vstart[v]; k < vstart[v + 1]; ++k) {
             const int64_t s = ventry[k];
             if (s == self) continue;
-            if (pseg_dist(q, S(s), Ee(s), proj) <= p.anastomosis_tol) return s;
-          }
-          if (extra)
-            for (int64_t s : vextra[v]) {
-              if (s == self) continue;
-              if (pseg_dist(q, S(s), Ee(s), proj) <= p.anastomosis_tol) return s;
+            V3 a, b;
+            if (current) {  // an anastomosed tip may have grown by up to tol
+              a = S(s), b = Ee(s);
+              const double mx = q.x - 0.5 * (a.x + b.x), my = q.y - 0.5 * (a.y + b.y), mz = q.z - 0.5 * (a.z + b.z);
+              if (mx * mx + my * my + mz * mz > reject2_cur) continue;
+            } else {
+              const Geo& g = vgeo[k];
+              a = {g.sx, g.sy, g.sz}, b = {g.ex, g.ey, g.ez};
+              const double mx = q.x - 0.5 * (a.x + b.x), my = q.y - 0.5 * (a.y + b.y), mz = q.z - 0.5 * (a.z + b.z);
+              if (mx * mx + my * my + mz * mz > reject2) continue;
             }
+            if (pseg_dist(q, a, b, proj) <= p.anastomosis_tol) return s;
+          }
+          if (extra) {
+            const auto it = vextra.find(v);
+            if (it != vextra.end())
+              for (int64_t s : it->second) {
+                if (s == self) continue;
+                if (pseg_dist(q, S(s), Ee(s), proj) <= p.anastomosis_tol) return s;
+              }
+          }
         }
     return -1;
   }
@@ -423,29 +502,31 @@ struct GrowNet {
     const int64_t nnx = std::max(gx0 + gnx - 1, ix) - nx0 + 1, nny = std::max(gy0 + gny - 1, iy) - ny0 + 1,
                   nnz = std::max(gz0 + gnz - 1, iz) - nz0 + 1;
     const int64_t NV = nnx * nny * nnz;
-    std::vector<int64_t> st2(NV + 1, 0), en2;
-    std::vector<std::vector<int64_t>> ex2(NV);
-    std::vector<uint8_t> d2(NV, 0);
-    en2.reserve(ventry.size());
     auto nid = [&](int64_t a, int64_t b, int64_t c) { return ((c - nz0) * nny + (b - ny0)) * nnx + (a - nx0); };
-    std::vector<int64_t> map(gnx * gny * gnz);
+    const int64_t NO = gnx * gny * gnz;
+    std::vector<int64_t> map(NO), inv(NV, -1);
     for (int64_t z = 0; z < gnz; ++z)
       for (int64_t y = 0; y < gny; ++y)
         for (int64_t x = 0; x < gnx; ++x) map[(z * gny + y) * gnx + x] = nid(x + gx0, y + gy0, z + gz0);
-    std::vector<int64_t> inv(NV, -1);
-    for (size_t o = 0; o < map.size(); ++o) inv[map[o]] = (int64_t)o;
+    for (int64_t o = 0; o < NO; ++o) inv[map[o]] = o;
+    std::vector<int64_t> st2(NV + 1, 0), en2;
+    std::vector<Geo> ge2;
+    std::vector<uint8_t> d2(NV, 0);
+    en2.reserve(ventry.size());
+    ge2.reserve(vgeo.size());
     for (int64_t v = 0; v < NV; ++v) {
       st2[v] = (int64_t)en2.size();
-      if (inv[v] >= 0) {
-        const int64_t o = inv[v];
-        en2.insert(en2.end(), ventry.begin() + vstart[o], ventry.begin() + vstart[o + 1]);
-        ex2[v] = std::move(vextra[o]);
-        d2[v] = vdirty[o];
-      }
+      const int64_t o = inv[v];
+      if (o < 0) continue;
+      en2.insert(en2.end(), ventry.begin() + vstart[o], ventry.begin() + vstart[o + 1]);
+      ge2.insert(ge2.end(), vgeo.begin() + vstart[o], vgeo.begin() + vstart[o + 1]);
+      d2[v] = vdirty[o];
     }
     st2[NV] = (int64_t)en2.size();
+    std::unordered_map<int64_t, std::vector<int64_t>> ex2;
+    for (auto& kv : vextra) ex2[map[kv.first]] = std::move(kv.second);
     gx0 = nx0, gy0 = ny0, gz0 = nz0, gnx = nnx, gny = nny, gnz = nnz;
-    vstart.swap(st2), ventry.swap(en2), vextra.swap(ex2), vdirty.swap(d2);
+    vstart.swap(st2), ventry.swap(en2), vgeo.swap(ge2), vextra.swap(ex2), vdirty.swap(d2);
     return vid(ix, iy, iz);
   }
 
@@ -534,13 +615,23 @@ struct GrowNet {
 
   // :429-445 + the history line of :571
   void stats_line(int step, char* line, double* total) {
-    int64_t segs = (int64_t)ord.size(), A = 0, P = 0, Sg = 0;
-    for (int64_t k = 0; k < segs; ++k) {
-      const char c = st[ord[k]];
-      A += c == 'A', P += c == 'P', Sg += c == 'S';
-    }
-    double L = 0;
-    for (int64_t k = 0; k < segs; ++k) L += len(ord[k]);
+    const int64_t segs = (int64_t)ord.size();
+    std::vector<std::array<int64_t, 3>> cnt3(std::max(1, threads), {0, 0, 0});
+    parallel_for(segs, threads, [&](int64_t lo, int64_t hi, int t) {
+      auto& c3 = cnt3[t];
+      for (int64_t k = lo; k < hi; ++k) {
+        const char c = st[ord[k]];
+        c3[0] += c == 'A', c3[1] += c == 'P', c3[2] += c == 'S';
+      }
+    });
+    int64_t A = 0, P = 0, Sg = 0;
+    for (auto& c3 : cnt3) A += c3[0], P += c3[1], Sg += c3[2];
+    lenbuf.resize(segs);
+    parallel_for(segs, threads, [&](int64_t lo, int64_t hi, int) {
+      for (int64_t k = lo; k < hi; ++k) lenbuf[k] = len(ord[k]);
+    });
+    double L = 0;  // summed serially in the reference's order (:132-137)
+    for (int64_t k = 0; k < segs; ++k) L += lenbuf[k];
     const int64_t hy = (int64_t)first.size();
     char* q = line;
     q = put_i64(q, step), *q++ = ',';
@@ -719,16 +810,31 @@ int mfea_grow(const mfea_grow_params* p, mfea_grow_net** out) {
   g->init();
   g->history = "step,hyphae,segments,active_tips,passive_tips,anastomosed,branches,total_length_mm\n";
   char line[256];
+  double tph[8] = {0};
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto lap = [&](int k, std::chrono::steady_clock::time_point& t0) {
+    const auto t1 = now();
+    tph[k] += std::chrono::duration<double>(t1 - t0).count();
+    t0 = t1;
+  };
   for (int t = 0; t < p->t_steps; ++t) {  // :561-581
+    auto t0 = now();
     g->translocate();
+    lap(0, t0);
     g->grow();
+    lap(1, t0);
     g->build_order();
     g->rebuild_hash();
+    lap(2, t0);
     g->anastomose();
+    lap(3, t0);
     g->uptake();
+    lap(4, t0);
     g->walls();
+    lap(5, t0);
     double L = 0;
     g->stats_line(t, line, &L);
+    lap(6, t0);
     g->history += line;
     if (p->snapshot_every > 0 && p->snapshot_dir && (t % p->snapshot_every == 0 || t == p->t_steps - 1)) {
       char fn[64];
@@ -747,6 +853,11 @@ int mfea_grow(const mfea_grow_params* p, mfea_grow_net** out) {
   }
   g->build_order();
   g->export_geometry();
+  if (p->verbose > 1)
+    std::fprintf(stderr,
+                 "phase s: translocate %.2f grow %.2f order+hash %.2f anastomose %.2f uptake %.2f walls %.2f "
+                 "stats %.2f\n",
+                 tph[0], tph[1], tph[2], tph[3], tph[4], tph[5], tph[6]);
   *out = g;
   return MFEA_OK;
 }

@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
     else if (a == "--snapshots") need(1), p.snapshot_every = std::atoi(argv[++i]);
     else if (a == "--threads") need(1), p.threads = std::atoi(argv[++i]);
     else if (a == "--quiet") p.verbose = 0;
+    else if (a == "--timing") p.verbose = 2;
     else if (a[0] != '-') p.seed = (unsigned)std::atoi(a.c_str());  // :531 (unsigned)atoi
     else {
       std::fprintf(stderr, "mfea_grow: unknown option %s\n", a.c_str());

@@ -134,6 +134,11 @@ __device__ __forceinline__ void sym_to(const double* s6, double* m) {
 }
 
 __device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gate != kRun; }
+// The V-cycle kernels load the gate with their first operands and test it only
+// before their stores: a test at entry puts one more dependent memory round
+// trip (≈ 1 µs: the flag was written on another XCD) in front of every launch,
+// and a gated launch (only after convergence) may read whatever it likes.
+__device__ __forceinline__ bool gate_open(const int32_t* gate) { return !gate || *gate == kRun; }
 
 // XCD-aware block order for the gathering kernels.  Blocks are dealt
 // round-robin over the 8 XCDs (b and b + 8 share one; MI355X_MICROARCH.md),
@@ -205,13 +210,15 @@ __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const 
   else sell_mac_u<ND, U, SUB>(col, val, npos, base, w, x, y);
 }
 
-// o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C)
+// o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C).  dinv_load / dinv_mul
+// split it so a kernel can issue the block's load before its gather.
 template <int ND, class TD, class C>
-__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t /*n*/, int64_t i, C s,
-                                           const C* v, C* o) {
-  C Di[ND * ND];
+__device__ __forceinline__ void dinv_load(const TD* __restrict__ dinv, int64_t i, C* Di) {
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) Di[c] = (C)dinv[i * (ND * ND) + c];
+}
+template <int ND, class C>
+__device__ __forceinline__ void dinv_mul(const C* Di, C s, const C* v, C* o) {
 #pragma unroll
   for (int a = 0; a < ND; ++a) {
     C acc = 0;
@@ -219,6 +226,13 @@ __device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t 
     for (int b = 0; b < ND; ++b) acc = fma(Di[a * ND + b], v[b], acc);
     o[a] = s * acc;
   }
+}
+template <int ND, class TD, class C>
+__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t /*n*/, int64_t i, C s,
+                                           const C* v, C* o) {
+  C Di[ND * ND];
+  dinv_load<ND>(dinv, i, Di);
+  dinv_mul<ND>(Di, s, v, o);
 }
 
 // C += Σ_t X[a_t]·Y[b_t] (TX: X[a_t]ᵀ·Y[b_t]) over one index list, in list
@@ -480,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
 template <int ND, class TB>
 __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
                                                       const int32_t* gate) {
-  if (gated(gate)) return;
+  const bool run = gate_open(gate);
   const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const int64_t n = L.A.n;
   if (i - (threadIdx.x & 63) >= n) return;
@@ -491,32 +505,35 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
   float y[ND];
   vload<ND>(b, ii, y);
   sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-  if (i < n) vstore<ND>(L.t, i, y);
+  if (i < n && run) vstore<ND>(L.t, i, y);
 }
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, const int32_t* gate) {
-  if (gated(gate)) return;
+  const bool run = gate_open(gate);
   const int64_t I = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& R = L.R;
   if (I - (threadIdx.x & 63) >= R.n) return;
   int64_t base;
   int w;
   slice_of(R, I, base, w);
+  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  float Di[ND * ND];
+  dinv_load<ND>(N.dinv32, I < R.n ? I : R.n - 1, Di);
   float bc[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
   sell_mac<ND, false>(R.col, R.val32, R.npos, base, w, L.t, bc);  // R = Pᵀ blocks
-  if (I >= R.n) return;
+  if (I >= R.n || !run) return;
   vstore<ND>(N.b, I, bc);
   float xn[ND];
-  dinv_apply<ND>(N.dinv32, N.A.n, I, N.coarsest ? 1.0f : (float)N.omega[0], bc, xn);
+  dinv_mul<ND>(Di, sc, bc, xn);
   vstore<ND>(N.x, I, xn);
 }
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, const int32_t* gate) {
-  if (gated(gate)) return;
+  const bool run = gate_open(gate);
   const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& P = L.P;
   if (i - (threadIdx.x & 63) >= P.n) return;
@@ -527,13 +544,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, co
   float x[ND];
   vload<ND>(L.x, ii, x);
   sell_mac<ND, false>(P.col, P.val32, P.npos, base, w, N.coarsest ? N.x : N.e, x);
-  if (i < P.n) vstore<ND>(L.x, i, x);
+  if (i < P.n && run) vstore<ND>(L.x, i, x);
 }
 
 template <int ND, class TB, class TE>
 __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
                                                      const int32_t* gate) {
-  if (gated(gate)) return;
+  const bool run = gate_open(gate);
   const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const int64_t n = L.A.n;
   if (i - (threadIdx.x & 63) >= n) return;
@@ -541,14 +558,16 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   int64_t base;
   int w;
   slice_of(L.A, ii, base, w);
-  float y[ND], x[ND], d[ND];
+  const float om = (float)L.omega[0];
+  float y[ND], x[ND], d[ND], Di[ND * ND];
   vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
+  dinv_load<ND>(L.dinv32, ii, Di);
   sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-  dinv_apply<ND>(L.dinv32, n, ii, (float)L.omega[0], y, d);
+  dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
-  if (i < n) vstore<ND>(e, i, x);
+  if (i < n && run) vstore<ND>(e, i, x);
 }
 
 // ---------------------------------------------------------------------------
@@ -588,14 +607,15 @@ __device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N
     int64_t base;
     int w;
     slice_of(L.R, I, base, w);
-    float bc[ND];
+    float bc[ND], Di[ND * ND];
+    dinv_load<ND>(N.dinv32, I < n ? I : n - 1, Di);
 #pragma unroll
     for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
     sell_mac<ND, false>(L.R.col, L.R.val32, L.R.npos, base, w, L.t, bc);
     if (I < n) {
       vstore<ND>(N.b, I, bc);
       float xn[ND];
-      dinv_apply<ND>(N.dinv32, N.A.n, I, sc, bc, xn);
+      dinv_mul<ND>(Di, sc, bc, xn);
       vstore<ND>(N.x, I, xn);
     }
   }
@@ -628,11 +648,12 @@ __device__ __forceinline__ void tail_post(const AmgLevD& L) {
     int64_t base;
     int w;
     slice_of(L.A, ii, base, w);
-    float y[ND], x[ND], d[ND];
+    float y[ND], x[ND], d[ND], Di[ND * ND];
     vload<ND>(L.b, ii, y);
     vload<ND>(L.x, ii, x);
+    dinv_load<ND>(L.dinv32, ii, Di);
     sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-    dinv_apply<ND>(L.dinv32, n, ii, om, y, d);
+    dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
     for (int a = 0; a < ND; ++a) x[a] += d[a];
     if (i < n) vstore<ND>(L.e, i, x);
@@ -700,7 +721,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, co
 template <int ND, bool FIRST, int BS, bool DIST>
 __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part,
                                                  AmgDist d) {
-  if (!FIRST && slots[j + 1].flag != kRun) return;
+  // the iteration's gate is tested only before the stores (gate_open)
+  const bool run = FIRST || slots[j + 1].flag == kRun;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
@@ -710,6 +732,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     int w;
     slice_of(L0.A, ii, base, w);
     double y[ND], u[ND], r[ND];
+    vload<ND>(cg.u, ii, u);  // own-row operands in flight with the gather
+    vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
     sell_mac<ND, false>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
@@ -728,9 +752,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
           for (int b = 0; b < ND; ++b) y[a] = fma(m[a * ND + b], ug[b], y[a]);
       }
     }
-    vload<ND>(cg.u, i, u);
-    vload<ND>(cg.r, i, r);
-    vstore<ND>(cg.w, i, y);
+    if (run) vstore<ND>(cg.w, i, y);
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
       acc[0] = fma(r[a], u[a], acc[0]);
@@ -739,6 +761,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
+  if (!run) return;  // grid-uniform
   store_block_partial<BS>(acc, part_buf(part, FIRST ? 0 : ((j & 1) ^ 1)));
   if (FIRST && blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;
@@ -792,19 +815,34 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
   } else {
     wave_partials<PU>(part_buf(part, j & 1), S);
   }
+  // the first pass's row operands are issued behind the partials (loads
+  // return in order: the scalars need only the partials) and are in flight
+  // while α, β are formed
+  const int64_t stride = (int64_t)gridDim.x * BS;
+  const int64_t i0 = (int64_t)blockIdx.x * BS + threadIdx.x;
+  double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
+  if (cg.n > 0) {
+    const int64_t k = i0 < cg.n ? i0 : cg.n - 1;
+    vload<ND>(cg.u, k, u);
+    vload<ND>(cg.w, k, w);
+    vload<ND>(cg.p, k, p);
+    vload<ND>(cg.s, k, s);
+    vload<ND>(cg.x, k, x);
+    vload<ND>(cg.r, k, r);
+  }
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
   cg_record(slots, j, S, cs);
   if (cs.status != kRun) return;
   const double alpha = cs.alpha, beta = cs.beta;
-  const int64_t stride = (int64_t)gridDim.x * BS;
-  for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < cg.n; i += stride) {
-    double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
-    vload<ND>(cg.u, i, u);
-    vload<ND>(cg.w, i, w);
-    vload<ND>(cg.p, i, p);
-    vload<ND>(cg.s, i, s);
-    vload<ND>(cg.x, i, x);
-    vload<ND>(cg.r, i, r);
+  for (int64_t i = i0; i < cg.n; i += stride) {
+    if (i != i0) {
+      vload<ND>(cg.u, i, u);
+      vload<ND>(cg.w, i, w);
+      vload<ND>(cg.p, i, p);
+      vload<ND>(cg.s, i, s);
+      vload<ND>(cg.x, i, x);
+      vload<ND>(cg.r, i, r);
+    }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
       p[a] = fma(beta, p[a], u[a]);

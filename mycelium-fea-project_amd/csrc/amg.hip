@@ -198,15 +198,23 @@ __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, cons
     }
   }
 }
-// Slices wider than U (the restriction's rows hold ≈ 6 blocks, the coarse
-// A rows 4–9) take one step of 2U loads instead of two dependent steps of U:
-// the width is slice-uniform, so the branch is too.
-template <int ND, bool SUB, class TV, class TX, class C>
+// Slices wider than U (the restriction's rows hold ≈ 7 blocks, the coarse
+// A rows 4–5) take one step of 2U loads instead of two dependent steps of U,
+// and with K = 3 slices wider than 2U (the restrictions reach 15–29 blocks on
+// every level) one step of 4U: every slice up to the step's width costs one
+// round trip of column loads and one of gathers.  The width is slice-uniform,
+// so the branches are too.  Each step costs registers, and a kernel's VGPR
+// count is its widest path's: the f64 SpMV, whose level-0 slices are ≤ 4 wide
+// for 98 % of the waves, stays at K = 1 (a 2U path put it at 139 VGPRs, one
+// 768-thread block per CU); the streaming level-0 kernels use K = 2; the
+// restrictions and the latency-bound coarse levels K = 3.
+template <int ND, bool SUB, int K = 2, class TV, class TX, class C>
 __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                          int64_t npos, int64_t base, int w,
                                          const TX* __restrict__ x, C* y) {
   constexpr int U = mac_unroll<ND>();
-  if (w > U) sell_mac_u<ND, 2 * U, SUB>(col, val, npos, base, w, x, y);
+  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB>(col, val, npos, base, w, x, y);
+  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB>(col, val, npos, base, w, x, y);
   else sell_mac_u<ND, U, SUB>(col, val, npos, base, w, x, y);
 }
 
@@ -491,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
 // ---------------------------------------------------------------------------
 // V-cycle (f32; level 0 reads r and writes u in f64)
 // ---------------------------------------------------------------------------
-template <int ND, class TB>
+template <int ND, class TB, int K>
 __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
                                                       const int32_t* gate) {
   const bool run = gate_open(gate);
@@ -504,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
   slice_of(L.A, ii, base, w);
   float y[ND];
   vload<ND>(b, ii, y);
-  sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   if (i < n && run) vstore<ND>(L.t, i, y);
 }
 
@@ -523,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   float bc[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
-  sell_mac<ND, false>(R.col, R.val32, R.npos, base, w, L.t, bc);  // R = Pᵀ blocks
+  sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.t, bc);  // R = Pᵀ blocks
   if (I >= R.n || !run) return;
   vstore<ND>(N.b, I, bc);
   float xn[ND];
@@ -547,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, co
   if (i < P.n && run) vstore<ND>(L.x, i, x);
 }
 
-template <int ND, class TB, class TE>
+template <int ND, class TB, class TE, int K>
 __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
                                                      const int32_t* gate) {
   const bool run = gate_open(gate);
@@ -563,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
   dinv_load<ND>(L.dinv32, ii, Di);
-  sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
@@ -736,7 +744,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    sell_mac<ND, false>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
+    sell_mac<ND, false, 1>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
     if (i >= cg.n) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
@@ -930,19 +938,19 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
   const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
   for (int l = 0; l < top; ++l) {
     if (l == 0)
-      hipLaunchKernelGGL((k_amg_resid<ND, double>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
+      hipLaunchKernelGGL((k_amg_resid<ND, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
     else
-      hipLaunchKernelGGL((k_amg_resid<ND, float>), rows_grid(lev[l].A.n), b, 0, s, lev[l], (const float*)lev[l].b, gate);
+      hipLaunchKernelGGL((k_amg_resid<ND, float, 3>), rows_grid(lev[l].A.n), b, 0, s, lev[l], (const float*)lev[l].b, gate);
     hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(lev[l + 1].A.n), b, 0, s, lev[l], lev[l + 1], gate);
   }
   if (tail > 0) hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, lev_dev, tail, nlev, gate);
   for (int l = top - 1; l >= 0; --l) {
     hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
     if (l == 0)
-      hipLaunchKernelGGL((k_amg_post<ND, double, double>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
+      hipLaunchKernelGGL((k_amg_post<ND, double, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
                          (const double*)cg.r, cg.u, gate);
     else
-      hipLaunchKernelGGL((k_amg_post<ND, float, float>), rows_grid(lev[l].A.n), b, 0, s, lev[l],
+      hipLaunchKernelGGL((k_amg_post<ND, float, float, 3>), rows_grid(lev[l].A.n), b, 0, s, lev[l],
                          (const float*)lev[l].b, lev[l].e, gate);
   }
 }

@@ -539,6 +539,125 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   vstore<ND>(N.x, I, xn);
 }
 
+// S lanes per row (S = 2, 4) for the SELL operators with wide rows: R's rows
+// hold 7–8 blocks on average and up to 29 (A below level 0: 4–5, up to 16),
+// so one lane per row issues dozens of scattered loads in sequence; here lane
+// `sub` of a row takes slots sub, sub + S, … and the S partial sums meet by a
+// fixed butterfly (deterministic).  The S lanes of a row are adjacent, so a
+// wave covers 64/S rows of one slice and each slot step reads S runs of 64/S
+// consecutive positions.  Every lane ends with the row's full sum.
+template <int ND, int S, bool SUB, class TV, class TX, class C>
+__device__ __forceinline__ void sell_mac_sub(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                             int64_t base, int w, int sub, const TX* __restrict__ x, C* y) {
+  constexpr int U = 2 * mac_unroll<ND>();
+  const int wu = (w + S - 1) / S;  // steps: the slice's, uniform
+  const int ws = w > sub ? (w - sub + S - 1) / S : 0;
+  for (int k = 0; k < wu; k += U) {
+    int32_t c[U];
+    int64_t q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q[u] = k + u < ws ? base + (int64_t)((k + u) * S + sub) * 64 : base;
+      c[u] = k + u < ws ? col[q[u]] : -1;
+    }
+    C m[U][ND * ND], xc[U][ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(val, 0, q[u], m[u]);
+      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
+#pragma unroll
+      for (int a = 0; a < ND; ++a)
+#pragma unroll
+        for (int b = 0; b < ND; ++b)
+          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < S; o <<= 1)
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] += __shfl_xor(y[a], o, 64);
+}
+
+template <int ND, int S>
+__global__ __launch_bounds__(kBlock) void k_amg_restrict_s(AmgLevD L, AmgLevD N, const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const int64_t t = xcd_block() * kBlock + threadIdx.x;
+  const AmgMatD& R = L.R;
+  const int64_t I = t / S;
+  const int sub = (int)(t % S);
+  if (I - (threadIdx.x & 63) / S >= R.n) return;  // whole wave past the end
+  const int64_t Ic = I < R.n ? I : R.n - 1;
+  int64_t base;
+  int w;
+  slice_of(R, Ic, base, w);
+  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  float Di[ND * ND], bc[ND];
+  dinv_load<ND>(N.dinv32, Ic, Di);
+#pragma unroll
+  for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
+  sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.t, bc);
+  if (I >= R.n || sub != 0 || !run) return;
+  vstore<ND>(N.b, I, bc);
+  float xn[ND];
+  dinv_mul<ND>(Di, sc, bc, xn);
+  vstore<ND>(N.x, I, xn);
+}
+
+// t = b − A x (f32 level ≥ 1) and e = x + ω D⁻¹ (b − A x) with S lanes per row
+template <int ND, int S>
+__global__ __launch_bounds__(kBlock) void k_amg_resid_s(AmgLevD L, const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const int64_t t = xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = L.A.n;
+  const int64_t i = t / S;
+  const int sub = (int)(t % S);
+  if (i - (threadIdx.x & 63) / S >= n) return;
+  const int64_t ii = i < n ? i : n - 1;
+  int64_t base;
+  int w;
+  slice_of(L.A, ii, base, w);
+  float y[ND];
+  vload<ND>(L.b, ii, y);
+  if (sub != 0) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0f;
+  }
+  sell_mac_sub<ND, S, true>(L.A.col, L.A.val32, base, w, sub, L.x, y);
+  if (i < n && sub == 0 && run) vstore<ND>(L.t, i, y);
+}
+template <int ND, int S>
+__global__ __launch_bounds__(kBlock) void k_amg_post_s(AmgLevD L, const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const int64_t t = xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = L.A.n;
+  const int64_t i = t / S;
+  const int sub = (int)(t % S);
+  if (i - (threadIdx.x & 63) / S >= n) return;
+  const int64_t ii = i < n ? i : n - 1;
+  int64_t base;
+  int w;
+  slice_of(L.A, ii, base, w);
+  const float om = (float)L.omega[0];
+  float y[ND], x[ND], d[ND], Di[ND * ND];
+  vload<ND>(L.b, ii, y);
+  vload<ND>(L.x, ii, x);
+  dinv_load<ND>(L.dinv32, ii, Di);
+  if (sub != 0) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0f;
+  }
+  sell_mac_sub<ND, S, true>(L.A.col, L.A.val32, base, w, sub, L.x, y);
+  dinv_mul<ND>(Di, om, y, d);
+#pragma unroll
+  for (int a = 0; a < ND; ++a) x[a] += d[a];
+  if (i < n && sub == 0 && run) vstore<ND>(L.e, i, x);
+}
+
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, const int32_t* gate) {
   const bool run = gate_open(gate);
@@ -931,6 +1050,42 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
   else setup_nd<3>(s, L, next, level0);
 }
 
+// lanes per row: the restriction by R's mean slice width, the f32 operators
+// below level 0 by A's (mfea_set_option "amg_restrict_lanes" / "amg_op_lanes"
+// > 0 override: 1, 2 or 4)
+static int lanes_for(const AmgMatD& M, int forced, double two, double four) {
+  if (forced > 0) return forced;
+  const double mean_w = M.n > 0 ? (double)M.npos / (double)(((M.n + 63) / 64) * 64) : 0.0;
+  return mean_w > four ? 4 : mean_w > two ? 2 : 1;
+}
+template <int ND>
+static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
+  const int64_t n = L.R.n;
+  const int S = lanes_for(L.R, L.rlanes, 2.5, 5.0);
+  const dim3 b(kBlock);
+  if (S == 4) hipLaunchKernelGGL((k_amg_restrict_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, N, gate);
+  else if (S == 2) hipLaunchKernelGGL((k_amg_restrict_s<ND, 2>), rows_grid(2 * n), b, 0, s, L, N, gate);
+  else hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(n), b, 0, s, L, N, gate);
+}
+template <int ND>
+static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t* gate) {
+  const int64_t n = L.A.n;
+  const int S = lanes_for(L.A, L.alanes, 3.5, 8.0);
+  const dim3 b(kBlock);
+  if (S == 4) {
+    if (post) hipLaunchKernelGGL((k_amg_post_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, gate);
+    else hipLaunchKernelGGL((k_amg_resid_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, gate);
+  } else if (S == 2) {
+    if (post) hipLaunchKernelGGL((k_amg_post_s<ND, 2>), rows_grid(2 * n), b, 0, s, L, gate);
+    else hipLaunchKernelGGL((k_amg_resid_s<ND, 2>), rows_grid(2 * n), b, 0, s, L, gate);
+  } else {
+    if (post)
+      hipLaunchKernelGGL((k_amg_post<ND, float, float, 3>), rows_grid(n), b, 0, s, L, (const float*)L.b, L.e, gate);
+    else
+      hipLaunchKernelGGL((k_amg_resid<ND, float, 3>), rows_grid(n), b, 0, s, L, (const float*)L.b, gate);
+  }
+}
+
 template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const AmgLevD* lev_dev,
                       int tail, const int32_t* gate) {
@@ -940,8 +1095,8 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
     if (l == 0)
       hipLaunchKernelGGL((k_amg_resid<ND, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
     else
-      hipLaunchKernelGGL((k_amg_resid<ND, float, 3>), rows_grid(lev[l].A.n), b, 0, s, lev[l], (const float*)lev[l].b, gate);
-    hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(lev[l + 1].A.n), b, 0, s, lev[l], lev[l + 1], gate);
+      launch_op<ND>(s, lev[l], false, gate);
+    launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
   }
   if (tail > 0) hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, lev_dev, tail, nlev, gate);
   for (int l = top - 1; l >= 0; --l) {
@@ -950,8 +1105,7 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
       hipLaunchKernelGGL((k_amg_post<ND, double, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
                          (const double*)cg.r, cg.u, gate);
     else
-      hipLaunchKernelGGL((k_amg_post<ND, float, float, 3>), rows_grid(lev[l].A.n), b, 0, s, lev[l],
-                         (const float*)lev[l].b, lev[l].e, gate);
+      launch_op<ND>(s, lev[l], true, gate);
   }
 }
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,

@@ -184,6 +184,8 @@ struct mfea_handle {
   int64_t opt_amg_tail_rows = 2048;  // GAMG: levels of at most this many rows run in one workgroup
   int opt_amg_max_levels = kAmgMaxLevels;  // GAMG: hierarchy depth cap
   int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
+  int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
+  int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
@@ -964,6 +966,8 @@ int upload_amg(mfea_handle* h, Part& pt) {
       d.t = F((size_t)nd * n);
       d.e = l ? F((size_t)nd * n) : nullptr;  // level 0 writes the CG's u
       d.coarsest = L.coarsest ? 1 : 0;
+      d.rlanes = h->opt_amg_rlanes;
+      d.alanes = h->opt_amg_alanes;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, true, true);
@@ -2199,6 +2203,20 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 768 or 1024");
     h->opt_amg_w_block = (int)value;
     for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
+  }
+  else if (n == "amg_restrict_lanes") {
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2 or 4");
+    h->opt_amg_rlanes = (int)value;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.rlanes = (int)value;
+  }
+  else if (n == "amg_op_lanes") {
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return fail(MFEA_EINVAL, "amg_op_lanes: 0 (by width), 1, 2 or 4");
+    h->opt_amg_alanes = (int)value;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.alanes = (int)value;
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "part_slack_pct") {

@@ -1147,6 +1147,7 @@ static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgC
                  double* part, const AmgDist* d) {
   switch (amg_w_block(cg)) {
     case 512: w_bs<ND, 512>(s, j, first, L0, cg, slots, part, d); break;
+    case 640: w_bs<ND, 640>(s, j, first, L0, cg, slots, part, d); break;
     case 768: w_bs<ND, 768>(s, j, first, L0, cg, slots, part, d); break;
     case 1024: w_bs<ND, 1024>(s, j, first, L0, cg, slots, part, d); break;
     default: w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part, d); break;

@@ -42,7 +42,7 @@ def main():
         eng.set_material(fs.E_mod, fs.A, fs.I)
         eng.set_mesh(xyz, e2n)
         eng.set_bc(top, bot)
-        res = {v: {"ms_step": [], "wall_ms": [], "iter_us": []} for v in a.values}
+        res = {v: {"ms_step": [], "wall_ms": [], "iter_us": [], "spmv_us": []} for v in a.values}
         U0 = None
         for rnd in range(a.rounds):
             for v in a.values:
@@ -56,6 +56,7 @@ def main():
                     res[v]["wall_ms"].append(1e3 * (time.perf_counter() - t))
                     res[v]["ms_step"].append(st.t_assemble_ms + st.t_rhs_ms + st.t_solve_ms + st.t_post_ms)
                 res[v]["iter_us"].append(1e3 * eng.profile_iteration(PC_GAMG, reps=30))
+                res[v]["spmv_us"].append(1e3 * eng.profile_spmv(reps=100))
                 U = eng.displacement()
                 if U0 is None:
                     U0 = U
@@ -67,7 +68,8 @@ def main():
                               "dU_vs_first": r["dU"], "setup_ms": r["setup_ms"],
                               "wall_ms_med": float(np.median(r["wall_ms"])),
                               "dev_ms_med": float(np.median(r["ms_step"])),
-                              "iter_us": [round(x, 2) for x in r["iter_us"]]}), flush=True)
+                              "iter_us": [round(x, 2) for x in r["iter_us"]],
+                              "spmv_us": [round(x, 2) for x in r["spmv_us"]]}), flush=True)
         eng.close()
 
 

@@ -55,6 +55,8 @@ def parse():
                     help="N > 1: one network cut over the GPUs, or N independent copies")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N > 1 partitioned: C3 per GPU (weak) or C3 cut N ways (strong)")
+    ap.add_argument("--device", type=int, default=None,
+                    help="HIP device of this rank (default LOCAL_RANK; rehearsal: several ranks on one GPU)")
     ap.add_argument("--parts", type=int, default=1,
                     help="1 GPU: run the partitioned solve with this many partitions on it")
     return ap.parse_args()
@@ -203,7 +205,7 @@ def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if a.device is None else a.device
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -289,7 +291,7 @@ def main():
         if dist is not None:
             import torch
             if torch.cuda.is_available():
-                torch.cuda.synchronize()
+                torch.cuda.synchronize(local)  # the engine's device, all its streams
             dist.barrier()
 
     for _ in range(a.warmup):

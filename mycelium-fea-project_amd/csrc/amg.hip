@@ -811,8 +811,8 @@ __global__ __launch_bounds__(kTailBS) void k_amg_tail(const AmgLevD* __restrict_
 // CG (f64)
 // ---------------------------------------------------------------------------
 // the V-cycle's first smoothing step x_0 = ω D⁻¹ r (f32), or — a single-level
-// hierarchy (no free-free coupling) is its own coarsest level — the exact
-// block solve u = D⁻¹ r (f64) straight into the CG's u
+// hierarchy (no free-free coupling) is its own coarsest level — the block
+// solve u = D⁻¹ r (f64, rounded to the f32 u) straight into the CG's u
 template <int ND>
 __device__ __forceinline__ void vcycle_entry(const AmgLevD& L0, const AmgCg& cg, int64_t i, const double* r) {
   if (L0.coarsest) {
@@ -1102,7 +1102,7 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
   for (int l = top - 1; l >= 0; --l) {
     hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
     if (l == 0)
-      hipLaunchKernelGGL((k_amg_post<ND, double, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
+      hipLaunchKernelGGL((k_amg_post<ND, double, float, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
                          (const double*)cg.r, cg.u, gate);
     else
       launch_op<ND>(s, lev[l], true, gate);

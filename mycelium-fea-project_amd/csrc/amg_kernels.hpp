@@ -67,7 +67,8 @@ struct AmgCg {
   double* s = nullptr;
   double* r = nullptr;  // level 0's V-cycle input
   double* w = nullptr;
-  double* u = nullptr;  // level 0's V-cycle output
+  float* u = nullptr;   // level 0's V-cycle output: the f32 cycle's values, stored
+                        // exactly (half the bytes of f64 for every gather of u)
 };
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered

@@ -996,7 +996,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
     pt.amg_cg.s = D((size_t)nd * nf);
     pt.amg_cg.w = D((size_t)nd * nf);
     pt.amg_cg.r = D((size_t)nd * nf);
-    pt.amg_cg.u = D((size_t)nd * nf);
+    pt.amg_cg.u = F((size_t)nd * nf);
   }
   HIPC(err);
   HIPC(pt.amg_lev_d.alloc(std::max(nlev, 1)));

@@ -152,3 +152,36 @@ def test_benchmark_sizes_match_direct(engine, nx, ny, chords):
         assert np.linalg.norm(A @ U[free] - b) <= 1e-12 * np.linalg.norm(b), pc
         if chords is False:
             assert np.all(U[2::3] == 0.0)  # planar: z decouples exactly
+
+
+# ---------------------------------------------------------------------------
+# V-cycle kernel variants (csrc/amg.hip): lanes per row of the restriction and
+# of the coarse operators.  Every variant converges to the direct solve.
+# ---------------------------------------------------------------------------
+def _variant_solves(engine, option, values, nx=1, ny=5):
+    from mfea import synth
+    xyz, e2n = synth.tiled_mesh(nx, ny)
+    top, bot = synth.grips(xyz)
+    engine.set_option("amg_tail_rows", 0)  # every level in its own kernels
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    out = {}
+    for v in values:
+        engine.set_option(option, v)
+        st = engine.solve(dy, -dy, _opts(1e-13))
+        assert st.status == 0, (option, v)
+        out[v] = (engine.displacement(), st.iters)
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    return out, fo.solve_system(K, known, vals)
+
+
+@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4]), ("amg_op_lanes", [1, 2, 4])])
+def test_vcycle_lane_splits_match_direct(engine, option, values):
+    out, Uref = _variant_solves(engine, option, values)
+    for v, (U, _) in out.items():
+        assert rel(U, Uref) <= 1e-10, (option, v, rel(U, Uref))
+

@@ -164,6 +164,8 @@ struct mfea_handle {
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipEvent_t ev[6] = {};
   hipEvent_t ev_setup = nullptr;
+  bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
+  bool in_step = false;        // mfea_step: the solve's end is waited for by post
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
   // host view of the element activity (single partition; keys the AMG plan):
@@ -759,10 +761,16 @@ int drive_chunks(mfea_handle* h, int chunk, int max_it, Enqueue&& enqueue, Solve
 // for `expected` iterations are queued back to back with no host wait, then
 // one chunk at a time until the device reports done.  A wrong guess costs a
 // chunk of early-exiting launches (too high) or one host round trip per
-// extra chunk (too low) — never correctness.
-template <class Enqueue>
+// extra chunk (too low) — never correctness.  `after` is queued behind every
+// batch before the host waits (the solve's epilogue: if that batch
+// converged, the stream is already past it when the host wakes; if not, the
+// next batch's copy supersedes it).
+struct NoEpilogue {
+  int operator()() const { return 0; }
+};
+template <class Enqueue, class After = NoEpilogue>
 int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&& enqueue,
-                  SolveState* out) {
+                  SolveState* out, After&& after = After{}) {
   hipStream_t s = h->stream;
   const int64_t max_chunks = (int64_t)max_it / chunk + 3;
   volatile SolveState* hs = h->h_state;
@@ -770,10 +778,12 @@ int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&&
   int64_t k = 0;
   const int64_t first = std::min<int64_t>(max_chunks, std::max(1, (expected + 1 + chunk - 1) / chunk));
   for (; k < first; ++k) RC(enqueue());
+  RC(after());
   HIPC(hipEventRecord(h->poll[0], s));
   RC(wait_event(h, h->poll[0]));
   while (!hs[0].done && k < max_chunks) {
     RC(enqueue());
+    RC(after());
     HIPC(hipEventRecord(h->poll[0], s));
     RC(wait_event(h, h->poll[0]));
     ++k;
@@ -787,20 +797,33 @@ int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&&
   return 0;
 }
 
+// device times of the last solve (its events must have completed)
+void solve_times(mfea_handle* h, mfea_stats* st) {
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+  st->t_rhs_ms = ms;
+  (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+  st->t_solve_ms = ms;
+  if (h->ev_setup_used) {
+    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev_setup);
+    st->t_setup_ms = ms;
+  }
+}
+
+// The solve's end: the status comes from the host copy of the final state
+// (drive_chunks / drive_planned waited for it); inside mfea_step the stream
+// is not waited for here — post's wait covers it and the times are read then
+// (one host round trip less per step).
 int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
   HIPC(hipEventRecord(h->ev[3], h->stream));
-  RC(wait_event(h, h->ev[3]));
+  if (!h->in_step) RC(wait_event(h, h->ev[3]));
   if (st) {
     st->iters = fin.iters;
     st->status = fin.status;
     st->bnorm = std::sqrt(fin.bb0);
     st->relres = fin.res0 > 0 ? std::sqrt(fin.res_final / fin.res0) : 0.0;
     st->n_free = 3 * h->n_free_global;
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
-    st->t_rhs_ms = ms;
-    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
-    st->t_solve_ms = ms;
+    if (!h->in_step) solve_times(h, st);
   }
   if (fin.status == -4) return fail(MFEA_EMAXIT, "PCG reached max_it without converging");
   if (fin.status == -5) return fail(MFEA_EBREAKDOWN, "PCG breakdown (p·Ap <= 0 or non-finite)");
@@ -1243,6 +1266,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   HIPC(hipEventRecord(h->ev[2], s));
   enqueue_amg_setup(h, pt, o->reg);
   HIPC(hipEventRecord(h->ev_setup, s));
+  h->ev_setup_used = true;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
   launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
@@ -1258,6 +1282,12 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const int expected = std::max(0, std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16) - 1);
   SolveState fin;
   int rc;
+  // x to row order behind every planned batch (see drive_planned)
+  auto finish = [&]() -> int {
+    launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
+    HIPC(hipGetLastError());
+    return 0;
+  };
   if (no_graph) {
     rc = drive_planned(h, chunk, o->max_it, expected,
                        [&]() -> int {
@@ -1265,7 +1295,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                          HIPC(hipGetLastError());
                          return 0;
                        },
-                       &fin);
+                       &fin, finish);
   } else {
     if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG ||
         h->graph_ell != tag) {
@@ -1286,17 +1316,12 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                          HIPC(hipGraphLaunch(h->graph, s));
                          return 0;
                        },
-                       &fin);
+                       &fin, finish);
   }
   if (rc) return rc;
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
-  launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
-  HIPC(hipGetLastError());
   rc = finish_solve(h, fin, st);
   if (st) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev_setup);
-    st->t_setup_ms = ms;
     st->amg_levels = (int32_t)pt.amg_lev.size();
     st->amg_rebuilt = rebuilt ? 1 : 0;
   }
@@ -1334,6 +1359,7 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   HIPC(hipEventRecord(h->ev[2], s));
   for (auto& pp : h->parts) enqueue_amg_setup(h, *pp, o->reg);
   HIPC(hipEventRecord(h->ev_setup, s));
+  h->ev_setup_used = true;
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const int nd = pt.amg.nd;
@@ -1399,9 +1425,6 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   HIPC(hipGetLastError());
   const int rc = finish_solve(h, fin, st);
   if (st) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, h->ev[2], h->ev_setup);
-    st->t_setup_ms = ms;
     st->amg_levels = (int32_t)p0.amg_lev.size();
     st->amg_rebuilt = rebuilt ? 1 : 0;
   }
@@ -1556,6 +1579,7 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
 
 int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
+  h->ev_setup_used = false;
   if (o->precond == MFEA_PC_GAMG)
     return partitioned(h) ? solve_amg_dist(h, dy_top, dy_bot, o, st) : solve_amg(h, dy_top, dy_bot, o, st);
   if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
@@ -1759,12 +1783,19 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   RC(assemble_impl(h, nullptr));
   // a solver failure stops the step loop here, as the reference does
   // (src/fea_petsc.cpp:346-354)
-  RC(solve_any(h, dy_top, dy_bot, &o, st));
-  RC(post_impl(h, max_strain, total_force, n_active, st));
-  if (st) {
+  h->in_step = true;
+  int rc = solve_any(h, dy_top, dy_bot, &o, st);
+  if (rc == 0) rc = post_impl(h, max_strain, total_force, n_active, st);
+  h->in_step = false;
+  if (rc) {
+    (void)sync_stream(h);
+    return rc;
+  }
+  if (st) {  // every event of the step has completed (post waited)
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
     st->t_assemble_ms = ms;
+    solve_times(h, st);
   }
   return 0;
 }

@@ -66,29 +66,33 @@ def amg_iteration_bytes(ai):
     """Algorithmic HBM bytes of one GAMG-PCG iteration: every
     launch of the iteration, each array counted once per launch.  The V-cycle
     is f32 (B = 4·ND² bytes per block, V = 4·ND per row vector), the CG f64
-    (V8 = 8·ND; A_0 in f64 for w = A u, B8 = 8·ND²) except the V-cycle output
-    u, stored f32.  Per level l (n rows, nb blocks of A_l, pb blocks of P_l =
-    R_l; level 0's b is the CG's f64 r, Vb = V8 there, V elsewhere):
-      resid    nb·(B+4) + (2V + Vb)·n              (A, x, b in; t out)
+    (V8 = 8·ND) except the V-cycle output u, stored f32.  A_0's blocks are
+    symmetric and stored as upper triangles (NS = ND(ND+1)/2 values: f64 for
+    w = A u, Bs8 = 8·NS; f32 for the level-0 V-cycle, Bs = 4·NS).  Per level l
+    (n rows, nb blocks of A_l, pb blocks of P_l = R_l; level 0's b is the
+    CG's f64 r, Vb = V8 there, V elsewhere; BA = Bs at level 0, B elsewhere):
+      resid    nb·(BA+4) + (2V + Vb)·n             (A, x, b in; t out)
       restrict pb·(B+4) + V·n + (2V + B)·n'        (Pᵀ, t in; b', x' out, D⁻¹')
       prolong  pb·(B+4) + 2V·n + V·n'              (P, x in/out, e' in)
-      post     nb·(B+4) + (2V + B + Vb)·n          (A, x, D⁻¹, b in; e out)
+      post     nb·(BA+4) + (2V + B + Vb)·n         (A, x, D⁻¹, b in; e out)
     CG: update (9·V8 + V + B + V)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀ out);
-        w      nb0·(B8+4) + (2·V8 + V)·n0          (A_0, r, u in; w out).
+        w      nb0·(Bs8+4) + (2·V8 + V)·n0         (A_0, r, u in; w out).
     """
     nd = ai["nd"]
-    B, V, B8, V8 = 4 * nd * nd, 4 * nd, 8 * nd * nd, 8 * nd
+    ns = nd * (nd + 1) // 2
+    B, V, V8, Bs, Bs8 = 4 * nd * nd, 4 * nd, 8 * nd, 4 * ns, 8 * ns
     rows, blocks, pbl = ai["rows"], ai["blocks"], ai["pblocks"]
     b = 0
     for l in range(ai["levels"] - 1):
         n, nn = rows[l], rows[l + 1]
         Vb = V8 if l == 0 else V
-        b += blocks[l] * (B + 4) + (2 * V + Vb) * n
+        BA = Bs if l == 0 else B
+        b += blocks[l] * (BA + 4) + (2 * V + Vb) * n
         b += pbl[l] * (B + 4) + V * n + (2 * V + B) * nn
         b += pbl[l] * (B + 4) + 2 * V * n + V * nn
-        b += blocks[l] * (B + 4) + (2 * V + B + Vb) * n
+        b += blocks[l] * (BA + 4) + (2 * V + B + Vb) * n
     n0 = rows[0]
-    b += (9 * V8 + V + B + V) * n0 + blocks[0] * (B8 + 4) + (2 * V8 + 4 * nd) * n0
+    b += (9 * V8 + V + B + V) * n0 + blocks[0] * (Bs8 + 4) + (2 * V8 + V) * n0
     return b
 
 
@@ -337,8 +341,8 @@ def main():
                        f"{ai['levels']}-level V-cycle + w = A u)")
         spmv_ms = eng.profile_spmv(reps=100)
         nd = ai["nd"]
-        spmv_bytes = ai["blocks"][0] * (8 * nd * nd + 4) + (2 * 8 + 4) * nd * ai["rows"][0]
-        kernel = f"k_amg_cg_w (SpMV w = A_0 u, f64 {nd}x{nd} blocks, + CG partial sums)"
+        spmv_bytes = ai["blocks"][0] * (8 * nd * (nd + 1) // 2 + 4) + (2 * 8 + 4) * nd * ai["rows"][0]
+        kernel = f"k_amg_cg_w (SpMV w = A_0 u, f64 symmetric {nd}x{nd} blocks, + CG partial sums)"
         kernel_ms, kernel_bytes = spmv_ms, spmv_bytes
         traffic = tj.get("spmv_bytes_per_launch") if tj.get("spmv_kernel") == "k_amg_cg_w" else None
         iter_traffic = tj.get("iteration_bytes") if tj.get("iter_kernel", "").startswith("GAMG") else None

@@ -54,6 +54,33 @@ __device__ __forceinline__ void bstore(T* __restrict__ v, int64_t /*npos*/, int6
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) v[q * (ND * ND) + c] = (T)m[c];
 }
+// symmetric blocks stored as their upper triangle (A_0: AmgMatD::sym)
+template <int ND>
+constexpr int nsym() { return ND * (ND + 1) / 2; }
+template <int ND, class T, class C>
+__device__ __forceinline__ void bload_sym(const T* __restrict__ v, int64_t q, C* m) {
+  constexpr int NS = nsym<ND>();
+  C t[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) t[c] = (C)v[q * NS + c];
+  if constexpr (ND == 2) {
+    m[0] = t[0]; m[1] = t[1];
+    m[2] = t[1]; m[3] = t[2];
+  } else {
+    m[0] = t[0]; m[1] = t[1]; m[2] = t[2];
+    m[3] = t[1]; m[4] = t[3]; m[5] = t[4];
+    m[6] = t[2]; m[7] = t[4]; m[8] = t[5];
+  }
+}
+template <int ND, class T, class C>
+__device__ __forceinline__ void bstore_sym(T* __restrict__ v, int64_t q, const C* m) {
+  if constexpr (ND == 2) {
+    v[q * 3 + 0] = (T)m[0]; v[q * 3 + 1] = (T)m[1]; v[q * 3 + 2] = (T)m[3];
+  } else {
+    v[q * 6 + 0] = (T)m[0]; v[q * 6 + 1] = (T)m[1]; v[q * 6 + 2] = (T)m[2];
+    v[q * 6 + 3] = (T)m[4]; v[q * 6 + 4] = (T)m[5]; v[q * 6 + 5] = (T)m[8];
+  }
+}
 template <int ND, class T, class C>
 __device__ __forceinline__ void vload(const T* __restrict__ v, int64_t i, C* o) {
 #pragma unroll
@@ -168,7 +195,7 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
 template <int ND>
 constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
 
-template <int ND, int U, bool SUB, class TV, class TX, class C>
+template <int ND, int U, bool SUB, bool SYM = false, class TV, class TX, class C>
 __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                            int64_t npos, int64_t base, int w,
                                            const TX* __restrict__ x, C* y) {
@@ -183,7 +210,8 @@ __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, cons
     C m[U][ND * ND], xc[U][ND];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      bload<ND>(val, npos, q[u], m[u]);
+      if constexpr (SYM) bload_sym<ND>(val, q[u], m[u]);
+      else bload<ND>(val, npos, q[u], m[u]);
       vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
     }
 #pragma unroll
@@ -208,14 +236,14 @@ __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, cons
 // for 98 % of the waves, stays at K = 1 (a 2U path put it at 139 VGPRs, one
 // 768-thread block per CU); the streaming level-0 kernels use K = 2; the
 // restrictions and the latency-bound coarse levels K = 3.
-template <int ND, bool SUB, int K = 2, class TV, class TX, class C>
+template <int ND, bool SUB, int K = 2, bool SYM = false, class TV, class TX, class C>
 __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                          int64_t npos, int64_t base, int w,
                                          const TX* __restrict__ x, C* y) {
   constexpr int U = mac_unroll<ND>();
-  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB>(col, val, npos, base, w, x, y);
-  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB>(col, val, npos, base, w, x, y);
-  else sell_mac_u<ND, U, SUB>(col, val, npos, base, w, x, y);
+  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB, SYM>(col, val, npos, base, w, x, y);
+  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB, SYM>(col, val, npos, base, w, x, y);
+  else sell_mac_u<ND, U, SUB, SYM>(col, val, npos, base, w, x, y);
 }
 
 // o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C).  dinv_load / dinv_mul
@@ -332,7 +360,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const 
     for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
   }
   bstore<ND>(A.val, A.npos, q, m);
-  bstore<ND>(A.val32, A.npos, q, m);
+  bstore_sym<ND>(A.sym, q, m);
+  bstore_sym<ND>(A.sym32, q, m);
 }
 
 // Block-Jacobi inverse, Gershgorin bound per block.  L0: level 0, whose
@@ -359,7 +388,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
         s6[5] += reg;
         sym_to<ND>(s6, D);
         bstore<ND>(A.val, A.npos, base, D);
-        bstore<ND>(A.val32, A.npos, base, D);
+        bstore_sym<ND>(A.sym, base, D);
+        bstore_sym<ND>(A.sym32, base, D);
       } else {
         bload<ND>(A.val, A.npos, base, D);
       }
@@ -512,7 +542,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
   slice_of(L.A, ii, base, w);
   float y[ND];
   vload<ND>(b, ii, y);
-  sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  if constexpr (K == 2)  // level 0: A_0's symmetric f32 blocks
+    sell_mac<ND, true, K, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
+  else
+    sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   if (i < n && run) vstore<ND>(L.t, i, y);
 }
 
@@ -690,7 +723,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
   dinv_load<ND>(L.dinv32, ii, Di);
-  sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+  if constexpr (K == 2)  // level 0: A_0's symmetric f32 blocks
+    sell_mac<ND, true, K, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
+  else
+    sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
@@ -863,7 +899,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    sell_mac<ND, false, 1>(L0.A.col, L0.A.val, L0.A.npos, base, w, cg.u, y);
+    sell_mac<ND, false, 1, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
     if (i >= cg.n) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {

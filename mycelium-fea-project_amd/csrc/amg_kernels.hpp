@@ -22,8 +22,13 @@ struct AmgMatD {
   int32_t wmax = 0;  // widest slice (host side: launch geometry)
   const int32_t* sptr = nullptr;
   const int32_t* col = nullptr;
-  double* val = nullptr;   // [npos][NB2] f64 (setup; A_0 also serves the CG's w = A u)
-  float* val32 = nullptr;  // [npos][NB2] f32 copy for the V-cycle
+  double* val = nullptr;   // [npos][NB2] f64 (setup)
+  float* val32 = nullptr;  // [npos][NB2] f32 copy for the V-cycle (levels ≥ 1)
+  // A_0 only (every block symmetric: K_ij = −Σ S_e, K_ii = Σ S_e + reg·I):
+  // the upper triangles, [npos][ND(ND+1)/2], for the CG's w = A u (f64) and
+  // the level-0 V-cycle kernels (f32) — 3/4 (ND = 2) of the full blocks' bytes
+  double* sym = nullptr;
+  float* sym32 = nullptr;
 };
 
 struct AmgLevD {

@@ -979,7 +979,12 @@ int upload_amg(mfea_handle* h, Part& pt) {
       const AmgLevel& L = pl.lev[l];
       AmgLevD& d = pt.amg_lev[l];
       const int64_t n = L.A.n;
-      d.A = mat(L.A, true, true);
+      d.A = mat(L.A, true, l > 0);
+      if (l == 0) {  // A_0: symmetric blocks for the CG and the level-0 V-cycle kernels
+        const size_t ns = (size_t)nd * (nd + 1) / 2;
+        d.A.sym = D(ns * d.A.npos);
+        d.A.sym32 = F(ns * d.A.npos);
+      }
       d.dinv = D((size_t)nb2 * n);
       d.dinv32 = F((size_t)nb2 * n);
       d.gpart = D((size_t)(n + kBlock - 1) / kBlock + 1);

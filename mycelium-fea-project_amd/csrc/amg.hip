@@ -1099,7 +1099,8 @@ static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, c
   const int64_t n = L.R.n;
   const int S = lanes_for(L.R, L.rlanes, 2.5, 5.0);
   const dim3 b(kBlock);
-  if (S == 4) hipLaunchKernelGGL((k_amg_restrict_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, N, gate);
+  if (S == 8) hipLaunchKernelGGL((k_amg_restrict_s<ND, 8>), rows_grid(8 * n), b, 0, s, L, N, gate);
+  else if (S == 4) hipLaunchKernelGGL((k_amg_restrict_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, N, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_restrict_s<ND, 2>), rows_grid(2 * n), b, 0, s, L, N, gate);
   else hipLaunchKernelGGL(k_amg_restrict<ND>, rows_grid(n), b, 0, s, L, N, gate);
 }

@@ -2241,8 +2241,8 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
   }
   else if (n == "amg_restrict_lanes") {
-    if (value != 0 && value != 1 && value != 2 && value != 4)
-      return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2 or 4");
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2, 4 or 8");
     h->opt_amg_rlanes = (int)value;
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.rlanes = (int)value;

@@ -343,7 +343,7 @@ __device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restri
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
                                                    const int32_t* __restrict__ lst) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
   if (q >= A.npos) return;
   const int t0 = ptr[q], t1 = ptr[q + 1];
   if (t0 == t1) return;
@@ -370,7 +370,7 @@ template <int ND, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
                                                      double reg) {
   __shared__ double red[kBlock / 64];
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& A = L.A;
   double g = 0.0;
   if (i - (threadIdx.x & 63) < A.n) {
@@ -456,13 +456,15 @@ __global__ __launch_bounds__(kBlock) void k_amg_omega(const double* __restrict__
   }
 }
 
-// P values, one thread per (row, slot k = blockIdx.y): every slot of a row
-// in flight at once instead of one after another
+// P values, one thread per (row, slot k): every slot of a row in flight at
+// once instead of one after another.  Block b = (row block b / wmax, slot
+// b % wmax), numbered XCD-aware: each XCD gets whole row ranges, all slots.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int k = blockIdx.y;
   const AmgMatD& P = L.P;
+  const int64_t xb = xcd_block();
+  const int k = (int)(xb % P.wmax);
+  const int64_t i = (xb / P.wmax) * kBlock + threadIdx.x;
   if (i - (threadIdx.x & 63) >= P.n) return;
   int64_t base;
   int w;
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
 // have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
   if (q < L.R.npos && L.R.col[q] >= 0) {  // R = Pᵀ (f32) in R's own SELL layout
     double p[ND * ND], t[ND * ND];
     bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
   if (q >= Ac.npos || Ac.col[q] < 0) return;
   double C[ND * ND];
 #pragma unroll
@@ -1077,7 +1079,8 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
   if (!level0) hipLaunchKernelGGL((k_amg_dinv<ND, false>), g, dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
   if (L.coarsest || !N) return;
-  hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.n).x, (unsigned)std::max(1, L.P.wmax)), dim3(kBlock), 0, s, L);
+  if (L.P.wmax > 0)
+    hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.n).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
   hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.npos, L.R.npos)), dim3(kBlock), 0, s, L);
   hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A);
 }

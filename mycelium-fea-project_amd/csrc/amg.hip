@@ -746,8 +746,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 // ---------------------------------------------------------------------------
 constexpr int kTailBS = 1024;
 
+// Phase bodies with the vectors passed explicitly (global memory for
+// k_amg_tail, LDS for k_amg_tail_lds — the compiler then addresses each kind
+// directly instead of through flat pointers); the operators come from L / N.
 template <int ND>
-__device__ __forceinline__ void tail_resid(const AmgLevD& L) {
+__device__ __forceinline__ void tail_resid(const AmgLevD& L, const float* b, const float* x, float* t) {
   const int64_t n = L.A.n;
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
     const int64_t i = r0 + threadIdx.x;
@@ -757,13 +760,14 @@ __device__ __forceinline__ void tail_resid(const AmgLevD& L) {
     int w;
     slice_of(L.A, ii, base, w);
     float y[ND];
-    vload<ND>(L.b, ii, y);
-    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-    if (i < n) vstore<ND>(L.t, i, y);
+    vload<ND>(b, ii, y);
+    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, x, y);
+    if (i < n) vstore<ND>(t, i, y);
   }
 }
 template <int ND>
-__device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N) {
+__device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N, const float* t, float* nb,
+                                              float* nx) {
   const int64_t n = L.R.n;
   const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
@@ -776,19 +780,18 @@ __device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N
     dinv_load<ND>(N.dinv32, I < n ? I : n - 1, Di);
 #pragma unroll
     for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
-    sell_mac<ND, false>(L.R.col, L.R.val32, L.R.npos, base, w, L.t, bc);
+    sell_mac<ND, false>(L.R.col, L.R.val32, L.R.npos, base, w, t, bc);
     if (I < n) {
-      vstore<ND>(N.b, I, bc);
+      vstore<ND>(nb, I, bc);
       float xn[ND];
       dinv_mul<ND>(Di, sc, bc, xn);
-      vstore<ND>(N.x, I, xn);
+      vstore<ND>(nx, I, xn);
     }
   }
 }
 template <int ND>
-__device__ __forceinline__ void tail_prolong(const AmgLevD& L, const AmgLevD& N) {
+__device__ __forceinline__ void tail_prolong(const AmgLevD& L, const float* e, float* x) {
   const int64_t n = L.P.n;
-  const float* e = N.coarsest ? N.x : N.e;
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
     const int64_t i = r0 + threadIdx.x;
     if (r0 + (threadIdx.x & ~63) >= n) break;
@@ -796,14 +799,14 @@ __device__ __forceinline__ void tail_prolong(const AmgLevD& L, const AmgLevD& N)
     int w;
     slice_of(L.P, i, base, w);
     const int64_t ii = i < n ? i : n - 1;
-    float x[ND];
-    vload<ND>(L.x, ii, x);
-    sell_mac<ND, false>(L.P.col, L.P.val32, L.P.npos, base, w, e, x);
-    if (i < n) vstore<ND>(L.x, i, x);
+    float xv[ND];
+    vload<ND>(x, ii, xv);
+    sell_mac<ND, false>(L.P.col, L.P.val32, L.P.npos, base, w, e, xv);
+    if (i < n) vstore<ND>(x, i, xv);
   }
 }
 template <int ND>
-__device__ __forceinline__ void tail_post(const AmgLevD& L) {
+__device__ __forceinline__ void tail_post(const AmgLevD& L, const float* b, const float* x, float* e_out) {
   const int64_t n = L.A.n;
   const float om = (float)L.omega[0];
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
@@ -813,35 +816,97 @@ __device__ __forceinline__ void tail_post(const AmgLevD& L) {
     int64_t base;
     int w;
     slice_of(L.A, ii, base, w);
-    float y[ND], x[ND], d[ND], Di[ND * ND];
-    vload<ND>(L.b, ii, y);
-    vload<ND>(L.x, ii, x);
+    float y[ND], xv[ND], d[ND], Di[ND * ND];
+    vload<ND>(b, ii, y);
+    vload<ND>(x, ii, xv);
     dinv_load<ND>(L.dinv32, ii, Di);
-    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    sell_mac<ND, true>(L.A.col, L.A.val32, L.A.npos, base, w, x, y);
     dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
-    for (int a = 0; a < ND; ++a) x[a] += d[a];
-    if (i < n) vstore<ND>(L.e, i, x);
+    for (int a = 0; a < ND; ++a) xv[a] += d[a];
+    if (i < n) vstore<ND>(e_out, i, xv);
   }
 }
 
+// The tail's levels travel BY VALUE in the kernel arguments: pointers read
+// from there are known to be global, while pointers read from a device array
+// of level views made every access of the tail a flat one (no global/LDS
+// distinction: each waits on both counters).
+constexpr int kTailMaxLev = 4;
+struct TailLevels {
+  AmgLevD lev[kTailMaxLev];  // levels l0 … l0 + count − 1
+};
 template <int ND>
-__global__ __launch_bounds__(kTailBS) void k_amg_tail(const AmgLevD* __restrict__ lev, int l0, int nlev,
+__global__ __launch_bounds__(kTailBS) void k_amg_tail(const TailLevels tl, int l0, int nlev,
                                                       const int32_t* gate) {
   if (gated(gate)) return;
+  const AmgLevD* lev = tl.lev - l0;
   for (int l = l0; l + 1 < nlev; ++l) {
-    const AmgLevD L = lev[l];
-    tail_resid<ND>(L);
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    tail_resid<ND>(L, L.b, L.x, L.t);
     __syncthreads();
-    tail_restrict<ND>(L, lev[l + 1]);
+    tail_restrict<ND>(L, N, L.t, N.b, N.x);
     __syncthreads();
   }
   for (int l = nlev - 2; l >= l0; --l) {
-    const AmgLevD L = lev[l];
-    tail_prolong<ND>(L, lev[l + 1]);
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    tail_prolong<ND>(L, N.coarsest ? N.x : N.e, L.x);
     __syncthreads();
-    tail_post<ND>(L);
+    tail_post<ND>(L, L.b, L.x, L.e);
     __syncthreads();
+  }
+}
+
+// The same tail with the V-cycle vectors of its levels in LDS (b, x, t per
+// level; a coarse level's output e lives in its t): every gather of a phase
+// reads LDS instead of L2, and a barrier waits for LDS stores only.  Level
+// l0's b, x are copied in from global memory first and its e is written
+// there; the operators stay in global memory.  kTailLdsMax bytes at most
+// (the launcher falls back to k_amg_tail beyond).
+constexpr int64_t kTailLdsMax = 64 * 1024;
+template <int ND>
+__device__ __forceinline__ int64_t tail_lds_off(const AmgLevD* __restrict__ lev, int l, int l0) {
+  int64_t off = 0;
+  for (int m = l0; m < l; ++m) off += 3 * ND * lev[m].A.n;
+  return off;
+}
+template <int ND>
+__global__ __launch_bounds__(kTailBS) void k_amg_tail_lds(const TailLevels tl, int l0, int nlev,
+                                                          const int32_t* gate) {
+  extern __shared__ float sm[];
+  if (gated(gate)) return;
+  const AmgLevD* lev = tl.lev - l0;
+  {
+    const AmgLevD G = lev[l0];
+    const int64_t n = G.A.n;
+    for (int64_t k = threadIdx.x; k < ND * n; k += kTailBS) {
+      sm[k] = G.b[k];
+      sm[ND * n + k] = G.x[k];
+    }
+  }
+  __syncthreads();
+  for (int l = l0; l + 1 < nlev; ++l) {
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    float* v = sm + tail_lds_off<ND>(lev, l, l0);  // b x t of level l
+    float* w = v + 3 * ND * L.A.n;                 // of level l + 1
+    tail_resid<ND>(L, v, v + ND * L.A.n, v + 2 * ND * L.A.n);
+    __syncthreads();
+    tail_restrict<ND>(L, N, v + 2 * ND * L.A.n, w, w + ND * N.A.n);
+    __syncthreads();
+  }
+  for (int l = nlev - 2; l >= l0; --l) {
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    float* v = sm + tail_lds_off<ND>(lev, l, l0);
+    float* w = v + 3 * ND * L.A.n;
+    // level l+1's output: its x if coarsest, else its e (held in its t)
+    tail_prolong<ND>(L, N.coarsest ? w + ND * N.A.n : w + 2 * ND * N.A.n, v + ND * L.A.n);
+    __syncthreads();
+    if (l > l0) {
+      tail_post<ND>(L, v, v + ND * L.A.n, v + 2 * ND * L.A.n);
+      __syncthreads();
+    } else {
+      tail_post<ND>(L, v, v + ND * L.A.n, L.e);
+    }
   }
 }
 
@@ -1127,7 +1192,7 @@ static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t*
 }
 
 template <int ND>
-static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const AmgLevD* lev_dev,
+static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
                       int tail, const int32_t* gate) {
   const dim3 b(kBlock);
   const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
@@ -1138,7 +1203,18 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
       launch_op<ND>(s, lev[l], false, gate);
     launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
   }
-  if (tail > 0) hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, lev_dev, tail, nlev, gate);
+  if (tail > 0) {
+    TailLevels tl;
+    int64_t lds = 0;
+    for (int l = tail; l < nlev; ++l) {
+      tl.lev[l - tail] = lev[l];
+      lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
+    }
+    if (lds <= kTailLdsMax)
+      hipLaunchKernelGGL(k_amg_tail_lds<ND>, dim3(1), dim3(kTailBS), (size_t)lds, s, tl, tail, nlev, gate);
+    else
+      hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, tl, tail, nlev, gate);
+  }
   for (int l = top - 1; l >= 0; --l) {
     hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
     if (l == 0)
@@ -1149,12 +1225,13 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
   }
 }
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       const AmgLevD* lev_dev, int tail, const int32_t* gate) {
+                       int tail, const int32_t* gate) {
   // one level: the coarsest solve u = D⁻¹ r is done by the producer of r
   if (nlev <= 1 || lev[0].A.n <= 0) return;
   if (tail >= nlev - 1) tail = 0;  // nothing below the coarsest to fuse
-  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, lev_dev, tail, gate);
-  else vcycle_nd<3>(s, lev, nlev, cg, lev_dev, tail, gate);
+  if (tail > 0 && nlev - tail > kTailMaxLev) tail = nlev - kTailMaxLev;  // the kernel argument holds 4 levels
+  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, tail, gate);
+  else vcycle_nd<3>(s, lev, nlev, cg, tail, gate);
 }
 
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows) {

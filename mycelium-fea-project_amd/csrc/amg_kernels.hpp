@@ -103,9 +103,9 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
-// single-workgroup launch (k_amg_tail) reading the level views at lev_dev.
+// single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       const AmgLevD* lev_dev, int tail, const int32_t* gate);
+                       int tail, const int32_t* gate);
 // first level l ≥ 1 (above the coarsest) with at most max_rows rows, or 0
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------

@@ -122,7 +122,6 @@ struct Part {
   DevBuf<double> amg_d;              // every f64 value / vector array, carved
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
-  DevBuf<AmgLevD> amg_lev_d;         // the same, on the device (k_amg_tail)
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
   AmgCg amg_cg;
   const int32_t* amg_a0_ptr = nullptr;
@@ -1027,9 +1026,6 @@ int upload_amg(mfea_handle* h, Part& pt) {
     pt.amg_cg.u = F((size_t)nd * nf);
   }
   HIPC(err);
-  HIPC(pt.amg_lev_d.alloc(std::max(nlev, 1)));
-  if (nlev)
-    HIPC(hipMemcpyAsync(pt.amg_lev_d.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
   {
     std::vector<int64_t> rows(nlev);
     for (int l = 0; l < nlev; ++l) rows[l] = pl.lev[l].A.n;
@@ -1127,7 +1123,7 @@ void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_update(s, nd, j, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
                     pt.amg_tail, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
   launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
 }
@@ -1201,7 +1197,7 @@ int enqueue_amg_dist_iteration(mfea_handle* h, int j) {
     const int nd = pt.amg.nd;
     launch_amg_cg_update(s, nd, j, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr,
                          &pt.amg_dist);
-    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
                       pt.amg_tail, &pt.slots.ptr[j + 1].flag);
     launch_amg_pack_u(s, nd, pt.amg_cg, pt.amg_dist);
   }
@@ -1235,7 +1231,7 @@ void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   for (int j = 0; j < chunk; ++j) {
-    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
                       pt.amg_tail, &pt.slots.ptr[j + 1].flag);
     launch_amg_cg_w(s, nd, j, false, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
     launch_amg_cg_update(s, nd, j + 1, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
@@ -1274,7 +1270,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   h->ev_setup_used = true;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
                     pt.amg_tail, nullptr);
   launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
   launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
@@ -1369,7 +1365,7 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
     Part& pt = *pp;
     const int nd = pt.amg.nd;
     launch_amg_cg_init(s, nd, pt.amg_lev[0], pt.amg_cg, cg_vecs(pt).r[0]);
-    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_lev_d.ptr,
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
                       pt.amg_tail, nullptr);
     launch_amg_pack_u(s, nd, pt.amg_cg, pt.amg_dist);
   }

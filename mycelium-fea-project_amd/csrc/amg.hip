@@ -531,7 +531,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
 // ---------------------------------------------------------------------------
 // V-cycle (f32; level 0 reads r and writes u in f64)
 // ---------------------------------------------------------------------------
-template <int ND, class TB, int K>
+// L0: level 0 — A_0's symmetric f32 blocks, 2U unroll for its narrow streaming
+// rows; otherwise the full f32 blocks with the 4U tier (sell_mac's K)
+template <int ND, class TB, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
                                                       const int32_t* gate) {
   const bool run = gate_open(gate);
@@ -544,10 +546,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
   slice_of(L.A, ii, base, w);
   float y[ND];
   vload<ND>(b, ii, y);
-  if constexpr (K == 2)  // level 0: A_0's symmetric f32 blocks
-    sell_mac<ND, true, K, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
+  if constexpr (L0)
+    sell_mac<ND, true, 2, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
   else
-    sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   if (i < n && run) vstore<ND>(L.t, i, y);
 }
 
@@ -709,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, co
   if (i < P.n && run) vstore<ND>(L.x, i, x);
 }
 
-template <int ND, class TB, class TE, int K>
+template <int ND, class TB, class TE, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
                                                      const int32_t* gate) {
   const bool run = gate_open(gate);
@@ -725,10 +727,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
   dinv_load<ND>(L.dinv32, ii, Di);
-  if constexpr (K == 2)  // level 0: A_0's symmetric f32 blocks
-    sell_mac<ND, true, K, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
+  if constexpr (L0)
+    sell_mac<ND, true, 2, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
   else
-    sell_mac<ND, true, K>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
   dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
@@ -1185,9 +1187,9 @@ static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t*
     else hipLaunchKernelGGL((k_amg_resid_s<ND, 2>), rows_grid(2 * n), b, 0, s, L, gate);
   } else {
     if (post)
-      hipLaunchKernelGGL((k_amg_post<ND, float, float, 3>), rows_grid(n), b, 0, s, L, (const float*)L.b, L.e, gate);
+      hipLaunchKernelGGL((k_amg_post<ND, float, float, false>), rows_grid(n), b, 0, s, L, (const float*)L.b, L.e, gate);
     else
-      hipLaunchKernelGGL((k_amg_resid<ND, float, 3>), rows_grid(n), b, 0, s, L, (const float*)L.b, gate);
+      hipLaunchKernelGGL((k_amg_resid<ND, float, false>), rows_grid(n), b, 0, s, L, (const float*)L.b, gate);
   }
 }
 
@@ -1198,7 +1200,7 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
   const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
   for (int l = 0; l < top; ++l) {
     if (l == 0)
-      hipLaunchKernelGGL((k_amg_resid<ND, double, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
+      hipLaunchKernelGGL((k_amg_resid<ND, double, true>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
     else
       launch_op<ND>(s, lev[l], false, gate);
     launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
@@ -1218,7 +1220,7 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
   for (int l = top - 1; l >= 0; --l) {
     hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
     if (l == 0)
-      hipLaunchKernelGGL((k_amg_post<ND, double, float, 2>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
+      hipLaunchKernelGGL((k_amg_post<ND, double, float, true>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
                          (const double*)cg.r, cg.u, gate);
     else
       launch_op<ND>(s, lev[l], true, gate);

@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
 template <int ND, int S, bool SUB, class TV, class TX, class C>
 __device__ __forceinline__ void sell_mac_sub(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                              int64_t base, int w, int sub, const TX* __restrict__ x, C* y) {
-  constexpr int U = 2 * mac_unroll<ND>();
+  constexpr int U = 2 * mac_unroll<ND>();  // (U = 4: C2 62.4 vs 60.8 µs per iteration)
   const int wu = (w + S - 1) / S;  // steps: the slice's, uniform
   const int ws = w > sub ? (w - sub + S - 1) / S : 0;
   for (int k = 0; k < wu; k += U) {

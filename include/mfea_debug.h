@@ -34,6 +34,7 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *   "ell_maxg" n         lane kernels: grid cap (0 = 512)
  *   "ell_compact" 0|1    lane kernels: compact halo records (1)
  *   "amg_tail_rows" n    GAMG: deep levels of ≤ n rows in one workgroup (2048; 0 off)
+ *   "amg_tail_lds" 0|1   GAMG: the tail's vectors in LDS (1) or global memory (0)
  *   "amg_restrict_lanes" 0|1|2|4|8  GAMG: lanes per coarse row of the restriction (0: by width)
  *   "amg_op_lanes" 0|1|2|4        GAMG: lanes per row of the operators below level 0 (0: by width)
  *   "dist_timeout_ms" n  RCCL waits: give up after n ms

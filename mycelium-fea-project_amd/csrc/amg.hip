@@ -1212,7 +1212,7 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
       tl.lev[l - tail] = lev[l];
       lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
     }
-    if (lds <= kTailLdsMax)
+    if (lds <= kTailLdsMax && lev[tail].tail_lds)
       hipLaunchKernelGGL(k_amg_tail_lds<ND>, dim3(1), dim3(kTailBS), (size_t)lds, s, tl, tail, nlev, gate);
     else
       hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, tl, tail, nlev, gate);

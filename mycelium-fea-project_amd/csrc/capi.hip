@@ -187,6 +187,7 @@ struct mfea_handle {
   int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
+  int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
@@ -995,6 +996,7 @@ int upload_amg(mfea_handle* h, Part& pt) {
       d.coarsest = L.coarsest ? 1 : 0;
       d.rlanes = h->opt_amg_rlanes;
       d.alanes = h->opt_amg_alanes;
+      d.tail_lds = h->opt_amg_tail_lds;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, true, true);
@@ -2249,6 +2251,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_alanes = (int)value;
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.alanes = (int)value;
+  }
+  else if (n == "amg_tail_lds") {
+    h->opt_amg_tail_lds = value != 0;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "part_slack_pct") {

@@ -179,9 +179,29 @@ def _variant_solves(engine, option, values, nx=1, ny=5):
     return out, fo.solve_system(K, known, vals)
 
 
-@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4]), ("amg_op_lanes", [1, 2, 4])])
+@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8]), ("amg_op_lanes", [1, 2, 4])])
 def test_vcycle_lane_splits_match_direct(engine, option, values):
     out, Uref = _variant_solves(engine, option, values)
     for v, (U, _) in out.items():
         assert rel(U, Uref) <= 1e-10, (option, v, rel(U, Uref))
+
+
+def test_tail_lds_and_global_bitwise_equal(engine):
+    """The single-workgroup tail with its vectors in LDS (k_amg_tail_lds) and
+    in global memory (k_amg_tail) run the same arithmetic: U bit for bit."""
+    from mfea import synth
+    xyz, e2n = synth.tiled_mesh(1, 5)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    out = {}
+    for v in (1, 0):
+        engine.set_option("amg_tail_lds", v)
+        st = engine.solve(dy, -dy, _opts(1e-10))
+        assert st.status == 0
+        out[v] = (engine.displacement(), st.iters)
+    assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0])
 

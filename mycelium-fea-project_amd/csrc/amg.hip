@@ -342,7 +342,8 @@ __device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restri
 // empty lists; the diagonal block is written by k_amg_dinv<ND, true>.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
-                                                   const int32_t* __restrict__ lst) {
+                                                   const int32_t* __restrict__ lst, double* omega0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) omega0[1] = 0.0;  // level 0's bound, max'ed by k_amg_dinv
   const int64_t q = xcd_block() * kBlock + threadIdx.x;
   if (q >= A.npos) return;
   const int t0 = ptr[q], t1 = ptr[q + 1];
@@ -431,29 +432,21 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
   if (threadIdx.x == 0) {
     double m = red[0];
     for (int k = 1; k < kBlock / 64; ++k) m = fmax(m, red[k]);
-    L.gpart[blockIdx.x] = m;
+    // the level's bound g = max over blocks: a max is order-free, so one
+    // atomic per block gives the same bits as any reduction (m ≥ 0, so its
+    // IEEE bits order as unsigned integers); zeroed by the kernel producing
+    // this level's A (k_amg_a0 / k_amg_ac)
+    atomicMax(reinterpret_cast<unsigned long long*>(&L.omega[1]),
+              static_cast<unsigned long long>(__double_as_longlong(m)));
   }
 }
 
 constexpr double kRhoFloor = 2.0;   // the exact level-0 bound (see the header)
 constexpr double kRhoSafety = 1.45; // ω·g ≤ (4/3)·1.45 < 2
 
-__global__ __launch_bounds__(kBlock) void k_amg_omega(const double* __restrict__ gpart, int64_t nb,
-                                                       double* omega) {
-  __shared__ double red[kBlock / 64];
-  double g = 0.0;
-  for (int64_t k = threadIdx.x; k < nb; k += kBlock) g = fmax(g, gpart[k]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double m = red[0];
-    for (int k = 1; k < kBlock / 64; ++k) m = fmax(m, red[k]);
-    const double rho = fmax(kRhoFloor, m / kRhoSafety);
-    omega[0] = (4.0 / 3.0) / rho;
-    omega[1] = m;
-  }
+// the smoother weight ω_l from the level's Gershgorin bound g = omega[1]
+__device__ __forceinline__ double amg_omega(const double* __restrict__ om) {
+  return (4.0 / 3.0) / fmax(kRhoFloor, om[1] / kRhoSafety);
 }
 
 // P values, one thread per (row, slot k): every slot of a row in flight at
@@ -482,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   }
   list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val, L.A.npos, S);
   mm_acc<ND>(Di, S, pm);
-  const double om = L.omega[0];
+  const double om = amg_omega(L.omega);
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
   if (J == L.agg[i]) {
@@ -517,7 +510,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac) {
+__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
   const int64_t q = xcd_block() * kBlock + threadIdx.x;
   if (q >= Ac.npos || Ac.col[q] < 0) return;
   double C[ND * ND];
@@ -562,7 +556,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   int64_t base;
   int w;
   slice_of(R, I, base, w);
-  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
   float Di[ND * ND];
   dinv_load<ND>(N.dinv32, I < R.n ? I : R.n - 1, Di);
   float bc[ND];
@@ -632,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict_s(AmgLevD L, AmgLevD N,
   int64_t base;
   int w;
   slice_of(R, Ic, base, w);
-  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
   float Di[ND * ND], bc[ND];
   dinv_load<ND>(N.dinv32, Ic, Di);
 #pragma unroll
@@ -679,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post_s(AmgLevD L, const int32_t*
   int64_t base;
   int w;
   slice_of(L.A, ii, base, w);
-  const float om = (float)L.omega[0];
+  const float om = (float)amg_omega(L.omega);
   float y[ND], x[ND], d[ND], Di[ND * ND];
   vload<ND>(L.b, ii, y);
   vload<ND>(L.x, ii, x);
@@ -722,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   int64_t base;
   int w;
   slice_of(L.A, ii, base, w);
-  const float om = (float)L.omega[0];
+  const float om = (float)amg_omega(L.omega);
   float y[ND], x[ND], d[ND], Di[ND * ND];
   vload<ND>(b, ii, y);
   vload<ND>(L.x, ii, x);
@@ -771,7 +765,7 @@ template <int ND>
 __device__ __forceinline__ void tail_restrict(const AmgLevD& L, const AmgLevD& N, const float* t, float* nb,
                                               float* nx) {
   const int64_t n = L.R.n;
-  const float sc = N.coarsest ? 1.0f : (float)N.omega[0];
+  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
     const int64_t I = r0 + threadIdx.x;
     if (r0 + (threadIdx.x & ~63) >= n) break;
@@ -810,7 +804,7 @@ __device__ __forceinline__ void tail_prolong(const AmgLevD& L, const float* e, f
 template <int ND>
 __device__ __forceinline__ void tail_post(const AmgLevD& L, const float* b, const float* x, float* e_out) {
   const int64_t n = L.A.n;
-  const float om = (float)L.omega[0];
+  const float om = (float)amg_omega(L.omega);
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
     const int64_t i = r0 + threadIdx.x;
     if (r0 + (threadIdx.x & ~63) >= n) break;
@@ -928,7 +922,7 @@ __device__ __forceinline__ void vcycle_entry(const AmgLevD& L0, const AmgCg& cg,
     float rf[ND], x0[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) rf[a] = (float)r[a];
-    dinv_apply<ND>(L0.dinv32, L0.A.n, i, (float)L0.omega[0], rf, x0);
+    dinv_apply<ND>(L0.dinv32, L0.A.n, i, (float)amg_omega(L0.omega), rf, x0);
     vstore<ND>(L0.x, i, x0);
   }
 }
@@ -1129,7 +1123,7 @@ template <int ND>
 static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
                   const int32_t* a, double reg) {
   if (L0.A.n <= 0) return;
-  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.npos), dim3(kBlock), 0, s, L0.A, sop, p, a);
+  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.npos), dim3(kBlock), 0, s, L0.A, sop, p, a, L0.omega);
   hipLaunchKernelGGL((k_amg_dinv<ND, true>), rows_grid(L0.A.n), dim3(kBlock), 0, s, L0, sop, row0, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
@@ -1144,12 +1138,11 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
   const dim3 g = rows_grid(L.A.n);
   // level 0's k_amg_dinv ran in launch_amg_a0 (it also forms the diagonal)
   if (!level0) hipLaunchKernelGGL((k_amg_dinv<ND, false>), g, dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
-  hipLaunchKernelGGL(k_amg_omega, dim3(1), dim3(kBlock), 0, s, L.gpart, (int64_t)g.x, L.omega);
   if (L.coarsest || !N) return;
   if (L.P.wmax > 0)
     hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.n).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
   hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.npos, L.R.npos)), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A);
+  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A, N->omega);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0) {
   if (nd == 2) setup_nd<2>(s, L, next, level0);

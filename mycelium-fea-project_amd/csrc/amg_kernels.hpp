@@ -35,8 +35,7 @@ struct AmgLevD {
   AmgMatD A;
   double* dinv = nullptr;
   float* dinv32 = nullptr;
-  double* gpart = nullptr;  // per-block Gershgorin maxima (setup)
-  double* omega = nullptr;  // [2]: smoother weight ω_l, Gershgorin bound g_l
+  double* omega = nullptr;  // [2]: [1] = Gershgorin bound g_l (ω_l = amg_omega(omega)); [0] unused
   // V-cycle vectors [n][ND], f32 (level 0: b = the CG's r, e = the CG's u, f64)
   float* b = nullptr;
   float* x = nullptr;

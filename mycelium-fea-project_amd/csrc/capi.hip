@@ -987,7 +987,6 @@ int upload_amg(mfea_handle* h, Part& pt) {
       }
       d.dinv = D((size_t)nb2 * n);
       d.dinv32 = F((size_t)nb2 * n);
-      d.gpart = D((size_t)(n + kBlock - 1) / kBlock + 1);
       d.omega = D(2);
       d.b = l ? F((size_t)nd * n) : nullptr;  // level 0 reads the CG's r
       d.x = F((size_t)nd * n);

@@ -337,8 +337,13 @@ def main():
     if pc == PC_GAMG:
         ai = eng.amg_info()
         iter_bytes = amg_iteration_bytes(ai)
-        iter_kernel = (f"GAMG-PCG iteration ({4 * (ai['levels'] - 1) + 2} launches: update + "
-                       f"{ai['levels']}-level V-cycle + w = A u)")
+        # levels from the first one of ≤ 2048 rows (above the coarsest) run in
+        # one single-workgroup launch (the engine's default amg_tail_rows)
+        nl = ai["levels"]
+        tail = next((l for l in range(1, nl - 1) if ai["rows"][l] <= 2048), 0)
+        launches = 2 + (4 * tail + 1 if tail else 4 * (nl - 1))
+        iter_kernel = (f"GAMG-PCG iteration ({launches} launches: update + "
+                       f"{nl}-level V-cycle + w = A u)")
         spmv_ms = eng.profile_spmv(reps=100)
         nd = ai["nd"]
         spmv_bytes = ai["blocks"][0] * (8 * nd * (nd + 1) // 2 + 4) + (2 * 8 + 4) * nd * ai["rows"][0]

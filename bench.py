@@ -96,6 +96,14 @@ def amg_iteration_bytes(ai):
     return b
 
 
+def amg_spmv_bytes(ai):
+    """Algorithmic bytes of one SpMV launch k_amg_cg_w: A_0's
+    symmetric f64 blocks with their column indices, r in and w out (f64), u in
+    (f32)."""
+    nd = ai["nd"]
+    return ai["blocks"][0] * (8 * nd * (nd + 1) // 2 + 4) + (2 * 8 + 4) * nd * ai["rows"][0]
+
+
 def iteration_bytes(info, block):
     """Algorithmic HBM bytes of one iteration launch.
 
@@ -346,7 +354,7 @@ def main():
                        f"{nl}-level V-cycle + w = A u)")
         spmv_ms = eng.profile_spmv(reps=100)
         nd = ai["nd"]
-        spmv_bytes = ai["blocks"][0] * (8 * nd * (nd + 1) // 2 + 4) + (2 * 8 + 4) * nd * ai["rows"][0]
+        spmv_bytes = amg_spmv_bytes(ai)
         kernel = f"k_amg_cg_w (SpMV w = A_0 u, f64 symmetric {nd}x{nd} blocks, + CG partial sums)"
         kernel_ms, kernel_bytes = spmv_ms, spmv_bytes
         traffic = tj.get("spmv_bytes_per_launch") if tj.get("spmv_kernel") == "k_amg_cg_w" else None

@@ -7,7 +7,7 @@ iteration count, the relative residual, the V-cycle iteration time
 (mfea_profile_iteration) and U's distance to the first value's U — values are
 interleaved per round so box drift hits all of them alike.
 
-    python tools/amg_ab.py --configs C3_1M C5_10M_dense --option amg_fused --values 1 0
+    python tools/amg_ab.py --configs C3_1M C5_10M_dense --option amg_restrict_lanes --values 0 2 4
 """
 import argparse
 import json
@@ -24,8 +24,8 @@ sys.path.insert(0, os.path.join(REPO, "mycelium-fea-project_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", nargs="+", default=["C3_1M"])
-    ap.add_argument("--option", default="amg_fused")
-    ap.add_argument("--values", nargs="+", type=int, default=[1, 0])
+    ap.add_argument("--option", default="amg_restrict_lanes")
+    ap.add_argument("--values", nargs="+", type=int, default=[0, 2, 4])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
     a = ap.parse_args()

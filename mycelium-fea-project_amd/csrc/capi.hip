@@ -260,7 +260,10 @@ int wait_event(mfea_handle* h, hipEvent_t ev) {
       h->comm = nullptr;
       return fail(MFEA_ECOMM, "RCCL: no progress before the deadline (peer lost?)");
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // spin for the first 200 µs (a converged chunk or a step's end is
+    // usually that close), then poll every 20 µs
+    if (dt > 200e-6) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else std::this_thread::yield();
   }
 }
 

@@ -40,8 +40,14 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *   "dist_timeout_ms" n  RCCL waits: give up after n ms
  *   "part_slack_pct" n   partition boundaries move ≤ n % of a strip to the
  *                        fewest crossing elements (35; 0 = equal free-node counts)
+ *   "amg_max_levels" 1..32  GAMG: hierarchy depth cap (32)
+ *   "amg_w_block" 0|256..1024  GAMG: threads per block of w = A u (0: by size)
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
+
+/* The current value of an option of mfea_set_option (as it would be passed
+ * back: part_slack_pct in percent, dist_timeout_ms in ms). */
+int mfea_get_option(mfea_handle* h, const char* name, int64_t* value);
 
 /* The MFEA_PC_GAMG hierarchy for the current active set (built if needed):
  * *n_levels levels; for level l < cap: rows[l] (nodes / aggregates),

@@ -2277,6 +2277,29 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   return 0;
 }
 
+int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
+  if (!h || !name || !value) return fail(MFEA_EINVAL, "NULL argument");
+  const std::string n(name);
+  if (n == "graph") *value = h->opt_graph;
+  else if (n == "dist_graph") *value = h->opt_dist_graph;
+  else if (n == "order") *value = h->opt_order;
+  else if (n == "lane_dof") *value = h->opt_lane_dof;
+  else if (n == "cg_kernel") *value = h->opt_cg_kernel;
+  else if (n == "ell_block") *value = h->opt_ell_block;
+  else if (n == "ell_maxg") *value = h->opt_ell_maxg;
+  else if (n == "ell_compact") *value = h->opt_ell_compact;
+  else if (n == "amg_tail_rows") *value = h->opt_amg_tail_rows;
+  else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
+  else if (n == "amg_w_block") *value = h->opt_amg_w_block;
+  else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
+  else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
+  else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
+  else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
+  else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
+  else return fail(MFEA_EINVAL, "unknown option " + n);
+  return 0;
+}
+
 int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
   if (nparts < 1 || nparts > kMaxRanks) return fail(MFEA_EINVAL, "nparts must be in [1, 64]");

@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # mfea_set_option defaults (include/mfea_debug.h)
 DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
-                   "dist_timeout_ms": 60000, "part_slack_pct": 35}
+                   "amg_max_levels": 32, "amg_w_block": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
+                   "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
@@ -117,6 +118,7 @@ _sig = {
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
     "mfea_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
+    "mfea_get_option": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
     "mfea_debug_amg_info": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P, C.c_int,
                                       C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
 }
@@ -298,16 +300,23 @@ class Engine:
         """mfea_set_option (include/mfea_debug.h): tuning / comparison knobs."""
         _check(_lib.mfea_set_option(self._h, name.encode(), int(value)))
 
+    def get_option(self, name: str) -> int:
+        """mfea_get_option: the option's current value."""
+        v = C.c_int64()
+        _check(_lib.mfea_get_option(self._h, name.encode(), C.byref(v)))
+        return v.value
+
     @contextlib.contextmanager
     def options(self, **kw):
-        """Set options for a block, then restore their defaults."""
+        """Set options for a block, then restore the values they had before."""
+        prev = {k: self.get_option(k) for k in kw}
         try:
             for k, v in kw.items():
                 self.set_option(k, v)
             yield self
         finally:
-            for k in kw:
-                self.set_option(k, DEFAULT_OPTIONS[k])
+            for k, v in prev.items():
+                self.set_option(k, v)
 
     # ---- setup --------------------------------------------------------------
     def set_material(self, E, A, I):

@@ -162,18 +162,19 @@ def _variant_solves(engine, option, values, nx=1, ny=5):
     from mfea import synth
     xyz, e2n = synth.tiled_mesh(nx, ny)
     top, bot = synth.grips(xyz)
-    engine.set_option("amg_tail_rows", 0)  # every level in its own kernels
-    engine.set_mesh(xyz, e2n)
-    engine.set_bc(top, bot)
-    engine.set_active(None)
-    engine.assemble()
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     out = {}
-    for v in values:
-        engine.set_option(option, v)
-        st = engine.solve(dy, -dy, _opts(1e-13))
-        assert st.status == 0, (option, v)
-        out[v] = (engine.displacement(), st.iters)
+    # every level in its own kernels; the session engine gets its options back
+    with engine.options(amg_tail_rows=0, **{option: values[0]}):
+        engine.set_mesh(xyz, e2n)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        engine.assemble()
+        for v in values:
+            engine.set_option(option, v)
+            st = engine.solve(dy, -dy, _opts(1e-13))
+            assert st.status == 0, (option, v)
+            out[v] = (engine.displacement(), st.iters)
     K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
     known, vals = fo.known_dof_map(top, bot, dy, -dy)
     return out, fo.solve_system(K, known, vals)
@@ -192,16 +193,52 @@ def test_tail_lds_and_global_bitwise_equal(engine):
     from mfea import synth
     xyz, e2n = synth.tiled_mesh(1, 5)
     top, bot = synth.grips(xyz)
-    engine.set_mesh(xyz, e2n)
-    engine.set_bc(top, bot)
-    engine.set_active(None)
-    engine.assemble()
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     out = {}
-    for v in (1, 0):
-        engine.set_option("amg_tail_lds", v)
-        st = engine.solve(dy, -dy, _opts(1e-10))
-        assert st.status == 0
-        out[v] = (engine.displacement(), st.iters)
+    with engine.options(amg_tail_rows=2048, amg_tail_lds=1):
+        engine.set_mesh(xyz, e2n)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        engine.assemble()
+        rows = engine.amg_info()["rows"]
+        # the tail runs only if some level below level 0 fits in it
+        assert len(rows) >= 3 and any(r <= 2048 for r in rows[1:]), rows
+        for v in (1, 0):
+            engine.set_option("amg_tail_lds", v)
+            st = engine.solve(dy, -dy, _opts(1e-10))
+            assert st.status == 0
+            out[v] = (engine.displacement(), st.iters)
     assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0])
 
+
+def test_converged_solve_leaves_no_stale_chunks(engine):
+    """A solve that converges in fewer chunks than the previous one planned
+    must not let the extra queued chunks touch x (cg.hip k_cg_advance poisons
+    the slot every queued chunk gates on): a loose solve after a tight one
+    equals the loose solve on a fresh handle bit for bit, and its reported
+    relres is the residual of the U it returns."""
+    from mfea import Engine
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    xyz, e2n, top, bot = _sim181147(engine)
+    engine.assemble()
+    assert engine.solve(dy, -dy, _opts(1e-13)).status == 0   # plans ~30+ iterations next
+    st = engine.solve(dy, -dy, _opts(1e-6))
+    U = engine.displacement()
+    with Engine(0) as fresh:
+        fresh.set_mesh(xyz, e2n)
+        fresh.set_bc(top, bot)
+        fresh.set_active(None)
+        fresh.assemble()
+        # under-planned (a looser solve first): chunks are queued one at a
+        # time once the plan is used up, so no chunk runs after convergence
+        assert fresh.solve(dy, -dy, _opts(1e-2)).iters < st.iters
+        st_f = fresh.solve(dy, -dy, _opts(1e-6))
+        U_f = fresh.displacement()
+    assert st.iters == st_f.iters
+    assert np.array_equal(U, U_f)
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    A, b, free = fo.free_system(K, known, vals)
+    true_rel = np.linalg.norm(b - A @ U[free]) / np.linalg.norm(b)
+    assert abs(true_rel - st.relres) <= 0.05 * st.relres, (true_rel, st.relres)

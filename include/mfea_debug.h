@@ -42,6 +42,9 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *                        fewest crossing elements (35; 0 = equal free-node counts)
  *   "amg_max_levels" 1..32  GAMG: hierarchy depth cap (32)
  *   "amg_w_block" 0|256..1024  GAMG: threads per block of w = A u (0: by size)
+ *   "amg_dist" 0|1       partitioned GAMG: block Jacobi over per-partition hierarchies (0)
+ *                        or the distributed V-cycle of one global hierarchy (1)
+ *   "amg_rep_rows" n     distributed V-cycle: levels of at most n rows replicated (32768)
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 
@@ -49,13 +52,28 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
  * back: part_slack_pct in percent, dist_timeout_ms in ms). */
 int mfea_get_option(mfea_handle* h, const char* name, int64_t* value);
 
-/* The MFEA_PC_GAMG hierarchy for the current active set (built if needed):
+/* The MFEA_PC_GAMG hierarchy for the current active set (built if needed;
+ * partitioned handles: the global hierarchy of option "amg_dist" 1):
  * *n_levels levels; for level l < cap: rows[l] (nodes / aggregates),
  * blocks[l] (stored ND×ND blocks of A_l, diagonal included) and pblocks[l]
  * (blocks of the prolongator P_l; 0 on the coarsest level).  *pair_items =
- * index-list entries of the numeric setup; *nd = DOFs per node. */
+ * index-list entries of the numeric setup; *nd = DOFs per node; *n_dist =
+ * levels split over the partitions (0: one partition). */
 int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
-                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd);
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist);
+
+/* One MFEA_PC_GAMG V-cycle u = M r on the assembled operator (call after
+ * mfea_assemble; runs the numeric setup first).  r, u: n_nodes × ND in
+ * original node order (ND = the hierarchy's DOFs per node, 2 on planar
+ * meshes); entries of grip nodes are ignored / written 0.  Partitioned
+ * handles run the distributed V-cycle (option "amg_dist" 1). */
+int mfea_debug_amg_vcycle(mfea_handle* h, const double* r, double* u);
+
+/* After mfea_debug_amg_vcycle: level l's V-cycle vector `which` (0 b, 1 x,
+ * 2 t, 3 e; level 0: b = the CG's r, e = its u) in the level's natural
+ * (aggregation) row order, n_l × ND; partitioned: each row from its owner.
+ * Returns the row count in *n. */
+int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t cap, int64_t* n);
 
 #ifdef __cplusplus
 }

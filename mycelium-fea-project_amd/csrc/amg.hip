@@ -179,6 +179,14 @@ __device__ __forceinline__ int64_t xcd_block() {
   return x * q + (x < r ? x : r) + i;
 }
 
+// position q of a RowRange's span belongs to one of its rows (only the
+// first and last slice can hold other ranks' rows)
+__device__ __forceinline__ bool pos_mine(const RowRange& g, int64_t q) {
+  if (q >= g.pf && q < g.pl) return true;
+  const int64_t row = 64 * (q < g.pf ? g.s0 : g.s1) + (q & 63);
+  return row >= g.lo && row < g.hi;
+}
+
 // slot range of the wave's slice (scalar loads, wave-uniform)
 __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
   const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));
@@ -344,8 +352,8 @@ template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
                                                    const int32_t* __restrict__ lst, double* omega0) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega0[1] = 0.0;  // level 0's bound, max'ed by k_amg_dinv
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
-  if (q >= A.npos) return;
+  const int64_t q = A.rg.p0 + xcd_block() * kBlock + threadIdx.x;
+  if (q >= A.rg.p1 || !pos_mine(A.rg, q)) return;
   const int t0 = ptr[q], t1 = ptr[q + 1];
   if (t0 == t1) return;
   double m[ND * ND];
@@ -371,14 +379,14 @@ template <int ND, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
                                                      double reg) {
   __shared__ double red[kBlock / 64];
-  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& A = L.A;
+  const int64_t i = A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
   double g = 0.0;
-  if (i - (threadIdx.x & 63) < A.n) {
+  if (i - (threadIdx.x & 63) < A.rg.hi) {
     int64_t base;
     int w;
     slice_of(A, i, base, w);
-    if (i < A.n) {
+    if (i >= A.rg.lo && i < A.rg.hi) {
       double D[ND * ND], Di[ND * ND];
       if (L0) {
         double s6[6];
@@ -457,12 +465,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   const AmgMatD& P = L.P;
   const int64_t xb = xcd_block();
   const int k = (int)(xb % P.wmax);
-  const int64_t i = (xb / P.wmax) * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= P.n) return;
+  const int64_t i = P.rg.lo64() + (xb / P.wmax) * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= P.rg.hi) return;
   int64_t base;
   int w;
   slice_of(P, i, base, w);
-  if (i >= P.n || k >= w) return;
+  if (i < P.rg.lo || i >= P.rg.hi || k >= w) return;
   const int64_t q = base + (int64_t)k * 64;
   const int32_t J = P.col[q];
   if (J < 0) return;
@@ -490,17 +498,19 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
 // have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
-  if (q < L.R.npos && L.R.col[q] >= 0) {  // R = Pᵀ (f32) in R's own SELL layout
+  const int64_t k = xcd_block() * kBlock + threadIdx.x;
+  const int64_t qr = L.R.rg.p0 + k;
+  if (qr < L.R.rg.p1 && L.R.col[qr] >= 0 && pos_mine(L.R.rg, qr)) {  // R = Pᵀ (f32) in R's own SELL layout
     double p[ND * ND], t[ND * ND];
-    bload<ND>(L.P.val, L.P.npos, L.rp[q], p);
+    bload<ND>(L.P.val, L.P.npos, L.rp[qr], p);
 #pragma unroll
     for (int a = 0; a < ND; ++a)
 #pragma unroll
       for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
-    bstore<ND>(L.R.val32, L.R.npos, q, t);
+    bstore<ND>(L.R.val32, L.R.npos, qr, t);
   }
-  if (q >= L.AP.npos || L.AP.col[q] < 0) return;
+  const int64_t q = L.AP.rg.p0 + k;
+  if (q >= L.AP.rg.p1 || L.AP.col[q] < 0 || !pos_mine(L.AP.rg, q)) return;
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
@@ -512,8 +522,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
-  if (q >= Ac.npos || Ac.col[q] < 0) return;
+  const int64_t q = L.ac_rg.p0 + xcd_block() * kBlock + threadIdx.x;
+  if (q >= L.ac_rg.p1 || Ac.col[q] < 0 || !pos_mine(L.ac_rg, q)) return;
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
@@ -531,8 +541,9 @@ template <int ND, class TB, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __restrict__ b,
                                                       const int32_t* gate) {
   const bool run = gate_open(gate);
-  const int64_t i = xcd_block() * kBlock + threadIdx.x;
-  const int64_t n = L.A.n;
+  const int64_t i = L.A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = L.A.rg.hi;
+  const bool mine = i >= L.A.rg.lo && i < n;
   if (i - (threadIdx.x & 63) >= n) return;
   const int64_t ii = i < n ? i : n - 1;
   int64_t base;
@@ -544,26 +555,27 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid(AmgLevD L, const TB* __res
     sell_mac<ND, true, 2, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
   else
     sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-  if (i < n && run) vstore<ND>(L.t, i, y);
+  if (mine && run) vstore<ND>(L.t, i, y);
 }
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, const int32_t* gate) {
   const bool run = gate_open(gate);
-  const int64_t I = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& R = L.R;
-  if (I - (threadIdx.x & 63) >= R.n) return;
+  const int64_t I = R.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = R.rg.hi;
+  if (I - (threadIdx.x & 63) >= n) return;
   int64_t base;
   int w;
   slice_of(R, I, base, w);
   const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
   float Di[ND * ND];
-  dinv_load<ND>(N.dinv32, I < R.n ? I : R.n - 1, Di);
+  dinv_load<ND>(N.dinv32, I < n ? I : n - 1, Di);
   float bc[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
   sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.t, bc);  // R = Pᵀ blocks
-  if (I >= R.n || !run) return;
+  if (I < R.rg.lo || I >= n || !run) return;
   vstore<ND>(N.b, I, bc);
   float xn[ND];
   dinv_mul<ND>(Di, sc, bc, xn);
@@ -619,10 +631,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict_s(AmgLevD L, AmgLevD N,
   const bool run = gate_open(gate);
   const int64_t t = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& R = L.R;
-  const int64_t I = t / S;
+  const int64_t I = R.rg.lo64() + t / S;
   const int sub = (int)(t % S);
-  if (I - (threadIdx.x & 63) / S >= R.n) return;  // whole wave past the end
-  const int64_t Ic = I < R.n ? I : R.n - 1;
+  const int64_t n = R.rg.hi;
+  if (I - (threadIdx.x & 63) / S >= n) return;  // whole wave past the end
+  const int64_t Ic = I < n ? I : n - 1;
   int64_t base;
   int w;
   slice_of(R, Ic, base, w);
@@ -632,7 +645,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict_s(AmgLevD L, AmgLevD N,
 #pragma unroll
   for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
   sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.t, bc);
-  if (I >= R.n || sub != 0 || !run) return;
+  if (I < R.rg.lo || I >= n || sub != 0 || !run) return;
   vstore<ND>(N.b, I, bc);
   float xn[ND];
   dinv_mul<ND>(Di, sc, bc, xn);
@@ -644,8 +657,8 @@ template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_resid_s(AmgLevD L, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t t = xcd_block() * kBlock + threadIdx.x;
-  const int64_t n = L.A.n;
-  const int64_t i = t / S;
+  const int64_t n = L.A.rg.hi;
+  const int64_t i = L.A.rg.lo64() + t / S;
   const int sub = (int)(t % S);
   if (i - (threadIdx.x & 63) / S >= n) return;
   const int64_t ii = i < n ? i : n - 1;
@@ -659,14 +672,14 @@ __global__ __launch_bounds__(kBlock) void k_amg_resid_s(AmgLevD L, const int32_t
     for (int a = 0; a < ND; ++a) y[a] = 0.0f;
   }
   sell_mac_sub<ND, S, true>(L.A.col, L.A.val32, base, w, sub, L.x, y);
-  if (i < n && sub == 0 && run) vstore<ND>(L.t, i, y);
+  if (i >= L.A.rg.lo && i < n && sub == 0 && run) vstore<ND>(L.t, i, y);
 }
 template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_post_s(AmgLevD L, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t t = xcd_block() * kBlock + threadIdx.x;
-  const int64_t n = L.A.n;
-  const int64_t i = t / S;
+  const int64_t n = L.A.rg.hi;
+  const int64_t i = L.A.rg.lo64() + t / S;
   const int sub = (int)(t % S);
   if (i - (threadIdx.x & 63) / S >= n) return;
   const int64_t ii = i < n ? i : n - 1;
@@ -686,31 +699,33 @@ __global__ __launch_bounds__(kBlock) void k_amg_post_s(AmgLevD L, const int32_t*
   dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
-  if (i < n && sub == 0 && run) vstore<ND>(L.e, i, x);
+  if (i >= L.A.rg.lo && i < n && sub == 0 && run) vstore<ND>(L.e, i, x);
 }
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_prolong(AmgLevD L, AmgLevD N, const int32_t* gate) {
   const bool run = gate_open(gate);
-  const int64_t i = xcd_block() * kBlock + threadIdx.x;
   const AmgMatD& P = L.P;
-  if (i - (threadIdx.x & 63) >= P.n) return;
+  const int64_t i = P.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = P.rg.hi;
+  if (i - (threadIdx.x & 63) >= n) return;
   int64_t base;
   int w;
   slice_of(P, i, base, w);
-  const int64_t ii = i < P.n ? i : P.n - 1;
+  const int64_t ii = i < n ? i : n - 1;
   float x[ND];
   vload<ND>(L.x, ii, x);
   sell_mac<ND, false>(P.col, P.val32, P.npos, base, w, N.coarsest ? N.x : N.e, x);
-  if (i < P.n && run) vstore<ND>(L.x, i, x);
+  if (i >= P.rg.lo && i < n && run) vstore<ND>(L.x, i, x);
 }
 
 template <int ND, class TB, class TE, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __restrict__ b, TE* __restrict__ e,
                                                      const int32_t* gate) {
   const bool run = gate_open(gate);
-  const int64_t i = xcd_block() * kBlock + threadIdx.x;
-  const int64_t n = L.A.n;
+  const int64_t i = L.A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = L.A.rg.hi;
+  const bool mine = i >= L.A.rg.lo && i < n;
   if (i - (threadIdx.x & 63) >= n) return;
   const int64_t ii = i < n ? i : n - 1;
   int64_t base;
@@ -728,7 +743,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
   dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
-  if (i < n && run) vstore<ND>(e, i, x);
+  if (mine && run) vstore<ND>(e, i, x);
 }
 
 // ---------------------------------------------------------------------------
@@ -929,8 +944,8 @@ __device__ __forceinline__ void vcycle_entry(const AmgLevD& L0, const AmgCg& cg,
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, const double* __restrict__ b_row) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= cg.n) return;
+  const int64_t i = cg.lo + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= cg.hi) return;
   double r[ND], z[ND];
 #pragma unroll
   for (int a = 0; a < ND; ++a) {
@@ -952,8 +967,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
-  for (int64_t i = xcd_block() * BS + threadIdx.x; i - lane < cg.n; i += stride) {
-    const int64_t ii = i < cg.n ? i : cg.n - 1;
+  for (int64_t i = cg.lo64() + xcd_block() * BS + threadIdx.x; i - lane < cg.hi; i += stride) {
+    const int64_t ii = i < cg.hi ? i : cg.hi - 1;
     int64_t base;
     int w;
     slice_of(L0.A, ii, base, w);
@@ -963,7 +978,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
     sell_mac<ND, false, 1, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
-    if (i >= cg.n) continue;
+    if (i < cg.lo || i >= cg.hi) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
         const int64_t q = d.gslot[t];
@@ -1045,10 +1060,10 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
   // return in order: the scalars need only the partials) and are in flight
   // while α, β are formed
   const int64_t stride = (int64_t)gridDim.x * BS;
-  const int64_t i0 = (int64_t)blockIdx.x * BS + threadIdx.x;
+  const int64_t i0 = cg.lo + (int64_t)blockIdx.x * BS + threadIdx.x;
   double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
-  if (cg.n > 0) {
-    const int64_t k = i0 < cg.n ? i0 : cg.n - 1;
+  if (cg.hi > cg.lo) {
+    const int64_t k = i0 < cg.hi ? i0 : cg.hi - 1;
     vload<ND>(cg.u, k, u);
     vload<ND>(cg.w, k, w);
     vload<ND>(cg.p, k, p);
@@ -1060,7 +1075,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
   cg_record(slots, j, S, cs);
   if (cs.status != kRun) return;
   const double alpha = cs.alpha, beta = cs.beta;
-  for (int64_t i = i0; i < cg.n; i += stride) {
+  for (int64_t i = i0; i < cg.hi; i += stride) {
     if (i != i0) {
       vload<ND>(cg.u, i, u);
       vload<ND>(cg.w, i, w);
@@ -1086,8 +1101,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
 
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_finish(AmgCg cg, double* __restrict__ x_row) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= cg.n) return;
+  const int64_t i = cg.lo + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= cg.hi) return;
 #pragma unroll
   for (int a = 0; a < ND; ++a) x_row[3 * (int64_t)cg.row0[i] + a] = cg.x[ND * i + a];
 }
@@ -1109,10 +1124,11 @@ static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBl
 // overrides the choice (mfea_set_option "amg_w_block").
 int amg_w_block(const AmgCg& cg) {
   if (cg.w_block > 0) return cg.w_block;
-  return cg.n > (int64_t)kCgMaxG * 512 ? 768 : cg.n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS;
+  const int64_t n = cg.hi > cg.lo ? cg.hi - cg.lo64() : 0;
+  return n > (int64_t)kCgMaxG * 512 ? 768 : n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS;
 }
 int64_t amg_w_grid(const AmgCg& cg) {
-  const int64_t n = cg.n;
+  const int64_t n = cg.hi > cg.lo ? cg.hi - cg.lo64() : 0;
   const int bs = amg_w_block(cg);
   const int64_t g = (n + bs - 1) / bs;
   return g < 1 ? 1 : (g > kCgMaxG ? kCgMaxG : g);
@@ -1123,8 +1139,8 @@ template <int ND>
 static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
                   const int32_t* a, double reg) {
   if (L0.A.n <= 0) return;
-  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.npos), dim3(kBlock), 0, s, L0.A, sop, p, a, L0.omega);
-  hipLaunchKernelGGL((k_amg_dinv<ND, true>), rows_grid(L0.A.n), dim3(kBlock), 0, s, L0, sop, row0, reg);
+  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.rg.npos()), dim3(kBlock), 0, s, L0.A, sop, p, a, L0.omega);
+  hipLaunchKernelGGL((k_amg_dinv<ND, true>), rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
                    const int32_t* a0_ptr, const int32_t* a0_a, double reg) {
@@ -1133,20 +1149,22 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 }
 
 template <int ND>
-static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool level0) {
+static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool level0, int stage) {
   if (L.A.n <= 0) return;
-  const dim3 g = rows_grid(L.A.n);
   // level 0's k_amg_dinv ran in launch_amg_a0 (it also forms the diagonal)
-  if (!level0) hipLaunchKernelGGL((k_amg_dinv<ND, false>), g, dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+  if (stage & kSetupDinv && !level0)
+    hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   if (L.coarsest || !N) return;
-  if (L.P.wmax > 0)
-    hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.n).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.npos, L.R.npos)), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(N->A.npos), dim3(kBlock), 0, s, L, N->A, N->omega);
+  if (stage & kSetupP && L.P.wmax > 0)
+    hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.rg.span()).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
+  if (stage & kSetupAP)
+    hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
+  if (stage & kSetupAC)
+    hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, N->A, N->omega);
 }
-void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0) {
-  if (nd == 2) setup_nd<2>(s, L, next, level0);
-  else setup_nd<3>(s, L, next, level0);
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0, int stage) {
+  if (nd == 2) setup_nd<2>(s, L, next, level0, stage);
+  else setup_nd<3>(s, L, next, level0, stage);
 }
 
 // lanes per row: the restriction by R's mean slice width, the f32 operators
@@ -1159,7 +1177,7 @@ static int lanes_for(const AmgMatD& M, int forced, double two, double four) {
 }
 template <int ND>
 static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
-  const int64_t n = L.R.n;
+  const int64_t n = L.R.rg.span();
   const int S = lanes_for(L.R, L.rlanes, 2.5, 5.0);
   const dim3 b(kBlock);
   if (S == 8) hipLaunchKernelGGL((k_amg_restrict_s<ND, 8>), rows_grid(8 * n), b, 0, s, L, N, gate);
@@ -1169,7 +1187,7 @@ static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, c
 }
 template <int ND>
 static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t* gate) {
-  const int64_t n = L.A.n;
+  const int64_t n = L.A.rg.span();
   const int S = lanes_for(L.A, L.alanes, 3.5, 8.0);
   const dim3 b(kBlock);
   if (S == 4) {
@@ -1186,16 +1204,38 @@ static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t*
   }
 }
 
+// the V-cycle's steps on level l (level 0 reads the CG's f64 r and writes
+// its u; the others their f32 b, e)
+template <int ND>
+static void resid_nd(hipStream_t s, const AmgLevD* lev, int l, const AmgCg& cg, const int32_t* gate) {
+  if (l == 0)
+    hipLaunchKernelGGL((k_amg_resid<ND, double, true>), rows_grid(lev[0].A.rg.span()), dim3(kBlock), 0, s, lev[0],
+                       (const double*)cg.r, gate);
+  else
+    launch_op<ND>(s, lev[l], false, gate);
+}
+template <int ND>
+static void post_nd(hipStream_t s, const AmgLevD* lev, int l, const AmgCg& cg, const int32_t* gate) {
+  if (l == 0)
+    hipLaunchKernelGGL((k_amg_post<ND, double, float, true>), rows_grid(lev[0].A.rg.span()), dim3(kBlock), 0, s,
+                       lev[0], (const double*)cg.r, cg.u, gate);
+  else
+    launch_op<ND>(s, lev[l], true, gate);
+}
+template <int ND>
+static void prolong_nd(hipStream_t s, const AmgLevD* lev, int l, const int32_t* gate) {
+  hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].P.rg.span()), dim3(kBlock), 0, s, lev[l], lev[l + 1], gate);
+}
+
+// The V-cycle of levels [l0, nlev) on level l0's b, x (the producer of b set
+// x = ω D⁻¹ b), leaving level l0's output in its e (level 0: the CG's u).
 template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                      int tail, const int32_t* gate) {
-  const dim3 b(kBlock);
+                      int tail, const int32_t* gate, int l0) {
+  if (tail > 0 && tail < l0) tail = l0;
   const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
-  for (int l = 0; l < top; ++l) {
-    if (l == 0)
-      hipLaunchKernelGGL((k_amg_resid<ND, double, true>), rows_grid(lev[0].A.n), b, 0, s, lev[0], (const double*)cg.r, gate);
-    else
-      launch_op<ND>(s, lev[l], false, gate);
+  for (int l = l0; l < top; ++l) {
+    resid_nd<ND>(s, lev, l, cg, gate);
     launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
   }
   if (tail > 0) {
@@ -1210,23 +1250,37 @@ static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& 
     else
       hipLaunchKernelGGL(k_amg_tail<ND>, dim3(1), dim3(kTailBS), 0, s, tl, tail, nlev, gate);
   }
-  for (int l = top - 1; l >= 0; --l) {
-    hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].A.n), b, 0, s, lev[l], lev[l + 1], gate);
-    if (l == 0)
-      hipLaunchKernelGGL((k_amg_post<ND, double, float, true>), rows_grid(lev[0].A.n), b, 0, s, lev[0],
-                         (const double*)cg.r, cg.u, gate);
-    else
-      launch_op<ND>(s, lev[l], true, gate);
+  for (int l = top - 1; l >= l0; --l) {
+    prolong_nd<ND>(s, lev, l, gate);
+    post_nd<ND>(s, lev, l, cg, gate);
   }
 }
+static int clamp_tail(int tail, int nlev) {
+  if (tail >= nlev - 1) return 0;  // nothing below the coarsest to fuse
+  if (tail > 0 && nlev - tail > kTailMaxLev) return nlev - kTailMaxLev;  // the kernel argument holds 4 levels
+  return tail;
+}
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       int tail, const int32_t* gate) {
+                       int tail, const int32_t* gate, int l0) {
   // one level: the coarsest solve u = D⁻¹ r is done by the producer of r
-  if (nlev <= 1 || lev[0].A.n <= 0) return;
-  if (tail >= nlev - 1) tail = 0;  // nothing below the coarsest to fuse
-  if (tail > 0 && nlev - tail > kTailMaxLev) tail = nlev - kTailMaxLev;  // the kernel argument holds 4 levels
-  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, tail, gate);
-  else vcycle_nd<3>(s, lev, nlev, cg, tail, gate);
+  if (nlev <= 1 || lev[0].A.n <= 0 || l0 >= nlev - 1) return;
+  tail = clamp_tail(tail, nlev);
+  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, tail, gate, l0);
+  else vcycle_nd<3>(s, lev, nlev, cg, tail, gate, l0);
+}
+void launch_amg_vstep(hipStream_t s, int nd, const AmgLevD* lev, int l, const AmgCg& cg, int step,
+                      const int32_t* gate) {
+  if (nd == 2) {
+    if (step == kStepResid) resid_nd<2>(s, lev, l, cg, gate);
+    else if (step == kStepRestrict) launch_restrict<2>(s, lev[l], lev[l + 1], gate);
+    else if (step == kStepProlong) prolong_nd<2>(s, lev, l, gate);
+    else post_nd<2>(s, lev, l, cg, gate);
+  } else {
+    if (step == kStepResid) resid_nd<3>(s, lev, l, cg, gate);
+    else if (step == kStepRestrict) launch_restrict<3>(s, lev[l], lev[l + 1], gate);
+    else if (step == kStepProlong) prolong_nd<3>(s, lev, l, gate);
+    else post_nd<3>(s, lev, l, cg, gate);
+  }
 }
 
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows) {
@@ -1236,9 +1290,9 @@ int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows) {
 }
 
 void launch_amg_cg_init(hipStream_t s, int nd, const AmgLevD& L0, const AmgCg& cg, const double* b_row) {
-  if (cg.n <= 0) return;
-  if (nd == 2) hipLaunchKernelGGL(k_amg_cg_init<2>, rows_grid(cg.n), dim3(kBlock), 0, s, L0, cg, b_row);
-  else hipLaunchKernelGGL(k_amg_cg_init<3>, rows_grid(cg.n), dim3(kBlock), 0, s, L0, cg, b_row);
+  if (cg.hi <= cg.lo) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_cg_init<2>, rows_grid(cg.hi - cg.lo), dim3(kBlock), 0, s, L0, cg, b_row);
+  else hipLaunchKernelGGL(k_amg_cg_init<3>, rows_grid(cg.hi - cg.lo), dim3(kBlock), 0, s, L0, cg, b_row);
 }
 
 template <int ND, int BS>
@@ -1291,7 +1345,7 @@ template <int ND, int BS, bool DIST>
 static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
                    const SolveState* st, double* part, const AmgDist& d) {
   const int64_t gw = amg_w_grid(cg);  // partials to reduce = the w kernel's blocks
-  int64_t gu = (cg.n + BS - 1) / BS;
+  int64_t gu = (cg.hi - cg.lo + BS - 1) / BS;
   gu = gu < 1 ? 1 : (gu > kCgMaxG ? kCgMaxG : gu);
   const dim3 g((unsigned)gu);
   switch (DIST ? 1 : pu_of_grid(gw)) {
@@ -1314,9 +1368,82 @@ void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const
 }
 
 void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row) {
-  if (cg.n <= 0) return;
-  if (nd == 2) hipLaunchKernelGGL(k_amg_finish<2>, rows_grid(cg.n), dim3(kBlock), 0, s, cg, x_row);
-  else hipLaunchKernelGGL(k_amg_finish<3>, rows_grid(cg.n), dim3(kBlock), 0, s, cg, x_row);
+  if (cg.hi <= cg.lo) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_finish<2>, rows_grid(cg.hi - cg.lo), dim3(kBlock), 0, s, cg, x_row);
+  else hipLaunchKernelGGL(k_amg_finish<3>, rows_grid(cg.hi - cg.lo), dim3(kBlock), 0, s, cg, x_row);
+}
+
+// ---------------------------------------------------------------------------
+// exchanges (distributed V-cycle / setup): pack / unpack of listed items
+// ---------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_xpack(const T* __restrict__ src, const int32_t* __restrict__ idx,
+                                                  int64_t n, int width, T* __restrict__ buf) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n * width) return;
+  const int64_t it = k / width, c = k - it * width;
+  buf[k] = src[(int64_t)idx[it] * width + c];
+}
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_xunpack(const T* __restrict__ buf, const int32_t* __restrict__ idx,
+                                                    int64_t n, int width, T* __restrict__ dst) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n * width) return;
+  const int64_t it = k / width, c = k - it * width;
+  dst[(int64_t)idx[it] * width + c] = buf[k];
+}
+void launch_xpack(hipStream_t s, const void* src, const int32_t* idx, int64_t n, int width, int bytes, void* buf) {
+  if (n <= 0) return;
+  if (bytes == 8)
+    hipLaunchKernelGGL(k_xpack<double>, rows_grid(n * width), dim3(kBlock), 0, s, (const double*)src, idx, n, width,
+                       (double*)buf);
+  else
+    hipLaunchKernelGGL(k_xpack<float>, rows_grid(n * width), dim3(kBlock), 0, s, (const float*)src, idx, n, width,
+                       (float*)buf);
+}
+void launch_xunpack(hipStream_t s, const void* buf, const int32_t* idx, int64_t n, int width, int bytes, void* dst) {
+  if (n <= 0) return;
+  if (bytes == 8)
+    hipLaunchKernelGGL(k_xunpack<double>, rows_grid(n * width), dim3(kBlock), 0, s, (const double*)buf, idx, n,
+                       width, (double*)dst);
+  else
+    hipLaunchKernelGGL(k_xunpack<float>, rows_grid(n * width), dim3(kBlock), 0, s, (const float*)buf, idx, n, width,
+                       (float*)dst);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_xinit_rows(AmgLevD N, const int32_t* __restrict__ rows, int64_t n,
+                                                           const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const int64_t i = rows[k];
+  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
+  float bc[ND], Di[ND * ND], xn[ND];
+  vload<ND>(N.b, i, bc);
+  dinv_load<ND>(N.dinv32, i, Di);
+  dinv_mul<ND>(Di, sc, bc, xn);
+  if (run) vstore<ND>(N.x, i, xn);
+}
+void launch_amg_xinit_rows(hipStream_t s, int nd, const AmgLevD& N, const int32_t* rows, int64_t n,
+                           const int32_t* gate) {
+  if (n <= 0) return;
+  if (nd == 2) hipLaunchKernelGGL(k_amg_xinit_rows<2>, rows_grid(n), dim3(kBlock), 0, s, N, rows, n, gate);
+  else hipLaunchKernelGGL(k_amg_xinit_rows<3>, rows_grid(n), dim3(kBlock), 0, s, N, rows, n, gate);
+}
+
+struct OmegaPtrs {
+  double* p[kMaxRanks];
+};
+__global__ void k_amg_bound_max(OmegaPtrs o, int n) {
+  if (threadIdx.x != 0) return;
+  double m = 0.0;
+  for (int k = 0; k < n; ++k) m = fmax(m, o.p[k][1]);
+  for (int k = 0; k < n; ++k) o.p[k][1] = m;
+}
+void launch_amg_bound_max(hipStream_t s, double* const* omegas, int n) {
+  OmegaPtrs o{};
+  for (int k = 0; k < n && k < kMaxRanks; ++k) o.p[k] = omegas[k];
+  hipLaunchKernelGGL(k_amg_bound_max, dim3(1), dim3(64), 0, s, o, n < kMaxRanks ? n : kMaxRanks);
 }
 
 }  // namespace mfea

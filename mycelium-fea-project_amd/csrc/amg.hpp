@@ -60,6 +60,13 @@ struct PosList {
 struct AmgLevel {
   SellPat A;                 // slot 0 of every row = its diagonal block
   bool coarsest = false;
+  // distributed plans (AmgPlan::n_dist > level): rank of every row (new
+  // labels), row boundaries per rank in the owner-major labelling of A / P
+  // rows (world + 1) and of the A·P rows (their own labelling)
+  std::vector<int32_t> owner;
+  std::vector<int64_t> own, ap_own;
+  std::vector<int32_t> aprow;  // distributed: row label → its A·P row label
+  std::vector<int32_t> nat;    // row label → natural (aggregation-order) index
   // ---- below: only for non-coarsest levels
   int64_t nc = 0;            // coarse rows (aggregates)
   std::vector<int32_t> agg;  // row → aggregate
@@ -83,6 +90,23 @@ struct AmgPlan {
   PosList a0;                 // per A_0 position: SELL slot positions (diag: none)
   int64_t pair_items = 0;     // Σ list lengths (memory / setup-traffic report)
   bool capped = false;        // max levels reached with couplings left
+  // distributed V-cycle (AmgDistSpec): levels [0, n_dist) are split over
+  // `world` ranks by row ranges; level n_dist and below are replicated (every
+  // rank holds and computes all of their rows).  n_dist = 0: one partition.
+  int world = 1;
+  int n_dist = 0;
+};
+
+// The distributed hierarchy (multi-GPU GAMG): ONE global
+// hierarchy, identical on every rank and equal to the one-partition
+// hierarchy (same aggregates), whose rows of levels [0, n_dist] are labelled
+// owner-major so each rank's rows are one contiguous range (an aggregate
+// belongs to the rank holding most of its rows).  A level is split while it
+// has more than rep_rows rows (level 0 always is).
+struct AmgDistSpec {
+  int world = 1;
+  std::vector<int32_t> owner;  // per Pattern free row [0, n_free): its rank
+  int64_t rep_rows = 32768;
 };
 
 // Builds the hierarchy for the free rows [0, P.n_free) of P with the element
@@ -90,8 +114,9 @@ struct AmgPlan {
 // max_levels caps the hierarchy (the coarsest level's block Jacobi is then
 // an inexact solve; plan.capped says so).  Measured: a cap costs far more in
 // iterations than it saves per cycle (C3: 16 → 35 iterations at 5 levels).
+// dist: the distributed form (NULL: one partition, the plan of before).
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
-                      int max_levels = kAmgMaxLevels);
+                      int max_levels = kAmgMaxLevels, const AmgDistSpec* dist = nullptr);
 
 // Partitioned solve (partition.hpp): the V-cycle is block Jacobi over the
 // partitions (each partition's hierarchy couples its own free rows only —
@@ -106,6 +131,45 @@ struct AmgHalo {
   std::vector<int32_t> gslot;      // SELL slot position of the assembled operator (K_ig = −S_e)
   std::vector<int32_t> grecv;      // index of the ghost's u in the received halo (xrecv order)
 };
+// ---- distributed V-cycle: one rank's share of a distributed plan ----------
+// One exchange of items (rows of a vector or SELL positions of a matrix):
+// per peer (ascending), the items this rank sends and receives, both sides
+// enumerating them in ascending item order (no negotiation).
+struct XPlan {
+  std::vector<int32_t> peers;
+  std::vector<int64_t> soff, scnt, roff, rcnt;  // per peer, in items
+  std::vector<int32_t> sidx, ridx;              // items, concatenated per peer
+  int64_t n_send() const { return (int64_t)sidx.size(); }
+  int64_t n_recv() const { return (int64_t)ridx.size(); }
+  bool empty() const { return sidx.empty() && ridx.empty(); }
+};
+struct AmgRank {
+  int rank = 0, world = 1, n_dist = 0;
+  // per level: rows this rank computes — A / P rows [lo, hi), A·P rows
+  // [aplo, aphi) — and of the level below, the coarse rows its restriction
+  // produces [rlo, rhi)
+  std::vector<int64_t> lo, hi, aplo, aphi, rlo, rhi;
+  // V-cycle, per split level l < n_dist: rows of level l read by this rank's
+  // A_l rows (x; level 0: also the CG's u), by its R_l rows (t), and rows of
+  // level l+1 read by its P_l rows (the coarse output; only while l+1 is split)
+  std::vector<XPlan> xa, xr, xp;
+  XPlan xg;  // level n_dist (replicated): every rank's restricted rows to all (b, x)
+  // numeric setup, per split level l: P positions of the rows its A·P and R
+  // rows read, A·P positions of the rows its A_{l+1} rows read
+  std::vector<XPlan> sp, sap;
+  XPlan sg;  // A positions of level n_dist: all-gather
+};
+// rank r's share of a distributed plan (plan.n_dist ≥ 1)
+std::string build_amg_rank(const AmgPlan& plan, int rank, AmgRank& out);
+// Level 0 of rank rk over ITS partition's pattern P (partition.hpp: local
+// node / element → global maps node_g, elem_g): row0 (level-0 row → P's row,
+// own rows only) and the A_0 slot lists (P's slots of every own row, by the
+// global level-0 row of their neighbour).  G: the whole mesh's pattern the
+// plan was built on; gkey: the global element activity.
+std::string build_amg_level0(const AmgPlan& plan, const Pattern& G, const AmgRank& rk, const Pattern& P,
+                             const std::vector<int64_t>& node_g, const std::vector<int64_t>& elem_g,
+                             const std::vector<uint8_t>& gkey, PosList& a0, std::vector<int32_t>& row0);
+
 // xsend_rows / xrecv_rows: Pattern rows of the plan's xsend / xrecv nodes
 std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
                            const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,

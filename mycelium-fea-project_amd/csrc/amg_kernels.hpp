@@ -16,10 +16,29 @@
 
 namespace mfea {
 
+// The rows of a matrix this rank computes (distributed V-cycle, amg.hpp
+// AmgRank; one partition: all of them) and their SELL positions.  A 64-row
+// slice ignores ownership, so the range's first and last slices may hold
+// other ranks' rows: positions below pf / from pl on are checked (pos_mine).
+struct RowRange {
+  int64_t lo = 0, hi = 0;  // rows [lo, hi)
+  int64_t p0 = 0, p1 = 0;  // SELL positions [p0, p1) of the slices holding them
+  int64_t pf = 0, pl = 0;  // end of the first slice's positions, start of the last's
+  int64_t s0 = 0, s1 = 0;  // first / last slice
+  int64_t rows() const { return hi > lo ? hi - lo : 0; }
+  // row kernels sweep from the slice boundary below lo (a wave's 64 rows
+  // must share one slice: slice_of reads the wave's first lane) and mask
+  // the rows below lo
+  __host__ __device__ int64_t lo64() const { return lo & ~(int64_t)63; }
+  int64_t span() const { return hi > lo ? hi - lo64() : 0; }
+  int64_t npos() const { return p1 > p0 ? p1 - p0 : 0; }
+};
+
 struct AmgMatD {
   int64_t n = 0;     // rows
   int64_t npos = 0;  // SELL positions (slot rows · 64)
   int32_t wmax = 0;  // widest slice (host side: launch geometry)
+  RowRange rg;       // rows this rank computes
   const int32_t* sptr = nullptr;
   const int32_t* col = nullptr;
   double* val = nullptr;   // [npos][NB2] f64 (setup)
@@ -60,11 +79,14 @@ struct AmgLevD {
   const int32_t* ac_ptr = nullptr;  // into level l+1's A.val
   const int32_t* ac_a = nullptr;
   const int32_t* ac_b = nullptr;
+  RowRange ac_rg;  // level l+1's A rows this rank's Galerkin product forms (= R's rows)
 };
 
 // CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
 struct AmgCg {
   int64_t n = 0;
+  int64_t lo = 0, hi = 0;  // level-0 rows this rank iterates (one partition: [0, n))
+  __host__ __device__ int64_t lo64() const { return lo & ~(int64_t)63; }
   int w_block = 0;  // w = A u kernel threads per block (0: by size)
   const int32_t* row0 = nullptr;  // level-0 row → Pattern (row-order) free row
   double* x = nullptr;
@@ -99,13 +121,33 @@ struct AmgDist {
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
                    const int32_t* a0_ptr, const int32_t* a0_a, double reg);
 // dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
-// (level0: its D⁻¹ was formed by launch_amg_a0)
-void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0);
+// (level0: its D⁻¹ was formed by launch_amg_a0).  stage: which of the four
+// steps (the distributed setup exchanges values between them)
+constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll = 15;
+void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0,
+                            int stage = kSetupAll);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).
+// l0 > 0: only levels [l0, nlev), on level l0's b and x (its output: e).
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       int tail, const int32_t* gate);
+                       int tail, const int32_t* gate, int l0 = 0);
+// one step of the V-cycle on level l (the distributed schedule interleaves
+// exchanges): t = b − A x, restriction into level l+1, x += P e_{l+1}, post-smoothing
+constexpr int kStepResid = 0, kStepRestrict = 1, kStepProlong = 2, kStepPost = 3;
+void launch_amg_vstep(hipStream_t s, int nd, const AmgLevD* lev, int l, const AmgCg& cg, int step,
+                      const int32_t* gate);
+// ---- exchanges of the distributed V-cycle and setup (amg.hpp XPlan): items
+// of `width` scalars, gathered into / scattered from a contiguous buffer
+void launch_xpack(hipStream_t s, const void* src, const int32_t* idx, int64_t n, int width, int bytes, void* buf);
+void launch_xunpack(hipStream_t s, const void* buf, const int32_t* idx, int64_t n, int width, int bytes, void* dst);
+// the first smoothing step x = s·D⁻¹ b (s = ω, 1 on the coarsest level) of
+// the listed rows of level N (the rows the replicated level's all-gather brought)
+void launch_amg_xinit_rows(hipStream_t s, int nd, const AmgLevD& N, const int32_t* rows, int64_t n,
+                           const int32_t* gate);
+// partitions on one device: every partition's Gershgorin bound g (omega[1])
+// set to the maximum over them (what an RCCL all-reduce max does across GPUs)
+void launch_amg_bound_max(hipStream_t s, double* const* omegas, int n);
 // first level l ≥ 1 (above the coarsest) with at most max_rows rows, or 0
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------

@@ -131,6 +131,19 @@ struct Part {
   AmgDist amg_dist;
   DevBuf<int32_t> amg_hi;  // send_rows | gptr | gslot | grecv
   DevBuf<double> amg_hd;   // usend | urecv
+  // distributed GAMG over the global hierarchy (mfea_handle::gamg): this
+  // partition's rows and exchange plans (amg.hpp AmgRank), the plans' item
+  // lists on the device and the staging buffers of one exchange
+  AmgRank amg_rank;
+  struct XDev {
+    const XPlan* x = nullptr;
+    const int32_t* s = nullptr;  // sidx
+    const int32_t* r = nullptr;  // ridx
+  };
+  std::vector<XDev> xd_a, xd_r, xd_p, xd_sp, xd_sap;
+  XDev xd_g, xd_sg;
+  DevBuf<int32_t> amg_xi;
+  DevBuf<double> amg_xs, amg_xr;
 };
 
 struct mfea_handle {
@@ -189,6 +202,19 @@ struct mfea_handle {
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
+  int opt_amg_dist = 1;           // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block Jacobi
+  int64_t opt_amg_rep_rows = 32768;  // distributed V-cycle: levels of at most this many rows are replicated
+  // distributed GAMG (partitioned handles, option "amg_dist" 1): the whole
+  // mesh's pattern and node owners (built with the partitions), and ONE
+  // global hierarchy for the current global element activity
+  Pattern gpat;
+  std::vector<int32_t> gowner;
+  AmgPlan gamg;
+  bool gamg_ok = false;
+  int64_t gamg_gen = 0;       // bumped on every rebuild (captured graphs hold its pointers)
+  int64_t act_gen = 1;        // bumped whenever the element activity may have changed
+  int64_t gamg_act_gen = 0;   // act_gen the hierarchy was built for
+  DevBuf<uint8_t> gact;       // RCCL: the global activity, max-all-reduced
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
   DevBuf<int32_t> c_indices;
@@ -446,6 +472,17 @@ int ensure_built(mfea_handle* h) {
     }
     RC(upload_part(h, pt, dm));
   }
+  if (dm) {  // distributed GAMG: the whole mesh's pattern and the node owners
+    h->gamg_ok = false;
+    h->gamg = AmgPlan();
+    h->gowner = part0(h).plan.owner;
+    const std::string err = build_pattern(h->N, h->xyz.data(), h->Ecount, h->e2n.data(), skip, h->top, h->bot,
+                                          order_mode(h), h->gpat);
+    if (!err.empty()) return fail(MFEA_EINVAL, err);
+  } else {
+    h->gpat = Pattern();
+  }
+  ++h->act_gen;
   {  // free DOFs of the whole mesh (reported in mfea_stats)
     std::vector<uint8_t> known(h->N, 0);
     for (int64_t t : h->top) known[t] = 1;
@@ -912,10 +949,27 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
 constexpr size_t kAmgAlign = 64;  // elements: every carved array starts 256/512-B aligned
 size_t amg_al(size_t n) { return (n + kAmgAlign - 1) / kAmgAlign * kAmgAlign; }
 
+// rows [lo, hi) of a SELL pattern and their positions (amg_kernels.hpp RowRange)
+RowRange row_range(const SellPat& S, int64_t lo, int64_t hi) {
+  RowRange g;
+  g.lo = lo;
+  g.hi = hi > lo ? hi : lo;
+  if (hi <= lo || S.sptr.size() < 2) return g;
+  g.s0 = lo >> 6;
+  g.s1 = (hi - 1) >> 6;
+  g.p0 = (int64_t)S.sptr[g.s0] * 64;
+  g.p1 = (int64_t)S.sptr[g.s1 + 1] * 64;
+  g.pf = (int64_t)S.sptr[g.s0 + 1] * 64;
+  g.pl = (int64_t)S.sptr[g.s1] * 64;
+  return g;
+}
+
 // Carves the plan's index arrays and the value / vector arrays out of two
 // device allocations and uploads the indices.  Pass 0 sizes, pass 1 carves.
-int upload_amg(mfea_handle* h, Part& pt) {
-  const AmgPlan& pl = pt.amg;
+// rk (distributed GAMG): this partition's row ranges, with its own level-0
+// lists over ITS pattern (a0, row0) in place of the plan's.
+int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
+               const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
   const int nd = pl.nd, nb2 = nd * nd;
   const int nlev = (int)pl.lev.size();
   hipStream_t s = h->stream;
@@ -982,7 +1036,9 @@ int upload_amg(mfea_handle* h, Part& pt) {
       const AmgLevel& L = pl.lev[l];
       AmgLevD& d = pt.amg_lev[l];
       const int64_t n = L.A.n;
+      const int64_t lo = rk ? rk->lo[l] : 0, hi = rk ? rk->hi[l] : n;
       d.A = mat(L.A, true, l > 0);
+      d.A.rg = row_range(L.A, lo, hi);
       if (l == 0) {  // A_0: symmetric blocks for the CG and the level-0 V-cycle kernels
         const size_t ns = (size_t)nd * (nd + 1) / 2;
         d.A.sym = D(ns * d.A.npos);
@@ -1002,11 +1058,16 @@ int upload_amg(mfea_handle* h, Part& pt) {
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, true, true);
+        d.P.rg = row_range(L.P, lo, hi);
         d.pv_ptr = I(L.pv.ptr);
         d.pv_a = I(L.pv.a);
+        const int64_t rlo = rk ? rk->rlo[l] : 0, rhi = rk ? rk->rhi[l] : L.R.n;
         d.R = mat(L.R, false, true);
+        d.R.rg = row_range(L.R, rlo, rhi);
+        d.ac_rg = row_range(pl.lev[l + 1].A, rlo, rhi);
         d.rp = I(L.rp);
         d.AP = mat(L.AP, false, false);
+        d.AP.rg = row_range(L.AP, rk ? rk->aplo[l] : 0, rk ? rk->aphi[l] : L.AP.n);
         d.apval = D((size_t)nb2 * d.AP.npos);
         d.ap_ptr = I(L.ap.ptr);
         d.ap_a = I(L.ap.a);
@@ -1016,12 +1077,14 @@ int upload_amg(mfea_handle* h, Part& pt) {
         d.ac_b = I(L.ac.b);
       }
     }
-    pt.amg_a0_ptr = I(pl.a0.ptr);
-    pt.amg_a0_a = I(pl.a0.a);
+    pt.amg_a0_ptr = I(a0 ? a0->ptr : pl.a0.ptr);
+    pt.amg_a0_a = I(a0 ? a0->a : pl.a0.a);
     const int64_t nf = nlev ? pl.lev[0].A.n : 0;
     pt.amg_cg.n = nf;
+    pt.amg_cg.lo = rk && nlev ? rk->lo[0] : 0;
+    pt.amg_cg.hi = rk && nlev ? rk->hi[0] : nf;
     pt.amg_cg.w_block = h->opt_amg_w_block;
-    pt.amg_cg.row0 = I(pl.row0);
+    pt.amg_cg.row0 = I(row0 ? *row0 : pl.row0);
     pt.amg_cg.x = D((size_t)nd * nf);
     pt.amg_cg.p = D((size_t)nd * nf);
     pt.amg_cg.s = D((size_t)nd * nf);
@@ -1033,7 +1096,10 @@ int upload_amg(mfea_handle* h, Part& pt) {
   {
     std::vector<int64_t> rows(nlev);
     for (int l = 0; l < nlev; ++l) rows[l] = pl.lev[l].A.n;
-    pt.amg_tail = amg_tail_level(rows.data(), nlev, h->opt_amg_tail_rows);
+    // the single-workgroup tail holds whole levels: never a split one
+    const int first = rk ? std::max(1, rk->n_dist) : 1;
+    pt.amg_tail = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_tail_rows) : 0;
+    if (pt.amg_tail > 0) pt.amg_tail += first - 1;
   }
   HIPC(hipStreamSynchronize(s));
   return 0;
@@ -1113,7 +1179,8 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
   const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
-  RC(upload_amg(h, pt));
+  h->gamg_ok = false;  // the device arrays now hold this plan
+  RC(upload_amg(h, pt, pt.amg));
   if (dm) RC(upload_amg_halo(h, pt, key));
   pt.amg_key = key;
   pt.amg_ok = true;
@@ -1328,6 +1395,424 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   rc = finish_solve(h, fin, st);
   if (st) {
     st->amg_levels = (int32_t)pt.amg_lev.size();
+    st->amg_rebuilt = rebuilt ? 1 : 0;
+  }
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Distributed GAMG over ONE global hierarchy (option "amg_dist" 1, the
+// default of partitioned handles).  Every rank builds the same
+// hierarchy from the whole mesh — the one-partition hierarchy, so the solve
+// needs the one-partition iteration count — and computes only its own rows of
+// the split levels (amg.hpp AmgRank); the values a rank's rows read from
+// other ranks arrive through the exchanges below.  Levels of at most
+// "amg_rep_rows" rows are replicated: every rank holds and computes all of them.
+// ---------------------------------------------------------------------------
+// The global element activity (original order).  Partitions on one device:
+// each partition's own elements; RCCL: a max-all-reduce of E bytes (a rank
+// contributes the elements it reports, 0 elsewhere).
+int global_active(mfea_handle* h, std::vector<uint8_t>& key) {
+  key.assign(h->Ecount, 0);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const int64_t E = pt.P.n_elems;
+    std::vector<uint8_t> a(E);
+    if (E) HIPC(hipMemcpy(a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    for (int64_t le = 0; le < E; ++le)
+      if (pt.plan.elem_own[le]) key[pt.plan.elem_g[le]] = a[le];
+  }
+  if (h->world > 1 && h->Ecount) {
+    HIPC(h->gact.alloc(h->Ecount));
+    HIPC(hipMemcpyAsync(h->gact.ptr, key.data(), h->Ecount, hipMemcpyHostToDevice, h->stream));
+    NCCLC(ncclAllReduce(h->gact.ptr, h->gact.ptr, (size_t)h->Ecount, ncclUint8, ncclMax, h->comm, h->stream));
+    HIPC(hipMemcpyAsync(key.data(), h->gact.ptr, h->Ecount, hipMemcpyDeviceToHost, h->stream));
+    RC(sync_stream(h));
+  }
+  return 0;
+}
+
+// the partition's exchange plans on the device (item lists carved from one
+// allocation) and staging buffers for the largest transfer
+int upload_xplans(mfea_handle* h, Part& pt) {
+  const AmgRank& rk = pt.amg_rank;
+  const int nd = h->gamg.nd;
+  size_t items = 0, stage = 1;
+  auto size = [&](const XPlan& x, int width_bytes) {
+    items += x.sidx.size() + x.ridx.size() + 2;
+    stage = std::max(stage, (size_t)std::max(x.n_send(), x.n_recv()) * width_bytes);
+  };
+  for (const auto& x : rk.xa) size(x, 4 * nd);
+  for (const auto& x : rk.xr) size(x, 4 * nd);
+  for (const auto& x : rk.xp) size(x, 4 * nd);
+  size(rk.xg, 4 * nd);
+  for (const auto& x : rk.sp) size(x, 8 * nd * nd);
+  for (const auto& x : rk.sap) size(x, 8 * nd * nd);
+  size(rk.sg, 8 * nd * nd);
+  HIPC(pt.amg_xi.alloc(items));
+  HIPC(pt.amg_xs.alloc(stage / 8 + 1));
+  HIPC(pt.amg_xr.alloc(stage / 8 + 1));
+  int32_t* ip = pt.amg_xi.ptr;
+  hipStream_t s = h->stream;
+  auto put = [&](const XPlan& x) -> Part::XDev {
+    Part::XDev d;
+    d.x = &x;
+    d.s = ip;
+    if (!x.sidx.empty()) (void)hipMemcpyAsync(ip, x.sidx.data(), x.sidx.size() * 4, hipMemcpyHostToDevice, s);
+    ip += x.sidx.size() + 1;
+    d.r = ip;
+    if (!x.ridx.empty()) (void)hipMemcpyAsync(ip, x.ridx.data(), x.ridx.size() * 4, hipMemcpyHostToDevice, s);
+    ip += x.ridx.size() + 1;
+    return d;
+  };
+  pt.xd_a.clear();
+  pt.xd_r.clear();
+  pt.xd_p.clear();
+  pt.xd_sp.clear();
+  pt.xd_sap.clear();
+  for (const auto& x : rk.xa) pt.xd_a.push_back(put(x));
+  for (const auto& x : rk.xr) pt.xd_r.push_back(put(x));
+  for (const auto& x : rk.xp) pt.xd_p.push_back(put(x));
+  pt.xd_g = put(rk.xg);
+  for (const auto& x : rk.sp) pt.xd_sp.push_back(put(x));
+  for (const auto& x : rk.sap) pt.xd_sap.push_back(put(x));
+  pt.xd_sg = put(rk.sg);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// (Re)build the global hierarchy when the element activity may have changed
+// (act_gen) and actually did.
+int ensure_gamg(mfea_handle* h, bool* rebuilt) {
+  *rebuilt = false;
+  if (h->gamg_ok && h->gamg_act_gen == h->act_gen) return 0;
+  std::vector<uint8_t> key;
+  RC(global_active(h, key));
+  if (h->gamg_ok && part0(h).amg_key == key) {
+    h->gamg_act_gen = h->act_gen;
+    return 0;
+  }
+  h->gamg_ok = false;
+  AmgDistSpec spec;
+  spec.world = nranks(h);
+  spec.rep_rows = h->opt_amg_rep_rows;
+  spec.owner.resize(h->gpat.n_free);
+  for (int64_t i = 0; i < h->gpat.n_free; ++i) spec.owner[i] = h->gowner[h->gpat.perm[i]];
+  std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec);
+  if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+  destroy_graph(h);
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    err = build_amg_rank(h->gamg, pt.rank, pt.amg_rank);
+    if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+    PosList a0;
+    std::vector<int32_t> row0;
+    err = build_amg_level0(h->gamg, h->gpat, pt.amg_rank, pt.P, pt.plan.node_g, pt.plan.elem_g, key, a0, row0);
+    if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+    pt.amg = AmgPlan();  // the block-Jacobi plan (if any) is stale now
+    pt.amg_ok = false;
+    RC(upload_amg(h, pt, h->gamg, &pt.amg_rank, &a0, &row0));
+    RC(upload_xplans(h, pt));
+    AmgDist& d = pt.amg_dist;
+    d = AmgDist{};
+    d.rank = pt.rank;
+    d.gall[0] = pt.dv.gall[0];
+    d.gall[1] = pt.dv.gall[1];
+    d.gsend = pt.dv.gsend;
+    pt.amg_key = key;
+  }
+  h->gamg_ok = true;
+  h->gamg_act_gen = h->act_gen;
+  ++h->gamg_gen;
+  *rebuilt = true;
+  return 0;
+}
+
+// One exchange of the distributed GAMG on every partition: pack the items of
+// plan(pt) from vec(pt) (width scalars of `bytes` each), one RCCL group of
+// point-to-point transfers (partitions on one device: device copies), unpack
+// into the same array.
+template <class GetPlan, class GetVec>
+int gx(mfea_handle* h, GetPlan plan, GetVec vec, int width, int bytes) {
+  hipStream_t s = h->stream;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Part::XDev& d = plan(pt);
+    launch_xpack(s, vec(pt), d.s, d.x->n_send(), width, bytes, pt.amg_xs.ptr);
+  }
+  HIPC(hipGetLastError());
+  const size_t item = (size_t)width * bytes;
+  if (h->world > 1) {
+    Part& pt = part0(h);
+    const XPlan& x = *plan(pt).x;
+    if (!x.peers.empty()) {
+      const ncclDataType_t t = bytes == 8 ? ncclFloat64 : ncclFloat32;
+      char* sb = reinterpret_cast<char*>(pt.amg_xs.ptr);
+      char* rb = reinterpret_cast<char*>(pt.amg_xr.ptr);
+      NCCLC(ncclGroupStart());
+      for (size_t i = 0; i < x.peers.size(); ++i) {
+        if (x.scnt[i])
+          NCCLC(ncclSend(sb + x.soff[i] * item, (size_t)(x.scnt[i] * width), t, x.peers[i], h->comm, s));
+        if (x.rcnt[i])
+          NCCLC(ncclRecv(rb + x.roff[i] * item, (size_t)(x.rcnt[i] * width), t, x.peers[i], h->comm, s));
+      }
+      NCCLC(ncclGroupEnd());
+    }
+  } else {
+    for (auto& a : h->parts) {
+      const XPlan& xa = *plan(*a).x;
+      for (size_t i = 0; i < xa.peers.size(); ++i) {
+        if (!xa.scnt[i]) continue;
+        Part& b = *h->parts[xa.peers[i]];
+        const XPlan& xb = *plan(b).x;
+        const auto it = std::lower_bound(xb.peers.begin(), xb.peers.end(), a->rank);
+        const size_t jb = (size_t)(it - xb.peers.begin());
+        if (it == xb.peers.end() || *it != a->rank || xb.rcnt[jb] != xa.scnt[i])
+          return fail(MFEA_EINVAL, "internal: asymmetric GAMG exchange plan");
+        HIPC(hipMemcpyAsync(reinterpret_cast<char*>(b.amg_xr.ptr) + xb.roff[jb] * item,
+                            reinterpret_cast<const char*>(a->amg_xs.ptr) + xa.soff[i] * item, xa.scnt[i] * item,
+                            hipMemcpyDeviceToDevice, s));
+      }
+    }
+  }
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Part::XDev& d = plan(pt);
+    launch_xunpack(s, pt.amg_xr.ptr, d.r, d.x->n_recv(), width, bytes, vec(pt));
+  }
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// level l's Gershgorin bound: the maximum over the ranks (every rank then
+// takes the same smoother weight ω_l and forms the same P_l)
+int bound_max(mfea_handle* h, int l) {
+  if (h->world > 1) {
+    double* om = part0(h).amg_lev[l].omega + 1;
+    NCCLC(ncclAllReduce(om, om, 1, ncclFloat64, ncclMax, h->comm, h->stream));
+    return 0;
+  }
+  std::vector<double*> oms;
+  for (auto& pp : h->parts) oms.push_back(pp->amg_lev[l].omega);
+  launch_amg_bound_max(h->stream, oms.data(), (int)oms.size());
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+// the per-solve numeric setup, split levels with their exchanges
+int enqueue_gamg_setup(mfea_handle* h, double reg) {
+  hipStream_t s = h->stream;
+  const AmgPlan& pl = h->gamg;
+  const int nd = pl.nd, nb2 = nd * nd, nlev = (int)pl.lev.size(), ns = pl.n_dist;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  }
+  HIPC(hipGetLastError());
+  RC(bound_max(h, 0));
+  for (int l = 0; l < nlev; ++l) {
+    const bool split = l < ns;
+    auto stage = [&](int st) -> int {
+      for (auto& pp : h->parts) {
+        Part& pt = *pp;
+        launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0, st);
+      }
+      HIPC(hipGetLastError());
+      return 0;
+    };
+    if (l > 0) {
+      RC(stage(kSetupDinv));
+      if (split) RC(bound_max(h, l));
+    }
+    if (pl.lev[l].coarsest) break;
+    RC(stage(kSetupP));
+    if (split)
+      RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_sp[l]; },
+            [l](Part& p) -> void* { return p.amg_lev[l].P.val; }, nb2, 8));
+    RC(stage(kSetupAP));
+    if (split)
+      RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_sap[l]; },
+            [l](Part& p) -> void* { return p.amg_lev[l].apval; }, nb2, 8));
+    RC(stage(kSetupAC));
+    if (l + 1 == ns && ns < nlev) {  // level ns is replicated: gather its A
+      RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_sg; },
+            [ns](Part& p) -> void* { return p.amg_lev[ns].A.val; }, nb2, 8));
+      RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_sg; },
+            [ns](Part& p) -> void* { return p.amg_lev[ns].A.val32; }, nb2, 4));
+    }
+  }
+  return 0;
+}
+
+// One distributed V-cycle on every partition (gate: iteration j's flag;
+// j < 0: ungated, the solve's first cycle)
+int enqueue_gamg_vcycle(mfea_handle* h, int j) {
+  hipStream_t s = h->stream;
+  const AmgPlan& pl = h->gamg;
+  const int nd = pl.nd, nlev = (int)pl.lev.size(), ns = pl.n_dist;
+  if (nlev <= 1) return 0;  // the update's vcycle_entry solved the only level
+  const int top = std::min(ns, nlev - 1);  // split levels with a level below
+  auto gate = [j](Part& pt) -> const int32_t* { return j < 0 ? nullptr : &pt.slots.ptr[j + 1].flag; };
+  auto steps = [&](int l, int step) {
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_amg_vstep(s, nd, pt.amg_lev.data(), l, pt.amg_cg, step, gate(pt));
+    }
+  };
+  for (int l = 0; l < top; ++l) {
+    RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_a[l]; },
+          [l](Part& p) -> void* { return p.amg_lev[l].x; }, nd, 4));
+    steps(l, kStepResid);
+    HIPC(hipGetLastError());
+    RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_r[l]; },
+          [l](Part& p) -> void* { return p.amg_lev[l].t; }, nd, 4));
+    steps(l, kStepRestrict);
+    HIPC(hipGetLastError());
+  }
+  if (ns < nlev) {  // the replicated levels: gather level ns's b, every rank runs them whole
+    RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_g; },
+          [ns](Part& p) -> void* { return p.amg_lev[ns].b; }, nd, 4));
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_amg_xinit_rows(s, nd, pt.amg_lev[ns], pt.xd_g.r, pt.xd_g.x->n_recv(), gate(pt));
+      launch_amg_vcycle(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg, pt.amg_tail, gate(pt), ns);
+    }
+    HIPC(hipGetLastError());
+  }
+  for (int l = top - 1; l >= 0; --l) {
+    if (l + 1 < ns) {  // the coarse output of a split level
+      const bool co = pl.lev[l + 1].coarsest;
+      RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_p[l]; },
+            [l, co](Part& p) -> void* { return co ? p.amg_lev[l + 1].x : p.amg_lev[l + 1].e; }, nd, 4));
+    }
+    steps(l, kStepProlong);
+    HIPC(hipGetLastError());
+    RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_a[l]; },
+          [l](Part& p) -> void* { return p.amg_lev[l].x; }, nd, 4));
+    steps(l, kStepPost);
+    HIPC(hipGetLastError());
+  }
+  return 0;
+}
+
+// one distributed GAMG iteration j: update (gathered sums) → V-cycle → u halo
+// → w = A_0 u → this rank's sums → all-gather of the sums
+int enqueue_gamg_iteration(mfea_handle* h, int j) {
+  hipStream_t s = h->stream;
+  const int nd = h->gamg.nd;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_update(s, nd, j, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr,
+                         &pt.amg_dist);
+  }
+  HIPC(hipGetLastError());
+  RC(enqueue_gamg_vcycle(h, j));
+  RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_a[0]; }, [](Part& p) -> void* { return p.amg_cg.u; },
+        nd, 4));
+  const int q = (j & 1) ^ 1;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_w(s, nd, j, false, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+    launch_amg_gsum(s, pt.amg_cg, cg_part_buf(pt, q), pt.amg_dist, q);
+  }
+  HIPC(hipGetLastError());
+  return xchg_sums(h, q);
+}
+
+int enqueue_gamg_chunk(mfea_handle* h, int chunk) {
+  for (int j = 0; j < chunk; ++j) RC(enqueue_gamg_iteration(h, j));
+  for (auto& pp : h->parts) launch_cg_advance(h->stream, chunk, pp->slots.ptr, pp->state.ptr, pp->mirror);
+  HIPC(hipGetLastError());
+  return 0;
+}
+
+int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o, mfea_stats* st) {
+  hipStream_t s = h->stream;
+  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
+    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
+  bool rebuilt = false;
+  RC(ensure_gamg(h, &rebuilt));
+  const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
+  const int W = nranks(h);
+  const int nd = h->gamg.nd;
+  HIPC(hipEventRecord(h->ev[1], s));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 0, cg_vecs(pt), pt.partials.ptr, tix(pt, 0),
+                  pt.red.ptr);
+  }
+  RC(gather4(h, 0));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
+    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
+    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  }
+  HIPC(hipEventRecord(h->ev[2], s));
+  RC(enqueue_gamg_setup(h, o->reg));
+  HIPC(hipEventRecord(h->ev_setup, s));
+  h->ev_setup_used = true;
+  // iteration 0's u and w: the V-cycle of r₀, ungated
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_init(s, nd, pt.amg_lev[0], pt.amg_cg, cg_vecs(pt).r[0]);
+  }
+  RC(enqueue_gamg_vcycle(h, -1));
+  RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_a[0]; }, [](Part& p) -> void* { return p.amg_cg.u; },
+        nd, 4));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_cg_w(s, nd, 0, true, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+    launch_amg_gsum(s, pt.amg_cg, cg_part_buf(pt, 0), pt.amg_dist, 0);
+  }
+  RC(xchg_sums(h, 0));
+  HIPC(hipGetLastError());
+  const int tag = -3000000 - (int)(h->gamg_gen % 1000000);
+  Part& p0 = part0(h);
+  const int expected = std::min(o->max_it, p0.amg_last_iters > 0 ? p0.amg_last_iters : 16);
+  SolveState fin;
+  if (!h->opt_dist_graph) {
+    RC(drive_planned(h, chunk, o->max_it, expected, [&]() -> int { return enqueue_gamg_chunk(h, chunk); }, &fin));
+  } else {
+    if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG || h->graph_ell != tag) {
+      destroy_graph(h);
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int rc = enqueue_gamg_chunk(h, chunk);
+      const hipError_t ce = hipStreamEndCapture(s, &g);
+      if (rc) return rc;
+      HIPC(ce);
+      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_chunk = chunk;
+      h->graph_precond = MFEA_PC_GAMG;
+      h->graph_ell = tag;
+    }
+    RC(drive_planned(h, chunk, o->max_it, expected,
+                     [&]() -> int {
+                       HIPC(hipGraphLaunch(h->graph, s));
+                       return 0;
+                     },
+                     &fin));
+  }
+  if (fin.status == 0) p0.amg_last_iters = fin.iters;
+  // x to row order, then the displacement halo (ghost rows of the post kernels)
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
+    launch_rows_pack(s, pt.xsend_rows.ptr, (int64_t)pt.plan.xsend_node.size(), pt.x.ptr, pt.xh_send);
+  }
+  RC(xchg_xhalo(h));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    launch_rows_unpack(s, pt.xrecv_rows.ptr, (int64_t)pt.plan.xrecv_node.size(), pt.xh_recv, pt.x.ptr);
+  }
+  HIPC(hipGetLastError());
+  const int rc = finish_solve(h, fin, st);
+  if (st) {
+    st->amg_levels = (int32_t)h->gamg.lev.size();
     st->amg_rebuilt = rebuilt ? 1 : 0;
   }
   return rc;
@@ -1570,6 +2055,7 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
+  if ((int64_t)h->h_red[1] != h->n_active) ++h->act_gen;  // elements only ever fail here
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
   // elements only ever fail here: a changed count means a changed set
@@ -1585,8 +2071,10 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
 int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
   h->ev_setup_used = false;
-  if (o->precond == MFEA_PC_GAMG)
-    return partitioned(h) ? solve_amg_dist(h, dy_top, dy_bot, o, st) : solve_amg(h, dy_top, dy_bot, o, st);
+  if (o->precond == MFEA_PC_GAMG) {
+    if (!partitioned(h)) return solve_amg(h, dy_top, dy_bot, o, st);
+    return h->opt_amg_dist ? solve_gamg_global(h, dy_top, dy_bot, o, st) : solve_amg_dist(h, dy_top, dy_bot, o, st);
+  }
   if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
     return fail(MFEA_EINVAL, "unknown preconditioner");
   return partitioned(h) ? solve_dist(h, dy_top, dy_bot, o, st) : solve_impl(h, dy_top, dy_bot, o, st);
@@ -1730,6 +2218,7 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
   RC(set_device(h));
   RC(ensure_built(h));
+  ++h->act_gen;
   if (h->Ecount == 0) return 0;
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -2185,16 +2674,17 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
 }
 
 int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
-                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd) {
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist) {
   if (!h || !n_levels || cap < 0 || (cap && (!rows || !blocks || !pblocks)))
     return fail(MFEA_EINVAL, "bad argument");
   RC(set_device(h));
   RC(ensure_built(h));
-  if (partitioned(h)) return fail(MFEA_ESTATE, "GAMG: single-partition handles only");
-  Part& pt = part0(h);
   bool rebuilt = false;
-  RC(ensure_amg(h, pt, &rebuilt));
-  const AmgPlan& pl = pt.amg;
+  if (partitioned(h) && !h->opt_amg_dist) return fail(MFEA_ESTATE, "GAMG block Jacobi: per-partition hierarchies");
+  if (partitioned(h)) RC(ensure_gamg(h, &rebuilt));
+  else RC(ensure_amg(h, part0(h), &rebuilt));
+  const AmgPlan& pl = partitioned(h) ? h->gamg : part0(h).amg;
+  if (n_dist) *n_dist = pl.n_dist;
   *n_levels = (int)pl.lev.size();
   for (int l = 0; l < std::min(cap, *n_levels); ++l) {
     const SellPat& A = pl.lev[l].A;
@@ -2260,6 +2750,17 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
+  else if (n == "amg_dist") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_dist: 0 (block Jacobi over partitions) or 1 (global hierarchy)");
+    h->opt_amg_dist = (int)value;
+    h->gamg_ok = false;
+    for (auto& pp : h->parts) pp->amg_ok = false;
+  }
+  else if (n == "amg_rep_rows") {
+    if (value < 0) return fail(MFEA_EINVAL, "amg_rep_rows: >= 0");
+    h->opt_amg_rep_rows = value;
+    h->gamg_ok = false;
+  }
   else if (n == "part_slack_pct") {
     if (value < 0 || value > 45) return fail(MFEA_EINVAL, "part_slack_pct: 0..45");
     h->opt_part_slack = value / 100.0;
@@ -2273,6 +2774,113 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       RC(gather_active(h, h->active_host));
     }
     h->dirty = true;
+  }
+  return 0;
+}
+
+int mfea_debug_amg_vcycle(mfea_handle* h, const double* r, double* u) {
+  if (!h || !r || !u) return fail(MFEA_EINVAL, "NULL argument");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  hipStream_t s = h->stream;
+  const bool dm = partitioned(h);
+  if (dm && !h->opt_amg_dist) return fail(MFEA_ESTATE, "mfea_debug_amg_vcycle: amg_dist 0 is not one operator");
+  bool rebuilt = false;
+  if (dm) {
+    RC(ensure_gamg(h, &rebuilt));
+    RC(enqueue_gamg_setup(h, 1e-12));
+  } else {
+    RC(ensure_amg(h, part0(h), &rebuilt));
+    enqueue_amg_setup(h, part0(h), 1e-12);
+  }
+  const int nd = dm ? h->gamg.nd : part0(h).amg.nd;
+  // r (node order) → each partition's row-order RHS buffer (its q), then
+  // the CG init (r, x = ω D⁻¹ r) and one V-cycle
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const Pattern& P = pt.P;
+    std::vector<double> b(3 * P.n_nodes, 0.0);
+    for (int64_t i = 0; i < P.n_free; ++i) {
+      const int64_t g = dm ? pt.plan.node_g[P.perm[i]] : P.perm[i];
+      for (int a = 0; a < nd; ++a) b[3 * i + a] = r[nd * g + a];
+    }
+    HIPC(hipMemcpy(pt.q.ptr, b.data(), b.size() * sizeof(double), hipMemcpyHostToDevice));
+    launch_amg_cg_init(s, nd, pt.amg_lev[0], pt.amg_cg, pt.q.ptr);
+  }
+  if (dm) {
+    RC(enqueue_gamg_vcycle(h, -1));
+  } else {
+    Part& pt = part0(h);
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, nullptr);
+  }
+  HIPC(hipGetLastError());
+  RC(sync_stream(h));
+  std::memset(u, 0, (size_t)h->N * nd * sizeof(double));
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const AmgCg& cg = pt.amg_cg;
+    std::vector<float> uf((size_t)nd * cg.n);
+    std::vector<int32_t> row0(cg.n);
+    if (cg.n) {
+      HIPC(hipMemcpy(uf.data(), cg.u, uf.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPC(hipMemcpy(row0.data(), cg.row0, row0.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    }
+    for (int64_t i = cg.lo; i < cg.hi; ++i) {
+      const int64_t lr = row0[i];
+      const int64_t g = dm ? pt.plan.node_g[pt.P.perm[lr]] : pt.P.perm[lr];
+      for (int a = 0; a < nd; ++a) u[nd * g + a] = uf[nd * i + a];
+    }
+  }
+  return 0;
+}
+
+int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t cap, int64_t* n) {
+  if (!h || !n || which < 0 || which > 6) return fail(MFEA_EINVAL, "bad argument");
+  RC(set_device(h));
+  const bool dm = partitioned(h);
+  const AmgPlan& pl = dm ? h->gamg : part0(h).amg;
+  if (l < 0 || l >= (int)pl.lev.size()) return fail(MFEA_EINVAL, "level out of range");
+  const int nd = pl.nd;
+  const AmgLevel& L = pl.lev[l];
+  *n = L.A.n;
+  const int w = which >= 4 && which != 5 ? nd * nd : nd;  // per-row width
+  if (!out) return 0;
+  if (cap < w * L.A.n) return fail(MFEA_EINVAL, "output too small");
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    const AmgLevD& d = pt.amg_lev[l];
+    std::vector<double> v((size_t)w * L.A.n, 0.0);
+    if (which == 4) {  // D⁻¹ blocks
+      HIPC(hipMemcpy(v.data(), d.dinv, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+    } else if (which == 5) {  // the Gershgorin bound g, every row
+      double om[2];
+      HIPC(hipMemcpy(om, d.omega, sizeof(om), hipMemcpyDeviceToHost));
+      std::fill(v.begin(), v.end(), om[1]);
+    } else if (which == 6) {  // diagonal blocks of A (slot 0 of every row)
+      std::vector<double> a((size_t)nd * nd * d.A.npos);
+      HIPC(hipMemcpy(a.data(), d.A.val, a.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < L.A.n; ++i)
+        for (int c = 0; c < nd * nd; ++c) v[(size_t)nd * nd * i + c] = a[(size_t)nd * nd * L.A.pos(i, 0) + c];
+    } else if (l == 0 && (which == 0 || which == 3)) {
+      if (which == 0) {
+        HIPC(hipMemcpy(v.data(), pt.amg_cg.r, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+      } else {
+        std::vector<float> f(v.size());
+        HIPC(hipMemcpy(f.data(), pt.amg_cg.u, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
+      }
+    } else {
+      const float* src = which == 0 ? d.b : which == 1 ? d.x : which == 2 ? d.t : d.e;
+      if (!src) return fail(MFEA_EINVAL, "no such vector on this level");
+      std::vector<float> f(v.size());
+      HIPC(hipMemcpy(f.data(), src, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
+    }
+    const bool split = dm && l < pl.n_dist;
+    const int64_t lo = split ? pt.amg_rank.lo[l] : 0, hi = split ? pt.amg_rank.hi[l] : L.A.n;
+    if (!split && pt.rank != 0) continue;
+    for (int64_t i = lo; i < hi; ++i)
+      for (int a = 0; a < w; ++a) out[(size_t)w * L.nat[i] + a] = v[(size_t)w * i + a];
   }
   return 0;
 }
@@ -2295,6 +2903,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
+  else if (n == "amg_dist") *value = h->opt_amg_dist;
+  else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);
   return 0;

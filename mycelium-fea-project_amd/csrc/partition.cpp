@@ -139,7 +139,8 @@ std::string build_partition(int64_t N, const double* xyz, int64_t E, const int64
     for (int c = 0; c < 2; ++c)
       if (e2n[2 * e + c] < 0 || e2n[2 * e + c] >= N)
         return "element " + std::to_string(e) + " references node out of range [0," + std::to_string(N) + ")";
-  const std::vector<int32_t> own = node_owner(N, xyz, E, e2n, top, bot, world, axis, slack, &plan.axis);
+  plan.owner = node_owner(N, xyz, E, e2n, top, bot, world, axis, slack, &plan.axis);
+  const std::vector<int32_t>& own = plan.owner;
   std::vector<uint8_t> known(N, 0);
   for (int64_t t : top) known[t] = 1;
   for (int64_t b : bot) known[b] = 1;

@@ -31,6 +31,7 @@ namespace mfea {
 
 struct PartPlan {
   int world = 1, rank = 0, axis = 0;
+  std::vector<int32_t> owner;     // rank of every global node (node_owner)
   // local mesh: nodes and elements in ascending global id
   std::vector<int64_t> node_g;    // local node → global node
   std::vector<uint8_t> ghost;     // local node owned by another rank

@@ -16,7 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
                    "amg_max_levels": 32, "amg_w_block": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
-                   "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35}
+                   "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": 1,
+                   "amg_rep_rows": 32768}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
@@ -119,8 +120,10 @@ _sig = {
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
     "mfea_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "mfea_get_option": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
+    "mfea_debug_amg_vcycle": (C.c_int, [_P, _P, _P]),
+    "mfea_debug_amg_vector": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_amg_info": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P, C.c_int,
-                                      C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(_lib, _name)
@@ -423,11 +426,32 @@ class Engine:
         pblocks = np.zeros(cap, dtype=np.int64)
         items = C.c_int64()
         nd = C.c_int()
+        ndist = C.c_int()
         _check(_lib.mfea_debug_amg_info(self._h, C.byref(nl), rows.ctypes.data, blocks.ctypes.data,
-                                        pblocks.ctypes.data, cap, C.byref(items), C.byref(nd)))
+                                        pblocks.ctypes.data, cap, C.byref(items), C.byref(nd), C.byref(ndist)))
         n = nl.value
         return {"levels": n, "rows": rows[:n].tolist(), "blocks": blocks[:n].tolist(),
-                "pblocks": pblocks[:n].tolist(), "pair_items": items.value, "nd": nd.value}
+                "pblocks": pblocks[:n].tolist(), "pair_items": items.value, "nd": nd.value,
+                "n_dist": ndist.value}
+
+    def amg_vcycle(self, r):
+        """mfea_debug_amg_vcycle: one GAMG V-cycle u = M r (n_nodes × ND, original
+        node order; call after assemble)."""
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        u = np.empty_like(r)
+        _check(_lib.mfea_debug_amg_vcycle(self._h, _ptr(r), _ptr(u)))
+        return u
+
+    def amg_vector(self, level, which):
+        """mfea_debug_amg_vector: a V-cycle vector (0 b, 1 x, 2 t, 3 e) of a
+        level after amg_vcycle, in the level's natural row order."""
+        n = C.c_int64()
+        _check(_lib.mfea_debug_amg_vector(self._h, int(level), int(which), None, 0, C.byref(n)))
+        nd = self.amg_info()["nd"]
+        w = nd * nd if which in (4, 6) else nd
+        out = np.zeros(n.value * w)
+        _check(_lib.mfea_debug_amg_vector(self._h, int(level), int(which), _ptr(out), out.size, C.byref(n)))
+        return out.reshape(n.value, w)
 
     # ---- reference-API helpers ------------------------------------------------
     def element_stiffness(self, p1s, p2s, E, A, I):

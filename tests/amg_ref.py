@@ -21,13 +21,17 @@ _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr
           "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b")
 
 
-def fetch_plan(shim, active, nd):
-    """build_amg on the shim's last pattern → list of per-level dicts of arrays."""
-    a = np.ascontiguousarray(active, dtype=np.uint8)
-    err = C.create_string_buffer(256)
-    nlev = shim.shim_amg(a.ctypes.data_as(C.c_void_p), int(nd), err, 256)
-    if nlev < 0:
-        raise RuntimeError(err.value.decode())
+def fetch_plan(shim, active, nd, build=True):
+    """build_amg on the shim's last pattern → list of per-level dicts of arrays
+    (build=False: the plan the shim built last, e.g. by shim_amg_dist)."""
+    if build:
+        a = np.ascontiguousarray(active, dtype=np.uint8)
+        err = C.create_string_buffer(256)
+        nlev = shim.shim_amg(a.ctypes.data_as(C.c_void_p), int(nd), err, 256)
+        if nlev < 0:
+            raise RuntimeError(err.value.decode())
+    else:
+        nlev = shim.shim_amg_array(0, b"nlev", None)
 
     def arr(l, name):
         n = shim.shim_amg_array(l, name.encode(), None)
@@ -43,6 +47,8 @@ def fetch_plan(shim, active, nd):
         for name in _NAMES:
             if name in ("A.sptr", "A.col") or not L["coarsest"]:
                 L[name] = arr(l, name)
+        for name in ("owner", "aprow"):
+            L[name] = arr(l, name)
         levels.append(L)
     levels[0]["row0"] = arr(0, "row0")
     levels[0]["a0.ptr"] = arr(0, "a0.ptr")

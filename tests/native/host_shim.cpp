@@ -92,10 +92,10 @@ int64_t shim_export(const uint8_t* active, double EA, double EI12, int64_t* indp
   return (int64_t)ix.size();
 }
 
-// Host SELL values (val[6][G] = −S_e per slot, diag[6][N]) of the last built
-// pattern, the same formula as shim_export (test input only).
-void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val, double* diag) {
-  const Pattern& P = g_P;
+// Host SELL values (val[6][G] = −S_e per slot, diag[6][N]) of a pattern, the
+// same formula as shim_export (test input only).
+static void sell_values(const Pattern& P, const uint8_t* active, double EA, double EI12, double* val,
+                        double* diag) {
   const int64_t N = P.n_nodes, G = P.n_slots() * kSlice;
   std::memset(val, 0, 6 * G * sizeof(double));
   for (int64_t i = 0; i < N; ++i) {
@@ -123,6 +123,9 @@ void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val
     for (int c = 0; c < 6; ++c) diag[c * N + i] = d[c];
   }
 }
+void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val, double* diag) {
+  sell_values(g_P, active, EA, EI12, val, diag);
+}
 
 // SA-AMG plan (amg_symbolic.cpp) of the last built pattern: returns the
 // number of levels (or -1, error in err).
@@ -137,16 +140,49 @@ int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   return (int)g_amg.lev.size();
 }
 
+// The distributed form (AmgDistSpec): owner_node = rank of every ORIGINAL
+// node (node_owner), world ranks, levels above rep_rows rows split.
+int shim_amg_dist(const uint8_t* active, int nd, int world, const int32_t* owner_node, int64_t rep_rows,
+                  char* err, int errn) {
+  std::vector<uint8_t> a(active, active + g_P.n_elems);
+  AmgDistSpec d;
+  d.world = world;
+  d.rep_rows = rep_rows;
+  d.owner.resize(g_P.n_free);
+  for (int64_t i = 0; i < g_P.n_free; ++i) d.owner[i] = owner_node[g_P.perm[i]];
+  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, &d);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return (int)g_amg.lev.size();
+}
+
+// owner rank of every node (partition.cpp node_owner) for world ranks
+int shim_node_owner(int64_t N, const double* xyz, int64_t E, const int64_t* e2n, int64_t ntop,
+                    const int64_t* top, int64_t nbot, const int64_t* bot, int world, int axis, double slack,
+                    int32_t* out) {
+  std::vector<int64_t> t(top, top + ntop), b(bot, bot + nbot);
+  int used = 0;
+  std::vector<int32_t> o = node_owner(N, xyz, E, e2n, t, b, world, axis, slack, &used);
+  std::memcpy(out, o.data(), o.size() * 4);
+  return used;
+}
+
 // one int32 array of level l by name; returns its length (out == NULL: size
 // only), -1 for an unknown name.  "n" / "nc" / "coarsest" return scalars.
 int64_t shim_amg_array(int l, const char* name, int32_t* out) {
-  const AmgLevel& L = g_amg.lev[l];
   const std::string n(name);
+  if (n == "nlev") return (int64_t)g_amg.lev.size();
+  const AmgLevel& L = g_amg.lev[l];
   const std::vector<int32_t>* v = nullptr;
   if (n == "n") return L.A.n;
   if (n == "nc") return L.nc;
   if (n == "coarsest") return L.coarsest ? 1 : 0;
-  if (n == "A.sptr") v = &L.A.sptr;
+  if (n == "n_dist") return g_amg.n_dist;
+  if (n == "owner") v = &L.owner;
+  else if (n == "aprow") v = &L.aprow;
+  else if (n == "A.sptr") v = &L.A.sptr;
   else if (n == "A.col") v = &L.A.col;
   else if (n == "agg") v = &L.agg;
   else if (n == "P.sptr") v = &L.P.sptr;
@@ -170,6 +206,120 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   else return -1;
   if (out && !v->empty()) std::memcpy(out, v->data(), v->size() * 4);
   return (int64_t)v->size();
+}
+
+// one rank's share of the last distributed plan (amg_dist.cpp)
+static AmgRank g_rank;
+int shim_amg_rank(int rank, char* err, int errn) {
+  std::string e = build_amg_rank(g_amg, rank, g_rank);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return g_rank.n_dist;
+}
+
+// rank arrays: "lo" "hi" "aplo" "aphi" "rlo" "rhi" (per level), or a plan
+// field "<plan>.<field>" with plan xa xr xp sp sap (level l) / xg sg and
+// field peers soff scnt roff rcnt sidx ridx; int64 out; returns the length
+int64_t shim_rank_array(const char* name, int l, int64_t* out) {
+  const std::string n(name);
+  const std::vector<int64_t>* v = nullptr;
+  if (n == "lo") v = &g_rank.lo;
+  else if (n == "hi") v = &g_rank.hi;
+  else if (n == "aplo") v = &g_rank.aplo;
+  else if (n == "aphi") v = &g_rank.aphi;
+  else if (n == "rlo") v = &g_rank.rlo;
+  else if (n == "rhi") v = &g_rank.rhi;
+  if (v) {
+    if (out) std::memcpy(out, v->data(), v->size() * 8);
+    return (int64_t)v->size();
+  }
+  const size_t dot = n.find('.');
+  if (dot == std::string::npos) return -1;
+  const std::string pn = n.substr(0, dot), fn = n.substr(dot + 1);
+  const XPlan* x = nullptr;
+  if (pn == "xa") x = &g_rank.xa.at(l);
+  else if (pn == "xr") x = &g_rank.xr.at(l);
+  else if (pn == "xp") x = &g_rank.xp.at(l);
+  else if (pn == "sp") x = &g_rank.sp.at(l);
+  else if (pn == "sap") x = &g_rank.sap.at(l);
+  else if (pn == "xg") x = &g_rank.xg;
+  else if (pn == "sg") x = &g_rank.sg;
+  else return -1;
+  std::vector<int64_t> t;
+  if (fn == "peers") t.assign(x->peers.begin(), x->peers.end());
+  else if (fn == "soff") t = x->soff;
+  else if (fn == "scnt") t = x->scnt;
+  else if (fn == "roff") t = x->roff;
+  else if (fn == "rcnt") t = x->rcnt;
+  else if (fn == "sidx") t.assign(x->sidx.begin(), x->sidx.end());
+  else if (fn == "ridx") t.assign(x->ridx.begin(), x->ridx.end());
+  else return -1;
+  if (out && !t.empty()) std::memcpy(out, t.data(), t.size() * 8);
+  return (int64_t)t.size();
+}
+
+// A_0 of rank r formed as the device does for the distributed solve: its
+// partition (build_partition, owners as node_owner with axis -1 and slack),
+// that partition's pattern and assembled values, build_amg_level0's lists.
+// out: [n_pos][nd*nd] blocks of the last distributed plan's level 0, written
+// for r's rows (diagonal = K_ii + reg·I), untouched elsewhere.
+int shim_level0_blocks(int64_t N, const double* xyz, int64_t E, const int64_t* e2n, int64_t ntop,
+                       const int64_t* top, int64_t nbot, const int64_t* bot, int world, int rank, double slack,
+                       const uint8_t* gactive, int nd, double EA, double EI12, double reg, double* out, char* err,
+                       int errn) {
+  std::vector<int64_t> t(top, top + ntop), b(bot, bot + nbot);
+  PartPlan pl;
+  std::string e = build_partition(N, xyz, E, e2n, false, t, b, world, rank, -1, slack, pl);
+  Pattern P;
+  if (e.empty())
+    e = build_pattern((int64_t)pl.node_g.size(), pl.xyz.data(), (int64_t)pl.elem_g.size(), pl.e2n.data(), false,
+                      pl.top, pl.bot, kOrderDFS, P, &pl.ghost);
+  AmgRank rk;
+  if (e.empty()) e = build_amg_rank(g_amg, rank, rk);
+  PosList a0;
+  std::vector<int32_t> row0;
+  std::vector<uint8_t> key(gactive, gactive + E);
+  if (e.empty()) e = build_amg_level0(g_amg, g_P, rk, P, pl.node_g, pl.elem_g, key, a0, row0);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  std::vector<uint8_t> lact(P.n_elems);
+  for (int64_t le = 0; le < P.n_elems; ++le) lact[le] = gactive[pl.elem_g[le]];
+  const int64_t G = P.n_slots() * kSlice, NL = P.n_nodes;
+  std::vector<double> val(6 * G), diag(6 * NL);
+  sell_values(P, lact.data(), EA, EI12, val.data(), diag.data());
+  const SellPat& A = g_amg.lev[0].A;
+  auto sym = [&](const double* s6, double* m) {  // (xx xy xz yy yz zz) → nd×nd
+    const int ix[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    for (int a = 0; a < nd; ++a)
+      for (int c = 0; c < nd; ++c) m[a * nd + c] = s6[ix[a][c]];
+  };
+  for (int64_t i = rk.lo[0]; i < rk.hi[0]; ++i) {
+    for (int k = 0; k < A.rlen[i]; ++k) {
+      const int64_t q = A.pos(i, k);
+      double m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      if (k == 0) {
+        double s6[6];
+        for (int c = 0; c < 6; ++c) s6[c] = diag[c * NL + row0[i]];
+        s6[0] += reg;
+        s6[3] += reg;
+        s6[5] += reg;
+        sym(s6, m);
+      } else {
+        for (int32_t tt = a0.ptr[q]; tt < a0.ptr[q + 1]; ++tt) {
+          double s6[6], e9[9];
+          for (int c = 0; c < 6; ++c) s6[c] = val[c * G + a0.a[tt]];
+          sym(s6, e9);
+          for (int c = 0; c < nd * nd; ++c) m[c] += e9[c];
+        }
+      }
+      for (int c = 0; c < nd * nd; ++c) out[q * nd * nd + c] = m[c];
+    }
+  }
+  return 0;
 }
 
 // Wave-local lanes of the last built pattern: returns n_lanes (or -1, error in

@@ -60,23 +60,94 @@ def test_partitioned_solve_matches_direct(peng, nparts, axis, precond):
         assert abs(st8.iters - int(sysz["pcg_iters_1e8"])) <= 3
 
 
-@pytest.mark.parametrize("nparts,axis", [(2, -1), (3, 0), (4, 1)])
-def test_partitioned_gamg_matches_direct(peng, nparts, axis):
-    """Block-Jacobi-over-partitions AMG inside the global CG (amg.hpp AmgHalo):
-    U to 1e-10 of the direct solve.  This network has no sparse gap for the
-    strip boundaries to follow, so the block-Jacobi coupling costs iterations
-    (≈ 190-310 at 1e-8 vs 17 on one partition) — still a fraction of
-    Jacobi-PCG's 1,644."""
+def _its_one_partition(engine, xyz, e2n, top, bot, dy, rtol=1e-8):
+    from mfea import PC_GAMG, make_opts
+    engine.set_parts(1)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    st = engine.solve(dy, -dy, make_opts(rtol=rtol, max_it=2000, precond=PC_GAMG))
+    assert st.status == 0
+    return st.iters, engine.displacement()
+
+
+@pytest.mark.parametrize("nparts,axis", [(2, -1), (3, 0), (4, 1), (4, -1)])
+def test_partitioned_gamg_matches_direct(peng, engine, nparts, axis):
+    """The distributed V-cycle of ONE global hierarchy (option "amg_dist" 1,
+    the default): U to 1e-10 of the direct solve, and the one-partition
+    iteration count (±3) at rtol 1e-8 although every strip boundary cuts
+    through this network's hyphae."""
     from mfea import PC_GAMG, make_opts
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
-    _sim181147(peng, nparts, axis)
-    peng.assemble()
     dy = float(sysz["dy"])
+    xyz, e2n, top, bot = _sim181147(peng, nparts, axis)
+    peng.assemble()
     st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
     assert st.status == 0 and st.amg_levels >= 3
     assert rel(peng.displacement(), sysz["U"]) <= 1e-10
+    assert peng.amg_info()["n_dist"] >= 1
     st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
+    it1, _ = _its_one_partition(engine, xyz, e2n, top, bot, dy)
+    assert abs(st8.iters - it1) <= 3, (st8.iters, it1)
+
+
+@pytest.mark.parametrize("rep_rows", [0, 300, 1 << 30])
+def test_partitioned_gamg_split_depths(peng, rep_rows):
+    """Every level split (0: the coarsest solve is local too), the default
+    split, and level 0 alone split: the same U to 1e-10 of the direct solve."""
+    from mfea import PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    with peng.options(amg_rep_rows=rep_rows):
+        _sim181147(peng, 3)
+        peng.assemble()
+        st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
+        info = peng.amg_info()
+        U = peng.displacement()
+    assert st.status == 0
+    if rep_rows == 0:
+        assert info["n_dist"] == info["levels"]
+    if rep_rows == 1 << 30:
+        assert info["n_dist"] == 1
+    assert rel(U, sysz["U"]) <= 1e-10
+
+
+@pytest.mark.parametrize("nparts,axis", [(2, -1), (3, 0), (4, 1)])
+def test_partitioned_block_jacobi_gamg_matches_direct(peng, nparts, axis):
+    """Option "amg_dist" 0: block Jacobi over per-partition hierarchies inside
+    the global CG (amg.hpp AmgHalo).  This network has no sparse gap for the
+    strip boundaries to follow, so the dropped couplings cost iterations
+    (≈ 190-310 at 1e-8 vs 17 on one partition); U still to 1e-10."""
+    from mfea import PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    with peng.options(amg_dist=0):
+        _sim181147(peng, nparts, axis)
+        peng.assemble()
+        dy = float(sysz["dy"])
+        st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
+        assert st.status == 0 and st.amg_levels >= 3
+        assert rel(peng.displacement(), sysz["U"]) <= 1e-10
+        st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
     assert st8.iters <= int(sysz["pcg_iters_1e8"]) // 4, st8.iters
+
+
+def test_partitioned_gamg_grown_network_8_parts(peng, engine):
+    """A network grown by the native producer (165k DOF, no tiling gaps) on 8
+    partitions: the one-partition iteration count (±3) and the same U."""
+    from mfea import PC_GAMG, grow_network, make_opts, scaled_grow_params, synth
+    xyz, e2n = grow_network(scaled_grow_params(3))
+    top, bot = synth.grips(xyz)
+    it1, U1 = _its_one_partition(engine, xyz, e2n, top, bot, 0.01)
+    peng.set_parts(8, -1)
+    peng.set_mesh(xyz, e2n)
+    peng.set_bc(top, bot)
+    peng.set_active(None)
+    peng.assemble()
+    st = peng.solve(0.01, -0.01, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
+    assert st.status == 0 and peng.info()["n_parts"] == 8
+    assert abs(st.iters - it1) <= 3, (st.iters, it1)
+    assert rel(peng.displacement(), U1) <= 1e-6
 
 
 @pytest.mark.parametrize("nparts,axis", [(2, 0), (4, 0), (2, 1), (4, -1), (8, -1)])

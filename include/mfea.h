@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 6
+#define MFEA_ABI_VERSION 7
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -47,8 +47,11 @@ extern "C" {
 #define MFEA_PC_BLOCK_JACOBI 1  /* 3×3 node-block Jacobi (exact inverse per block)   */
 #define MFEA_PC_GAMG 2          /* smoothed-aggregation AMG V-cycle, the counterpart of
                                    the reference sweep's `-pc_type gamg`
-                                   (src/fea_petsc_solverAndPC.cpp:330-391); single-
-                                   partition handles, unpreconditioned stopping norm */
+                                   (src/fea_petsc_solverAndPC.cpp:330-391); stops on the
+                                   unpreconditioned norm.  Partitioned handles: ONE global
+                                   hierarchy whose large levels are split over the ranks
+                                   (the one-partition iteration count; mfea_debug.h option
+                                   "amg_dist" 0: block Jacobi over per-partition ones) */
 
 /* stopping norm (mfea_solve_opts.norm) */
 #define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
@@ -238,20 +241,41 @@ void mfea_grow_free(mfea_grow_net* g);
  * src/fea_petsc_parallel.cpp:169-171, 234-268, 330-409 and its MPI reductions.
  * unique_id: the 128-byte ncclUniqueId made by rank 0 (mfea_dist_unique_id)
  * and broadcast by the caller.  Every rank then passes the WHOLE mesh and the
- * same grips to mfea_set_mesh / mfea_set_bc; the handle keeps the strip of
- * nodes it owns (partition.hpp: equal free-node counts along one axis), the
- * elements touching them and the far ends of cut elements as ghost rows.
- * Each CG iteration runs one kernel per GPU plus one RCCL group (cut-row CG
- * records to the strip neighbours + the 4 partial sums to every rank); all
- * ranks derive bitwise identical α, β and stopping decisions.
+ * same grips to mfea_set_mesh / mfea_set_bc; the handle keeps the part of the
+ * network it owns (partition.hpp: a px × py grid of strips with equal
+ * free-node counts, boundaries at the fewest crossing elements), the elements
+ * touching it and the far ends of cut elements as ghost rows.
+ * Exchanges per CG iteration (one RCCL group of point-to-point transfers each):
+ *   Jacobi / block Jacobi — one kernel per GPU, one group (the cut rows' CG
+ *     records to the neighbours + the 4 partial sums to every rank);
+ *   GAMG (distributed V-cycle) — per split level a halo of the smoother's x
+ *     and of the residual on the way down and of the coarse correction and x
+ *     on the way up, one all-gather into the first replicated level, the u
+ *     halo of w = A u and the sums: 4·(split levels) + 2 groups.
+ * All ranks derive bitwise identical α, β and stopping decisions.
  * Partitioned handles: mfea_get_displacement writes the owned nodes' entries,
  * mfea_get_stress / mfea_get_active the entries of elements whose first node
- * is owned (others untouched); mfea_post returns the global force and count. */
+ * is owned (others untouched; mfea_gather_results collects all on rank 0);
+ * mfea_post returns the global force and count. */
 int mfea_dist_unique_id(uint8_t* unique_id /* 128 bytes */);
 int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id);
-/* Strip axis of the partition: 0 = x, 1 = y, -1 (default) = the longer
- * bounding-box extent.  Takes effect at the next build. */
+/* Partition layout: 0 = strips along x, 1 = along y, -1 (default) = the
+ * px × py grid (a factorisation of the world size) whose boundaries cross the
+ * fewest elements (partition.hpp).  Takes effect at the next build. */
 int mfea_set_partition_axis(mfea_handle* h, int axis);
+/* Which nodes / elements this handle reports (1 = its own): every node
+ * belongs to one partition, every element to the partition of its first
+ * node.  Either array may be NULL.  One partition: all ones. */
+int mfea_get_ownership(mfea_handle* h, uint8_t* node_owned /* n_nodes */, uint8_t* elem_owned /* n_elems */);
+/* The step's records gathered on rank 0 — the displacement of every node and
+ * the stress / activity of every element, as one partition would return them
+ * (the reference gathers U to rank 0, src/fea_petsc_parallel.cpp:373-378,
+ * while every rank writes the same record files, :491-574; here rank 0 alone
+ * writes).  Collective over the RCCL world: every rank calls it; rank 0's
+ * arrays are filled, the others' are not touched (may be NULL).  Handles
+ * without an RCCL world fill the arrays directly.  Any array may be NULL. */
+int mfea_gather_results(mfea_handle* h, double* U /* 3·n_nodes */, double* stress /* n_elems */,
+                        uint8_t* active /* n_elems */);
 
 #ifdef __cplusplus
 }

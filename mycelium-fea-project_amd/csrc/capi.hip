@@ -2945,6 +2945,109 @@ int mfea_dist_unique_id(uint8_t* unique_id) {
   return 0;
 }
 
+int mfea_get_ownership(mfea_handle* h, uint8_t* node_owned, uint8_t* elem_owned) {
+  if (!h) return fail(MFEA_EINVAL, "NULL handle");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  if (!partitioned(h)) {
+    if (node_owned) std::memset(node_owned, 1, (size_t)h->N);
+    if (elem_owned) std::memset(elem_owned, 1, (size_t)h->Ecount);
+    return 0;
+  }
+  if (node_owned) std::memset(node_owned, 0, (size_t)h->N);
+  if (elem_owned) std::memset(elem_owned, 0, (size_t)h->Ecount);
+  for (auto& pp : h->parts) {
+    const PartPlan& pl = pp->plan;
+    if (node_owned)
+      for (size_t ln = 0; ln < pl.node_g.size(); ++ln)
+        if (!pl.ghost[ln]) node_owned[pl.node_g[ln]] = 1;
+    if (elem_owned)
+      for (size_t le = 0; le < pl.elem_g.size(); ++le)
+        if (pl.elem_own[le]) elem_owned[pl.elem_g[le]] = 1;
+  }
+  return 0;
+}
+
+int mfea_gather_results(mfea_handle* h, double* U, double* stress, uint8_t* active) {
+  if (!h) return fail(MFEA_EINVAL, "NULL handle");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  const int64_t N = h->N, E = h->Ecount;
+  if (h->world <= 1) {
+    if (U) RC(mfea_get_displacement(h, U));
+    if (stress && E) RC(mfea_get_stress(h, stress));
+    if (active && E) RC(mfea_get_active(h, active));
+    return 0;
+  }
+  // this rank's values of its own nodes / elements (ascending global id);
+  // every rank knows every rank's counts (the partition is deterministic)
+  const int W = h->world, me = h->rank;
+  std::vector<double> Ul(3 * N, 0.0), Sl(E, 0.0);
+  std::vector<uint8_t> Al(E, 1), nown(N), eown(E);
+  RC(mfea_get_displacement(h, Ul.data()));
+  if (E) {
+    RC(mfea_get_stress(h, Sl.data()));
+    RC(mfea_get_active(h, Al.data()));
+  }
+  auto node_rank = [&](int64_t n) { return h->gowner[n]; };
+  auto elem_rank = [&](int64_t e) {
+    const int64_t a = h->e2n[2 * e], b = h->e2n[2 * e + 1];
+    return (a < 0 || a >= N || b < 0 || b >= N) ? -1 : h->gowner[a];  // skipped elements: nobody's
+  };
+  std::vector<int64_t> len(W, 0), off(W + 1, 0);
+  for (int64_t n = 0; n < N; ++n) len[node_rank(n)] += 3;
+  for (int64_t e = 0; e < E; ++e)
+    if (elem_rank(e) >= 0) len[elem_rank(e)] += 2;
+  for (int p = 0; p < W; ++p) off[p + 1] = off[p] + len[p];
+  hipStream_t s = h->stream;
+  DevBuf<double> buf;
+  if (me != 0) {
+    std::vector<double> pk;
+    pk.reserve(len[me]);
+    for (int64_t n = 0; n < N; ++n)
+      if (node_rank(n) == me)
+        for (int a = 0; a < 3; ++a) pk.push_back(Ul[3 * n + a]);
+    for (int64_t e = 0; e < E; ++e)
+      if (elem_rank(e) == me) {
+        pk.push_back(Sl[e]);
+        pk.push_back(Al[e] ? 1.0 : 0.0);
+      }
+    HIPC(buf.alloc(pk.size() + 1));
+    HIPC(hipMemcpy(buf.ptr, pk.data(), pk.size() * sizeof(double), hipMemcpyHostToDevice));
+    NCCLC(ncclGroupStart());
+    if (!pk.empty()) NCCLC(ncclSend(buf.ptr, pk.size(), ncclFloat64, 0, h->comm, s));
+    NCCLC(ncclGroupEnd());
+    return sync_stream(h);
+  }
+  HIPC(buf.alloc(off[W] + 1));
+  NCCLC(ncclGroupStart());
+  for (int p = 1; p < W; ++p)
+    if (len[p]) NCCLC(ncclRecv(buf.ptr + off[p], (size_t)len[p], ncclFloat64, p, h->comm, s));
+  NCCLC(ncclGroupEnd());
+  RC(sync_stream(h));
+  std::vector<double> all(off[W]);
+  if (off[W]) HIPC(hipMemcpy(all.data(), buf.ptr, off[W] * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<int64_t> at(off.begin(), off.end() - 1);
+  for (int64_t n = 0; n < N; ++n) {
+    const int p = node_rank(n);
+    for (int a = 0; a < 3; ++a) {
+      const double v = p == 0 ? Ul[3 * n + a] : all[at[p]++];
+      if (U) U[3 * n + a] = v;
+    }
+  }
+  for (int64_t e = 0; e < E; ++e) {
+    const int p = elem_rank(e);
+    double sv = Sl[e], av = Al[e];
+    if (p > 0) {
+      sv = all[at[p]++];
+      av = all[at[p]++];
+    }
+    if (stress) stress[e] = sv;
+    if (active) active[e] = av != 0.0 ? 1 : 0;
+  }
+  return 0;
+}
+
 int mfea_dist_init(mfea_handle* h, int rank, int world, const uint8_t* unique_id) {
   if (!h || !unique_id) return fail(MFEA_EINVAL, "NULL argument");
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world)

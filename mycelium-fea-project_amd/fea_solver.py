@@ -45,10 +45,11 @@ GRIP_LENGTH = 1.5
 # solver settings of the device PCG (no counterpart in the direct-solve reference)
 RTOL = 1e-13
 MAX_IT = 200000
-PRECOND = _capi.PC_GAMG  # partitioned runs: one hierarchy per partition (amg.hpp AmgHalo)
+PRECOND = _capi.PC_GAMG  # partitioned runs: the distributed V-cycle of one global hierarchy
 REG = 1e-12  # src/fea_solver.py:125
 
 _engine = None
+_world_joined = False
 
 
 def get_engine(device: int | None = None) -> _capi.Engine:
@@ -58,6 +59,56 @@ def get_engine(device: int | None = None) -> _capi.Engine:
         dev = int(os.environ.get("LOCAL_RANK", "0")) if device is None else device
         _engine = _capi.Engine(dev)
     return _engine
+
+
+def dist_env():
+    """(rank, world) of a multi-process launch — ``python -m torch.distributed.run
+    --nproc-per-node N fea_solver.py <dir>``, one process per GPU, as the
+    reference's ``mpirun -np N fea_petsc_parallel.exe <dir>`` (README.md:18;
+    rank/size src/fea_petsc_parallel.cpp:169-171) — else (0, 1)."""
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def _join_world(eng, rank, world):
+    """Joins this process's handle to the RCCL world: rank 0 makes the
+    communicator id, torch.distributed (gloo, launcher plumbing only) carries
+    it to the other ranks.  Once per process."""
+    global _world_joined
+    if _world_joined:
+        return
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    obj = [_capi.dist_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    eng.dist_init(rank, world, obj[0])
+    _world_joined = True
+
+
+def gather_records(node_owned, elem_owned, U, stress, active, rank, world):
+    """One step's records of the whole mesh on rank 0: every node's U from the
+    rank owning the node, every element's stress / activity from the rank
+    owning it (its first node's).  The values travel as they are (a -0.0
+    displacement stays -0.0 in the CSV, which a sum-reduction would not keep).
+    Replaces the reference's VecScatterCreateToZero + MPI_Bcast of U
+    (src/fea_petsc_parallel.cpp:373-391); returns None on the other ranks."""
+    import torch.distributed as dist
+    U3 = np.asarray(U).reshape(-1, 3)
+    payload = (np.flatnonzero(node_owned), U3[node_owned], np.flatnonzero(elem_owned),
+               np.asarray(stress)[elem_owned], np.asarray(active)[elem_owned])
+    out = [None] * world if rank == 0 else None
+    dist.gather_object(payload, out, dst=0)
+    if rank != 0:
+        return None
+    Ug, Sg, Ag = np.zeros_like(U3), np.zeros(len(stress)), np.ones(len(active), dtype=bool)
+    seen_n, seen_e = np.zeros(len(U3), bool), np.zeros(len(stress), bool)
+    for ni, uv, ei, sv, av in out:
+        Ug[ni], Sg[ei], Ag[ei] = uv, sv, av
+        seen_n[ni] = True
+        seen_e[ei] = True
+    if not (seen_n.all() and seen_e.all()):
+        raise RuntimeError("record gather: a node or element is owned by no rank")
+    return Ug.reshape(-1), Sg, Ag
 
 
 def _opts(rtol=None, max_it=None, precond=None):
@@ -130,13 +181,21 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     node_displacements,force_displacement}.csv, runtime.txt and
     solve_runtime.txt.  Module constants are read at call time, as in the
     reference.  out_format='petsc' writes the fea_petsc.cpp formatting instead
-    (src/fea_petsc.cpp:433-516).  nparts > 1 runs the multi-GPU partitioned
-    solve with that many partitions on this one device (mfea_debug_set_parts)."""
+    (src/fea_petsc.cpp:433-516).
+
+    Multi-GPU: launched as N processes (``torch.distributed.run``, dist_env),
+    every rank solves its partition of the mesh (RCCL between the GPUs) and
+    rank 0 alone gathers the records and writes the files — the reference's
+    MPI variant has every rank write the same files (src/fea_petsc_parallel.cpp:
+    491-574).  nparts > 1 in ONE process runs that partitioned solve with its
+    partitions all on this device (mfea_debug_set_parts)."""
     start_time = time.time()
-    say = print if verbose else (lambda *a, **k: None)
+    rank, world = dist_env()
+    say = print if verbose and rank == 0 else (lambda *a, **k: None)
     say(f"🔧 Running FEA on geometry from {results_dir}")
     fea_dir = os.path.join(results_dir, "fea_results")
-    os.makedirs(fea_dir, exist_ok=True)
+    if rank == 0:
+        os.makedirs(fea_dir, exist_ok=True)
     nodes = pd.read_csv(os.path.join(results_dir, "nodes.csv"))
     elems = pd.read_csv(os.path.join(results_dir, "elements.csv"))
     coords = nodes[["x", "y", "z"]].values
@@ -151,16 +210,21 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     say(f"Top nodes: {len(top)}, Bottom nodes: {len(bot)}")
 
     eng = get_engine()
-    eng.set_parts(nparts)
+    if world > 1:
+        _join_world(eng, rank, world)
+    else:
+        eng.set_parts(nparts)
     eng.set_material(E_mod, A, I)
     eng.set_mesh(coords, e2n)
     eng.set_bc(top, bot)
     eng.set_active(None)
     opts = _opts(rtol, max_it, precond)
+    node_owned, elem_owned = eng.ownership() if world > 1 else (None, None)
 
     stress_record, active_record, disp_record, force_disp_curve, solve_times = [], [], [], [], []
-    with open(os.path.join(fea_dir, "solve_runtime.txt"), "w") as f:
-        f.write("step, runtime_s\n")
+    if rank == 0:
+        with open(os.path.join(fea_dir, "solve_runtime.txt"), "w") as f:
+            f.write("step, runtime_s\n")
     for step in range(N_STEPS):
         disp_factor = step / (N_STEPS - 1)
         dy_top = +DISPLACEMENT_MAX * disp_factor
@@ -174,23 +238,30 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
             break
         t1 = time.time()
         solve_times.append(t1 - t0)
-        with open(os.path.join(fea_dir, "solve_runtime.txt"), "a") as f:
-            f.write(f"{step+1}, {t1 - t0:.6f}\n")
-        force_disp_curve.append([dy_top - dy_bot, total_force])
-        stress_record.append(eng.stress())
-        active_record.append(eng.active())
-        disp_record.append(eng.displacement())
+        if world > 1:
+            rec = gather_records(node_owned, elem_owned, eng.displacement(), eng.stress(), eng.active(),
+                                 rank, world)
+        else:
+            rec = (eng.displacement(), eng.stress(), eng.active())
+        if rank == 0:
+            with open(os.path.join(fea_dir, "solve_runtime.txt"), "a") as f:
+                f.write(f"{step+1}, {t1 - t0:.6f}\n")
+            force_disp_curve.append([dy_top - dy_bot, total_force])
+            disp_record.append(rec[0])
+            stress_record.append(rec[1])
+            active_record.append(rec[2])
         if n_active == 0:
             say(f"⚠️  Simulation stopped early at step {step+1}.")
             break
 
-    write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_record,
-                  force_disp_curve, out_format)
-    say(f"✅ FEA completed. Results saved to {fea_dir}")
-    total_time = time.time() - start_time
-    with open(os.path.join(fea_dir, "runtime.txt"), "w") as f:
-        f.write(f"Total FEA runtime: {total_time:.6f} seconds\n")
-    say(f"⏱️ Total runtime: {total_time:.3f} seconds")
+    if rank == 0:
+        write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_record,
+                      force_disp_curve, out_format)
+        say(f"✅ FEA completed. Results saved to {fea_dir}")
+        total_time = time.time() - start_time
+        with open(os.path.join(fea_dir, "runtime.txt"), "w") as f:
+            f.write(f"Total FEA runtime: {total_time:.6f} seconds\n")
+        say(f"⏱️ Total runtime: {total_time:.3f} seconds")
     return {"force": np.asarray(force_disp_curve), "stress": np.asarray(stress_record),
             "active": np.asarray(active_record), "U": np.asarray(disp_record)}
 
@@ -227,7 +298,8 @@ def main(argv=None):
     ap.add_argument("--pc", choices=["gamg", "jacobi", "bjacobi"], default="gamg")
     ap.add_argument("--format", choices=["python", "petsc"], default="python")
     ap.add_argument("--parts", type=int, default=1,
-                    help="partitions of the multi-GPU solve, all on this device")
+                    help="partitions of the multi-GPU solve, all on this device (one process); "
+                         "for one GPU per process launch with torch.distributed.run instead")
     a = ap.parse_args(argv)
     N_STEPS, DISPLACEMENT_MAX, MAX_STRAIN, REG = a.n_steps, a.disp_max, a.max_strain, a.reg
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,

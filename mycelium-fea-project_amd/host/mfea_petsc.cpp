@@ -23,10 +23,23 @@
 // engine's SA-AMG V-cycle and stops on the unpreconditioned residual (the
 // default norm under gamg; asking for the preconditioned one is an error);
 // -pc_type icc/ilu/sor and other -ksp_type are rejected.
+//
+// Multi-GPU: launched as N processes — `mpirun -np N mfea_petsc <dir>` as the
+// reference's `mpirun -np 4 ./fea_petsc_parallel.exe` (README.md:18), or
+// torch.distributed.run — every process takes its rank / size / local rank
+// from the launcher's environment (OMPI_COMM_WORLD_*, PMI_*, RANK /
+// WORLD_SIZE / LOCAL_RANK), drives the GPU of its local rank and joins the
+// RCCL world (mfea_dist_init); rank 0 hands the communicator id to the others
+// through a file (MFEA_UID_FILE, default <dir>/fea_results/.mfea_uid).
+// Every rank solves its partition; rank 0 alone prints, gathers the records
+// (mfea_gather_results) and writes the files — the reference has every rank
+// write the same files (src/fea_petsc_parallel.cpp:491-574).
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <unistd.h>
 
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -158,6 +171,55 @@ void read_elems(const std::string& path, std::vector<int64_t>& e2n) {
   }
 }
 
+// rank, world size, local rank of a multi-process launch (else 0, 1, -1)
+struct Launch {
+  int rank = 0, world = 1, local = -1;
+};
+int env_int(const char* const* names, int dflt) {
+  for (int k = 0; names[k]; ++k)
+    if (const char* v = std::getenv(names[k])) return std::atoi(v);
+  return dflt;
+}
+Launch launch_env() {
+  static const char* const rank[] = {"OMPI_COMM_WORLD_RANK", "PMI_RANK", "RANK", nullptr};
+  static const char* const size[] = {"OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "WORLD_SIZE", nullptr};
+  static const char* const local[] = {"OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "LOCAL_RANK", nullptr};
+  Launch l;
+  l.rank = env_int(rank, 0);
+  l.world = env_int(size, 1);
+  l.local = env_int(local, -1);
+  return l;
+}
+
+// Rank 0 writes the 128-byte RCCL id to `path` (temp file + rename: readers
+// never see a partial file); the others wait for a file no older than their
+// own start (a previous run's file is ignored), up to 120 s.
+void exchange_uid(const Launch& l, const std::string& path, uint8_t* uid,
+                  std::chrono::system_clock::time_point started) {
+  if (l.rank == 0) {
+    if (mfea_dist_unique_id(uid) != MFEA_OK) die("mfea_dist_unique_id failed");
+    const std::string tmp = path + ".tmp";
+    std::FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f || std::fwrite(uid, 1, 128, f) != 128 || std::fclose(f) != 0) die("cannot write " + tmp);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) die("cannot create " + path);
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto since = std::chrono::system_clock::to_time_t(started) - 5;
+  for (;;) {
+    struct stat st;
+    if (stat(path.c_str(), &st) == 0 && st.st_mtime >= since && st.st_size == 128) {
+      std::FILE* f = std::fopen(path.c_str(), "rb");
+      const bool ok = f && std::fread(uid, 1, 128, f) == 128;
+      if (f) std::fclose(f);
+      if (ok) return;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+      die("rank " + std::to_string(l.rank) + ": no communicator id from rank 0 in " + path);
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+}
+
 std::string last_error() {
   char buf[512];
   mfea_last_error(buf, sizeof(buf));
@@ -186,10 +248,14 @@ int main(int argc, char** argv) {
     std::printf("Usage: %s <results_dir>\n", argv[0]);
     return 1;
   }
+  const auto started = std::chrono::system_clock::now();
+  const Launch L = launch_env();
+  if (L.world < 1 || L.rank < 0 || L.rank >= L.world) die("bad rank / world size in the environment");
+  const bool root = L.rank == 0;
   const std::string fea_dir = o.dir + "/fea_results";
   struct stat st;
   if (stat(fea_dir.c_str(), &st) != 0) mkdir(fea_dir.c_str(), 0755);
-  std::printf("🔧 Running FEA on geometry from %s\n", o.dir.c_str());
+  if (root) std::printf("🔧 Running FEA on geometry from %s\n", o.dir.c_str());
   const auto t_start = std::chrono::high_resolution_clock::now();
 
   std::vector<double> xyz;
@@ -217,15 +283,18 @@ int main(int argc, char** argv) {
     if (std::fabs(xyz[3 * i + 1] - y_max) < o.grip) top.push_back(i);
     if (std::fabs(xyz[3 * i + 1] - y_min) < o.grip) bot.push_back(i);
   }
-  std::printf("Top nodes: %zu, Bottom nodes: %zu\n", top.size(), bot.size());
+  if (root) std::printf("Top nodes: %zu, Bottom nodes: %zu\n", top.size(), bot.size());
 
   int device = o.device;
-  if (device < 0) {
-    const char* lr = std::getenv("LOCAL_RANK");
-    device = lr ? std::atoi(lr) : 0;
-  }
+  if (device < 0) device = L.local >= 0 ? L.local : 0;
   mfea_handle* h = nullptr;
   check(mfea_create(device, &h), "mfea_create");
+  if (L.world > 1) {
+    const char* uf = std::getenv("MFEA_UID_FILE");
+    uint8_t uid[128];
+    exchange_uid(L, uf ? std::string(uf) : fea_dir + "/.mfea_uid", uid, started);
+    check(mfea_dist_init(h, L.rank, L.world, uid), "mfea_dist_init");
+  }
   // out-of-range node ids are skipped, as src/fea_petsc.cpp:241 does
   check(mfea_set_mesh(h, N, xyz.data(), E, e2n.data(), MFEA_MESH_SKIP_INVALID), "mfea_set_mesh");
   check(mfea_set_bc(h, (int64_t)top.size(), top.data(), (int64_t)bot.size(), bot.data()),
@@ -248,32 +317,35 @@ int main(int argc, char** argv) {
   for (int step = 0; step < o.n_steps; ++step) {
     const double f = (double)step / (double)(o.n_steps - 1);
     const double dy_top = +o.disp_max * f, dy_bot = -o.disp_max * f;
-    std::printf("➡️  Step %d/%d | dy_top=%.6f, dy_bot=%.6f\n", step + 1, o.n_steps, dy_top, dy_bot);
+    if (root) std::printf("➡️  Step %d/%d | dy_top=%.6f, dy_bot=%.6f\n", step + 1, o.n_steps, dy_top, dy_bot);
     double force = 0.0;
     int64_t n_active = 0;
     mfea_stats stt;
     const int rc = mfea_step(h, dy_top, dy_bot, &so, o.max_strain, &force, &n_active, &stt);
     if (rc == MFEA_EMAXIT || rc == MFEA_EBREAKDOWN) {
       // KSPConvergedReason: KSP_DIVERGED_ITS = -3, KSP_DIVERGED_BREAKDOWN = -5
-      std::printf("❌ Solver failed to converge at step %d. Reason %d\n", step + 1,
-                  rc == MFEA_EMAXIT ? -3 : -5);
+      if (root)
+        std::printf("❌ Solver failed to converge at step %d. Reason %d\n", step + 1, rc == MFEA_EMAXIT ? -3 : -5);
       break;
     }
     check(rc, "mfea_step");
     // KSP_CONVERGED_RTOL = 2, KSP_CONVERGED_ATOL = 3 (a zero right-hand side)
     const int reason = stt.bnorm == 0.0 ? 3 : 2;
-    std::printf("KSP converged reason: %d\n", reason);
-    std::printf("KSP Object: 1 MPI process (mfea, device %d)\n  type: cg, %d iterations, "
-                "final relative residual %.3e\n  tolerances: relative=%g, absolute=%g, "
-                "maximum iterations=%d\n  using %s norm type for convergence test\n"
-                "PC Object: type %s\n",
-                device, stt.iters, stt.relres, o.rtol, o.atol, o.max_it,
-                o.norm == MFEA_NORM_PRECONDITIONED ? "PRECONDITIONED" : "UNPRECONDITIONED",
-                o.precond == MFEA_PC_JACOBI ? "jacobi" : "bjacobi (3x3 node blocks)");
-    check(mfea_get_displacement(h, U.data()), "mfea_get_displacement");
-    if (E) {
-      check(mfea_get_stress(h, S.data()), "mfea_get_stress");
-      check(mfea_get_active(h, A.data()), "mfea_get_active");
+    if (root) {
+      std::printf("KSP converged reason: %d\n", reason);
+      std::printf("KSP Object: %d MPI process%s (mfea, device %d)\n  type: cg, %d iterations, "
+                  "final relative residual %.3e\n  tolerances: relative=%g, absolute=%g, "
+                  "maximum iterations=%d\n  using %s norm type for convergence test\n"
+                  "PC Object: type %s\n",
+                  L.world, L.world > 1 ? "es" : "", device, stt.iters, stt.relres, o.rtol, o.atol, o.max_it,
+                  o.norm == MFEA_NORM_PRECONDITIONED ? "PRECONDITIONED" : "UNPRECONDITIONED",
+                  o.precond == MFEA_PC_JACOBI ? "jacobi" : o.precond == MFEA_PC_GAMG ? "gamg" : "bjacobi (3x3 node blocks)");
+    }
+    // the whole mesh's records on rank 0 (collective; one process: a copy)
+    check(mfea_gather_results(h, U.data(), E ? S.data() : nullptr, E ? A.data() : nullptr), "mfea_gather_results");
+    if (!root) {
+      if (n_active == 0) break;
+      continue;
     }
     fd.push_back(dy_top - dy_bot);
     fd.push_back(force);
@@ -287,6 +359,7 @@ int main(int argc, char** argv) {
     }
   }
   mfea_destroy(h);
+  if (!root) return 0;
 
   // src/fea_petsc.cpp:433-516: a record file is written when it holds a step
   if (steps) {

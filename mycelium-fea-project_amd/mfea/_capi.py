@@ -107,6 +107,8 @@ _sig = {
     "mfea_dist_unique_id": (C.c_int, [_P]),
     "mfea_dist_init": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "mfea_set_partition_axis": (C.c_int, [_P, C.c_int]),
+    "mfea_get_ownership": (C.c_int, [_P, _P, _P]),
+    "mfea_gather_results": (C.c_int, [_P, _P, _P, _P]),
     "mfea_write_record_csv": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _P, _P,
                                         C.c_int]),
     "mfea_grow_default_params": (None, [C.POINTER(GrowParams)]),
@@ -389,6 +391,23 @@ class Engine:
         if self.n_elems:
             _check(_lib.mfea_get_active(self._h, _ptr(a)))
         return a.astype(bool)
+
+    def ownership(self):
+        """(node_owned, elem_owned) bool arrays: what this handle reports
+        (mfea_get_ownership; one partition: everything)."""
+        n = np.empty(self.n_nodes, dtype=np.uint8)
+        e = np.empty(self.n_elems, dtype=np.uint8)
+        _check(_lib.mfea_get_ownership(self._h, _ptr(n), _ptr(e)))
+        return n.astype(bool), e.astype(bool)
+
+    def gather_results(self):
+        """mfea_gather_results: (U, stress, active) of the whole mesh on rank
+        0 of an RCCL world (None elsewhere); collective."""
+        U = np.empty(3 * self.n_nodes)
+        S = np.empty(self.n_elems)
+        A = np.empty(self.n_elems, dtype=np.uint8)
+        _check(_lib.mfea_gather_results(self._h, _ptr(U), _ptr(S), _ptr(A)))
+        return U, S, A.astype(bool)
 
     def info(self) -> dict:
         inf = Info()

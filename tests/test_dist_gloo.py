@@ -308,3 +308,52 @@ def test_plans_are_consistent_without_processes(world):
         got = np.concatenate([p["node_g"][x] for x in _split(p["xrecv_node"], p["xrecv_cnt"])]) \
             if len(p["xrecv_cnt"]) else np.zeros(0, int)
         assert set(ghost_free.tolist()) == set(got.tolist())
+
+
+# ---------------------------------------------------------------------------
+# The multi-process drop-in's record gather (fea_solver.gather_records): rank 0
+# receives every node's U and every element's stress / activity from its owner
+# ---------------------------------------------------------------------------
+def _gather_worker(rank, world, port, out_q):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        import fea_solver as fs
+        N, E = 11, 7
+        node_owner = np.arange(N) % world
+        elem_owner = (np.arange(E) * 5) % world
+        U = np.full(3 * N, np.nan)          # what a partitioned handle leaves in foreign entries
+        S = np.full(E, np.nan)
+        A = np.zeros(E, dtype=bool)
+        mine_n, mine_e = node_owner == rank, elem_owner == rank
+        ref_U = np.arange(3 * N, dtype=float) * 0.25 - 2.0
+        ref_U[1::3] = -0.0                  # signed zeros must survive the gather
+        ref_S = np.linspace(-1.0, 1.0, E)
+        ref_A = np.arange(E) % 2 == 0
+        U.reshape(-1, 3)[mine_n] = ref_U.reshape(-1, 3)[mine_n]
+        S[mine_e] = ref_S[mine_e]
+        A[mine_e] = ref_A[mine_e]
+        rec = fs.gather_records(mine_n, mine_e, U, S, A, rank, world)
+        if rank == 0:
+            Ug, Sg, Ag = rec
+            ok = (np.array_equal(Ug, ref_U) and np.array_equal(np.signbit(Ug), np.signbit(ref_U))
+                  and np.array_equal(Sg, ref_S) and np.array_equal(Ag, ref_A))
+            out_q.put(ok)
+        else:
+            out_q.put(rec is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_record_gather_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert all(q.get(timeout=10) for _ in range(WORLD))

@@ -291,3 +291,30 @@ def test_partitioned_failures_match_committed_golden(tmp_path):
     Ar = np.unpackbits(z["bits"], axis=1)[:, : int(z["n_elems"])].astype(bool)
     A = read_rt(res / "active_elements.csv").values[:, :-1].astype(bool)
     assert np.array_equal(A, Ar)
+
+
+def test_dropin_partitioned_csvs_match_one_partition(tmp_path):
+    """The drop-in's records on 3 partitions (the multi-GPU plan, one device)
+    equal the one-partition records: same files, same columns, the same
+    failures; U and stress to 1e-10, the force (a sum with heavy
+    cancellation) to 1e-8."""
+    import pandas as pd
+    out = []
+    for n in (1, 3):
+        d = tmp_path / f"p{n}"
+        d.mkdir()
+        res = _run_dropin(d, "sim_20251117_175809", 40, 0.02, 1.5, n)
+        out.append({f: pd.read_csv(res / f, float_precision="round_trip")
+                    for f in ("force_displacement.csv", "stress_record.csv", "active_elements.csv",
+                              "node_displacements.csv")})
+    a, b = out
+    for f in a:
+        assert list(a[f].columns) == list(b[f].columns) and a[f].shape == b[f].shape, f
+    assert a["active_elements.csv"].equals(b["active_elements.csv"])
+    for f, tol in (("node_displacements.csv", 1e-10), ("stress_record.csv", 1e-8)):
+        A, B = a[f].values[:, :-1], b[f].values[:, :-1]
+        for k in range(1, len(A)):
+            assert rel(B[k], A[k]) <= tol, (f, k)
+    Fa, Fb = a["force_displacement.csv"].values, b["force_displacement.csv"].values
+    assert np.array_equal(Fa[:, 0], Fb[:, 0])
+    assert np.abs(Fb[:, 1] - Fa[:, 1]).max() <= 1e-8 * np.abs(Fa[:, 1]).max()

@@ -171,7 +171,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     from mfea import _capi
     assert declared == set(_capi.EXPORTED)
-    assert _capi.abi_version() == 6
+    assert _capi.abi_version() == 7
 
 
 def test_create_without_gpu_fails_cleanly():

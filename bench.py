@@ -59,6 +59,10 @@ def parse():
                     help="HIP device of this rank (default LOCAL_RANK; rehearsal: several ranks on one GPU)")
     ap.add_argument("--parts", type=int, default=1,
                     help="1 GPU: run the partitioned solve with this many partitions on it")
+    ap.add_argument("--no-full-run", action="store_true",
+                    help="skip the 40-step run (all load steps, with failures) after the timed steps")
+    ap.add_argument("--no-jacobi", action="store_true",
+                    help="skip the Jacobi-PCG leg (SURVEY §8d's iteration metric) after the timed steps")
     return ap.parse_args()
 
 
@@ -137,6 +141,56 @@ def iteration_bytes(info, block):
     minv = 48 if block else 24
     b = info["n_free_nodes"] * (120 + minv + 120 + 48 + 4) + info["free_incidences"] * 52
     return b, "k_cg_iter (SELL: update + SpMV + reduction)"
+
+
+def full_run(eng, opts, fs):
+    """The reference's whole driver loop on the bench network (src/fea_solver.py:
+    216-295): N_STEPS load steps from the intact mesh, elements failing as they
+    go, every step on device (no CSV IO).  Reports the wall time of the run, each
+    step's wall time and iteration count, and the steps whose new active set
+    rebuilt the GAMG hierarchy (host symbolic phase + upload + graph capture)."""
+    import time as _t
+    eng.set_active(None)
+    per, its, rebuilt, n_act = [], [], [], []
+    t0 = _t.perf_counter()
+    for step in range(fs.N_STEPS):
+        dy = fs.DISPLACEMENT_MAX * step / (fs.N_STEPS - 1)
+        t = _t.perf_counter()
+        f, na, st = eng.step(dy, -dy, opts, fs.MAX_STRAIN)
+        per.append(1e3 * (_t.perf_counter() - t))
+        its.append(st.iters)
+        rebuilt.append(st.amg_rebuilt)
+        n_act.append(na)
+        if na == 0:
+            break
+    wall = _t.perf_counter() - t0
+    med = float(np.median([p for p, r in zip(per, rebuilt) if not r] or per))
+    reb = [p for p, r in zip(per, rebuilt) if r]
+    return {"steps": len(per), "wall_s": wall, "step_ms": per, "cg_iters": its, "n_active": n_act,
+            "rebuild_steps": int(sum(rebuilt)), "rebuild_step_ms": reb,
+            "rebuild_overhead_ms": float(sum(p - med for p in reb)), "median_step_ms": med,
+            "note": "all 40 load steps from the intact mesh, failures included; a step whose active set "
+                    "changed rebuilds the GAMG hierarchy (rebuild_overhead_ms = those steps' time above "
+                    "the median step); no CSV IO"}
+
+
+def full_run_reference(opts, fs, device):
+    """The 40-step run on the reference's own network results/sim_20251117_181147
+    (22,125 DOF; elements fail from step 27 on, so the GAMG hierarchy is rebuilt
+    for each new active set), beside the reference's end-to-end walls for it."""
+    from mfea import Engine, synth
+    xyz, e2n = synth.load_mesh(synth.BASE_TILE)
+    top, bot = synth.grips(xyz, 1.5)  # the reference run's grip band (results/.../fea_results)
+    with Engine(device) as eng:
+        eng.set_material(fs.E_mod, fs.A, fs.I)
+        eng.set_mesh(xyz, e2n)
+        eng.set_bc(top, bot)
+        r = full_run(eng, opts, fs)
+    r["reference"] = {"python_wall_s": 71.76, "python_solve_step_ms_mean": 20.4,
+                      "source": "results/sim_20251117_181147/fea_results/runtime.txt:1 (whole fea_solver.py run, "
+                                "PNG plots included); results/sim_20251117_181147_cpp/fea_results/"
+                                "solve_runtime_1.txt (solve_system + K@U per step, 40 steps)"}
+    return r
 
 
 def cpu_model():
@@ -341,7 +395,10 @@ def main():
                 tj = {}
         except Exception:
             tj = {}
-    iter_ms = eng.profile_iteration(pc, reps=200 if pc != PC_GAMG else 50)
+    # partitioned GAMG: the whole iteration interleaves exchanges, so only the
+    # SpMV of rank 0's rows is profiled (its bytes: rank 0's share of A_0 by rows)
+    split = mode in ("partitioned", "parts") and pc == PC_GAMG
+    iter_ms = None if split else eng.profile_iteration(pc, reps=200 if pc != PC_GAMG else 50)
     if pc == PC_GAMG:
         ai = eng.amg_info()
         iter_bytes = amg_iteration_bytes(ai)
@@ -355,6 +412,8 @@ def main():
         spmv_ms = eng.profile_spmv(reps=100)
         nd = ai["nd"]
         spmv_bytes = amg_spmv_bytes(ai)
+        if split:
+            spmv_bytes = int(spmv_bytes * nf / max(ai["rows"][0], 1))
         kernel = f"k_amg_cg_w (SpMV w = A_0 u, f64 symmetric {nd}x{nd} blocks, + CG partial sums)"
         kernel_ms, kernel_bytes = spmv_ms, spmv_bytes
         traffic = tj.get("spmv_bytes_per_launch") if tj.get("spmv_kernel") == "k_amg_cg_w" else None
@@ -414,16 +473,37 @@ def main():
             "avg_launch_us": kernel_ms * 1e3,
         },
     }
-    if pc == PC_GAMG:
+    if split:
+        out["roofline"]["note"] = ("rank 0's w = A_0 u over its own rows; bytes = the whole A_0's scaled by "
+                                   "its share of the rows")
+    if pc == PC_GAMG and not split:
         ia = iter_bytes / (iter_ms * 1e-3) / 1e9
         out["roofline_iteration"] = {
             "kernel": iter_kernel, "bound": "hbm", "achieved": ia, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": ia / PEAK_HBM_GBPS, "traffic": iter_traffic, "alg_bytes_per_iteration": iter_bytes,
             "avg_iteration_us": iter_ms * 1e3}
+    if pc == PC_GAMG:
         out["amg"] = {"levels": ai["levels"], "rows": ai["rows"], "blocks": ai["blocks"],
-                      "setup_pair_items": ai["pair_items"]}
+                      "setup_pair_items": ai["pair_items"], "split_levels": ai["n_dist"]}
+    if mode in ("partitioned", "parts") and pc == PC_GAMG:
+        ch = eng.get_option("amg_dist_chosen")
+        out["config"]["amg_partitions"] = {
+            0: "block Jacobi over per-partition hierarchies", 1: "distributed V-cycle of one global hierarchy",
+            -1: "undecided"}[ch] + " (option amg_dist -1: the faster of the two, measured in warmup)"
     if note:
         out["note"] = note
+
+    # ---- legs after the timed region (not part of `value`)
+    if not a.no_jacobi and pc == PC_GAMG:
+        # SURVEY §8(d)'s iteration metric: Jacobi-PCG to rtol 1e-8 on the same step
+        eng.set_active(None)
+        fj, nj, sj = eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=PC_JACOBI), fs.MAX_STRAIN)
+        out["jacobi_iters_1e8"] = sj.iters
+        out["jacobi_step_ms"] = sj.t_assemble_ms + sj.t_rhs_ms + sj.t_solve_ms + sj.t_post_ms
+    if not a.no_full_run:
+        out["full_run"] = full_run(eng, opts, fs)
+        if world == 1 and mode == "1gpu":
+            out["full_run_reference_network"] = full_run_reference(opts, fs, local)
 
     if rank == 0 and not a.no_cpu and world == 1:
         cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof)

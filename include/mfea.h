@@ -50,8 +50,9 @@ extern "C" {
                                    (src/fea_petsc_solverAndPC.cpp:330-391); stops on the
                                    unpreconditioned norm.  Partitioned handles: ONE global
                                    hierarchy whose large levels are split over the ranks
-                                   (the one-partition iteration count; mfea_debug.h option
-                                   "amg_dist" 0: block Jacobi over per-partition ones) */
+                                   (the one-partition iteration count) or block Jacobi over
+                                   per-partition ones — per active set the faster of the
+                                   two, measured (mfea_debug.h option "amg_dist") */
 
 /* stopping norm (mfea_solve_opts.norm) */
 #define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
@@ -181,7 +182,8 @@ int mfea_get_info(mfea_handle* h, mfea_info* info);
 int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms);
 /* MFEA_PC_GAMG: the SpMV kernel alone — w = A_0 u (f64 blocks) with the CG's
  * four partial sums — replayed `reps` times back to back as one captured
- * graph between two HIP events; average launch duration.  After a GAMG solve. */
+ * graph between two HIP events; average launch duration.  After a GAMG solve
+ * (partitioned handles: the first partition's kernel over its own rows). */
 int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms);
 
 /* ---- record writer (host only: needs no device, no handle) ------------------ */

@@ -42,14 +42,17 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *                        fewest crossing elements (35; 0 = equal free-node counts)
  *   "amg_max_levels" 1..32  GAMG: hierarchy depth cap (32)
  *   "amg_w_block" 0|256..1024  GAMG: threads per block of w = A u (0: by size)
- *   "amg_dist" 0|1       partitioned GAMG: block Jacobi over per-partition hierarchies (0)
- *                        or the distributed V-cycle of one global hierarchy (1)
+ *   "amg_dist" -1|0|1    partitioned GAMG: block Jacobi over per-partition hierarchies (0),
+ *                        the distributed V-cycle of one global hierarchy (1), or per
+ *                        active set whichever of the two solved faster (-1)
  *   "amg_rep_rows" n     distributed V-cycle: levels of at most n rows replicated (32768)
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 
 /* The current value of an option of mfea_set_option (as it would be passed
- * back: part_slack_pct in percent, dist_timeout_ms in ms). */
+ * back: part_slack_pct in percent, dist_timeout_ms in ms), or of the
+ * read-only "amg_dist_chosen": the form option "amg_dist" -1 picked for the
+ * current active set (0 block Jacobi, 1 global hierarchy, -1 not yet). */
 int mfea_get_option(mfea_handle* h, const char* name, int64_t* value);
 
 /* The MFEA_PC_GAMG hierarchy for the current active set (built if needed;

@@ -109,6 +109,18 @@ struct AmgDistSpec {
   int64_t rep_rows = 32768;
 };
 
+// Strength of connection for the level-0 aggregation (PyAMG's symmetric
+// strength, PETSc GAMG's -pc_gamg_threshold): a coupling i–j is strong when
+// ‖A_ij‖ ≥ θ·√(‖A_ii‖‖A_jj‖), the block norms estimated from the element
+// stiffnesses on the host (‖S_e‖ = EA/L · √(1 + (kb_kax/L²)²), kb_kax =
+// 12EI / EA: the bending-to-axial ratio's constant; ‖A_ii‖ ≈ Σ_e ‖S_e‖).
+// Aggregation follows strong couplings only; P's smoothing and the Galerkin
+// products keep every coupling.  θ = 0: every coupling strong.
+struct AmgStrength {
+  double theta = 0.0;
+  double kb_kax = 0.0;
+};
+
 // Builds the hierarchy for the free rows [0, P.n_free) of P with the element
 // activity `active` (P's element order).  Returns "" on success.
 // max_levels caps the hierarchy (the coarsest level's block Jacobi is then
@@ -116,7 +128,8 @@ struct AmgDistSpec {
 // iterations than it saves per cycle (C3: 16 → 35 iterations at 5 levels).
 // dist: the distributed form (NULL: one partition, the plan of before).
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
-                      int max_levels = kAmgMaxLevels, const AmgDistSpec* dist = nullptr);
+                      int max_levels = kAmgMaxLevels, const AmgDistSpec* dist = nullptr,
+                      const AmgStrength& strength = AmgStrength());
 
 // Partitioned solve (partition.hpp): the V-cycle is block Jacobi over the
 // partitions (each partition's hierarchy couples its own free rows only —

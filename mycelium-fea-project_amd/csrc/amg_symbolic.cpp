@@ -14,6 +14,7 @@
 //      the level-0 A / R layouts 52 % / 28 % in natural order, 97 % / 81 %
 //      with 4096-row windows.
 #include <algorithm>
+#include <cmath>
 #include <numeric>
 
 #include "amg.hpp"
@@ -53,14 +54,17 @@ struct LevelCsr {
 // neighbour from pass 1; (3) a node still left roots an aggregate with its
 // unaggregated neighbours.  Isolated rows (no off-diagonal) stay out (-1):
 // they are decoupled, so the smoother alone solves them up to a scalar.
-// A's rows hold their diagonal first.
-int64_t aggregate(const Csr& A, std::vector<int32_t>& agg) {
+// A's rows hold their diagonal first.  strong (per CSR entry, optional):
+// only strong couplings make neighbours; a row whose couplings are all weak
+// roots a singleton aggregate in pass 3 (it keeps a coarse representative).
+int64_t aggregate(const Csr& A, std::vector<int32_t>& agg, const std::vector<uint8_t>* strong = nullptr) {
   const int64_t n = A.n;
   agg.assign(n, -1);
   std::vector<int8_t> pass(n, 0);
   int64_t na = 0;
   auto nbrs = [&](int64_t i, auto&& f) {
-    for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k) f((int64_t)A.col[k]);
+    for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k)
+      if (!strong || (*strong)[k]) f((int64_t)A.col[k]);
   };
   for (int64_t i = 0; i < n; ++i) {
     if (agg[i] >= 0 || A.len(i) <= 1) continue;
@@ -295,7 +299,7 @@ std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npo
 }  // namespace
 
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
-                      int max_levels, const AmgDistSpec* dist) {
+                      int max_levels, const AmgDistSpec* dist, const AmgStrength& strength) {
   max_levels = std::max(1, std::min(max_levels, kAmgMaxLevels));
   plan = AmgPlan();
   plan.nd = nd;
@@ -311,6 +315,31 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   // ---- stage 1, level 0: free rows, neighbours through active free-free elements
   std::vector<LevelCsr> lv(1);
   Lists a0;  // per A_0 entry: SELL slot positions of the assembled operator
+  // level-0 strength (AmgStrength): per A_0 entry Σ ‖S_e‖ of its elements,
+  // per row Σ ‖S_e‖ of every active incident element (its diagonal's estimate)
+  const bool use_strength = strength.theta > 0.0;
+  std::vector<double> w_entry, d_row;
+  auto enorm = [&](int64_t i, int64_t j) {
+    double v[3], L2 = 0.0;
+    for (int c = 0; c < 3; ++c) {
+      v[c] = P.xyz_perm[3 * j + c] - P.xyz_perm[3 * i + c];
+      L2 += v[c] * v[c];
+    }
+    const double L = std::max(std::sqrt(L2), 1e-12), q = strength.kb_kax / (L * L);
+    return std::sqrt(1.0 + q * q) / L;
+  };
+  if (use_strength) {
+    d_row.assign(nf, 0.0);
+    for (int64_t i = 0; i < nf; ++i) {
+      const int64_t base = (int64_t)P.slice_ptr[i >> 6] * 64 + (i & 63);
+      for (int t = 0; t < P.row_len[i]; ++t) {
+        const int64_t pos = base + (int64_t)t * 64;
+        const int32_t j = P.s_col[pos], e = P.s_elem[pos];
+        if (j < 0 || e < 0 || !active[e]) continue;
+        d_row[i] += enorm(i, j);
+      }
+    }
+  }
   // level-0 natural order = the Pattern's (depth-first: hyphal chains
   // contiguous, so a slice's gathers hit few cache lines).  Measured and
   // dropped: a Hilbert-curve order of the nodes (C3: 2× the cache lines per
@@ -333,13 +362,16 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       std::stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       A.col.push_back((int32_t)i);
       a0.ptr.push_back(a0.ptr.back());
+      if (use_strength) w_entry.push_back(0.0);
       for (size_t t = 0; t < nb.size(); ++t) {
         if (t == 0 || nb[t].first != nb[t - 1].first) {
           A.col.push_back(nb[t].first);
           a0.ptr.push_back(a0.ptr.back());
+          if (use_strength) w_entry.push_back(0.0);
         }
         a0.a.push_back(nb[t].second);
         ++a0.ptr.back();
+        if (use_strength) w_entry.back() += enorm(i, nb[t].first);
       }
       A.ptr.push_back((int64_t)A.col.size());
     }
@@ -352,9 +384,17 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   // 19 → 25 / 28 / 34 iterations at 2 / 4 / 8 ranks on a grown 165k-DOF
   // network: its cut couplings are strong).  Aggregates crossing a cut only
   // widen the halos.
+  std::vector<uint8_t> strong0;
+  if (use_strength) {
+    const Csr& A = lv[0].A;
+    strong0.assign(A.col.size(), 1);
+    for (int64_t i = 0; i < A.n; ++i)
+      for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k)
+        strong0[k] = w_entry[k] >= strength.theta * std::sqrt(d_row[i] * d_row[A.col[k]]);
+  }
   for (int l = 0;; ++l) {
     LevelCsr& L = lv[l];
-    const int64_t na = aggregate(L.A, L.agg);
+    const int64_t na = aggregate(L.A, L.agg, l == 0 && use_strength ? &strong0 : nullptr);
     if (na == 0 || l + 1 == max_levels) {
       plan.capped = na > 0;  // couplings left: the coarsest block Jacobi is then inexact
       L.agg.clear();

@@ -135,6 +135,9 @@ struct Part {
   // partition's rows and exchange plans (amg.hpp AmgRank), the plans' item
   // lists on the device and the staging buffers of one exchange
   AmgRank amg_rank;
+  PosList g_a0;                 // its level-0 lists over this partition's pattern
+  std::vector<int32_t> g_row0;
+  int dev_plan = -1;            // which plan the device arrays hold: 0 its own (pt.amg), 1 the global one
   struct XDev {
     const XPlan* x = nullptr;
     const int32_t* s = nullptr;  // sidx
@@ -202,7 +205,8 @@ struct mfea_handle {
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
-  int opt_amg_dist = 1;           // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block Jacobi
+  int opt_amg_dist = -1;          // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block
+                                  // Jacobi over per-partition hierarchies, -1 whichever solves faster (measured)
   int64_t opt_amg_rep_rows = 32768;  // distributed V-cycle: levels of at most this many rows are replicated
   // distributed GAMG (partitioned handles, option "amg_dist" 1): the whole
   // mesh's pattern and node owners (built with the partitions), and ONE
@@ -210,11 +214,21 @@ struct mfea_handle {
   Pattern gpat;
   std::vector<int32_t> gowner;
   AmgPlan gamg;
+  std::vector<uint8_t> gamg_key;  // the global activity gamg was built for
   bool gamg_ok = false;
-  int64_t gamg_gen = 0;       // bumped on every rebuild (captured graphs hold its pointers)
+  int64_t gamg_gen = 0;       // bumped on every upload (captured graphs hold its pointers)
+  int64_t gamg_plan_gen = 0;  // bumped on every host rebuild (a new active set)
   int64_t act_gen = 1;        // bumped whenever the element activity may have changed
   int64_t gamg_act_gen = 0;   // act_gen the hierarchy was built for
   DevBuf<uint8_t> gact;       // RCCL: the global activity, max-all-reduced
+  // option "amg_dist" -1: per active set (gamg_plan_gen), the first GAMG
+  // solve runs the global hierarchy, the next block Jacobi; the faster
+  // (host-timed, plan builds excluded) serves the set's further solves
+  struct {
+    int64_t gen = -1;
+    int choice = -1;
+    double t[2] = {-1.0, -1.0};
+  } amg_auto;
   // generic CSR path scratch
   DevBuf<int64_t> c_indptr;
   DevBuf<int32_t> c_indices;
@@ -1174,14 +1188,22 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
     RC(current_active(h, pt));
   }
   const std::vector<uint8_t>& key = dm ? local : h->act_host;
-  if (pt.amg_ok && pt.amg_key == key) return 0;
+  if (pt.amg_ok && pt.amg_key == key) {
+    if (!dm || pt.dev_plan == 0) return 0;
+    destroy_graph(h);  // the device holds the global plan: upload this one again
+    RC(upload_amg(h, pt, pt.amg));
+    RC(upload_amg_halo(h, pt, key));
+    pt.dev_plan = 0;
+    ++pt.amg_gen;
+    return 0;
+  }
   pt.amg_ok = false;
   const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
-  h->gamg_ok = false;  // the device arrays now hold this plan
   RC(upload_amg(h, pt, pt.amg));
   if (dm) RC(upload_amg_halo(h, pt, key));
+  pt.dev_plan = 0;
   pt.amg_key = key;
   pt.amg_ok = true;
   ++pt.amg_gen;
@@ -1482,37 +1504,56 @@ int upload_xplans(mfea_handle* h, Part& pt) {
   return 0;
 }
 
-// (Re)build the global hierarchy when the element activity may have changed
-// (act_gen) and actually did.
-int ensure_gamg(mfea_handle* h, bool* rebuilt) {
+// (Re)build the global hierarchy (host) when the element activity may have
+// changed (act_gen) and actually did.
+int ensure_gamg_plan(mfea_handle* h, bool* rebuilt) {
   *rebuilt = false;
-  if (h->gamg_ok && h->gamg_act_gen == h->act_gen) return 0;
-  std::vector<uint8_t> key;
-  RC(global_active(h, key));
-  if (h->gamg_ok && part0(h).amg_key == key) {
-    h->gamg_act_gen = h->act_gen;
-    return 0;
+  bool host_ok = h->gamg_ok && h->gamg_act_gen == h->act_gen;
+  if (!host_ok && h->gamg_ok) {
+    std::vector<uint8_t> key;
+    RC(global_active(h, key));
+    host_ok = key == h->gamg_key;
+    if (host_ok) h->gamg_act_gen = h->act_gen;
   }
-  h->gamg_ok = false;
-  AmgDistSpec spec;
-  spec.world = nranks(h);
-  spec.rep_rows = h->opt_amg_rep_rows;
-  spec.owner.resize(h->gpat.n_free);
-  for (int64_t i = 0; i < h->gpat.n_free; ++i) spec.owner[i] = h->gowner[h->gpat.perm[i]];
-  std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec);
-  if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
-  destroy_graph(h);
+  if (!host_ok) {
+    std::vector<uint8_t> key;
+    RC(global_active(h, key));
+    h->gamg_ok = false;
+    AmgDistSpec spec;
+    spec.world = nranks(h);
+    spec.rep_rows = h->opt_amg_rep_rows;
+    spec.owner.resize(h->gpat.n_free);
+    for (int64_t i = 0; i < h->gpat.n_free; ++i) spec.owner[i] = h->gowner[h->gpat.perm[i]];
+    std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec);
+    if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      err = build_amg_rank(h->gamg, pt.rank, pt.amg_rank);
+      if (err.empty())
+        err = build_amg_level0(h->gamg, h->gpat, pt.amg_rank, pt.P, pt.plan.node_g, pt.plan.elem_g, key, pt.g_a0,
+                               pt.g_row0);
+      if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+      pt.dev_plan = -1;
+    }
+    h->gamg_key = std::move(key);
+    h->gamg_ok = true;
+    h->gamg_act_gen = h->act_gen;
+    ++h->gamg_plan_gen;
+    *rebuilt = true;
+  }
+  return 0;
+}
+
+// ... and have the device arrays hold it (they may hold the block-Jacobi plans)
+int ensure_gamg(mfea_handle* h, bool* rebuilt) {
+  RC(ensure_gamg_plan(h, rebuilt));
+  bool up = false;
   for (auto& pp : h->parts) {
     Part& pt = *pp;
-    err = build_amg_rank(h->gamg, pt.rank, pt.amg_rank);
-    if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
-    PosList a0;
-    std::vector<int32_t> row0;
-    err = build_amg_level0(h->gamg, h->gpat, pt.amg_rank, pt.P, pt.plan.node_g, pt.plan.elem_g, key, a0, row0);
-    if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
-    pt.amg = AmgPlan();  // the block-Jacobi plan (if any) is stale now
-    pt.amg_ok = false;
-    RC(upload_amg(h, pt, h->gamg, &pt.amg_rank, &a0, &row0));
+    if (pt.dev_plan == 1) continue;
+    if (!up) destroy_graph(h);
+    up = true;
+    RC(upload_amg(h, pt, h->gamg, &pt.amg_rank, &pt.g_a0, &pt.g_row0));
     RC(upload_xplans(h, pt));
     AmgDist& d = pt.amg_dist;
     d = AmgDist{};
@@ -1520,12 +1561,9 @@ int ensure_gamg(mfea_handle* h, bool* rebuilt) {
     d.gall[0] = pt.dv.gall[0];
     d.gall[1] = pt.dv.gall[1];
     d.gsend = pt.dv.gsend;
-    pt.amg_key = key;
+    pt.dev_plan = 1;
   }
-  h->gamg_ok = true;
-  h->gamg_act_gen = h->act_gen;
-  ++h->gamg_gen;
-  *rebuilt = true;
+  if (up) ++h->gamg_gen;
   return 0;
 }
 
@@ -2068,12 +2106,59 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   return 0;
 }
 
+// Partitioned GAMG: option "amg_dist" 1 the distributed V-cycle of the
+// global hierarchy, 0 block Jacobi over per-partition hierarchies, -1 (the
+// default) whichever solved faster: per active set the first solve runs the
+// global hierarchy, the second block Jacobi (plan builds and uploads outside
+// the clock), later ones the faster of the two.  The block-Jacobi form wins
+// where the partition boundaries cut weak couplings (strips between tiles:
+// the same iteration count with two exchanges per iteration instead of
+// 4·levels + 2); the global form wherever the cut couplings matter (the
+// grown networks: 17 iterations instead of 190-310).  A variant that fails
+// (max_it, breakdown) hands the step to the other.
+int solve_amg_part(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o, mfea_stats* st) {
+  auto run = [&](int mode) {
+    return mode ? solve_gamg_global(h, dy_top, dy_bot, o, st) : solve_amg_dist(h, dy_top, dy_bot, o, st);
+  };
+  if (h->opt_amg_dist >= 0) return run(h->opt_amg_dist);
+  auto& a = h->amg_auto;
+  bool rebuilt = false;
+  RC(ensure_gamg_plan(h, &rebuilt));  // the active set's identity (a content compare)
+  if (a.gen != h->gamg_plan_gen) {
+    a.gen = h->gamg_plan_gen;
+    a.choice = -1;
+    a.t[0] = a.t[1] = -1.0;
+  }
+  if (a.choice >= 0) return run(a.choice);
+  const int mode = a.t[1] < 0 ? 1 : 0;
+  if (mode) {
+    RC(ensure_gamg(h, &rebuilt));
+  } else {
+    for (auto& pp : h->parts) {
+      bool rb = false;
+      RC(ensure_amg(h, *pp, &rb));
+      rebuilt = rebuilt || rb;
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = run(mode);
+  if (rc == 0) rc = sync_stream(h);
+  a.t[mode] = rc == 0 ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 1e300;
+  if (a.t[0] >= 0 && a.t[1] >= 0) a.choice = a.t[1] <= a.t[0] ? 1 : 0;
+  if (rc == MFEA_EMAXIT || rc == MFEA_EBREAKDOWN) {
+    a.choice = 1 - mode;
+    rc = run(a.choice);
+  }
+  if (st && rebuilt) st->amg_rebuilt = 1;
+  return rc;
+}
+
 int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
   h->ev_setup_used = false;
   if (o->precond == MFEA_PC_GAMG) {
     if (!partitioned(h)) return solve_amg(h, dy_top, dy_bot, o, st);
-    return h->opt_amg_dist ? solve_gamg_global(h, dy_top, dy_bot, o, st) : solve_amg_dist(h, dy_top, dy_bot, o, st);
+    return solve_amg_part(h, dy_top, dy_bot, o, st);
   }
   if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
     return fail(MFEA_EINVAL, "unknown preconditioner");
@@ -2562,10 +2647,12 @@ int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms) {
   if (!h || !avg_ms || reps <= 0) return fail(MFEA_EINVAL, "bad argument");
   RC(set_device(h));
   RC(ensure_built(h));
+  // partitioned: partition 0's w kernel over its own rows (the plan its device
+  // arrays hold: its block-Jacobi hierarchy or its share of the global one)
   Part& pt = part0(h);
-  if (partitioned(h) || !pt.amg_ok) return fail(MFEA_ESTATE, "profile the SpMV after a single-partition GAMG solve");
+  if (!(partitioned(h) ? pt.dev_plan >= 0 : pt.amg_ok)) return fail(MFEA_ESTATE, "profile the SpMV after a GAMG solve");
   hipStream_t s = h->stream;
-  const int nd = pt.amg.nd;
+  const int nd = pt.dev_plan == 1 ? h->gamg.nd : pt.amg.nd;
   hipGraph_t g;
   hipGraphExec_t ge = nullptr;
   HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -2751,10 +2838,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "amg_dist") {
-    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_dist: 0 (block Jacobi over partitions) or 1 (global hierarchy)");
+    if (value < -1 || value > 1)
+      return fail(MFEA_EINVAL, "amg_dist: 0 (block Jacobi over partitions), 1 (global hierarchy), -1 (faster)");
     h->opt_amg_dist = (int)value;
-    h->gamg_ok = false;
-    for (auto& pp : h->parts) pp->amg_ok = false;
+    h->amg_auto.gen = -1;
   }
   else if (n == "amg_rep_rows") {
     if (value < 0) return fail(MFEA_EINVAL, "amg_rep_rows: >= 0");
@@ -2904,6 +2991,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;
+  else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);

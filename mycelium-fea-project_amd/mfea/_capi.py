@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
                    "amg_max_levels": 32, "amg_w_block": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
-                   "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": 1,
+                   "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,
                    "amg_rep_rows": 32768}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 

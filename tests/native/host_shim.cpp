@@ -130,9 +130,15 @@ void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val
 // SA-AMG plan (amg_symbolic.cpp) of the last built pattern: returns the
 // number of levels (or -1, error in err).
 static AmgPlan g_amg;
+static AmgStrength g_strength;
+// strength of connection of the next shim_amg / shim_amg_dist (amg.hpp AmgStrength)
+void shim_amg_strength(double theta, double kb_kax) {
+  g_strength.theta = theta;
+  g_strength.kb_kax = kb_kax;
+}
 int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   std::vector<uint8_t> a(active, active + g_P.n_elems);
-  std::string e = build_amg(g_P, a, nd, g_amg);
+  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, nullptr, g_strength);
   if (!e.empty()) {
     std::snprintf(err, errn, "%s", e.c_str());
     return -1;
@@ -150,7 +156,7 @@ int shim_amg_dist(const uint8_t* active, int nd, int world, const int32_t* owner
   d.rep_rows = rep_rows;
   d.owner.resize(g_P.n_free);
   for (int64_t i = 0; i < g_P.n_free; ++i) d.owner[i] = owner_node[g_P.perm[i]];
-  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, &d);
+  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, &d, g_strength);
   if (!e.empty()) {
     std::snprintf(err, errn, "%s", e.c_str());
     return -1;

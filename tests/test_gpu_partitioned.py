@@ -74,20 +74,21 @@ def _its_one_partition(engine, xyz, e2n, top, bot, dy, rtol=1e-8):
 
 @pytest.mark.parametrize("nparts,axis", [(2, -1), (3, 0), (4, 1), (4, -1)])
 def test_partitioned_gamg_matches_direct(peng, engine, nparts, axis):
-    """The distributed V-cycle of ONE global hierarchy (option "amg_dist" 1,
-    the default): U to 1e-10 of the direct solve, and the one-partition
+    """The distributed V-cycle of ONE global hierarchy (option "amg_dist" 1):
+    U to 1e-10 of the direct solve, and the one-partition
     iteration count (±3) at rtol 1e-8 although every strip boundary cuts
     through this network's hyphae."""
     from mfea import PC_GAMG, make_opts
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     dy = float(sysz["dy"])
-    xyz, e2n, top, bot = _sim181147(peng, nparts, axis)
-    peng.assemble()
-    st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
-    assert st.status == 0 and st.amg_levels >= 3
-    assert rel(peng.displacement(), sysz["U"]) <= 1e-10
-    assert peng.amg_info()["n_dist"] >= 1
-    st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
+    with peng.options(amg_dist=1):
+        xyz, e2n, top, bot = _sim181147(peng, nparts, axis)
+        peng.assemble()
+        st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
+        assert st.status == 0 and st.amg_levels >= 3
+        assert rel(peng.displacement(), sysz["U"]) <= 1e-10
+        assert peng.amg_info()["n_dist"] >= 1
+        st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
     it1, _ = _its_one_partition(engine, xyz, e2n, top, bot, dy)
     assert abs(st8.iters - it1) <= 3, (st8.iters, it1)
 
@@ -99,7 +100,7 @@ def test_partitioned_gamg_split_depths(peng, rep_rows):
     from mfea import PC_GAMG, make_opts
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     dy = float(sysz["dy"])
-    with peng.options(amg_rep_rows=rep_rows):
+    with peng.options(amg_rep_rows=rep_rows, amg_dist=1):
         _sim181147(peng, 3)
         peng.assemble()
         st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
@@ -132,6 +133,24 @@ def test_partitioned_block_jacobi_gamg_matches_direct(peng, nparts, axis):
     assert st8.iters <= int(sysz["pcg_iters_1e8"]) // 4, st8.iters
 
 
+def test_partitioned_gamg_auto_mode_picks_the_faster(peng, engine):
+    """Option "amg_dist" -1 (the default): the first solve of an active set
+    runs the global hierarchy, the second block Jacobi, the third the faster
+    — on this network (no gaps for the cuts to follow) the global one, with
+    the one-partition iteration count."""
+    from mfea import PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    assert peng.get_option("amg_dist") == -1
+    xyz, e2n, top, bot = _sim181147(peng, 3)
+    peng.assemble()
+    its = [peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG)).iters for _ in range(3)]
+    it1, _ = _its_one_partition(engine, xyz, e2n, top, bot, dy)
+    assert abs(its[0] - it1) <= 3 and its[1] > 4 * it1, (its, it1)
+    assert its[2] == its[0], its
+    assert rel(peng.displacement(), sysz["U"]) <= 1e-6
+
+
 def test_partitioned_gamg_grown_network_8_parts(peng, engine):
     """A network grown by the native producer (165k DOF, no tiling gaps) on 8
     partitions: the one-partition iteration count (±3) and the same U."""
@@ -144,7 +163,8 @@ def test_partitioned_gamg_grown_network_8_parts(peng, engine):
     peng.set_bc(top, bot)
     peng.set_active(None)
     peng.assemble()
-    st = peng.solve(0.01, -0.01, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
+    with peng.options(amg_dist=1):
+        st = peng.solve(0.01, -0.01, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
     assert st.status == 0 and peng.info()["n_parts"] == 8
     assert abs(st.iters - it1) <= 3, (st.iters, it1)
     assert rel(peng.displacement(), U1) <= 1e-6
@@ -176,17 +196,18 @@ def test_partitioned_gamg_iterations_on_tiled_network(peng, engine, nparts, axis
     assert rel(Us[1], Us[0]) <= 1e-6
 
 
-@pytest.mark.parametrize("precond", [0, 2])
-def test_partitioned_graph_replay_equals_eager(peng, precond):
+@pytest.mark.parametrize("precond,amg_dist", [(0, -1), (2, 1), (2, 0)])
+def test_partitioned_graph_replay_equals_eager(peng, precond, amg_dist):
     """The chunk (kernels + exchanges) as a hipGraph replay and as eager
-    launches: the same operations in the same order, bit-equal U."""
+    launches: the same operations in the same order, bit-equal U (GAMG: the
+    distributed V-cycle and block Jacobi)."""
     from mfea import make_opts
     _sim181147(peng, 3)
     peng.assemble()
     opts = make_opts(rtol=1e-10, max_it=200000, precond=precond)
     out = []
     for g in (1, 0):
-        with peng.options(dist_graph=g):
+        with peng.options(dist_graph=g, amg_dist=amg_dist):
             st = peng.solve(0.01, -0.01, opts)
             out.append((st.iters, peng.displacement()))
     assert out[0][0] == out[1][0]
@@ -311,7 +332,9 @@ def test_dropin_partitioned_csvs_match_one_partition(tmp_path):
     for f in a:
         assert list(a[f].columns) == list(b[f].columns) and a[f].shape == b[f].shape, f
     assert a["active_elements.csv"].equals(b["active_elements.csv"])
-    for f, tol in (("node_displacements.csv", 1e-10), ("stress_record.csv", 1e-8)):
+    # stress = E·n·(u2 − u1)/L: a difference of nearly equal displacements,
+    # so its relative agreement is ~1e3 × U's
+    for f, tol in (("node_displacements.csv", 1e-10), ("stress_record.csv", 1e-7)):
         A, B = a[f].values[:, :-1], b[f].values[:, :-1]
         for k in range(1, len(A)):
             assert rel(B[k], A[k]) <= tol, (f, k)

@@ -66,7 +66,7 @@ def parse():
     return ap.parse_args()
 
 
-def amg_iteration_bytes(ai):
+def amg_iteration_bytes(ai, compact=None):
     """Algorithmic HBM bytes of one GAMG-PCG iteration: every
     launch of the iteration, each array counted once per launch.  The V-cycle
     is f32 (B = 4·ND² bytes per block, V = 4·ND per row vector), the CG f64
@@ -79,6 +79,10 @@ def amg_iteration_bytes(ai):
       restrict pb·(B+4) + V·n + (2V + B)·n'        (Pᵀ, t in; b', x' out, D⁻¹')
       prolong  pb·(B+4) + 2V·n + V·n'              (P, x in/out, e' in)
       post     nb·(BA+4) + (2V + B + Vb)·n         (A, x, D⁻¹, b in; e out)
+    The compact cycle (amg_cycle 1; tb blocks of P̃_l = R̃_ᵀ per level):
+      down     tb·(B+4) + nb·(BA+4) + (Vb + 2V + B)·n + (B + 2V)·n'
+               (R̃, A, b once, x, D⁻¹ in; c out; D⁻¹' in, b', x' out)
+      up       tb·(B+4) + 2V·n + V·n'                (P̃, c in, e out; e' in)
     CG: update (9·V8 + V + B + V)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀ out);
         w      nb0·(Bs8+4) + (2·V8 + V)·n0         (A_0, r, u in; w out).
     """
@@ -86,11 +90,18 @@ def amg_iteration_bytes(ai):
     ns = nd * (nd + 1) // 2
     B, V, V8, Bs, Bs8 = 4 * nd * nd, 4 * nd, 8 * nd, 4 * ns, 8 * ns
     rows, blocks, pbl = ai["rows"], ai["blocks"], ai["pblocks"]
+    if compact is None:
+        compact = ai.get("cycle", 0) == 1
     b = 0
     for l in range(ai["levels"] - 1):
         n, nn = rows[l], rows[l + 1]
         Vb = V8 if l == 0 else V
         BA = Bs if l == 0 else B
+        if compact:
+            tb = ai["ptblocks"][l]
+            b += tb * (B + 4) + blocks[l] * (BA + 4) + (Vb + 2 * V + B) * n + (B + 2 * V) * nn
+            b += tb * (B + 4) + 2 * V * n + V * nn
+            continue
         b += blocks[l] * (BA + 4) + (2 * V + Vb) * n
         b += pbl[l] * (B + 4) + V * n + (2 * V + B) * nn
         b += pbl[l] * (B + 4) + 2 * V * n + V * nn
@@ -402,13 +413,18 @@ def main():
     if pc == PC_GAMG:
         ai = eng.amg_info()
         iter_bytes = amg_iteration_bytes(ai)
-        # levels from the first one of ≤ 2048 rows (above the coarsest) run in
-        # one single-workgroup launch (the engine's default amg_tail_rows)
         nl = ai["levels"]
-        tail = next((l for l in range(1, nl - 1) if ai["rows"][l] <= 2048), 0)
-        launches = 2 + (4 * tail + 1 if tail else 4 * (nl - 1))
+        if ai.get("cycle", 0) == 1:  # compact cycle: two sweeps per level
+            launches = 2 + 2 * (nl - 1)
+            form = "compact"
+        else:
+            # levels from the first one of ≤ 2048 rows (above the coarsest) run
+            # in one single-workgroup launch (the engine's default amg_tail_rows)
+            tail = next((l for l in range(1, nl - 1) if ai["rows"][l] <= 2048), 0)
+            launches = 2 + (4 * tail + 1 if tail else 4 * (nl - 1))
+            form = "four-step"
         iter_kernel = (f"GAMG-PCG iteration ({launches} launches: update + "
-                       f"{nl}-level V-cycle + w = A u)")
+                       f"{nl}-level {form} V-cycle + w = A u)")
         spmv_ms = eng.profile_spmv(reps=100)
         nd = ai["nd"]
         spmv_bytes = amg_spmv_bytes(ai)

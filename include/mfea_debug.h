@@ -61,9 +61,11 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value);
  * blocks[l] (stored ND×ND blocks of A_l, diagonal included) and pblocks[l]
  * (blocks of the prolongator P_l; 0 on the coarsest level).  *pair_items =
  * index-list entries of the numeric setup; *nd = DOFs per node; *n_dist =
- * levels split over the partitions (0: one partition). */
+ * levels split over the partitions (0: one partition); ptblocks (may be
+ * NULL): blocks of the compact cycle's P̃_l = (I − ω D⁻¹ A) P_l (= of R̃_l). */
 int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
-                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist);
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist,
+                        int64_t* ptblocks);
 
 /* One MFEA_PC_GAMG V-cycle u = M r on the assembled operator (call after
  * mfea_assemble; runs the numeric setup first).  r, u: n_nodes × ND in

@@ -33,314 +33,10 @@
 // u = M r the V-cycle output: per iteration one update kernel (reads the
 // previous partials, forms α, β, the stopping test), the V-cycle, and one
 // w = A_0 u kernel (f64 A_0) that writes the next partials (γ, δ, ‖r‖², ‖u‖²).
-#include "amg_kernels.hpp"
-#include "device_util.hpp"
+#include "amg_dev.hpp"
 
 namespace mfea {
 
-// ---- block / vector helpers (T = storage type, C = compute type) -----------
-// Blocks are stored block-major ([position][NB2]): a SELL slot's 64 lanes read
-// 64 consecutive blocks (one contiguous run, 16/32-B vector loads per lane),
-// and the setup's index-list gathers fetch one contiguous block per item
-// instead of NB2 separate cache lines (the component-major layout made the
-// Galerkin products ≈ 0.7 TB/s effective).
-template <int ND, class T, class C>
-__device__ __forceinline__ void bload(const T* __restrict__ v, int64_t /*npos*/, int64_t q, C* m) {
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) m[c] = (C)v[q * (ND * ND) + c];
-}
-template <int ND, class T, class C>
-__device__ __forceinline__ void bstore(T* __restrict__ v, int64_t /*npos*/, int64_t q, const C* m) {
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) v[q * (ND * ND) + c] = (T)m[c];
-}
-// symmetric blocks stored as their upper triangle (A_0: AmgMatD::sym)
-template <int ND>
-constexpr int nsym() { return ND * (ND + 1) / 2; }
-template <int ND, class T, class C>
-__device__ __forceinline__ void bload_sym(const T* __restrict__ v, int64_t q, C* m) {
-  constexpr int NS = nsym<ND>();
-  C t[NS];
-#pragma unroll
-  for (int c = 0; c < NS; ++c) t[c] = (C)v[q * NS + c];
-  if constexpr (ND == 2) {
-    m[0] = t[0]; m[1] = t[1];
-    m[2] = t[1]; m[3] = t[2];
-  } else {
-    m[0] = t[0]; m[1] = t[1]; m[2] = t[2];
-    m[3] = t[1]; m[4] = t[3]; m[5] = t[4];
-    m[6] = t[2]; m[7] = t[4]; m[8] = t[5];
-  }
-}
-template <int ND, class T, class C>
-__device__ __forceinline__ void bstore_sym(T* __restrict__ v, int64_t q, const C* m) {
-  if constexpr (ND == 2) {
-    v[q * 3 + 0] = (T)m[0]; v[q * 3 + 1] = (T)m[1]; v[q * 3 + 2] = (T)m[3];
-  } else {
-    v[q * 6 + 0] = (T)m[0]; v[q * 6 + 1] = (T)m[1]; v[q * 6 + 2] = (T)m[2];
-    v[q * 6 + 3] = (T)m[4]; v[q * 6 + 4] = (T)m[5]; v[q * 6 + 5] = (T)m[8];
-  }
-}
-template <int ND, class T, class C>
-__device__ __forceinline__ void vload(const T* __restrict__ v, int64_t i, C* o) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a) o[a] = (C)v[ND * i + a];
-}
-template <int ND, class T, class C>
-__device__ __forceinline__ void vstore(T* __restrict__ v, int64_t i, const C* o) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a) v[ND * i + a] = (T)o[a];
-}
-// C += A B
-template <int ND>
-__device__ __forceinline__ void mm_acc(const double* A, const double* Bm, double* C) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a)
-#pragma unroll
-    for (int b = 0; b < ND; ++b) {
-      double s = C[a * ND + b];
-#pragma unroll
-      for (int k = 0; k < ND; ++k) s = fma(A[a * ND + k], Bm[k * ND + b], s);
-      C[a * ND + b] = s;
-    }
-}
-// C += Aᵀ B
-template <int ND>
-__device__ __forceinline__ void mtm_acc(const double* A, const double* Bm, double* C) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a)
-#pragma unroll
-    for (int b = 0; b < ND; ++b) {
-      double s = C[a * ND + b];
-#pragma unroll
-      for (int k = 0; k < ND; ++k) s = fma(A[k * ND + a], Bm[k * ND + b], s);
-      C[a * ND + b] = s;
-    }
-}
-// exact inverse (adjugate / determinant); a singular block (a free row with
-// no active element and reg = 0) gets 0, as PCJACOBI's guard does
-template <int ND>
-__device__ __forceinline__ void binv(const double* m, double* o) {
-  if constexpr (ND == 2) {
-    const double det = m[0] * m[3] - m[1] * m[2];
-    const double id = det != 0.0 ? 1.0 / det : 0.0;
-    o[0] = m[3] * id;
-    o[1] = -m[1] * id;
-    o[2] = -m[2] * id;
-    o[3] = m[0] * id;
-  } else {
-    const double c00 = m[4] * m[8] - m[5] * m[7];
-    const double c01 = m[5] * m[6] - m[3] * m[8];
-    const double c02 = m[3] * m[7] - m[4] * m[6];
-    const double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
-    const double id = det != 0.0 ? 1.0 / det : 0.0;
-    o[0] = c00 * id;
-    o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
-    o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
-    o[3] = c01 * id;
-    o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
-    o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
-    o[6] = c02 * id;
-    o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
-    o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
-  }
-}
-// symmetric block of the assembled operator (xx xy xz yy yz zz) → ND×ND
-template <int ND>
-__device__ __forceinline__ void sym_to(const double* s6, double* m) {
-  if constexpr (ND == 2) {
-    m[0] = s6[0];
-    m[1] = s6[1];
-    m[2] = s6[1];
-    m[3] = s6[3];
-  } else {
-    m[0] = s6[0]; m[1] = s6[1]; m[2] = s6[2];
-    m[3] = s6[1]; m[4] = s6[3]; m[5] = s6[4];
-    m[6] = s6[2]; m[7] = s6[4]; m[8] = s6[5];
-  }
-}
-
-__device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gate != kRun; }
-// The V-cycle kernels load the gate with their first operands and test it only
-// before their stores: a test at entry puts one more dependent memory round
-// trip (≈ 1 µs: the flag was written on another XCD) in front of every launch,
-// and a gated launch (only after convergence) may read whatever it likes.
-__device__ __forceinline__ bool gate_open(const int32_t* gate) { return !gate || *gate == kRun; }
-
-// XCD-aware block order for the gathering kernels.  Blocks are dealt
-// round-robin over the 8 XCDs (b and b + 8 share one; MI355X_MICROARCH.md),
-// each with its own L2: numbering the blocks so that every XCD's share is one
-// contiguous row range keeps the neighbour rows a wave gathers in ITS L2
-// instead of fetching the same lines into several.  A bijection on
-// [0, gridDim.x); used for speed only, nothing depends on the placement.
-__device__ __forceinline__ int64_t xcd_block() {
-  const int64_t g = gridDim.x, b = blockIdx.x;
-  const int64_t q = g >> 3, r = g & 7, x = b & 7, i = b >> 3;
-  return x * q + (x < r ? x : r) + i;
-}
-
-// position q of a RowRange's span belongs to one of its rows (only the
-// first and last slice can hold other ranks' rows)
-__device__ __forceinline__ bool pos_mine(const RowRange& g, int64_t q) {
-  if (q >= g.pf && q < g.pl) return true;
-  const int64_t row = 64 * (q < g.pf ? g.s0 : g.s1) + (q & 63);
-  return row >= g.lo && row < g.hi;
-}
-
-// slot range of the wave's slice (scalar loads, wave-uniform)
-__device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
-  const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));
-  const int a = M.sptr[s], b = M.sptr[s + 1];
-  base = (int64_t)a * 64 + (row & 63);
-  width = b - a;
-}
-
-// y ±= Σ_k M_k x_{col_k} over every SELL slot of one row (the diagonal
-// included).  U slots per step with all their loads issued before the first
-// FMA: a row costs ⌈w/U⌉ dependent memory round trips instead of w (the
-// per-thread chain col → value, x is what bounds the small levels).  Slots
-// past the row's width or padded (col < 0) contribute exact zeros.
-template <int ND>
-constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
-
-template <int ND, int U, bool SUB, bool SYM = false, class TV, class TX, class C>
-__device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                           int64_t npos, int64_t base, int w,
-                                           const TX* __restrict__ x, C* y) {
-  for (int k = 0; k < w; k += U) {
-    int32_t c[U];
-    int64_t q[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = k + u < w ? base + (int64_t)(k + u) * 64 : base;
-      c[u] = k + u < w ? col[q[u]] : -1;
-    }
-    C m[U][ND * ND], xc[U][ND];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (SYM) bload_sym<ND>(val, q[u], m[u]);
-      else bload<ND>(val, npos, q[u], m[u]);
-      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
-#pragma unroll
-      for (int a = 0; a < ND; ++a)
-#pragma unroll
-        for (int b = 0; b < ND; ++b)
-          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
-    }
-  }
-}
-// Slices wider than U (the restriction's rows hold ≈ 7 blocks, the coarse
-// A rows 4–5) take one step of 2U loads instead of two dependent steps of U,
-// and with K = 3 slices wider than 2U (the restrictions reach 15–29 blocks on
-// every level) one step of 4U: every slice up to the step's width costs one
-// round trip of column loads and one of gathers.  The width is slice-uniform,
-// so the branches are too.  Each step costs registers, and a kernel's VGPR
-// count is its widest path's: the f64 SpMV, whose level-0 slices are ≤ 4 wide
-// for 98 % of the waves, stays at K = 1 (a 2U path put it at 139 VGPRs, one
-// 768-thread block per CU); the streaming level-0 kernels use K = 2; the
-// restrictions and the latency-bound coarse levels K = 3.
-template <int ND, bool SUB, int K = 2, bool SYM = false, class TV, class TX, class C>
-__device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                         int64_t npos, int64_t base, int w,
-                                         const TX* __restrict__ x, C* y) {
-  constexpr int U = mac_unroll<ND>();
-  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB, SYM>(col, val, npos, base, w, x, y);
-  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB, SYM>(col, val, npos, base, w, x, y);
-  else sell_mac_u<ND, U, SUB, SYM>(col, val, npos, base, w, x, y);
-}
-
-// o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C).  dinv_load / dinv_mul
-// split it so a kernel can issue the block's load before its gather.
-template <int ND, class TD, class C>
-__device__ __forceinline__ void dinv_load(const TD* __restrict__ dinv, int64_t i, C* Di) {
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Di[c] = (C)dinv[i * (ND * ND) + c];
-}
-template <int ND, class C>
-__device__ __forceinline__ void dinv_mul(const C* Di, C s, const C* v, C* o) {
-#pragma unroll
-  for (int a = 0; a < ND; ++a) {
-    C acc = 0;
-#pragma unroll
-    for (int b = 0; b < ND; ++b) acc = fma(Di[a * ND + b], v[b], acc);
-    o[a] = s * acc;
-  }
-}
-template <int ND, class TD, class C>
-__device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t /*n*/, int64_t i, C s,
-                                           const C* v, C* o) {
-  C Di[ND * ND];
-  dinv_load<ND>(dinv, i, Di);
-  dinv_mul<ND>(Di, s, v, o);
-}
-
-// C += Σ_t X[a_t]·Y[b_t] (TX: X[a_t]ᵀ·Y[b_t]) over one index list, in list
-// order, U pairs' loads in flight per step (every pair is two dependent hops:
-// index, then blocks).  Lists longer than 4 take steps of 8 (the Galerkin
-// product's lists run ≈ 2–30 pairs).
-template <int ND, bool TX, int U>
-__device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __restrict__ la,
-                                           const int32_t* __restrict__ lb, const double* __restrict__ X,
-                                           const double* __restrict__ Y, double* C) {
-  for (int t = t0; t < t1; t += U) {
-    int32_t ia[U], ib[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int tt = t + u < t1 ? t + u : t0;
-      ia[u] = la[tt];
-      ib[u] = lb[tt];
-    }
-    double x[U][ND * ND], y[U][ND * ND];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      bload<ND>(X, 0, ia[u], x[u]);
-      bload<ND>(Y, 0, ib[u], y[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
-      if (TX) mtm_acc<ND>(x[u], y[u], C);
-      else mm_acc<ND>(x[u], y[u], C);
-    }
-  }
-}
-template <int ND, bool TX>
-__device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const int32_t* __restrict__ lb, const double* __restrict__ X,
-                                         int64_t /*nx*/, const double* __restrict__ Y, int64_t /*ny*/, double* C) {
-  if (t1 - t0 > 4) pair_sum_u<ND, TX, 8>(t0, t1, la, lb, X, Y, C);
-  else pair_sum_u<ND, TX, 4>(t0, t1, la, lb, X, Y, C);
-}
-// S += Σ_t X[a_t] over one index list, in list order
-template <int ND, int U>
-__device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __restrict__ la,
-                                           const double* __restrict__ X, double* S) {
-  for (int t = t0; t < t1; t += U) {
-    int32_t ia[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) ia[u] = la[t + u < t1 ? t + u : t0];
-    double x[U][ND * ND];
-#pragma unroll
-    for (int u = 0; u < U; ++u) bload<ND>(X, 0, ia[u], x[u]);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) S[c] += x[u][c];
-    }
-  }
-}
-template <int ND>
-__device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const double* __restrict__ X, int64_t /*nx*/, double* S) {
-  if (t1 - t0 > 4) list_sum_u<ND, 8>(t0, t1, la, X, S);
-  else list_sum_u<ND, 4>(t0, t1, la, X, S);
-}
 
 // ---------------------------------------------------------------------------
 // numeric setup (f64, with f32 copies for the V-cycle)
@@ -449,13 +145,6 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
   }
 }
 
-constexpr double kRhoFloor = 2.0;   // the exact level-0 bound (see the header)
-constexpr double kRhoSafety = 1.45; // ω·g ≤ (4/3)·1.45 < 2
-
-// the smoother weight ω_l from the level's Gershgorin bound g = omega[1]
-__device__ __forceinline__ double amg_omega(const double* __restrict__ om) {
-  return (4.0 / 3.0) / fmax(kRhoFloor, om[1] / kRhoSafety);
-}
 
 // P values, one thread per (row, slot k): every slot of a row in flight at
 // once instead of one after another.  Block b = (row block b / wmax, slot
@@ -516,6 +205,55 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
   pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val, L.A.npos, L.P.val, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
+}
+
+// The compact cycle's transfers (amg.hpp AmgLevel::PT), after A·P:
+// P̃(i, J) = P(i, J) − ω D_i⁻¹ (A·P)(i, J) on A·P's pattern (f64, stored f32),
+// one thread per (row, slot) as k_amg_pvals
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
+  const AmgMatD& T = L.PT;
+  const int64_t xb = xcd_block();
+  const int k = (int)(xb % T.wmax);
+  const int64_t i = (xb / T.wmax) * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= T.n) return;
+  int64_t base;
+  int w;
+  slice_of(T, i, base, w);
+  if (i >= T.n || k >= w) return;
+  const int64_t q = base + (int64_t)k * 64;
+  if (T.col[q] < 0) return;
+  const int32_t qp = L.pt_p[q];
+  double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
+  dinv_load<ND>(L.dinv, i, Di);
+  bload<ND>(L.apval, 0, L.pt_ap[q], ap);
+  if (qp >= 0) bload<ND>(L.P.val, 0, qp, pm);
+  else {
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+  mm_acc<ND>(Di, ap, m);
+  const double om = amg_omega(L.omega);
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);
+  bstore<ND>(T.val32, 0, q, pm);
+}
+// R̃ = P̃ᵀ in RT's own SELL layout, one position per thread
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L) {
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
+  if (q >= L.RT.npos) return;
+  const int32_t src = L.rt_pt[q];
+  if (src < 0) return;
+  float p[ND * ND], t[ND * ND];
+  bload<ND>(L.PT.val32, 0, src, p);
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
+  bstore<ND>(L.RT.val32, 0, q, t);
 }
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
@@ -582,49 +320,6 @@ __global__ __launch_bounds__(kBlock) void k_amg_restrict(AmgLevD L, AmgLevD N, c
   vstore<ND>(N.x, I, xn);
 }
 
-// S lanes per row (S = 2, 4) for the SELL operators with wide rows: R's rows
-// hold 7–8 blocks on average and up to 29 (A below level 0: 4–5, up to 16),
-// so one lane per row issues dozens of scattered loads in sequence; here lane
-// `sub` of a row takes slots sub, sub + S, … and the S partial sums meet by a
-// fixed butterfly (deterministic).  The S lanes of a row are adjacent, so a
-// wave covers 64/S rows of one slice and each slot step reads S runs of 64/S
-// consecutive positions.  Every lane ends with the row's full sum.
-template <int ND, int S, bool SUB, class TV, class TX, class C>
-__device__ __forceinline__ void sell_mac_sub(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                             int64_t base, int w, int sub, const TX* __restrict__ x, C* y) {
-  constexpr int U = 2 * mac_unroll<ND>();  // (U = 4: C2 62.4 vs 60.8 µs per iteration)
-  const int wu = (w + S - 1) / S;  // steps: the slice's, uniform
-  const int ws = w > sub ? (w - sub + S - 1) / S : 0;
-  for (int k = 0; k < wu; k += U) {
-    int32_t c[U];
-    int64_t q[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = k + u < ws ? base + (int64_t)((k + u) * S + sub) * 64 : base;
-      c[u] = k + u < ws ? col[q[u]] : -1;
-    }
-    C m[U][ND * ND], xc[U][ND];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      bload<ND>(val, 0, q[u], m[u]);
-      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
-#pragma unroll
-      for (int a = 0; a < ND; ++a)
-#pragma unroll
-        for (int b = 0; b < ND; ++b)
-          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
-    }
-  }
-#pragma unroll
-  for (int o = 1; o < S; o <<= 1)
-#pragma unroll
-    for (int a = 0; a < ND; ++a) y[a] += __shfl_xor(y[a], o, 64);
-}
 
 template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_restrict_s(AmgLevD L, AmgLevD N, const int32_t* gate) {
@@ -744,6 +439,92 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 #pragma unroll
   for (int a = 0; a < ND; ++a) x[a] += d[a];
   if (mine && run) vstore<ND>(e, i, x);
+}
+
+// ---------------------------------------------------------------------------
+// The compact cycle (amg.hpp AmgLevel::PT): two sweeps per level.
+// Down: blocks [0, gc) form the coarse right-hand side b_{l+1} = R̃ b_l (S
+// lanes per coarse row) and x_{l+1} = s D⁻¹ b_{l+1}; blocks from gc on the
+// smoothed part c_l = x_l + ω D⁻¹ (b_l − A x_l), kept in t_l.  Both read only
+// b_l and x_l, so one launch holds them.  L0: b = the CG's f64 r, A_0's
+// symmetric f32 blocks.
+template <int ND, int S, class TB, bool L0>
+__global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, const TB* __restrict__ b, int64_t gc,
+                                                     const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const int64_t xb = xcd_block();
+  if (xb < gc) {
+    const AmgMatD& R = L.RT;
+    const int64_t t = xb * kBlock + threadIdx.x;
+    const int64_t n = R.n;
+    const int64_t I = t / S;
+    const int sub = (int)(t % S);
+    if (I - (threadIdx.x & 63) / S >= n) return;
+    const int64_t Ic = I < n ? I : n - 1;
+    int64_t base;
+    int w;
+    slice_of(R, Ic, base, w);
+    const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
+    float Di[ND * ND], bc[ND];
+    dinv_load<ND>(N.dinv32, Ic, Di);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
+    if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, b, bc);
+    else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, b, bc);
+    if (I >= n || sub != 0 || !run) return;
+    vstore<ND>(N.b, I, bc);
+    float xn[ND];
+    dinv_mul<ND>(Di, sc, bc, xn);
+    vstore<ND>(N.x, I, xn);
+  } else {
+    const int64_t i = (xb - gc) * kBlock + threadIdx.x;
+    const int64_t n = L.A.n;
+    if (i - (threadIdx.x & 63) >= n) return;
+    const int64_t ii = i < n ? i : n - 1;
+    int64_t base;
+    int w;
+    slice_of(L.A, ii, base, w);
+    const float om = (float)amg_omega(L.omega);
+    float y[ND], x[ND], d[ND], Di[ND * ND];
+    vload<ND>(b, ii, y);
+    vload<ND>(L.x, ii, x);
+    dinv_load<ND>(L.dinv32, ii, Di);
+    if constexpr (L0)
+      sell_mac<ND, true, 2, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
+    else
+      sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
+    dinv_mul<ND>(Di, om, y, d);
+#pragma unroll
+    for (int a = 0; a < ND; ++a) x[a] += d[a];
+    if (i < n && run) vstore<ND>(L.t, i, x);
+  }
+}
+
+// Up: e_l = c_l + P̃ e_{l+1} (the coarsest level's output is its x), S lanes
+// per row; level 0 writes the CG's u
+template <int ND, int S, class TE>
+__global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __restrict__ e, const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const AmgMatD& T = L.PT;
+  const int64_t t = xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = T.n;
+  const int64_t i = t / S;
+  const int sub = (int)(t % S);
+  if (i - (threadIdx.x & 63) / S >= n) return;
+  const int64_t ii = i < n ? i : n - 1;
+  int64_t base;
+  int w;
+  slice_of(T, ii, base, w);
+  float y[ND];
+  vload<ND>(L.t, ii, y);
+  if (sub != 0) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) y[a] = 0.0f;
+  }
+  const float* src = N.coarsest ? N.x : N.e;
+  if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
+  else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
+  if (i < n && sub == 0 && run) vstore<ND>(e, i, y);
 }
 
 // ---------------------------------------------------------------------------
@@ -1157,8 +938,13 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
   if (L.coarsest || !N) return;
   if (stage & kSetupP && L.P.wmax > 0)
     hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.rg.span()).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
-  if (stage & kSetupAP)
+  if (stage & kSetupAP) {
     hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
+    if (L.compact && L.PT.wmax > 0) {
+      hipLaunchKernelGGL(k_amg_ptv<ND>, dim3(rows_grid(L.PT.n).x * (unsigned)L.PT.wmax), dim3(kBlock), 0, s, L);
+      hipLaunchKernelGGL(k_amg_rtv<ND>, rows_grid(L.RT.npos), dim3(kBlock), 0, s, L);
+    }
+  }
   if (stage & kSetupAC)
     hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, N->A, N->omega);
 }
@@ -1175,10 +961,12 @@ static int lanes_for(const AmgMatD& M, int forced, double two, double four) {
   const double mean_w = M.n > 0 ? (double)M.npos / (double)(((M.n + 63) / 64) * 64) : 0.0;
   return mean_w > four ? 4 : mean_w > two ? 2 : 1;
 }
+int amg_restrict_lanes(const AmgLevD& L) { return lanes_for(L.R, L.rlanes, 2.5, 5.0); }
+int amg_op_lanes(const AmgLevD& L) { return lanes_for(L.A, L.alanes, 3.5, 8.0); }
 template <int ND>
 static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int64_t n = L.R.rg.span();
-  const int S = lanes_for(L.R, L.rlanes, 2.5, 5.0);
+  const int S = amg_restrict_lanes(L);
   const dim3 b(kBlock);
   if (S == 8) hipLaunchKernelGGL((k_amg_restrict_s<ND, 8>), rows_grid(8 * n), b, 0, s, L, N, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_restrict_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, N, gate);
@@ -1188,7 +976,7 @@ static void launch_restrict(hipStream_t s, const AmgLevD& L, const AmgLevD& N, c
 template <int ND>
 static void launch_op(hipStream_t s, const AmgLevD& L, bool post, const int32_t* gate) {
   const int64_t n = L.A.rg.span();
-  const int S = lanes_for(L.A, L.alanes, 3.5, 8.0);
+  const int S = amg_op_lanes(L);
   const dim3 b(kBlock);
   if (S == 4) {
     if (post) hipLaunchKernelGGL((k_amg_post_s<ND, 4>), rows_grid(4 * n), b, 0, s, L, gate);
@@ -1227,11 +1015,68 @@ static void prolong_nd(hipStream_t s, const AmgLevD* lev, int l, const int32_t* 
   hipLaunchKernelGGL(k_amg_prolong<ND>, rows_grid(lev[l].P.rg.span()), dim3(kBlock), 0, s, lev[l], lev[l + 1], gate);
 }
 
+// the compact cycle's sweeps (lanes per row by the matrices' mean widths)
+int amg_down_lanes(const AmgLevD& L) { return lanes_for(L.RT, L.rlanes, 2.5, 5.0); }
+int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, 0, 3.5, 8.0); }
+template <int ND, class TB, bool L0>
+static void down_tb(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const TB* b, const int32_t* gate) {
+  const int S = amg_down_lanes(L);
+  const int64_t gc = rows_grid(S * L.RT.n).x;
+  const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
+  if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
+  else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
+  else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
+  else hipLaunchKernelGGL((k_amg_down<ND, 1, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
+}
+template <int ND, class TE>
+static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, const int32_t* gate) {
+  const int S = amg_up_lanes(L);
+  const dim3 g(rows_grid(S * L.PT.n));
+  if (S == 4) hipLaunchKernelGGL((k_amg_up<ND, 4, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
+  else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
+  else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
+}
+template <int ND>
+static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const int32_t* gate, int l0) {
+  for (int l = l0; l + 1 < nlev; ++l) {
+    if (l == 0) down_tb<ND, double, true>(s, lev[0], lev[1], (const double*)cg.r, gate);
+    else down_tb<ND, float, false>(s, lev[l], lev[l + 1], (const float*)lev[l].b, gate);
+  }
+  for (int l = nlev - 2; l >= l0; --l) {
+    if (l == 0) up_te<ND, float>(s, lev[0], lev[1], cg.u, gate);
+    else up_te<ND, float>(s, lev[l], lev[l + 1], lev[l].e, gate);
+  }
+}
+bool amg_compact_ok(const AmgLevD* lev, int nlev, int l0) {
+  for (int l = l0; l + 1 < nlev; ++l)
+    if (!lev[l].compact || lev[l].PT.n != lev[l].A.n || lev[l].A.rg.lo != 0 || lev[l].A.rg.hi != lev[l].A.n)
+      return false;
+  return nlev - l0 >= 2;
+}
+
 // The V-cycle of levels [l0, nlev) on level l0's b, x (the producer of b set
 // x = ω D⁻¹ b), leaving level l0's output in its e (level 0: the CG's u).
 template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
                       int tail, const int32_t* gate, int l0) {
+  if (cg.cycle == 1 && amg_compact_ok(lev, nlev, l0)) {
+    compact_nd<ND>(s, lev, nlev, cg, gate, l0);
+    return;
+  }
+  // levels [deep, nlev) in the persistent launch (amg_deep.hip), if they fit it
+  const int deep = cg.deep > 0 ? (cg.deep > l0 ? cg.deep : (l0 > 0 ? l0 : 1)) : 0;
+  if (deep > 0 && deep < nlev - 1 && cg.deep_bar && amg_deep_fits(lev, nlev, deep)) {
+    for (int l = l0; l < deep; ++l) {
+      resid_nd<ND>(s, lev, l, cg, gate);
+      launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
+    }
+    launch_amg_deep(s, ND, lev, nlev, deep, cg, gate);
+    for (int l = deep - 1; l >= l0; --l) {
+      prolong_nd<ND>(s, lev, l, gate);
+      post_nd<ND>(s, lev, l, cg, gate);
+    }
+    return;
+  }
   if (tail > 0 && tail < l0) tail = l0;
   const int top = tail > 0 ? tail : nlev - 1;  // levels [top, nlev) run inside k_amg_tail
   for (int l = l0; l < top; ++l) {

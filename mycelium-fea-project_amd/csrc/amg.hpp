@@ -77,6 +77,18 @@ struct AmgLevel {
   SellPat AP;                // n × nc
   PosList ap;                // AP(i, J) = Σ A[a] · P[b]
   PosList ac;                // A_{l+1}(I, J) = Σ P[a]ᵀ · AP[b]   (positions of level l+1's A)
+  // the compact cycle (amg.hip, option amg_cycle 1): the smoothed transfer
+  // P̃ = (I − ω D⁻¹ A) P on A·P's pattern with the level's own row labels,
+  // and R̃ = P̃ᵀ.  With them one V(1,1) cycle level is two sweeps instead of four:
+  //   down  b_{l+1} = R̃ b_l,  c_l = x_l + ω D⁻¹ (b_l − A x_l)   (x_l = ω D⁻¹ b_l)
+  //   up    e_l = c_l + P̃ e_{l+1}
+  // (e = x + P e' + ω D⁻¹(b − A(x + P e')) = c + (I − ω D⁻¹ A) P e', and
+  // R(b − A x) = R (I − ω A D⁻¹) b = P̃ᵀ b: the same preconditioner).
+  SellPat PT;                  // n × nc
+  std::vector<int32_t> pt_ap;  // PT position → its A·P position
+  std::vector<int32_t> pt_p;   // PT position → the P position of the same block, or -1
+  SellPat RT;                  // nc × n
+  std::vector<int32_t> rt_pt;  // RT position → PT position (value = PT[rt_pt]ᵀ)
 };
 
 struct AmgPlan {

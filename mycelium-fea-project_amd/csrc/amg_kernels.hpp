@@ -80,6 +80,13 @@ struct AmgLevD {
   const int32_t* ac_a = nullptr;
   const int32_t* ac_b = nullptr;
   RowRange ac_rg;  // level l+1's A rows this rank's Galerkin product forms (= R's rows)
+  // the compact cycle (amg.hpp AmgLevel::PT): P̃ (f32, PT.val32) and R̃ = P̃ᵀ
+  // (RT.val32), formed by the setup after A·P when compact is set
+  int compact = 0;
+  AmgMatD PT, RT;
+  const int32_t* pt_ap = nullptr;
+  const int32_t* pt_p = nullptr;
+  const int32_t* rt_pt = nullptr;
 };
 
 // CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
@@ -96,6 +103,15 @@ struct AmgCg {
   double* w = nullptr;
   float* u = nullptr;   // level 0's V-cycle output: the f32 cycle's values, stored
                         // exactly (half the bytes of f64 for every gather of u)
+  // the persistent deep-level V-cycle (amg_deep.hip): levels [deep, nlev) in
+  // ONE launch of deep_wgs workgroups (deep = 0: per-level launches and the
+  // single-workgroup tail); deep_bar: its barrier words (zero between launches)
+  int deep = 0;
+  int deep_wgs = 0;
+  unsigned* deep_bar = nullptr;
+  // 1: the compact cycle (two sweeps per level, AmgLevD::PT) where every
+  // level of the cycle has it (compact set: unsplit levels); 0: four steps
+  int cycle = 0;
 };
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered
@@ -123,7 +139,7 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 // dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
 // (level0: its D⁻¹ was formed by launch_amg_a0).  stage: which of the four
 // steps (the distributed setup exchanges values between them)
-constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll = 15;
+constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll = 15;  // (kSetupAP: + P̃, R̃)
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0,
                             int stage = kSetupAll);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
@@ -148,6 +164,25 @@ void launch_amg_xinit_rows(hipStream_t s, int nd, const AmgLevD& N, const int32_
 // partitions on one device: every partition's Gershgorin bound g (omega[1])
 // set to the maximum over them (what an RCCL all-reduce max does across GPUs)
 void launch_amg_bound_max(hipStream_t s, double* const* omegas, int n);
+// lanes per row of level L's restriction (1, 2, 4, 8) and of its f32
+// operator below level 0 (1, 2, 4): by the mean slice width, or the option
+int amg_restrict_lanes(const AmgLevD& L);
+int amg_op_lanes(const AmgLevD& L);
+// the compact cycle: lanes per row of its down (R̃) and up (P̃) sweeps; whether
+// levels [l0, nlev) all have it
+int amg_down_lanes(const AmgLevD& L);
+int amg_up_lanes(const AmgLevD& L);
+bool amg_compact_ok(const AmgLevD* lev, int nlev, int l0);
+// ---- the deep-level V-cycle in one persistent launch (amg_deep.hip) --------
+// levels [l0, nlev) of the cycle on level l0's b, x (output: its e), deep_wgs
+// workgroups synchronised by grid barriers on deep_bar.  False (nothing
+// launched) when the levels do not fit the launch (kDeepMaxLev, row ranges).
+constexpr int kDeepMaxLev = 8;
+constexpr int kDeepBarWords = 320;     // 8 shards + done + timeout, 128 B apart
+constexpr int kDeepTimeoutWord = 288;  // sticky: a barrier wait gave up
+bool amg_deep_fits(const AmgLevD* lev, int nlev, int l0);
+bool launch_amg_deep(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int l0, const AmgCg& cg,
+                     const int32_t* gate);
 // first level l ≥ 1 (above the coarsest) with at most max_rows rows, or 0
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------

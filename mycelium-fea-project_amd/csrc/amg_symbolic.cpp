@@ -501,6 +501,38 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
         for (int64_t i = 0; i < L.A.n; ++i) out.aprow[perm[l][i]] = pap[i];
       }
     }
+    // the compact cycle's P̃ (A·P's entries, the level's row labels) and R̃ = P̃ᵀ
+    {
+      std::vector<int32_t> ePT, eRT;
+      if (!(err = layout(L.AP, perm[l], &perm[l + 1], out.PT, ePT)).empty()) return err;
+      out.pt_ap.assign(out.PT.n_pos(), -1);
+      out.pt_p.assign(out.PT.n_pos(), -1);
+      for (int64_t i = 0; i < L.A.n; ++i) {  // both rows ascending in J: merge
+        int64_t k = L.P.ptr[i];
+        for (int64_t e = L.AP.ptr[i]; e < L.AP.ptr[i + 1]; ++e) {
+          out.pt_ap[ePT[e]] = eAP[e];
+          while (k < L.P.ptr[i + 1] && L.P.col[k] < L.AP.col[e]) ++k;
+          if (k < L.P.ptr[i + 1] && L.P.col[k] == L.AP.col[e]) out.pt_p[ePT[e]] = eP[k];
+        }
+      }
+      Csr RT;  // transpose of A·P: coarse row J → fine rows ascending
+      std::vector<int32_t> rt_e(L.AP.col.size());
+      RT.n = L.nc;
+      RT.ptr.assign(L.nc + 1, 0);
+      for (int32_t J : L.AP.col) RT.ptr[J + 1]++;
+      for (int64_t J = 0; J < L.nc; ++J) RT.ptr[J + 1] += RT.ptr[J];
+      RT.col.resize(L.AP.col.size());
+      std::vector<int64_t> fill(RT.ptr.begin(), RT.ptr.end() - 1);
+      for (int64_t i = 0; i < L.A.n; ++i)
+        for (int64_t e = L.AP.ptr[i]; e < L.AP.ptr[i + 1]; ++e) {
+          const int64_t t = fill[L.AP.col[e]]++;
+          RT.col[t] = (int32_t)i;
+          rt_e[t] = (int32_t)e;
+        }
+      if (!(err = layout(RT, perm[l + 1], &perm[l], out.RT, eRT)).empty()) return err;
+      out.rt_pt.assign(out.RT.n_pos(), -1);
+      for (size_t t = 0; t < rt_e.size(); ++t) out.rt_pt[eRT[t]] = ePT[rt_e[t]];
+    }
     if (!(err = to_pos(L.pv, eP, out.P.n_pos(), &eA[l], nullptr, false, out.pv, plan.pair_items)).empty())
       return err;
     out.rp.assign(out.R.n_pos(), -1);

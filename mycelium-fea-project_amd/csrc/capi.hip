@@ -123,6 +123,8 @@ struct Part {
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
+  int amg_first = 1;                 // first level the tail / the deep launch may start at (not split)
+  DevBuf<unsigned> amg_deep_bar;     // the deep launch's barrier words (amg_deep.hip)
   AmgCg amg_cg;
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
@@ -204,6 +206,10 @@ struct mfea_handle {
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
+  int opt_amg_cycle = 1;       // GAMG: 1 the compact V-cycle (two sweeps per level), 0 four steps
+  int opt_amg_deep = 0;        // GAMG: first level of the persistent deep launch (-1: by amg_deep_rows, 0: none)
+  int64_t opt_amg_deep_rows = 262144;  // GAMG: the deep launch starts at the first level of at most this many rows
+  int opt_amg_deep_wgs = 128;  // GAMG: workgroups of the deep launch (8..256)
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   int opt_amg_dist = -1;          // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block
                                   // Jacobi over per-partition hierarchies, -1 whichever solves faster (measured)
@@ -982,6 +988,31 @@ RowRange row_range(const SellPat& S, int64_t lo, int64_t hi) {
 // device allocations and uploads the indices.  Pass 0 sizes, pass 1 carves.
 // rk (distributed GAMG): this partition's row ranges, with its own level-0
 // lists over ITS pattern (a0, row0) in place of the plan's.
+// The persistent deep-level launch of the V-cycle (amg_deep.hip): its first
+// level (option amg_deep, or the first unsplit level of at most amg_deep_rows
+// rows), its workgroups and its barrier words (zeroed once; every launch
+// leaves them zero).
+int set_amg_deep(mfea_handle* h, Part& pt) {
+  const int nlev = (int)pt.amg_lev.size();
+  int deep = 0;
+  if (h->opt_amg_deep > 0) deep = std::max(pt.amg_first, h->opt_amg_deep);
+  else if (h->opt_amg_deep < 0)
+    for (int l = pt.amg_first; l + 1 < nlev; ++l)
+      if (pt.amg_lev[l].A.n <= h->opt_amg_deep_rows) {
+        deep = l;
+        break;
+      }
+  if (deep >= nlev - 1 || !amg_deep_fits(pt.amg_lev.data(), nlev, deep)) deep = 0;
+  if (deep > 0 && !pt.amg_deep_bar.ptr) {
+    HIPC(pt.amg_deep_bar.alloc(kDeepBarWords));
+    HIPC(hipMemset(pt.amg_deep_bar.ptr, 0, kDeepBarWords * sizeof(unsigned)));
+  }
+  pt.amg_cg.deep = deep;
+  pt.amg_cg.deep_wgs = h->opt_amg_deep_wgs;
+  pt.amg_cg.deep_bar = pt.amg_deep_bar.ptr;
+  return 0;
+}
+
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
                const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
   const int nd = pl.nd, nb2 = nd * nd;
@@ -1089,6 +1120,18 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         d.ac_ptr = I(L.ac.ptr);
         d.ac_a = I(L.ac.a);
         d.ac_b = I(L.ac.b);
+        // the compact cycle's P̃ / R̃ (one partition's hierarchy only: the
+        // distributed V-cycle exchanges per four-step step)
+        if (!rk && L.PT.n == n) {
+          d.PT = mat(L.PT, false, true);
+          d.PT.rg = row_range(L.PT, 0, n);
+          d.pt_ap = I(L.pt_ap);
+          d.pt_p = I(L.pt_p);
+          d.RT = mat(L.RT, false, true);
+          d.RT.rg = row_range(L.RT, 0, L.RT.n);
+          d.rt_pt = I(L.rt_pt);
+          d.compact = h->opt_amg_cycle;
+        }
       }
     }
     pt.amg_a0_ptr = I(a0 ? a0->ptr : pl.a0.ptr);
@@ -1098,6 +1141,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.lo = rk && nlev ? rk->lo[0] : 0;
     pt.amg_cg.hi = rk && nlev ? rk->hi[0] : nf;
     pt.amg_cg.w_block = h->opt_amg_w_block;
+    pt.amg_cg.cycle = h->opt_amg_cycle;
     pt.amg_cg.row0 = I(row0 ? *row0 : pl.row0);
     pt.amg_cg.x = D((size_t)nd * nf);
     pt.amg_cg.p = D((size_t)nd * nf);
@@ -1114,7 +1158,9 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     const int first = rk ? std::max(1, rk->n_dist) : 1;
     pt.amg_tail = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_tail_rows) : 0;
     if (pt.amg_tail > 0) pt.amg_tail += first - 1;
+    pt.amg_first = first;
   }
+  RC(set_amg_deep(h, pt));
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -2761,7 +2807,8 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
 }
 
 int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* blocks,
-                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist) {
+                        int64_t* pblocks, int cap, int64_t* pair_items, int* nd, int* n_dist,
+                        int64_t* ptblocks) {
   if (!h || !n_levels || cap < 0 || (cap && (!rows || !blocks || !pblocks)))
     return fail(MFEA_EINVAL, "bad argument");
   RC(set_device(h));
@@ -2782,6 +2829,11 @@ int mfea_debug_amg_info(mfea_handle* h, int* n_levels, int64_t* rows, int64_t* b
     int64_t pb = 0;
     for (int32_t r : pl.lev[l].P.rlen) pb += r;
     pblocks[l] = pb;
+    if (ptblocks) {
+      int64_t tb = 0;
+      for (int32_t r : pl.lev[l].PT.rlen) tb += r;
+      ptblocks[l] = tb;
+    }
   }
   if (pair_items) *pair_items = pl.pair_items;
   if (nd) *nd = pl.nd;
@@ -2835,6 +2887,30 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_tail_lds = value != 0;
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
+  }
+  else if (n == "amg_cycle") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_cycle: 0 (four steps per level) or 1 (compact)");
+    h->opt_amg_cycle = (int)value;
+    for (auto& pp : h->parts) {
+      pp->amg_cg.cycle = (int)value;
+      for (auto& L : pp->amg_lev)
+        if (L.PT.n > 0) L.compact = (int)value;
+    }
+  }
+  else if (n == "amg_deep" || n == "amg_deep_rows" || n == "amg_deep_wgs") {
+    if (n == "amg_deep") {
+      if (value < -1 || value >= kAmgMaxLevels) return fail(MFEA_EINVAL, "amg_deep: -1 (by amg_deep_rows), 0 (none) or a level");
+      h->opt_amg_deep = (int)value;
+    } else if (n == "amg_deep_rows") {
+      if (value < 0) return fail(MFEA_EINVAL, "amg_deep_rows: >= 0");
+      h->opt_amg_deep_rows = value;
+    } else {
+      if (value < 8 || value > 256) return fail(MFEA_EINVAL, "amg_deep_wgs: 8..256");
+      h->opt_amg_deep_wgs = (int)value;
+    }
+    RC(set_device(h));
+    for (auto& pp : h->parts)
+      if (!pp->amg_lev.empty()) RC(set_amg_deep(h, *pp));
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "amg_dist") {
@@ -2989,6 +3065,24 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
+  else if (n == "amg_cycle") *value = h->opt_amg_cycle;
+  else if (n == "amg_deep") *value = h->opt_amg_deep;
+  else if (n == "amg_deep_rows") *value = h->opt_amg_deep_rows;
+  else if (n == "amg_deep_wgs") *value = h->opt_amg_deep_wgs;
+  else if (n == "amg_deep_level") {  // read-only: the first level of partition 0's deep launch (0: none)
+    *value = h->parts.empty() ? 0 : h->parts[0]->amg_cg.deep;
+  }
+  else if (n == "amg_deep_timeouts") {  // read-only: a deep launch gave up a barrier wait (never expected)
+    *value = 0;
+    RC(set_device(h));
+    for (auto& pp : h->parts)
+      if (pp->amg_deep_bar.ptr) {
+        unsigned w[kDeepBarWords];
+        HIPC(hipStreamSynchronize(h->stream));
+        HIPC(hipMemcpy(w, pp->amg_deep_bar.ptr, sizeof w, hipMemcpyDeviceToHost));
+        *value += w[kDeepTimeoutWord] != 0;
+      }
+  }
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;
   else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided

@@ -17,7 +17,7 @@ DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
                    "amg_max_levels": 32, "amg_w_block": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
                    "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,
-                   "amg_rep_rows": 32768}
+                   "amg_rep_rows": 32768, "amg_cycle": 1, "amg_deep": 0, "amg_deep_rows": 262144, "amg_deep_wgs": 128}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
@@ -125,7 +125,7 @@ _sig = {
     "mfea_debug_amg_vcycle": (C.c_int, [_P, _P, _P]),
     "mfea_debug_amg_vector": (C.c_int, [_P, C.c_int, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_amg_info": (C.c_int, [_P, C.POINTER(C.c_int), _P, _P, _P, C.c_int,
-                                      C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+                                      C.POINTER(C.c_int64), C.POINTER(C.c_int), C.POINTER(C.c_int), _P]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(_lib, _name)
@@ -446,12 +446,15 @@ class Engine:
         items = C.c_int64()
         nd = C.c_int()
         ndist = C.c_int()
+        ptblocks = np.zeros(cap, dtype=np.int64)
         _check(_lib.mfea_debug_amg_info(self._h, C.byref(nl), rows.ctypes.data, blocks.ctypes.data,
-                                        pblocks.ctypes.data, cap, C.byref(items), C.byref(nd), C.byref(ndist)))
+                                        pblocks.ctypes.data, cap, C.byref(items), C.byref(nd), C.byref(ndist),
+                                        ptblocks.ctypes.data))
         n = nl.value
         return {"levels": n, "rows": rows[:n].tolist(), "blocks": blocks[:n].tolist(),
-                "pblocks": pblocks[:n].tolist(), "pair_items": items.value, "nd": nd.value,
-                "n_dist": ndist.value}
+                "pblocks": pblocks[:n].tolist(), "ptblocks": ptblocks[:n].tolist(),
+                "pair_items": items.value, "nd": nd.value, "n_dist": ndist.value,
+                "cycle": self.get_option("amg_cycle")}
 
     def amg_vcycle(self, r):
         """mfea_debug_amg_vcycle: one GAMG V-cycle u = M r (n_nodes × ND, original

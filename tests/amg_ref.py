@@ -18,7 +18,8 @@ import scipy.sparse as sp
 RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
 
 _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
-          "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b")
+          "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b",
+          "PT.sptr", "PT.col", "pt_ap", "pt_p", "RT.sptr", "RT.col", "rt_pt")
 
 
 def fetch_plan(shim, active, nd, build=True):
@@ -149,6 +150,48 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
         Acb = seg_sum(np.einsum("pba,pbc->pac", Pb[L["ac.a"]], APb[L["ac.b"]]), L["ac.ptr"])
         levels[l + 1]["Ab"] = Acb
     return levels
+
+
+def compact_transfers(levels):
+    """The compact cycle's P̃ = (I − ω D⁻¹ A) P and R̃ = P̃ᵀ (csrc/amg.hip
+    k_amg_ptv / k_amg_rtv) from the plan's PT / RT index maps: P̃(i, J) =
+    P(i, J) − ω D_i⁻¹ (A·P)(i, J) on A·P's pattern with the level's row labels."""
+    for L in levels:
+        if L["coarsest"]:
+            break
+        n, nd = L["n"], L["dinv"].shape[1]
+        row, _ = pos_rows(L["PT.sptr"], n)
+        ok = (L["PT.col"] >= 0) & (row >= 0)
+        PTb = np.zeros((len(row), nd, nd))
+        pp = L["pt_p"]
+        base = np.where((pp >= 0)[:, None, None], L["Pb"][np.maximum(pp, 0)], 0.0)
+        DAP = np.einsum("pab,pbc->pac", L["dinv"][np.maximum(row, 0)], L["APb"][np.maximum(L["pt_ap"], 0)])
+        PTb[ok] = (base - L["omega"] * DAP)[ok]
+        L["PTb"] = PTb
+        L["Pt"] = to_scipy(PTb, L["PT.sptr"], L["PT.col"], n, L["nc"], nd)
+        rok = L["rt_pt"] >= 0
+        RTb = np.zeros((len(L["rt_pt"]), nd, nd))
+        RTb[rok] = np.transpose(PTb[L["rt_pt"][rok]], (0, 2, 1))
+        L["Rt"] = to_scipy(RTb, L["RT.sptr"], L["RT.col"], L["nc"], n, nd)
+    return levels
+
+
+def vcycle_compact(levels, b, l=0):
+    """The same V(1,1) cycle in two sweeps per level (amg.hpp AmgLevel::PT):
+    c = x + ω D⁻¹ (b − A x) with x = ω D⁻¹ b, e = c + P̃ M' (R̃ b)."""
+    L = levels[l]
+    nd = L["dinv"].shape[1]
+    Dinv = L["dinv"]
+
+    def dapply(v, s):
+        return s * np.einsum("iab,ib->ia", Dinv, v.reshape(-1, nd)).ravel()
+
+    if L["coarsest"]:
+        return dapply(b, 1.0)
+    A, w = L["A"], L["omega"]
+    x = dapply(b, w)
+    c = x + dapply(b - A @ x, w)
+    return c + L["Pt"] @ vcycle_compact(levels, L["Rt"] @ b, l + 1)
 
 
 def vcycle(levels, b, l=0):

@@ -206,6 +206,13 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   else if (n == "ac.ptr") v = &L.ac.ptr;
   else if (n == "ac.a") v = &L.ac.a;
   else if (n == "ac.b") v = &L.ac.b;
+  else if (n == "PT.sptr") v = &L.PT.sptr;
+  else if (n == "PT.col") v = &L.PT.col;
+  else if (n == "pt_ap") v = &L.pt_ap;
+  else if (n == "pt_p") v = &L.pt_p;
+  else if (n == "RT.sptr") v = &L.RT.sptr;
+  else if (n == "RT.col") v = &L.RT.col;
+  else if (n == "rt_pt") v = &L.rt_pt;
   else if (n == "row0") v = &g_amg.row0;
   else if (n == "a0.ptr") v = &g_amg.a0.ptr;
   else if (n == "a0.a") v = &g_amg.a0.a;

@@ -171,3 +171,25 @@ def test_aggregates_respect_components_after_failures(shim):
     ref = spsolve(Kff.tocsc(), b)
     x, _ = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13)
     assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10
+
+
+def test_compact_cycle_transfers_and_cycle(shim):
+    """The compact cycle's plan (PT / RT patterns and index maps, csrc/amg_symbolic.cpp):
+    P̃ = (I − ω D⁻¹ A) P and R̃ = P̃ᵀ exactly as SciPy forms them, and the two-sweep
+    cycle equal to the four-step V(1,1) cycle (the same preconditioner)."""
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    amg_ref.compact_transfers(levels)
+    for L in levels[:-1]:
+        n, nd = L["n"], 2
+        Dinv = sp.block_diag(list(L["dinv"]), format="csr")
+        ref = (L["P"] - L["omega"] * (Dinv @ L["A"] @ L["P"])).tocsr()
+        assert _rel(L["Pt"], ref) <= 1e-13
+        assert _rel(L["Rt"], L["Pt"].T.tocsr()) == 0.0
+        # every P block sits inside A·P's pattern: pt_p covers all of P's entries
+        assert np.count_nonzero(L["pt_p"] >= 0) == np.count_nonzero(L["P.col"] >= 0)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        r = rng.standard_normal(Kff.shape[0])
+        u4, u2 = amg_ref.vcycle(levels, r), amg_ref.vcycle_compact(levels, r)
+        assert np.linalg.norm(u4 - u2) <= 1e-12 * np.linalg.norm(u4)

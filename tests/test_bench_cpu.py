@@ -46,3 +46,17 @@ def test_spmv_bytes_are_the_w_kernels_share(bench):
     # 3-D: 6 stored values per symmetric block
     ai3 = {"nd": 3, "levels": 2, "rows": [n, 1], "blocks": [nb, 1], "pblocks": [1, 0]}
     assert bench.amg_spmv_bytes(ai3) == nb * (48 + 4) + 60 * n
+
+
+def test_amg_iteration_bytes_compact_by_hand(bench):
+    """The compact cycle (two sweeps per level with P̃ / R̃ of tb blocks)."""
+    n, nn, nb, tb = 1000, 300, 4000, 2500
+    ai = {"nd": 2, "levels": 2, "rows": [n, nn], "blocks": [nb, nn], "pblocks": [1800, 0],
+          "ptblocks": [tb, 0], "cycle": 1}
+    B, V, V8, Bs, Bs8 = 16, 8, 16, 12, 24
+    down = tb * (B + 4) + nb * (Bs + 4) + (V8 + 2 * V + B) * n + (B + 2 * V) * nn
+    up = tb * (B + 4) + 2 * V * n + V * nn
+    update = (9 * V8 + V + B + V) * n
+    w = nb * (Bs8 + 4) + (2 * V8 + V) * n
+    assert bench.amg_iteration_bytes(ai) == down + up + update + w
+    assert bench.amg_iteration_bytes(ai, compact=False) == bench.amg_iteration_bytes(dict(ai, cycle=0))

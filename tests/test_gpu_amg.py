@@ -165,7 +165,7 @@ def _variant_solves(engine, option, values, nx=1, ny=5):
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     out = {}
     # every level in its own kernels; the session engine gets its options back
-    with engine.options(amg_tail_rows=0, **{option: values[0]}):
+    with engine.options(amg_tail_rows=0, amg_deep=0, amg_cycle=0, **{option: values[0]}):
         engine.set_mesh(xyz, e2n)
         engine.set_bc(top, bot)
         engine.set_active(None)
@@ -195,7 +195,7 @@ def test_tail_lds_and_global_bitwise_equal(engine):
     top, bot = synth.grips(xyz)
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     out = {}
-    with engine.options(amg_tail_rows=2048, amg_tail_lds=1):
+    with engine.options(amg_tail_rows=2048, amg_tail_lds=1, amg_deep=0, amg_cycle=0):
         engine.set_mesh(xyz, e2n)
         engine.set_bc(top, bot)
         engine.set_active(None)
@@ -242,3 +242,115 @@ def test_converged_solve_leaves_no_stale_chunks(engine):
     A, b, free = fo.free_system(K, known, vals)
     true_rel = np.linalg.norm(b - A @ U[free]) / np.linalg.norm(b)
     assert abs(true_rel - st.relres) <= 0.05 * st.relres, (true_rel, st.relres)
+
+
+# ---------------------------------------------------------------------------
+# the persistent deep-level launch (csrc/amg_deep.hip): the levels below level
+# 0 as phases of ONE launch separated by grid barriers.  Same arithmetic as the
+# per-level launches (same lanes per row, slot order, butterflies): U and the
+# iteration count bit for bit, at every start level and workgroup count, across
+# repeated launches (graph replay, rebuilds) — and no barrier wait gave up.
+# ---------------------------------------------------------------------------
+def _deep_case(engine, mesh):
+    from mfea import synth
+    if mesh == "sim135507_3d":
+        nodes, elems = load_mesh("sim_20251115_135507")
+        xyz = nodes[["x", "y", "z"]].values
+        top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 0.5)
+        e2n = elems[["n1", "n2"]].values
+    else:
+        nx, ny, chords = {"C2_1x5": (1, 5, False), "C3_6x8": (6, 8, False), "C5_2x2": (2, 2, True)}[mesh]
+        xyz, e2n = synth.tiled_mesh(nx, ny, chords=chords)
+        top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    engine.set_active(None)
+    engine.assemble()
+    return xyz, e2n, top, bot
+
+
+@pytest.mark.parametrize("mesh", ["C2_1x5", "C3_6x8", "C5_2x2", "sim135507_3d"])
+def test_deep_launch_bitwise_equals_per_level_launches(engine, mesh):
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    with engine.options(amg_tail_rows=0, amg_deep=0, amg_deep_wgs=128, amg_cycle=0):
+        xyz, e2n, top, bot = _deep_case(engine, mesh)
+        nlev = len(engine.amg_info()["rows"])
+        assert nlev >= 3
+        st0 = engine.solve(dy, -dy, _opts(1e-10))
+        U0 = engine.displacement()
+        assert engine.get_option("amg_deep_level") == 0
+        runs = 0
+        for level in range(1, nlev - 1):
+            for wgs in (8, 64, 256):
+                engine.set_option("amg_deep", level)
+                engine.set_option("amg_deep_wgs", wgs)
+                assert engine.get_option("amg_deep_level") == level
+                for _ in range(2):   # the barrier words are reused launch after launch
+                    st = engine.solve(dy, -dy, _opts(1e-10))
+                    assert st.status == 0 and st.iters == st0.iters, (level, wgs, st.iters, st0.iters)
+                    assert np.array_equal(engine.displacement(), U0), (level, wgs)
+                runs += 1
+        assert runs >= 3
+        assert engine.get_option("amg_deep_timeouts") == 0
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    assert rel(U0, fo.solve_system(K, known, vals)) <= 1e-8
+
+
+def test_deep_launch_default_and_failure_steps(engine):
+    """amg_deep -1 (from the first level of at most amg_deep_rows rows) over
+    load steps with failures (hierarchy rebuilds, new barrier buffers' first
+    use), against the direct solve."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    active = np.ones(len(e2n), bool)
+    with engine.options(amg_deep=-1, amg_cycle=0):
+        for step in (10, 25, 39):
+            dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+            engine.set_active(active)
+            f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
+            assert engine.get_option("amg_deep_level") >= 1
+            K = fo.assemble_global_stiffness(xyz, e2n, active)
+            known, vals = fo.known_dof_map(top, bot, dy, -dy)
+            assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10, step
+            active = engine.active()
+        assert engine.get_option("amg_deep_timeouts") == 0
+
+
+# ---------------------------------------------------------------------------
+# the compact cycle (amg_cycle 1: two sweeps per level with P̃ = (I − ωD⁻¹A)P,
+# R̃ = P̃ᵀ; tests/test_amg_cpu.py pins it against the four-step cycle): the
+# direct solve's U, and the four-step cycle's iteration count (the same
+# preconditioner up to f32 rounding)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mesh", ["C2_1x5", "C3_6x8", "C5_2x2", "sim135507_3d"])
+def test_compact_cycle_matches_direct(engine, mesh):
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    its = {}
+    with engine.options(amg_cycle=0):
+        xyz, e2n, top, bot = _deep_case(engine, mesh)
+        for cyc in (0, 1):
+            engine.set_option("amg_cycle", cyc)
+            its[cyc] = engine.solve(dy, -dy, _opts(1e-8)).iters
+            st = engine.solve(dy, -dy, _opts(1e-13))
+            assert st.status == 0, cyc
+            U = engine.displacement()
+            K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+            known, vals = fo.known_dof_map(top, bot, dy, -dy)
+            A, b, free = fo.free_system(K, known, vals)
+            assert rel(U, fo.solve_system(K, known, vals)) <= 1e-10, (cyc, mesh)
+            assert np.linalg.norm(A @ U[free] - b) <= 1e-12 * np.linalg.norm(b)
+    assert abs(its[1] - its[0]) <= 1, its
+
+
+def test_compact_cycle_failure_steps(engine):
+    xyz, e2n, top, bot = _sim181147(engine)
+    active = np.ones(len(e2n), bool)
+    with engine.options(amg_cycle=1):
+        for step in (10, 25, 39):
+            dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+            engine.set_active(active)
+            f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
+            K = fo.assemble_global_stiffness(xyz, e2n, active)
+            known, vals = fo.known_dof_map(top, bot, dy, -dy)
+            assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10, step
+            active = engine.active()

@@ -119,6 +119,9 @@ int mfea_assemble(mfea_handle* h);
 /* Dirichlet elimination, RHS and preconditioned CG on device.
  * Replaces solve_system (src/fea_solver.py:112-135) and MatZeroRowsColumnsIS +
  * diag regularisation + KSPSolve (src/fea_petsc.cpp:286-357).
+ * Solves the operator of the last mfea_assemble; a handle (re)built since
+ * (mfea_set_mesh / mfea_set_bc, or a layout option of mfea_set_option) is
+ * assembled for its current active set first.
  * Returns MFEA_EMAXIT / MFEA_EBREAKDOWN on solver failure (stats still filled);
  * the Python shim maps them to np.linalg.LinAlgError (src/fea_solver.py:250-254). */
 int mfea_solve(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* opts,
@@ -204,6 +207,12 @@ int mfea_profile_spmv(mfea_handle* h, int reps, double* avg_ms);
 #define MFEA_REC_FORCE 3  /* force_displacement.csv  */
 int mfea_write_record_csv(const char* path, int style, int kind, int64_t n_rows, int64_t n_cols,
                           const double* values, const uint8_t* flags, int n_threads);
+/* The same record as a NumPy .npy sidecar (the CSV's text is what
+ * dominates at 1 M DOF; a binary copy reloads in milliseconds): the raw
+ * n_rows × n_cols array without the step column, '<f8' (values) or '|b1'
+ * (flags, ACTIVE), C order, readable by np.load(allow_pickle=False). */
+int mfea_write_record_npy(const char* path, int kind, int64_t n_rows, int64_t n_cols, const double* values,
+                          const uint8_t* flags);
 
 /* ---- network producer (host only) ------------------------------------------- */
 /* The hyphal growth model of src/mycelium_sim_2D.cpp (main :529-588, process

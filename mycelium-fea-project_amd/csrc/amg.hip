@@ -702,6 +702,105 @@ __global__ __launch_bounds__(kTailBS) void k_amg_tail_lds(const TailLevels tl, i
   }
 }
 
+// The compact cycle's tail (k_amg_down / k_amg_up of levels [l0, nlev) in ONE
+// workgroup, their vectors in LDS: b, x, c per level, a coarse level's output
+// e over its b — b_l is dead once its down sweep has run).  A down phase
+// sweeps the next level's rows (R̃ b) and then this level's (c), a wave never
+// straddling the two.  Up to kCTailLdsMax bytes: MI355X has 160 KB of LDS.
+constexpr int64_t kCTailLdsMax = 160 * 1024;
+template <int ND>
+__device__ __forceinline__ void ctail_down(const AmgLevD& L, const AmgLevD& N, const float* b, const float* x,
+                                           float* c, float* nb, float* nx) {
+  const int64_t nc = L.RT.n, nf = L.A.n, nc64 = (nc + 63) & ~(int64_t)63;
+  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
+  const float om = (float)amg_omega(L.omega);
+  for (int64_t r0 = 0; r0 < nc64 + nf; r0 += kTailBS) {
+    const int64_t k = r0 + threadIdx.x, wave0 = r0 + (threadIdx.x & ~63);
+    if (wave0 >= nc64 + nf) break;
+    int64_t base;
+    int w;
+    if (wave0 < nc64) {  // coarse row I: b' = R̃ b, x' = s D'⁻¹ b'
+      const int64_t I = k, Ic = I < nc ? I : nc - 1;
+      slice_of(L.RT, Ic, base, w);
+      float bc[ND], Di[ND * ND];
+      dinv_load<ND>(N.dinv32, Ic, Di);
+#pragma unroll
+      for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
+      sell_mac<ND, false, 3>(L.RT.col, L.RT.val32, L.RT.npos, base, w, b, bc);
+      if (I < nc) {
+        vstore<ND>(nb, I, bc);
+        float xn[ND];
+        dinv_mul<ND>(Di, sc, bc, xn);
+        vstore<ND>(nx, I, xn);
+      }
+    } else {  // fine row i: c = x + ω D⁻¹ (b − A x)
+      const int64_t i = k - nc64, ii = i < nf ? i : nf - 1;
+      slice_of(L.A, ii, base, w);
+      float y[ND], xv[ND], d[ND], Di[ND * ND];
+      vload<ND>(b, ii, y);
+      vload<ND>(x, ii, xv);
+      dinv_load<ND>(L.dinv32, ii, Di);
+      sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, x, y);
+      dinv_mul<ND>(Di, om, y, d);
+#pragma unroll
+      for (int a = 0; a < ND; ++a) xv[a] += d[a];
+      if (i < nf) vstore<ND>(c, i, xv);
+    }
+  }
+}
+template <int ND>
+__device__ __forceinline__ void ctail_up(const AmgLevD& L, const float* c, const float* src, float* e) {
+  const int64_t n = L.PT.n;
+  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
+    const int64_t i = r0 + threadIdx.x;
+    if (r0 + (threadIdx.x & ~63) >= n) break;
+    const int64_t ii = i < n ? i : n - 1;
+    int64_t base;
+    int w;
+    slice_of(L.PT, ii, base, w);
+    float y[ND];
+    vload<ND>(c, ii, y);
+    sell_mac<ND, false, 3>(L.PT.col, L.PT.val32, L.PT.npos, base, w, src, y);
+    if (i < n) vstore<ND>(e, i, y);
+  }
+}
+template <int ND>
+__global__ __launch_bounds__(kTailBS) void k_amg_ctail_lds(const TailLevels tl, int l0, int nlev,
+                                                           const int32_t* gate) {
+  extern __shared__ float sm[];
+  if (gated(gate)) return;
+  const AmgLevD* lev = tl.lev - l0;
+  {
+    const AmgLevD G = lev[l0];
+    const int64_t n = G.A.n;
+    for (int64_t k = threadIdx.x; k < ND * n; k += kTailBS) {
+      sm[k] = G.b[k];
+      sm[ND * n + k] = G.x[k];
+    }
+  }
+  __syncthreads();
+  for (int l = l0; l + 1 < nlev; ++l) {
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    float* v = sm + tail_lds_off<ND>(lev, l, l0);  // b x c of level l
+    float* w = v + 3 * ND * L.A.n;                 // of level l + 1
+    ctail_down<ND>(L, N, v, v + ND * L.A.n, v + 2 * ND * L.A.n, w, w + ND * N.A.n);
+    __syncthreads();
+  }
+  for (int l = nlev - 2; l >= l0; --l) {
+    const AmgLevD L = lev[l], N = lev[l + 1];
+    float* v = sm + tail_lds_off<ND>(lev, l, l0);
+    float* w = v + 3 * ND * L.A.n;
+    // level l+1's output: its x if coarsest, else its e (held over its b)
+    const float* src = N.coarsest ? w + ND * N.A.n : w;
+    if (l > l0) {
+      ctail_up<ND>(L, v + 2 * ND * L.A.n, src, v);
+      __syncthreads();
+    } else {
+      ctail_up<ND>(L, v + 2 * ND * L.A.n, src, L.e);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // CG (f64)
 // ---------------------------------------------------------------------------
@@ -1036,13 +1135,45 @@ static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, cons
   else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
 }
+// levels [tail, nlev) of the compact cycle in one workgroup (k_amg_ctail_lds)
+// when their vectors fit its LDS; returns whether it was launched
 template <int ND>
-static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const int32_t* gate, int l0) {
-  for (int l = l0; l + 1 < nlev; ++l) {
+static bool ctail_nd(hipStream_t s, const AmgLevD* lev, int nlev, int tail, const int32_t* gate) {
+  if (tail <= 0 || tail >= nlev - 1 || nlev - tail > kTailMaxLev || !lev[tail].tail_lds) return false;
+  TailLevels tl;
+  int64_t lds = 0;
+  for (int l = tail; l < nlev; ++l) {
+    tl.lev[l - tail] = lev[l];
+    lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
+  }
+  if (lds > kCTailLdsMax) return false;
+  static bool attr = false;  // dynamic LDS above 64 KB must be allowed once per kernel
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_amg_ctail_lds<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kCTailLdsMax);
+    (void)hipFuncSetAttribute((const void*)k_amg_ctail_lds<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kCTailLdsMax);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_amg_ctail_lds<ND>, dim3(1), dim3(kTailBS), (size_t)lds, s, tl, tail, nlev, gate);
+  return true;
+}
+template <int ND>
+static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, int tail,
+                       const int32_t* gate, int l0) {
+  int top = nlev - 1;  // levels [top, nlev) run in the tail launch
+  if (tail > l0) {
+    // the tail needs its levels' vectors to fit LDS: probe from the requested level down
+    int64_t lds = 0;
+    for (int l = tail; l < nlev; ++l) lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
+    if (lds <= kCTailLdsMax && tail < nlev - 1 && nlev - tail <= kTailMaxLev && lev[tail].tail_lds) top = tail;
+  }
+  for (int l = l0; l < top; ++l) {
     if (l == 0) down_tb<ND, double, true>(s, lev[0], lev[1], (const double*)cg.r, gate);
     else down_tb<ND, float, false>(s, lev[l], lev[l + 1], (const float*)lev[l].b, gate);
   }
-  for (int l = nlev - 2; l >= l0; --l) {
+  if (top < nlev - 1) ctail_nd<ND>(s, lev, nlev, top, gate);
+  for (int l = top - 1; l >= l0; --l) {
     if (l == 0) up_te<ND, float>(s, lev[0], lev[1], cg.u, gate);
     else up_te<ND, float>(s, lev[l], lev[l + 1], lev[l].e, gate);
   }
@@ -1060,7 +1191,7 @@ template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
                       int tail, const int32_t* gate, int l0) {
   if (cg.cycle == 1 && amg_compact_ok(lev, nlev, l0)) {
-    compact_nd<ND>(s, lev, nlev, cg, gate, l0);
+    compact_nd<ND>(s, lev, nlev, cg, cg.ctail, gate, l0);
     return;
   }
   // levels [deep, nlev) in the persistent launch (amg_deep.hip), if they fit it

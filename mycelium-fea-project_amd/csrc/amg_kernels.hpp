@@ -112,6 +112,7 @@ struct AmgCg {
   // 1: the compact cycle (two sweeps per level, AmgLevD::PT) where every
   // level of the cycle has it (compact set: unsplit levels); 0: four steps
   int cycle = 0;
+  int ctail = 0;  // the compact cycle's single-workgroup LDS tail: its first level (0: none)
 };
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered

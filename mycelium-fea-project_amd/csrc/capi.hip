@@ -165,6 +165,7 @@ struct mfea_handle {
   std::vector<int64_t> top, bot;
   int64_t n_free_global = 0;
   bool has_mesh = false, dirty = true;
+  bool assembled = false;  // the operator holds an assembly since the last (re)build
   std::vector<uint8_t> active_host;  // pending upload, original element order (empty = none)
   std::vector<std::unique_ptr<Part>> parts;
   // partitioning: nparts partitions on this device (world == 1), or this
@@ -206,6 +207,9 @@ struct mfea_handle {
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
+  int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
+  int64_t opt_amg_ctail_rows = 0;  // GAMG compact cycle: levels of at most this many rows in one workgroup
+                                   // (measured slower than their launches at C2 / C3: off)
   int opt_amg_cycle = 1;       // GAMG: 1 the compact V-cycle (two sweeps per level), 0 four steps
   int opt_amg_deep = 0;        // GAMG: first level of the persistent deep launch (-1: by amg_deep_rows, 0: none)
   int64_t opt_amg_deep_rows = 262144;  // GAMG: the deep launch starts at the first level of at most this many rows
@@ -460,6 +464,7 @@ int ensure_built(mfea_handle* h) {
   if (!h->has_mesh) return fail(MFEA_ESTATE, "no mesh: call mfea_set_mesh first");
   if (!h->dirty) return 0;
   destroy_graph(h);
+  h->assembled = false;
   const bool dm = h->world > 1 || h->nparts > 1;
   const int np = h->world > 1 ? 1 : h->nparts;
   const bool skip = (h->mesh_flags & MFEA_MESH_SKIP_INVALID) != 0;
@@ -988,6 +993,15 @@ RowRange row_range(const SellPat& S, int64_t lo, int64_t hi) {
 // device allocations and uploads the indices.  Pass 0 sizes, pass 1 carves.
 // rk (distributed GAMG): this partition's row ranges, with its own level-0
 // lists over ITS pattern (a0, row0) in place of the plan's.
+// strength of connection of the level-0 aggregation (option amg_theta_ppm;
+// amg.hpp AmgStrength): θ and the bending-to-axial constant 12EI / EA
+AmgStrength amg_strength(const mfea_handle* h) {
+  AmgStrength st;
+  st.theta = h->opt_amg_theta_ppm * 1e-6;
+  st.kb_kax = h->mat.EA > 0.0 ? h->mat.EI12 / h->mat.EA : 0.0;
+  return st;
+}
+
 // The persistent deep-level launch of the V-cycle (amg_deep.hip): its first
 // level (option amg_deep, or the first unsplit level of at most amg_deep_rows
 // rows), its workgroups and its barrier words (zeroed once; every launch
@@ -1159,6 +1173,8 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_tail = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_tail_rows) : 0;
     if (pt.amg_tail > 0) pt.amg_tail += first - 1;
     pt.amg_first = first;
+    int ct = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_ctail_rows) : 0;
+    pt.amg_cg.ctail = ct > 0 ? ct + first - 1 : 0;
   }
   RC(set_amg_deep(h, pt));
   HIPC(hipStreamSynchronize(s));
@@ -1244,7 +1260,8 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
     return 0;
   }
   pt.amg_ok = false;
-  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels);
+  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels, nullptr,
+                                    amg_strength(h));
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   RC(upload_amg(h, pt, pt.amg));
@@ -1570,7 +1587,8 @@ int ensure_gamg_plan(mfea_handle* h, bool* rebuilt) {
     spec.rep_rows = h->opt_amg_rep_rows;
     spec.owner.resize(h->gpat.n_free);
     for (int64_t i = 0; i < h->gpat.n_free; ++i) spec.owner[i] = h->gowner[h->gpat.perm[i]];
-    std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec);
+    std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec,
+                                amg_strength(h));
     if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
     for (auto& pp : h->parts) {
       Part& pt = *pp;
@@ -2092,6 +2110,7 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
 
 int assemble_impl(mfea_handle* h, mfea_stats* st) {
   hipStream_t s = h->stream;
+  h->assembled = true;
   HIPC(hipEventRecord(h->ev[0], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -2388,6 +2407,9 @@ int mfea_solve(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   RC(ensure_built(h));
   mfea_solve_opts o = opts ? *opts : default_opts();
   if (st) std::memset(st, 0, sizeof(*st));
+  // a (re)build (new mesh / BCs, a layout option) left the operator empty:
+  // assemble the current active set first rather than solve a zero operator
+  if (!h->assembled) RC(assemble_impl(h, nullptr));
   return solve_any(h, dy_top, dy_bot, &o, st);
 }
 
@@ -2858,6 +2880,7 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   } else if (n == "ell_maxg") h->opt_ell_maxg = value;
   else if (n == "ell_compact") { h->opt_ell_compact = value != 0; rebuild = true; }
   else if (n == "amg_tail_rows") { h->opt_amg_tail_rows = value; rebuild = true; }
+  else if (n == "amg_ctail_rows") { h->opt_amg_ctail_rows = value; rebuild = true; }
   else if (n == "amg_max_levels") {
     if (value < 1 || value > kAmgMaxLevels) return fail(MFEA_EINVAL, "amg_max_levels: 1..32");
     h->opt_amg_max_levels = (int)value;
@@ -2887,6 +2910,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_tail_lds = value != 0;
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
+  }
+  else if (n == "amg_theta_ppm") {
+    if (value < 0 || value > 1000000) return fail(MFEA_EINVAL, "amg_theta_ppm: 0..1000000");
+    h->opt_amg_theta_ppm = value;
+    rebuild = true;
   }
   else if (n == "amg_cycle") {
     if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_cycle: 0 (four steps per level) or 1 (compact)");
@@ -3060,12 +3088,14 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "ell_maxg") *value = h->opt_ell_maxg;
   else if (n == "ell_compact") *value = h->opt_ell_compact;
   else if (n == "amg_tail_rows") *value = h->opt_amg_tail_rows;
+  else if (n == "amg_ctail_rows") *value = h->opt_amg_ctail_rows;
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
   else if (n == "amg_w_block") *value = h->opt_amg_w_block;
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;
+  else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_deep") *value = h->opt_amg_deep;
   else if (n == "amg_deep_rows") *value = h->opt_amg_deep_rows;
   else if (n == "amg_deep_wgs") *value = h->opt_amg_deep_wgs;
@@ -3115,6 +3145,12 @@ int mfea_write_record_csv(const char* path, int style, int kind, int64_t n_rows,
                           const double* values, const uint8_t* flags, int n_threads) {
   const std::string err =
       write_record_csv(path, style, kind, n_rows, n_cols, values, flags, n_threads);
+  return err.empty() ? 0 : fail(MFEA_EINVAL, err);
+}
+
+int mfea_write_record_npy(const char* path, int kind, int64_t n_rows, int64_t n_cols, const double* values,
+                          const uint8_t* flags) {
+  const std::string err = write_record_npy(path, kind, n_rows, n_cols, values, flags);
   return err.empty() ? 0 : fail(MFEA_EINVAL, err);
 }
 

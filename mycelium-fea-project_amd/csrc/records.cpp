@@ -189,4 +189,45 @@ std::string write_record_csv(const char* path, int style, int kind, int64_t n_ro
   return ok ? "" : std::string("write failed: ") + path;
 }
 
+// NumPy .npy (format 1.0): magic, version, little-endian header length, the
+// header dict padded with spaces to a 64-byte boundary and ended by '\n', then
+// the C-order data — '<f8' for stress / displacement / force, '|b1' (one byte
+// 0/1 per cell) for the activity.  np.load(allow_pickle=False) reads it.
+std::string write_record_npy(const char* path, int kind, int64_t n_rows, int64_t n_cols, const double* values,
+                             const uint8_t* flags) {
+  if (!path) return "NULL path";
+  if (kind < MFEA_REC_STRESS || kind > MFEA_REC_FORCE) return "unknown record kind";
+  if (n_rows < 0 || n_cols < 0) return "negative record size";
+  const bool b1 = kind == MFEA_REC_ACTIVE;
+  if (n_rows > 0 && n_cols > 0 && (b1 ? !flags : !values)) return "NULL record array";
+  char dict[160];
+  const int dn = std::snprintf(dict, sizeof dict, "{'descr': '%s', 'fortran_order': False, 'shape': (%lld, %lld), }",
+                               b1 ? "|b1" : "<f8", (long long)n_rows, (long long)n_cols);
+  std::string h("\x93NUMPY\x01\x00", 8);
+  const size_t total = (10 + (size_t)dn + 1 + 63) / 64 * 64;  // magic 6 + version 2 + length 2
+  const size_t hl = total - 10;
+  h.push_back((char)(hl & 0xff));
+  h.push_back((char)(hl >> 8));
+  h.append(dict, (size_t)dn);
+  h.append(hl - (size_t)dn - 1, ' ');
+  h.push_back('\n');
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return std::string("cannot open ") + path;
+  bool ok = std::fwrite(h.data(), 1, h.size(), f) == h.size();
+  const size_t cells = (size_t)n_rows * (size_t)n_cols;
+  if (ok && cells) {
+    if (b1) {
+      std::vector<uint8_t> row((size_t)n_cols);
+      for (int64_t r = 0; ok && r < n_rows; ++r) {
+        for (int64_t c = 0; c < n_cols; ++c) row[c] = flags[r * n_cols + c] ? 1 : 0;
+        ok = std::fwrite(row.data(), 1, row.size(), f) == row.size();
+      }
+    } else {
+      ok = std::fwrite(values, sizeof(double), cells, f) == cells;
+    }
+  }
+  if (std::fclose(f) != 0) ok = false;
+  return ok ? "" : std::string("write failed: ") + path;
+}
+
 }  // namespace mfea

@@ -14,4 +14,8 @@ std::string write_record_csv(const char* path, int style, int kind, int64_t n_ro
                              int64_t n_cols, const double* values, const uint8_t* flags,
                              int n_threads);
 
+// The same record as a NumPy .npy sidecar (mfea_write_record_npy in mfea.h).
+std::string write_record_npy(const char* path, int kind, int64_t n_rows, int64_t n_cols, const double* values,
+                             const uint8_t* flags);
+
 }  // namespace mfea

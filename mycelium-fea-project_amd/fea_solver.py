@@ -173,7 +173,7 @@ def _grips(nodes, coords, tol):
 
 
 def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=None,
-               out_format="python", verbose=True, nparts=1):
+               out_format="python", verbose=True, nparts=1, npy=False):
     """The reference step loop (src/fea_solver.py:186-335) with the hot path on device.
 
     Reads <results_dir>/nodes.csv + elements.csv, runs N_STEPS load steps and
@@ -181,7 +181,8 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
     node_displacements,force_displacement}.csv, runtime.txt and
     solve_runtime.txt.  Module constants are read at call time, as in the
     reference.  out_format='petsc' writes the fea_petsc.cpp formatting instead
-    (src/fea_petsc.cpp:433-516).
+    (src/fea_petsc.cpp:433-516).  npy=True also writes every record as a .npy
+    sidecar next to its CSV (the raw per-step array, no step column).
 
     Multi-GPU: launched as N processes (``torch.distributed.run``, dist_env),
     every rank solves its partition of the mesh (RCCL between the GPUs) and
@@ -256,7 +257,7 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
 
     if rank == 0:
         write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_record,
-                      force_disp_curve, out_format)
+                      force_disp_curve, out_format, npy=npy)
         say(f"✅ FEA completed. Results saved to {fea_dir}")
         total_time = time.time() - start_time
         with open(os.path.join(fea_dir, "runtime.txt"), "w") as f:
@@ -267,7 +268,7 @@ def fea_solver(results_dir, tol=GRIP_LENGTH, *, rtol=None, max_it=None, precond=
 
 
 def write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_record,
-                  force_disp_curve, out_format="python"):
+                  force_disp_curve, out_format="python", npy=False):
     """CSV writers, src/fea_solver.py:297-316 (pandas) / src/fea_petsc.cpp:433-516,
     through the native multi-threaded writer (mfea_write_record_csv), which
     reproduces both byte for byte.  The C++ driver writes a record file only
@@ -282,6 +283,8 @@ def write_records(fea_dir, n_nodes, n_elems, stress_record, active_record, disp_
         if petsc and not len(rec):
             continue
         _capi.write_record_csv(os.path.join(fea_dir, name), style, kind, rec, n_cols=ncol)
+        if npy:
+            _capi.write_record_npy(os.path.join(fea_dir, name[:-4] + ".npy"), kind, rec, n_cols=ncol)
 
 
 def main(argv=None):
@@ -297,6 +300,7 @@ def main(argv=None):
     ap.add_argument("--reg", type=float, default=REG)
     ap.add_argument("--pc", choices=["gamg", "jacobi", "bjacobi"], default="gamg")
     ap.add_argument("--format", choices=["python", "petsc"], default="python")
+    ap.add_argument("--npy", action="store_true", help="also write each record as a .npy sidecar")
     ap.add_argument("--parts", type=int, default=1,
                     help="partitions of the multi-GPU solve, all on this device (one process); "
                          "for one GPU per process launch with torch.distributed.run instead")
@@ -305,7 +309,7 @@ def main(argv=None):
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,
                precond={"gamg": _capi.PC_GAMG, "jacobi": _capi.PC_JACOBI,
                         "bjacobi": _capi.PC_BLOCK_JACOBI}[a.pc],
-               out_format=a.format, nparts=a.parts)
+               out_format=a.format, nparts=a.parts, npy=a.npy)
 
 
 if __name__ == "__main__":

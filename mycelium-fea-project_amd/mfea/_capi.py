@@ -17,7 +17,7 @@ DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
                    "amg_max_levels": 32, "amg_w_block": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
                    "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,
-                   "amg_rep_rows": 32768, "amg_cycle": 1, "amg_deep": 0, "amg_deep_rows": 262144, "amg_deep_wgs": 128}
+                   "amg_rep_rows": 32768, "amg_cycle": 1, "amg_ctail_rows": 0, "amg_theta_ppm": 0, "amg_deep": 0, "amg_deep_rows": 262144, "amg_deep_wgs": 128}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
@@ -109,6 +109,7 @@ _sig = {
     "mfea_set_partition_axis": (C.c_int, [_P, C.c_int]),
     "mfea_get_ownership": (C.c_int, [_P, _P, _P]),
     "mfea_gather_results": (C.c_int, [_P, _P, _P, _P]),
+    "mfea_write_record_npy": (C.c_int, [C.c_char_p, C.c_int, C.c_int64, C.c_int64, _P, _P]),
     "mfea_write_record_csv": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int64, C.c_int64, _P, _P,
                                         C.c_int]),
     "mfea_grow_default_params": (None, [C.POINTER(GrowParams)]),
@@ -201,6 +202,21 @@ def write_record_csv(path, style, kind, records, n_cols=None, threads=None):
     p = a.ctypes.data_as(_P) if a.size else None
     _check(_lib.mfea_write_record_csv(os.fsencode(path), int(style), int(kind), nr, nc,
                                       None if flags else p, p if flags else None, int(threads)))
+
+
+def write_record_npy(path, kind, records, n_cols=None):
+    """The record as a .npy sidecar through the native writer
+    (mfea_write_record_npy): float64 rows, or bool rows for REC_ACTIVE."""
+    flags = kind == REC_ACTIVE
+    dt = np.uint8 if flags else np.float64
+    if len(records):
+        a = np.ascontiguousarray(np.asarray(records), dtype=dt).reshape(len(records), -1)
+    else:
+        a = np.zeros((0, n_cols or 0), dtype=dt)
+    nr, nc = a.shape
+    p = a.ctypes.data_as(_P) if a.size else None
+    _check(_lib.mfea_write_record_npy(os.fsencode(path), int(kind), nr, nc,
+                                      None if flags else p, p if flags else None))
 
 
 def grow_params(**kw) -> GrowParams:

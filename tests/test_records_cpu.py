@@ -129,3 +129,29 @@ def test_writer_errors_are_reported(tmp_path):
     with pytest.raises(_capi.MfeaError, match="cannot open"):
         _capi.write_record_csv(str(tmp_path / "no" / "f.csv"), _capi.CSV_PANDAS, _capi.REC_STRESS,
                                np.zeros((1, 3)))
+
+
+def test_npy_sidecar_roundtrip(tmp_path):
+    """mfea_write_record_npy: np.load(allow_pickle=False) returns the record
+    array itself (float64 bit for bit incl. NaN / ±0 / subnormals, bool for the
+    activity), for every kind and for an empty record."""
+    rng = np.random.default_rng(5)
+    vals = _adversarial(rng, 3 * 257)[:3 * 257].reshape(3, 257)
+    for kind, rec in ((_capi.REC_STRESS, vals), (_capi.REC_DISP, vals[:, :255]),
+                      (_capi.REC_FORCE, vals[:, :2])):
+        p = tmp_path / f"k{kind}.npy"
+        _capi.write_record_npy(str(p), kind, rec)
+        got = np.load(p, allow_pickle=False)
+        assert got.dtype == np.float64 and got.shape == rec.shape
+        assert np.array_equal(got.view(np.uint64), np.ascontiguousarray(rec).view(np.uint64))
+    act = rng.random((4, 1000)) < 0.7
+    p = tmp_path / "act.npy"
+    _capi.write_record_npy(str(p), _capi.REC_ACTIVE, act)
+    got = np.load(p, allow_pickle=False)
+    assert got.dtype == np.bool_ and np.array_equal(got, act)
+    p = tmp_path / "empty.npy"
+    _capi.write_record_npy(str(p), _capi.REC_STRESS, [], n_cols=7)
+    assert np.load(p, allow_pickle=False).shape == (0, 7)
+    # the header is 64-byte aligned, as numpy writes it
+    raw = (tmp_path / "act.npy").read_bytes()
+    assert raw[:8] == b"\x93NUMPY\x01\x00" and (10 + int.from_bytes(raw[8:10], "little")) % 64 == 0

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
   if (T.col[q] < 0) return;
   const int32_t qp = L.pt_p[q];
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
-  dinv_load<ND>(L.dinv, i, Di);
+  dinv_load<ND>(L.dinv, L.pt_row[i], Di);
   bload<ND>(L.apval, 0, L.pt_ap[q], ap);
   if (qp >= 0) bload<ND>(L.P.val, 0, qp, pm);
   else {
@@ -501,22 +501,24 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, const
 }
 
 // Up: e_l = c_l + P̃ e_{l+1} (the coarsest level's output is its x), S lanes
-// per row; level 0 writes the CG's u
+// per row; level 0 writes the CG's u.  P̃'s rows run in A·P's order: row a is
+// the level's row pt_row[a] (c gathered, e scattered — within 4096-row windows)
 template <int ND, int S, class TE>
 __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __restrict__ e, const int32_t* gate) {
   const bool run = gate_open(gate);
   const AmgMatD& T = L.PT;
   const int64_t t = xcd_block() * kBlock + threadIdx.x;
   const int64_t n = T.n;
-  const int64_t i = t / S;
+  const int64_t a = t / S;
   const int sub = (int)(t % S);
-  if (i - (threadIdx.x & 63) / S >= n) return;
-  const int64_t ii = i < n ? i : n - 1;
+  if (a - (threadIdx.x & 63) / S >= n) return;
+  const int64_t aa = a < n ? a : n - 1;
   int64_t base;
   int w;
-  slice_of(T, ii, base, w);
+  slice_of(T, aa, base, w);
+  const int64_t i = L.pt_row[aa];
   float y[ND];
-  vload<ND>(L.t, ii, y);
+  vload<ND>(L.t, i, y);
   if (sub != 0) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0f;
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
   const float* src = N.coarsest ? N.x : N.e;
   if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
   else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
-  if (i < n && sub == 0 && run) vstore<ND>(e, i, y);
+  if (a < n && sub == 0 && run) vstore<ND>(e, i, y);
 }
 
 // ---------------------------------------------------------------------------
@@ -752,16 +754,17 @@ template <int ND>
 __device__ __forceinline__ void ctail_up(const AmgLevD& L, const float* c, const float* src, float* e) {
   const int64_t n = L.PT.n;
   for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
-    const int64_t i = r0 + threadIdx.x;
+    const int64_t a = r0 + threadIdx.x;
     if (r0 + (threadIdx.x & ~63) >= n) break;
-    const int64_t ii = i < n ? i : n - 1;
+    const int64_t aa = a < n ? a : n - 1;
     int64_t base;
     int w;
-    slice_of(L.PT, ii, base, w);
+    slice_of(L.PT, aa, base, w);
+    const int64_t i = L.pt_row[aa];
     float y[ND];
-    vload<ND>(c, ii, y);
+    vload<ND>(c, i, y);
     sell_mac<ND, false, 3>(L.PT.col, L.PT.val32, L.PT.npos, base, w, src, y);
-    if (i < n) vstore<ND>(e, i, y);
+    if (a < n) vstore<ND>(e, i, y);
   }
 }
 template <int ND>
@@ -1115,7 +1118,14 @@ static void prolong_nd(hipStream_t s, const AmgLevD* lev, int l, const int32_t* 
 }
 
 // the compact cycle's sweeps (lanes per row by the matrices' mean widths)
-int amg_down_lanes(const AmgLevD& L) { return lanes_for(L.RT, L.rlanes, 2.5, 5.0); }
+// R̃ rows hold 8–12 blocks on C3's levels (R's 5–7): 8 lanes from a mean of 6
+// (C3 iteration 84.3 vs 86.3 µs at 4 lanes, C2 41.6 vs 44.3)
+int amg_down_lanes(const AmgLevD& L) {
+  if (L.rlanes > 0) return L.rlanes;
+  const int64_t rows = ((L.RT.n + 63) / 64) * 64;
+  const double mean_w = rows > 0 ? (double)L.RT.npos / (double)rows : 0.0;
+  return mean_w > 6.0 ? 8 : lanes_for(L.RT, 0, 2.5, 5.0);
+}
 int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, 0, 3.5, 8.0); }
 template <int ND, class TB, bool L0>
 static void down_tb(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const TB* b, const int32_t* gate) {

@@ -84,7 +84,8 @@ struct AmgLevel {
   //   up    e_l = c_l + P̃ e_{l+1}
   // (e = x + P e' + ω D⁻¹(b − A(x + P e')) = c + (I − ω D⁻¹ A) P e', and
   // R(b − A x) = R (I − ω A D⁻¹) b = P̃ᵀ b: the same preconditioner).
-  SellPat PT;                  // n × nc
+  SellPat PT;                  // n × nc, rows labelled as A·P's
+  std::vector<int32_t> pt_row; // PT row → the level's row
   std::vector<int32_t> pt_ap;  // PT position → its A·P position
   std::vector<int32_t> pt_p;   // PT position → the P position of the same block, or -1
   SellPat RT;                  // nc × n

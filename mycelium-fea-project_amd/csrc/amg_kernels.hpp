@@ -84,6 +84,7 @@ struct AmgLevD {
   // (RT.val32), formed by the setup after A·P when compact is set
   int compact = 0;
   AmgMatD PT, RT;
+  const int32_t* pt_row = nullptr;  // PT row → level row (P̃ has A·P's row order)
   const int32_t* pt_ap = nullptr;
   const int32_t* pt_p = nullptr;
   const int32_t* rt_pt = nullptr;

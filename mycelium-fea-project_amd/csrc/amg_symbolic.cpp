@@ -490,21 +490,26 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     // A·P is only reached through the setup's index lists, so its rows get a
     // labelling of their own, by A·P length (C3 level 0: 1.69 M → 0.92 M
     // positions)
+    std::vector<int32_t> pap;
     {
       std::vector<int64_t> key(L.A.n);
       for (int64_t i = 0; i < L.A.n; ++i) key[i] = L.AP.len(i);
       const bool om = dist && l < n_dist;
-      const std::vector<int32_t> pap = sort_perm(key, om ? &own[l] : nullptr, world, om ? &out.ap_own : nullptr);
+      pap = sort_perm(key, om ? &own[l] : nullptr, world, om ? &out.ap_own : nullptr);
       if (!(err = layout(L.AP, pap, &perm[l + 1], out.AP, eAP)).empty()) return err;
       if (om) {
         out.aprow.assign(L.A.n, 0);
         for (int64_t i = 0; i < L.A.n; ++i) out.aprow[perm[l][i]] = pap[i];
       }
     }
-    // the compact cycle's P̃ (A·P's entries, the level's row labels) and R̃ = P̃ᵀ
+    // the compact cycle's P̃ on A·P's entries AND layout (its rows by A·P
+    // length: C3 level 0 fills 88 % of its positions, 48 % in the level's own
+    // row order), pt_row naming each row's level row; R̃ = P̃ᵀ
     {
       std::vector<int32_t> ePT, eRT;
-      if (!(err = layout(L.AP, perm[l], &perm[l + 1], out.PT, ePT)).empty()) return err;
+      if (!(err = layout(L.AP, pap, &perm[l + 1], out.PT, ePT)).empty()) return err;
+      out.pt_row.assign(L.A.n, 0);
+      for (int64_t i = 0; i < L.A.n; ++i) out.pt_row[pap[i]] = perm[l][i];
       out.pt_ap.assign(out.PT.n_pos(), -1);
       out.pt_p.assign(out.PT.n_pos(), -1);
       for (int64_t i = 0; i < L.A.n; ++i) {  // both rows ascending in J: merge

@@ -1139,6 +1139,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         if (!rk && L.PT.n == n) {
           d.PT = mat(L.PT, false, true);
           d.PT.rg = row_range(L.PT, 0, n);
+          d.pt_row = I(L.pt_row);
           d.pt_ap = I(L.pt_ap);
           d.pt_p = I(L.pt_p);
           d.RT = mat(L.RT, false, true);

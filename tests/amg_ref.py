@@ -19,7 +19,7 @@ RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
 
 _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
           "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b",
-          "PT.sptr", "PT.col", "pt_ap", "pt_p", "RT.sptr", "RT.col", "rt_pt")
+          "PT.sptr", "PT.col", "pt_row", "pt_ap", "pt_p", "RT.sptr", "RT.col", "rt_pt")
 
 
 def fetch_plan(shim, active, nd, build=True):
@@ -160,7 +160,8 @@ def compact_transfers(levels):
         if L["coarsest"]:
             break
         n, nd = L["n"], L["dinv"].shape[1]
-        row, _ = pos_rows(L["PT.sptr"], n)
+        arow, _ = pos_rows(L["PT.sptr"], n)          # P̃'s own (A·P) row order
+        row = np.where(arow >= 0, L["pt_row"][np.maximum(arow, 0)], -1)   # the level's rows
         ok = (L["PT.col"] >= 0) & (row >= 0)
         PTb = np.zeros((len(row), nd, nd))
         pp = L["pt_p"]
@@ -168,7 +169,10 @@ def compact_transfers(levels):
         DAP = np.einsum("pab,pbc->pac", L["dinv"][np.maximum(row, 0)], L["APb"][np.maximum(L["pt_ap"], 0)])
         PTb[ok] = (base - L["omega"] * DAP)[ok]
         L["PTb"] = PTb
-        L["Pt"] = to_scipy(PTb, L["PT.sptr"], L["PT.col"], n, L["nc"], nd)
+        # as a matrix over the level's rows: relabel A·P rows → level rows
+        Pa = to_scipy(PTb, L["PT.sptr"], L["PT.col"], n, L["nc"], nd).tocoo()
+        r = L["pt_row"][Pa.row // nd] * nd + Pa.row % nd
+        L["Pt"] = sp.csr_matrix((Pa.data, (r, Pa.col)), shape=Pa.shape)
         rok = L["rt_pt"] >= 0
         RTb = np.zeros((len(L["rt_pt"]), nd, nd))
         RTb[rok] = np.transpose(PTb[L["rt_pt"][rok]], (0, 2, 1))

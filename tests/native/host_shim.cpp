@@ -209,6 +209,7 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   else if (n == "PT.sptr") v = &L.PT.sptr;
   else if (n == "PT.col") v = &L.PT.col;
   else if (n == "pt_ap") v = &L.pt_ap;
+  else if (n == "pt_row") v = &L.pt_row;
   else if (n == "pt_p") v = &L.pt_p;
   else if (n == "RT.sptr") v = &L.RT.sptr;
   else if (n == "RT.col") v = &L.RT.col;

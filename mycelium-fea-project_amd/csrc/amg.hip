@@ -239,21 +239,67 @@ __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);
   bstore<ND>(T.val32, 0, q, pm);
+  bstore<ND>(T.val, 0, q, pm);
 }
-// R̃ = P̃ᵀ in RT's own SELL layout, one position per thread
+// R̂ = s' D'_J⁻¹ P̃ᵀ D_i / ω in RT's own SELL layout, one thread per (row J,
+// slot) as k_amg_pvals: the scalings of x = ω D⁻¹ b on both sides folded in,
+// so the down sweep maps x_l to x_{l+1} directly (D_i: A's diagonal block,
+// slot 0 of row i)
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L) {
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
-  if (q >= L.RT.npos) return;
-  const int32_t src = L.rt_pt[q];
-  if (src < 0) return;
-  float p[ND * ND], t[ND * ND];
-  bload<ND>(L.PT.val32, 0, src, p);
+__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
+  const AmgMatD& T = L.RT;
+  const int64_t xb = xcd_block();
+  const int k = (int)(xb % T.wmax);
+  const int64_t J = (xb / T.wmax) * kBlock + threadIdx.x;
+  if (J - (threadIdx.x & 63) >= T.n) return;
+  int64_t base;
+  int w;
+  slice_of(T, J, base, w);
+  if (J >= T.n || k >= w) return;
+  const int64_t q = base + (int64_t)k * 64;
+  const int32_t i = T.col[q];
+  if (i < 0) return;
+  double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
+  bload<ND>(L.PT.val, 0, L.rt_pt[q], p);
+  dinv_load<ND>(N.dinv, J, Dn);
+  bload<ND>(L.A.val, 0, (int64_t)L.A.sptr[i >> 6] * 64 + (i & 63), D);
+  const double sc = (N.coarsest ? 1.0 : amg_omega(N.omega)) / amg_omega(L.omega);
 #pragma unroll
   for (int a = 0; a < ND; ++a)
 #pragma unroll
-    for (int b = 0; b < ND; ++b) t[a * ND + b] = p[b * ND + a];
-  bstore<ND>(L.RT.val32, 0, q, t);
+    for (int c = 0; c < ND; ++c) t[a * ND + c] = p[c * ND + a];  // P̃ᵀ block
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) u[c] = o[c] = 0.0;
+  mm_acc<ND>(Dn, t, u);
+  mm_acc<ND>(u, D, o);
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) o[c] *= sc;
+  bstore<ND>(T.val32, 0, q, o);
+}
+// Ã = ω D_i⁻¹ A_ij (compact cycle), one thread per (row, slot)
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
+  const AmgMatD& A = L.A;
+  const int64_t xb = xcd_block();
+  const int k = (int)(xb % A.wmax);
+  const int64_t i = (xb / A.wmax) * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= A.n) return;
+  int64_t base;
+  int w;
+  slice_of(A, i, base, w);
+  if (i >= A.n || k >= w) return;
+  const int64_t q = base + (int64_t)k * 64;
+  if (A.col[q] < 0) return;
+  double Di[ND * ND], m[ND * ND], o[ND * ND];
+  dinv_load<ND>(L.dinv, i, Di);
+  bload<ND>(A.val, 0, q, m);
+  const double om = amg_omega(L.omega);
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) o[c] = 0.0;
+  mm_acc<ND>(Di, m, o);
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) o[c] *= om;
+  bstore<ND>(A.at32, 0, q, o);
 }
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
@@ -442,15 +488,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 }
 
 // ---------------------------------------------------------------------------
-// The compact cycle (amg.hpp AmgLevel::PT): two sweeps per level.
-// Down: blocks [0, gc) form the coarse right-hand side b_{l+1} = R̃ b_l (S
-// lanes per coarse row) and x_{l+1} = s D⁻¹ b_{l+1}; blocks from gc on the
-// smoothed part c_l = x_l + ω D⁻¹ (b_l − A x_l), kept in t_l.  Both read only
-// b_l and x_l, so one launch holds them.  L0: b = the CG's f64 r, A_0's
-// symmetric f32 blocks.
-template <int ND, int S, class TB, bool L0>
-__global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, const TB* __restrict__ b, int64_t gc,
-                                                     const int32_t* gate) {
+// The compact cycle (amg.hpp AmgLevel::PT): two sweeps per level, on the
+// level's smoothed iterate x_l = s D⁻¹ b_l alone (b is never formed).
+// Down: blocks [0, gc) form the next level's x_{l+1} = R̂ x_l (S lanes per
+// coarse row), blocks from gc on the smoothed part c_l = 2 x_l − Ã x_l
+// (= x + ω D⁻¹ (b − A x)), kept in t_l.  Both read only x_l.
+template <int ND, int S>
+__global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64_t gc, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t xb = xcd_block();
   if (xb < gc) {
@@ -464,18 +508,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, const
     int64_t base;
     int w;
     slice_of(R, Ic, base, w);
-    const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
-    float Di[ND * ND], bc[ND];
-    dinv_load<ND>(N.dinv32, Ic, Di);
+    float xc[ND];
 #pragma unroll
-    for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
-    if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, b, bc);
-    else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, b, bc);
-    if (I >= n || sub != 0 || !run) return;
-    vstore<ND>(N.b, I, bc);
-    float xn[ND];
-    dinv_mul<ND>(Di, sc, bc, xn);
-    vstore<ND>(N.x, I, xn);
+    for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
+    if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.x, xc);
+    else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.x, xc);
+    if (I < n && sub == 0 && run) vstore<ND>(N.x, I, xc);
   } else {
     const int64_t i = (xb - gc) * kBlock + threadIdx.x;
     const int64_t n = L.A.n;
@@ -484,19 +522,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, const
     int64_t base;
     int w;
     slice_of(L.A, ii, base, w);
-    const float om = (float)amg_omega(L.omega);
-    float y[ND], x[ND], d[ND], Di[ND * ND];
-    vload<ND>(b, ii, y);
+    float x[ND], y[ND];
     vload<ND>(L.x, ii, x);
-    dinv_load<ND>(L.dinv32, ii, Di);
-    if constexpr (L0)
-      sell_mac<ND, true, 2, true>(L.A.col, L.A.sym32, L.A.npos, base, w, L.x, y);
-    else
-      sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, L.x, y);
-    dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
-    for (int a = 0; a < ND; ++a) x[a] += d[a];
-    if (i < n && run) vstore<ND>(L.t, i, x);
+    for (int a = 0; a < ND; ++a) y[a] = x[a] + x[a];
+    sell_mac<ND, true, 2>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    if (i < n && run) vstore<ND>(L.t, i, y);
   }
 }
 
@@ -705,48 +736,35 @@ __global__ __launch_bounds__(kTailBS) void k_amg_tail_lds(const TailLevels tl, i
 }
 
 // The compact cycle's tail (k_amg_down / k_amg_up of levels [l0, nlev) in ONE
-// workgroup, their vectors in LDS: b, x, c per level, a coarse level's output
-// e over its b — b_l is dead once its down sweep has run).  A down phase
-// sweeps the next level's rows (R̃ b) and then this level's (c), a wave never
-// straddling the two.  Up to kCTailLdsMax bytes: MI355X has 160 KB of LDS.
+// workgroup, their vectors in LDS).  A down phase sweeps the next level's rows
+// (R̂ x) and then this level's (c), a wave never straddling the two.  Up to
+// kCTailLdsMax bytes: MI355X has 160 KB of LDS.
 constexpr int64_t kCTailLdsMax = 160 * 1024;
 template <int ND>
-__device__ __forceinline__ void ctail_down(const AmgLevD& L, const AmgLevD& N, const float* b, const float* x,
-                                           float* c, float* nb, float* nx) {
+__device__ __forceinline__ void ctail_down(const AmgLevD& L, const float* x, float* c, float* nx) {
   const int64_t nc = L.RT.n, nf = L.A.n, nc64 = (nc + 63) & ~(int64_t)63;
-  const float sc = N.coarsest ? 1.0f : (float)amg_omega(N.omega);
-  const float om = (float)amg_omega(L.omega);
   for (int64_t r0 = 0; r0 < nc64 + nf; r0 += kTailBS) {
     const int64_t k = r0 + threadIdx.x, wave0 = r0 + (threadIdx.x & ~63);
     if (wave0 >= nc64 + nf) break;
     int64_t base;
     int w;
-    if (wave0 < nc64) {  // coarse row I: b' = R̃ b, x' = s D'⁻¹ b'
+    if (wave0 < nc64) {  // coarse row I: x' = R̂ x
       const int64_t I = k, Ic = I < nc ? I : nc - 1;
       slice_of(L.RT, Ic, base, w);
-      float bc[ND], Di[ND * ND];
-      dinv_load<ND>(N.dinv32, Ic, Di);
+      float xc[ND];
 #pragma unroll
-      for (int a = 0; a < ND; ++a) bc[a] = 0.0f;
-      sell_mac<ND, false, 3>(L.RT.col, L.RT.val32, L.RT.npos, base, w, b, bc);
-      if (I < nc) {
-        vstore<ND>(nb, I, bc);
-        float xn[ND];
-        dinv_mul<ND>(Di, sc, bc, xn);
-        vstore<ND>(nx, I, xn);
-      }
-    } else {  // fine row i: c = x + ω D⁻¹ (b − A x)
+      for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
+      sell_mac<ND, false, 3>(L.RT.col, L.RT.val32, L.RT.npos, base, w, x, xc);
+      if (I < nc) vstore<ND>(nx, I, xc);
+    } else {  // fine row i: c = 2x − Ã x
       const int64_t i = k - nc64, ii = i < nf ? i : nf - 1;
       slice_of(L.A, ii, base, w);
-      float y[ND], xv[ND], d[ND], Di[ND * ND];
-      vload<ND>(b, ii, y);
+      float xv[ND], y[ND];
       vload<ND>(x, ii, xv);
-      dinv_load<ND>(L.dinv32, ii, Di);
-      sell_mac<ND, true, 3>(L.A.col, L.A.val32, L.A.npos, base, w, x, y);
-      dinv_mul<ND>(Di, om, y, d);
 #pragma unroll
-      for (int a = 0; a < ND; ++a) xv[a] += d[a];
-      if (i < nf) vstore<ND>(c, i, xv);
+      for (int a = 0; a < ND; ++a) y[a] = xv[a] + xv[a];
+      sell_mac<ND, true, 3>(L.A.col, L.A.at32, L.A.npos, base, w, x, y);
+      if (i < nf) vstore<ND>(c, i, y);
     }
   }
 }
@@ -768,6 +786,14 @@ __device__ __forceinline__ void ctail_up(const AmgLevD& L, const float* c, const
   }
 }
 template <int ND>
+__device__ __forceinline__ int64_t ctail_lds_off(const AmgLevD* __restrict__ lev, int l, int l0) {
+  int64_t off = 0;
+  for (int m = l0; m < l; ++m) off += 2 * ND * lev[m].A.n;
+  return off;
+}
+// LDS per level: x then c (a level's output e overwrites its x, dead after
+// its down sweep; the coarsest level's output is its x)
+template <int ND>
 __global__ __launch_bounds__(kTailBS) void k_amg_ctail_lds(const TailLevels tl, int l0, int nlev,
                                                            const int32_t* gate) {
   extern __shared__ float sm[];
@@ -775,31 +801,24 @@ __global__ __launch_bounds__(kTailBS) void k_amg_ctail_lds(const TailLevels tl, 
   const AmgLevD* lev = tl.lev - l0;
   {
     const AmgLevD G = lev[l0];
-    const int64_t n = G.A.n;
-    for (int64_t k = threadIdx.x; k < ND * n; k += kTailBS) {
-      sm[k] = G.b[k];
-      sm[ND * n + k] = G.x[k];
-    }
+    for (int64_t k = threadIdx.x; k < ND * G.A.n; k += kTailBS) sm[k] = G.x[k];
   }
   __syncthreads();
   for (int l = l0; l + 1 < nlev; ++l) {
-    const AmgLevD L = lev[l], N = lev[l + 1];
-    float* v = sm + tail_lds_off<ND>(lev, l, l0);  // b x c of level l
-    float* w = v + 3 * ND * L.A.n;                 // of level l + 1
-    ctail_down<ND>(L, N, v, v + ND * L.A.n, v + 2 * ND * L.A.n, w, w + ND * N.A.n);
+    const AmgLevD L = lev[l];
+    float* v = sm + ctail_lds_off<ND>(lev, l, l0);  // x c of level l
+    ctail_down<ND>(L, v, v + ND * L.A.n, v + 2 * ND * L.A.n);
     __syncthreads();
   }
   for (int l = nlev - 2; l >= l0; --l) {
-    const AmgLevD L = lev[l], N = lev[l + 1];
-    float* v = sm + tail_lds_off<ND>(lev, l, l0);
-    float* w = v + 3 * ND * L.A.n;
-    // level l+1's output: its x if coarsest, else its e (held over its b)
-    const float* src = N.coarsest ? w + ND * N.A.n : w;
+    const AmgLevD L = lev[l];
+    float* v = sm + ctail_lds_off<ND>(lev, l, l0);
+    const float* src = v + 2 * ND * L.A.n;  // level l+1's output, held over its x
     if (l > l0) {
-      ctail_up<ND>(L, v + 2 * ND * L.A.n, src, v);
+      ctail_up<ND>(L, v + ND * L.A.n, src, v);
       __syncthreads();
     } else {
-      ctail_up<ND>(L, v + 2 * ND * L.A.n, src, L.e);
+      ctail_up<ND>(L, v + ND * L.A.n, src, L.e);
     }
   }
 }
@@ -846,7 +865,7 @@ template <int ND, bool FIRST, int BS, bool DIST>
 __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part,
                                                  AmgDist d) {
   // the iteration's gate is tested only before the stores (gate_open)
-  const bool run = FIRST || slots[j + 1].flag == kRun;
+  const bool run = FIRST || flag_load(&slots[j + 1].flag) == kRun;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
@@ -1042,10 +1061,6 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
     hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.rg.span()).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
   if (stage & kSetupAP) {
     hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
-    if (L.compact && L.PT.wmax > 0) {
-      hipLaunchKernelGGL(k_amg_ptv<ND>, dim3(rows_grid(L.PT.n).x * (unsigned)L.PT.wmax), dim3(kBlock), 0, s, L);
-      hipLaunchKernelGGL(k_amg_rtv<ND>, rows_grid(L.RT.npos), dim3(kBlock), 0, s, L);
-    }
   }
   if (stage & kSetupAC)
     hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, N->A, N->omega);
@@ -1053,6 +1068,22 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0, int stage) {
   if (nd == 2) setup_nd<2>(s, L, next, level0, stage);
   else setup_nd<3>(s, L, next, level0, stage);
+}
+
+template <int ND>
+static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev) {
+  for (int l = 0; l + 1 < nlev; ++l) {
+    const AmgLevD& L = lev[l];
+    if (!L.compact || L.PT.wmax <= 0) continue;
+    hipLaunchKernelGGL(k_amg_ptv<ND>, dim3(rows_grid(L.PT.n).x * (unsigned)L.PT.wmax), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_rtv<ND>, dim3(rows_grid(L.RT.n).x * (unsigned)L.RT.wmax), dim3(kBlock), 0, s, L,
+                       lev[l + 1]);
+    hipLaunchKernelGGL(k_amg_atv<ND>, dim3(rows_grid(L.A.n).x * (unsigned)L.A.wmax), dim3(kBlock), 0, s, L);
+  }
+}
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev) {
+  if (nd == 2) compact_setup_nd<2>(s, lev, nlev);
+  else compact_setup_nd<3>(s, lev, nlev);
 }
 
 // lanes per row: the restriction by R's mean slice width, the f32 operators
@@ -1127,15 +1158,15 @@ int amg_down_lanes(const AmgLevD& L) {
   return mean_w > 6.0 ? 8 : lanes_for(L.RT, 0, 2.5, 5.0);
 }
 int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, 0, 3.5, 8.0); }
-template <int ND, class TB, bool L0>
-static void down_tb(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const TB* b, const int32_t* gate) {
+template <int ND>
+static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int S = amg_down_lanes(L);
   const int64_t gc = rows_grid(S * L.RT.n).x;
   const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
-  if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
-  else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
-  else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
-  else hipLaunchKernelGGL((k_amg_down<ND, 1, TB, L0>), g, dim3(kBlock), 0, s, L, N, b, gc, gate);
+  if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);
 }
 template <int ND, class TE>
 static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, const int32_t* gate) {
@@ -1154,7 +1185,7 @@ static bool ctail_nd(hipStream_t s, const AmgLevD* lev, int nlev, int tail, cons
   int64_t lds = 0;
   for (int l = tail; l < nlev; ++l) {
     tl.lev[l - tail] = lev[l];
-    lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
+    lds += 2 * ND * lev[l].A.n * (int64_t)sizeof(float);
   }
   if (lds > kCTailLdsMax) return false;
   static bool attr = false;  // dynamic LDS above 64 KB must be allowed once per kernel
@@ -1175,13 +1206,10 @@ static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg&
   if (tail > l0) {
     // the tail needs its levels' vectors to fit LDS: probe from the requested level down
     int64_t lds = 0;
-    for (int l = tail; l < nlev; ++l) lds += 3 * ND * lev[l].A.n * (int64_t)sizeof(float);
+    for (int l = tail; l < nlev; ++l) lds += 2 * ND * lev[l].A.n * (int64_t)sizeof(float);
     if (lds <= kCTailLdsMax && tail < nlev - 1 && nlev - tail <= kTailMaxLev && lev[tail].tail_lds) top = tail;
   }
-  for (int l = l0; l < top; ++l) {
-    if (l == 0) down_tb<ND, double, true>(s, lev[0], lev[1], (const double*)cg.r, gate);
-    else down_tb<ND, float, false>(s, lev[l], lev[l + 1], (const float*)lev[l].b, gate);
-  }
+  for (int l = l0; l < top; ++l) down_nd<ND>(s, lev[l], lev[l + 1], gate);
   if (top < nlev - 1) ctail_nd<ND>(s, lev, nlev, top, gate);
   for (int l = top - 1; l >= l0; --l) {
     if (l == 0) up_te<ND, float>(s, lev[0], lev[1], cg.u, gate);

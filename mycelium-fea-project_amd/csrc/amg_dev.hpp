@@ -133,8 +133,25 @@ __device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gat
 // The V-cycle kernels load the gate with their first operands and test it only
 // before their stores: a test at entry puts one more dependent memory round
 // trip (≈ 1 µs: the flag was written on another XCD) in front of every launch,
-// and a gated launch (only after convergence) may read whatever it likes.
-__device__ __forceinline__ bool gate_open(const int32_t* gate) { return !gate || *gate == kRun; }
+// and a gated launch (only after convergence) may read whatever it likes.  The
+// flag is read by a VECTOR load (agent scope): a scalar load of it — what a
+// plain read of a uniform address compiles to — was waited for at the kernel's
+// first instruction, the round trip this is meant to hide.
+__device__ __forceinline__ int flag_load(const int32_t* p) {
+  // an opaque per-lane zero: the value stays a per-lane one, so the compiler
+  // waits for the load where the flag is used (the stores), not where a uniform
+  // copy of it would have to be settled (the first branch of the kernel)
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return __hip_atomic_load((__attribute__((address_space(1))) int*)p + z, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// (no branch on gate == NULL: a branch makes the compiler settle the flag's
+// value — and wait for its load — where the paths join, at the top)
+__device__ const int32_t kRunWord = kRun;
+__device__ __forceinline__ bool gate_open(const int32_t* gate) {
+  return flag_load(gate ? gate : &kRunWord) == kRun;
+}
 
 // XCD-aware block order for the gathering kernels.  Blocks are dealt
 // round-robin over the 8 XCDs (b and b + 8 share one; MI355X_MICROARCH.md),

@@ -48,6 +48,8 @@ struct AmgMatD {
   // the level-0 V-cycle kernels (f32) — 3/4 (ND = 2) of the full blocks' bytes
   double* sym = nullptr;
   float* sym32 = nullptr;
+  // the compact cycle: Ã = ω D⁻¹ A (f32 full blocks) of the smoothed part c = 2x − Ã x
+  float* at32 = nullptr;
 };
 
 struct AmgLevD {
@@ -80,8 +82,9 @@ struct AmgLevD {
   const int32_t* ac_a = nullptr;
   const int32_t* ac_b = nullptr;
   RowRange ac_rg;  // level l+1's A rows this rank's Galerkin product forms (= R's rows)
-  // the compact cycle (amg.hpp AmgLevel::PT): P̃ (f32, PT.val32) and R̃ = P̃ᵀ
-  // (RT.val32), formed by the setup after A·P when compact is set
+  // the compact cycle (amg.hpp AmgLevel::PT): P̃ (f32, PT.val32) and the scaled
+  // restriction R̂ = s' D'⁻¹ P̃ᵀ D / ω (RT.val32; s' = ω' or 1 on the coarsest
+  // level), formed by launch_amg_compact_setup once every level is set up
   int compact = 0;
   AmgMatD PT, RT;
   const int32_t* pt_row = nullptr;  // PT row → level row (P̃ has A·P's row order)
@@ -144,6 +147,9 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll = 15;  // (kSetupAP: + P̃, R̃)
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0,
                             int stage = kSetupAll);
+// the compact cycle's operators of every level (after every level's setup:
+// R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).

@@ -1137,7 +1137,8 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         // the compact cycle's P̃ / R̃ (one partition's hierarchy only: the
         // distributed V-cycle exchanges per four-step step)
         if (!rk && L.PT.n == n) {
-          d.PT = mat(L.PT, false, true);
+          d.PT = mat(L.PT, true, true);  // f64 P̃ too: R̂ is formed from it
+          d.A.at32 = F((size_t)nb2 * d.A.npos);
           d.PT.rg = row_range(L.PT, 0, n);
           d.pt_row = I(L.pt_row);
           d.pt_ap = I(L.pt_ap);
@@ -1403,6 +1404,7 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   for (int l = 0; l < nlev; ++l)
     launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
+  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev);
 }
 
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,

@@ -198,6 +198,33 @@ def vcycle_compact(levels, b, l=0):
     return c + L["Pt"] @ vcycle_compact(levels, L["Rt"] @ b, l + 1)
 
 
+def vcycle_scaled(levels, r):
+    """The compact cycle as the device runs it (csrc/amg.hip k_amg_down /
+    k_amg_up): on x_l = s_l D_l⁻¹ b_l alone, with R̂_l = s_{l+1} D_{l+1}⁻¹ R̃_l D_l / ω_l
+    (s = ω, 1 on the coarsest level) and Ã_l = ω_l D_l⁻¹ A_l:
+    c_l = 2 x_l − Ã_l x_l, x_{l+1} = R̂_l x_l, e_l = c_l + P̃_l e_{l+1}, e = x on the coarsest."""
+    def blk(M):
+        return sp.block_diag(list(M), format="csr")
+
+    def down_up(l, x):
+        L = levels[l]
+        if L["coarsest"]:
+            return x
+        N = levels[l + 1]
+        s_n = 1.0 if N["coarsest"] else N["omega"]
+        D = blk(np.linalg.inv(L["dinv"]))
+        Rhat = (s_n * blk(N["dinv"]) @ L["Rt"] @ D / L["omega"]).tocsr()
+        At = (L["omega"] * blk(L["dinv"]) @ L["A"]).tocsr()
+        c = 2.0 * x - At @ x
+        return c + L["Pt"] @ down_up(l + 1, Rhat @ x)
+
+    L0 = levels[0]
+    nd = L0["dinv"].shape[1]
+    s0 = 1.0 if L0["coarsest"] else L0["omega"]
+    x0 = s0 * np.einsum("iab,ib->ia", L0["dinv"], r.reshape(-1, nd)).ravel()
+    return down_up(0, x0)
+
+
 def vcycle(levels, b, l=0):
     L = levels[l]
     nd = L["dinv"].shape[1]

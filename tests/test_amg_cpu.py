@@ -193,3 +193,5 @@ def test_compact_cycle_transfers_and_cycle(shim):
         r = rng.standard_normal(Kff.shape[0])
         u4, u2 = amg_ref.vcycle(levels, r), amg_ref.vcycle_compact(levels, r)
         assert np.linalg.norm(u4 - u2) <= 1e-12 * np.linalg.norm(u4)
+        us = amg_ref.vcycle_scaled(levels, r)   # the device's form: x only, R̂ and Ã
+        assert np.linalg.norm(u4 - us) <= 1e-12 * np.linalg.norm(u4)

@@ -526,7 +526,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     vload<ND>(L.x, ii, x);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = x[a] + x[a];
-    sell_mac<ND, true, 2>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    if (L.nt) sell_mac<ND, true, 2, false, true>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    else sell_mac<ND, true, 2>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
     if (i < n && run) vstore<ND>(L.t, i, y);
   }
 }
@@ -879,7 +880,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    sell_mac<ND, false, 1, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
+    if (cg.nt) sell_mac<ND, false, 1, true, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
+    else sell_mac<ND, false, 1, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
     if (i < cg.lo || i >= cg.hi) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {

@@ -108,6 +108,7 @@ struct AmgPlan {
   // rank holds and computes all of their rows).  n_dist = 0: one partition.
   int world = 1;
   int n_dist = 0;
+  bool spatial = false;  // rows labelled in Z-order (AmgLayout)
 };
 
 // The distributed hierarchy (multi-GPU GAMG): ONE global
@@ -134,6 +135,22 @@ struct AmgStrength {
   double kb_kax = 0.0;
 };
 
+// Row labels of the device layout (stage 2 of the symbolic phase).  The
+// aggregation always runs in the natural order (depth-first: hyphal chains
+// contiguous — the order the iteration counts depend on); the labels only
+// decide where rows sit in the SELL slices and vectors.  spatial = 1: every
+// level's rows by the Morton (Z-order) key of their coordinates (level 0 the
+// nodes', coarse levels their aggregates' centroids), then the usual
+// 4096-row length windows — on chord-dense networks the depth-first order
+// puts a fifth of the couplings more than 49k rows apart (C5: 22 % of A_0's
+// entries; 0.1 % in Z-order), so the gathers of x / u miss every L2.
+// spatial = -1: Z-order when more than far_frac of A_0's off-diagonal entries
+// lie more than 4096 rows apart in the natural order.  Unsplit plans only.
+struct AmgLayout {
+  int spatial = 0;
+  double far_frac = 0.10;
+};
+
 // Builds the hierarchy for the free rows [0, P.n_free) of P with the element
 // activity `active` (P's element order).  Returns "" on success.
 // max_levels caps the hierarchy (the coarsest level's block Jacobi is then
@@ -142,7 +159,7 @@ struct AmgStrength {
 // dist: the distributed form (NULL: one partition, the plan of before).
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
                       int max_levels = kAmgMaxLevels, const AmgDistSpec* dist = nullptr,
-                      const AmgStrength& strength = AmgStrength());
+                      const AmgStrength& strength = AmgStrength(), const AmgLayout& layout = AmgLayout());
 
 // Partitioned solve (partition.hpp): the V-cycle is block Jacobi over the
 // partitions (each partition's hierarchy couples its own free rows only —

@@ -86,6 +86,7 @@ struct AmgLevD {
   // restriction R̂ = s' D'⁻¹ P̃ᵀ D / ω (RT.val32; s' = ω' or 1 on the coarsest
   // level), formed by launch_amg_compact_setup once every level is set up
   int compact = 0;
+  int nt = 0;  // the compact sweeps stream this level's Ã with non-temporal loads
   AmgMatD PT, RT;
   const int32_t* pt_row = nullptr;  // PT row → level row (P̃ has A·P's row order)
   const int32_t* pt_ap = nullptr;
@@ -116,7 +117,8 @@ struct AmgCg {
   // 1: the compact cycle (two sweeps per level, AmgLevD::PT) where every
   // level of the cycle has it (compact set: unsplit levels); 0: four steps
   int cycle = 0;
-  int ctail = 0;  // the compact cycle's single-workgroup LDS tail: its first level (0: none)
+  int ctail = 0;
+  int nt = 0;  // the SpMV w = A_0 u streams A_0 with non-temporal loads (u stays in L2)  // the compact cycle's single-workgroup LDS tail: its first level (0: none)
 };
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered

@@ -210,10 +210,12 @@ std::string coarsen(LevelCsr& L, Csr& An) {
 // (owner-major, natural order inside a rank), the windows inside each rank's
 // segment; bounds (world + 1) receives the segments' first new rows.
 std::vector<int32_t> sort_perm(const std::vector<int64_t>& key, const std::vector<int32_t>* own = nullptr,
-                               int world = 1, std::vector<int64_t>* bounds = nullptr) {
+                               int world = 1, std::vector<int64_t>* bounds = nullptr,
+                               const std::vector<int32_t>* base = nullptr) {
   const int64_t n = (int64_t)key.size();
   std::vector<int32_t> order(n), perm(n);
-  std::iota(order.begin(), order.end(), 0);
+  if (base) order = *base;  // a base order of the rows instead of the natural one (Z-order)
+  else std::iota(order.begin(), order.end(), 0);
   std::vector<int64_t> seg{0, n};
   if (own) {
     std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return (*own)[x] < (*own)[y]; });
@@ -230,6 +232,37 @@ std::vector<int32_t> sort_perm(const std::vector<int64_t>& key, const std::vecto
   for (int64_t k = 0; k < n; ++k) perm[order[k]] = (int32_t)k;
   if (bounds) *bounds = seg;
   return perm;
+}
+
+// Z-order (Morton) of points in the plane / space: 21 bits per axis over the
+// bounding box (3-D when any z differs), ties by index
+std::vector<int32_t> morton_order(const std::vector<double>& xyz, int64_t n) {
+  double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+  for (int64_t i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) {
+      lo[c] = std::min(lo[c], xyz[3 * i + c]);
+      hi[c] = std::max(hi[c], xyz[3 * i + c]);
+    }
+  const bool d3 = n > 0 && hi[2] > lo[2];
+  double span = 0.0;
+  for (int c = 0; c < (d3 ? 3 : 2); ++c) span = std::max(span, hi[c] - lo[c]);
+  const double sc = span > 0.0 ? ((1 << 21) - 1) / span : 0.0;
+  auto spread = [](uint64_t v, int step) {  // bit b → bit step·b
+    uint64_t r = 0;
+    for (int b = 0; b < 21; ++b) r |= ((v >> b) & 1ull) << (step * b);
+    return r;
+  };
+  std::vector<uint64_t> key(n);
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t k = 0;
+    for (int c = 0; c < (d3 ? 3 : 2); ++c)
+      k |= spread((uint64_t)((xyz[3 * i + c] - lo[c]) * sc), d3 ? 3 : 2) << c;
+    key[i] = k;
+  }
+  std::vector<int32_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+  return order;
 }
 
 // SELL-64 of M with rows relabelled by rperm and columns by cperm; epos[e] =
@@ -299,7 +332,8 @@ std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npo
 }  // namespace
 
 std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int nd, AmgPlan& plan,
-                      int max_levels, const AmgDistSpec* dist, const AmgStrength& strength) {
+                      int max_levels, const AmgDistSpec* dist, const AmgStrength& strength,
+                      const AmgLayout& lay) {
   max_levels = std::max(1, std::min(max_levels, kAmgMaxLevels));
   plan = AmgPlan();
   plan.nd = nd;
@@ -451,6 +485,26 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   const int nlev = (int)lv.size();
   std::vector<std::vector<int32_t>> perm(nlev);
   plan.lev.resize(nlev);
+  // Z-order labels (AmgLayout): decided on level 0's natural-order locality
+  bool spatial = !dist && lay.spatial > 0;
+  if (!dist && lay.spatial < 0) {
+    const Csr& A = lv[0].A;
+    int64_t off = 0, far = 0;
+    for (int64_t i = 0; i < A.n; ++i)
+      for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k) {
+        ++off;
+        far += std::llabs((long long)A.col[k] - (long long)i) > 4096;
+      }
+    spatial = off > 0 && (double)far > lay.far_frac * (double)off;
+  }
+  plan.spatial = spatial;
+  std::vector<double> cxyz;  // natural-order coordinates of the current level's rows
+  std::vector<std::vector<int32_t>> bases(nlev);  // per level: its Z-order (spatial)
+  if (spatial) {
+    cxyz.assign(3 * (size_t)nf, 0.0);
+    for (int64_t i = 0; i < nf; ++i)
+      for (int c = 0; c < 3; ++c) cxyz[3 * i + c] = P.xyz_perm[3 * i + c];
+  }
   for (int l = 0; l < nlev; ++l) {
     const int64_t n = lv[l].A.n;
     std::vector<int64_t> key(n);
@@ -458,7 +512,26 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     // levels [0, n_dist] owner-major (level n_dist: its rows are produced by
     // their rank's restriction, then gathered by every rank)
     const bool om = dist && l <= n_dist && l < (int)own.size();
-    perm[l] = sort_perm(key, om ? &own[l] : nullptr, world, om ? &plan.lev[l].own : nullptr);
+    std::vector<int32_t> base;
+    if (spatial) {
+      base = morton_order(cxyz, n);
+      if (l + 1 < nlev) {  // the next level's coordinates: centroids of the aggregates
+        std::vector<double> nx(3 * (size_t)lv[l].nc, 0.0);
+        std::vector<int64_t> cnt(lv[l].nc, 0);
+        for (int64_t i = 0; i < n; ++i) {
+          const int32_t a = lv[l].agg[i];
+          if (a < 0) continue;
+          ++cnt[a];
+          for (int c = 0; c < 3; ++c) nx[3 * a + c] += cxyz[3 * i + c];
+        }
+        for (int64_t a = 0; a < lv[l].nc; ++a)
+          for (int c = 0; c < 3; ++c) nx[3 * a + c] /= (double)std::max<int64_t>(cnt[a], 1);
+        cxyz.swap(nx);
+      }
+    }
+    perm[l] = sort_perm(key, om ? &own[l] : nullptr, world, om ? &plan.lev[l].own : nullptr,
+                        spatial ? &base : nullptr);
+    bases[l] = std::move(base);
     if (om) {
       plan.lev[l].owner.assign(n, 0);
       for (int64_t i = 0; i < n; ++i) plan.lev[l].owner[perm[l][i]] = own[l][i];
@@ -495,7 +568,8 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       std::vector<int64_t> key(L.A.n);
       for (int64_t i = 0; i < L.A.n; ++i) key[i] = L.AP.len(i);
       const bool om = dist && l < n_dist;
-      pap = sort_perm(key, om ? &own[l] : nullptr, world, om ? &out.ap_own : nullptr);
+      pap = sort_perm(key, om ? &own[l] : nullptr, world, om ? &out.ap_own : nullptr,
+                      spatial ? &bases[l] : nullptr);
       if (!(err = layout(L.AP, pap, &perm[l + 1], out.AP, eAP)).empty()) return err;
       if (om) {
         out.aprow.assign(L.A.n, 0);

@@ -180,6 +180,8 @@ struct mfea_handle {
   // graph cache (single partition)
   hipGraphExec_t graph = nullptr;
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
+  hipGraphExec_t graph_big = nullptr;  // GAMG: the planned batch's long chunks
+  int graph_big_chunk = 0, graph_big_ell = -1;
   hipEvent_t ev[6] = {};
   hipEvent_t ev_setup = nullptr;
   bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
@@ -207,6 +209,9 @@ struct mfea_handle {
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
+  int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
+  int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
+                       // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
   int64_t opt_amg_ctail_rows = 0;  // GAMG compact cycle: levels of at most this many rows in one workgroup
                                    // (measured slower than their launches at C2 / C3: off)
@@ -249,6 +254,7 @@ struct mfea_handle {
 namespace {
 
 constexpr int kMaxChunk = 64;
+constexpr int kAmgBigChunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
 // lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6; plus per
 // compact halo record (ell_vecs): h × 2 18, hM 6
 constexpr int64_t kEllDoubles = 18 + 6 + 3 + 3 + 18 + 6 + 18 + 6;
@@ -267,6 +273,10 @@ double* cg_part_buf(Part& pt, int par) { return pt.cg_part.ptr + (size_t)par * 4
 
 void destroy_graph(mfea_handle* h) {
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  if (h->graph_big) (void)hipGraphExecDestroy(h->graph_big);
+  h->graph_big = nullptr;
+  h->graph_big_chunk = 0;
+  h->graph_big_ell = -1;
   h->graph = nullptr;
   h->graph_chunk = 0;
   h->graph_precond = -1;
@@ -862,6 +872,43 @@ int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&&
   return 0;
 }
 
+// drive_planned with chunks of two sizes: the planned batch (`expected`
+// updates) as long chunks of `big` iterations plus short ones of `small` for
+// the remainder — one chunk boundary (advance kernel + graph-to-graph gap,
+// ≈ 13 µs) per `big` iterations instead of per `small`, while a batch never
+// overshoots the expected count by more than small − 1 — then short chunks
+// one at a time until the device reports done.  enqueue(size) queues one.
+template <class Enqueue, class After = NoEpilogue>
+int drive_sized(mfea_handle* h, int big, int small, int max_it, int expected, Enqueue&& enqueue,
+                SolveState* out, After&& after = After{}) {
+  hipStream_t s = h->stream;
+  volatile SolveState* hs = h->h_state;
+  hs[0].done = 0;
+  const int need = std::max(1, expected + 1);  // updates the batch assumes, as drive_planned
+  const int nbig = big > small ? need / big : 0;
+  const int nsmall = (need - nbig * big + small - 1) / small;
+  int64_t done_its = 0;
+  for (int k = 0; k < nbig; ++k, done_its += big) RC(enqueue(big));
+  for (int k = 0; k < nsmall; ++k, done_its += small) RC(enqueue(small));
+  RC(after());
+  HIPC(hipEventRecord(h->poll[0], s));
+  RC(wait_event(h, h->poll[0]));
+  while (!hs[0].done && done_its < (int64_t)max_it + 3 * small) {
+    RC(enqueue(small));
+    RC(after());
+    HIPC(hipEventRecord(h->poll[0], s));
+    RC(wait_event(h, h->poll[0]));
+    done_its += small;
+  }
+  RC(sync_stream(h));
+  *out = h->h_state[0];
+  if (!out->done) {
+    out->status = MFEA_EMAXIT;
+    out->iters = max_it;
+  }
+  return 0;
+}
+
 // device times of the last solve (its events must have completed)
 void solve_times(mfea_handle* h, mfea_stats* st) {
   float ms = 0;
@@ -1006,6 +1053,18 @@ AmgStrength amg_strength(const mfea_handle* h) {
 // level (option amg_deep, or the first unsplit level of at most amg_deep_rows
 // rows), its workgroups and its barrier words (zeroed once; every launch
 // leaves them zero).
+// non-temporal level-0 operator streams (option amg_nt), meant to keep the
+// gathered u / x in the XCD's L2 while A_0 streams past: measured slower at
+// both sizes (SpMV C3 9.7 → 12.8 µs, C5 215 → 244 µs), so off by default
+void set_amg_nt(mfea_handle* h, Part& pt) {
+  if (pt.amg_lev.empty()) return;
+  const AmgLevD& L0 = pt.amg_lev[0];
+  const double a0_bytes = (double)L0.A.npos * (8.0 * pt.amg.nd * (pt.amg.nd + 1) / 2 + 4.0);
+  const int on = h->opt_amg_nt < 0 ? (a0_bytes > 128e6 ? 1 : 0) : h->opt_amg_nt;
+  pt.amg_cg.nt = on;
+  pt.amg_lev[0].nt = on;
+}
+
 int set_amg_deep(mfea_handle* h, Part& pt) {
   const int nlev = (int)pt.amg_lev.size();
   int deep = 0;
@@ -1179,6 +1238,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.ctail = ct > 0 ? ct + first - 1 : 0;
   }
   RC(set_amg_deep(h, pt));
+  set_amg_nt(h, pt);
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -1262,8 +1322,10 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
     return 0;
   }
   pt.amg_ok = false;
+  AmgLayout lay;
+  lay.spatial = h->opt_amg_spatial;
   const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels, nullptr,
-                                    amg_strength(h));
+                                    amg_strength(h), lay);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   RC(upload_amg(h, pt, pt.amg));
@@ -1457,26 +1519,41 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                        },
                        &fin, finish);
   } else {
+    auto capture = [&](hipGraphExec_t* ge, int n) -> int {
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      enqueue_amg_chunk(h, pt, n);
+      HIPC(hipStreamEndCapture(s, &g));
+      hipError_t e = hipGraphInstantiate(ge, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      return 0;
+    };
     if (h->graph == nullptr || h->graph_chunk != chunk || h->graph_precond != MFEA_PC_GAMG ||
         h->graph_ell != tag) {
       destroy_graph(h);
-      hipGraph_t g;
-      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      enqueue_amg_chunk(h, pt, chunk);
-      HIPC(hipStreamEndCapture(s, &g));
-      hipError_t e = hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(g);
-      HIPC(e);
+      RC(capture(&h->graph, chunk));
       h->graph_chunk = chunk;
       h->graph_precond = MFEA_PC_GAMG;
       h->graph_ell = tag;
     }
-    rc = drive_planned(h, chunk, o->max_it, expected,
-                       [&]() -> int {
-                         HIPC(hipGraphLaunch(h->graph, s));
-                         return 0;
-                       },
-                       &fin, finish);
+    // the planned batch in long chunks (default solves only: a caller's
+    // chunk size is kept as given); measured at C3 / C2: chunks of 8 in the
+    // batch 2.24 / 1.15 ms per step against 2.36 / 1.20 with chunks of 2
+    const int big = o->chunk > 0 ? chunk : kAmgBigChunk;
+    if (big > chunk && (h->graph_big == nullptr || h->graph_big_chunk != big || h->graph_big_ell != tag)) {
+      if (h->graph_big) (void)hipGraphExecDestroy(h->graph_big);
+      h->graph_big = nullptr;
+      RC(capture(&h->graph_big, big));
+      h->graph_big_chunk = big;
+      h->graph_big_ell = tag;
+    }
+    rc = drive_sized(h, big, chunk, o->max_it, expected,
+                     [&](int n) -> int {
+                       HIPC(hipGraphLaunch(n == chunk ? h->graph : h->graph_big, s));
+                       return 0;
+                     },
+                     &fin, finish);
   }
   if (rc) return rc;
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
@@ -2914,6 +2991,16 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
   }
+  else if (n == "amg_spatial") {
+    if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_spatial: -1 (by locality), 0 or 1");
+    h->opt_amg_spatial = (int)value;
+    rebuild = true;
+  }
+  else if (n == "amg_nt") {
+    if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_nt: -1 (by size), 0 or 1");
+    h->opt_amg_nt = (int)value;
+    for (auto& pp : h->parts) set_amg_nt(h, *pp);
+  }
   else if (n == "amg_theta_ppm") {
     if (value < 0 || value > 1000000) return fail(MFEA_EINVAL, "amg_theta_ppm: 0..1000000");
     h->opt_amg_theta_ppm = value;
@@ -3099,6 +3186,11 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
+  else if (n == "amg_nt") *value = h->opt_amg_nt;
+  else if (n == "amg_spatial") *value = h->opt_amg_spatial;
+  else if (n == "amg_spatial_chosen") {  // read-only: partition 0's plan is in Z-order
+    *value = h->parts.empty() ? 0 : (h->parts[0]->amg.spatial ? 1 : 0);
+  }
   else if (n == "amg_deep") *value = h->opt_amg_deep;
   else if (n == "amg_deep_rows") *value = h->opt_amg_deep_rows;
   else if (n == "amg_deep_wgs") *value = h->opt_amg_deep_wgs;

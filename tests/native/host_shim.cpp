@@ -131,6 +131,10 @@ void shim_sell_values(const uint8_t* active, double EA, double EI12, double* val
 // number of levels (or -1, error in err).
 static AmgPlan g_amg;
 static AmgStrength g_strength;
+static AmgLayout g_layout;
+// row labels of the next shim_amg (amg.hpp AmgLayout: 0 depth-first, 1 Z-order, -1 by locality)
+void shim_amg_layout(int spatial) { g_layout.spatial = spatial; }
+int shim_amg_spatial() { return g_amg.spatial ? 1 : 0; }
 // strength of connection of the next shim_amg / shim_amg_dist (amg.hpp AmgStrength)
 void shim_amg_strength(double theta, double kb_kax) {
   g_strength.theta = theta;
@@ -138,7 +142,7 @@ void shim_amg_strength(double theta, double kb_kax) {
 }
 int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   std::vector<uint8_t> a(active, active + g_P.n_elems);
-  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, nullptr, g_strength);
+  std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, nullptr, g_strength, g_layout);
   if (!e.empty()) {
     std::snprintf(err, errn, "%s", e.c_str());
     return -1;

@@ -195,3 +195,27 @@ def test_compact_cycle_transfers_and_cycle(shim):
         assert np.linalg.norm(u4 - u2) <= 1e-12 * np.linalg.norm(u4)
         us = amg_ref.vcycle_scaled(levels, r)   # the device's form: x only, R̂ and Ã
         assert np.linalg.norm(u4 - us) <= 1e-12 * np.linalg.norm(u4)
+
+
+def test_spatial_labels_keep_the_hierarchy(shim):
+    """Z-order row labels (amg.hpp AmgLayout): the same aggregates, so the same
+    Galerkin products and the same PCG iteration count as depth-first labels,
+    with the labels a permutation of the depth-first ones."""
+    xyz, e2n, top, bot = _golden22k()
+    shim.shim_amg_layout.argtypes = [C.c_int]
+    shim.shim_amg_spatial.restype = C.c_int
+    out = {}
+    try:
+        for sp_ in (0, 1):
+            shim.shim_amg_layout(sp_)
+            levels, Kff, b, nodes0 = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+            assert shim.shim_amg_spatial() == sp_
+            for l in range(len(levels) - 1):
+                L, Nx = levels[l], levels[l + 1]
+                assert _rel(Nx["A"], (L["P"].T @ L["A"] @ L["P"]).tocsr()) <= 1e-13
+            _, it = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-8)
+            out[sp_] = (it, [L["n"] for L in levels], np.sort(nodes0))
+    finally:
+        shim.shim_amg_layout(0)
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    assert np.array_equal(out[0][2], out[1][2])

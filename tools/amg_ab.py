@@ -28,12 +28,14 @@ def main():
     ap.add_argument("--values", nargs="+", type=int, default=[0, 2, 4])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--chunk", type=int, nargs="*", default=[0],
+                    help="solve chunk sizes to sweep as well (0: the engine's default)")
     a = ap.parse_args()
     import fea_solver as fs
     from mfea import PC_GAMG, Engine, make_opts, synth
     from mfea.synth import CONFIGS
     dy = fs.DISPLACEMENT_MAX * 20 / (fs.N_STEPS - 1)
-    opts = make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG)
+    opts_of = {c: make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG, chunk=c) for c in a.chunk}
     for cfg in a.configs:
         nx, ny = CONFIGS[cfg]
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
@@ -42,10 +44,12 @@ def main():
         eng.set_material(fs.E_mod, fs.A, fs.I)
         eng.set_mesh(xyz, e2n)
         eng.set_bc(top, bot)
-        res = {v: {"ms_step": [], "wall_ms": [], "iter_us": [], "spmv_us": []} for v in a.values}
+        runs = [(v, c) for v in a.values for c in a.chunk]
+        res = {r: {"ms_step": [], "wall_ms": [], "iter_us": [], "spmv_us": []} for r in runs}
         U0 = None
         for rnd in range(a.rounds):
-            for v in a.values:
+            for v, c in runs:
+                opts = opts_of[c]
                 eng.set_option(a.option, v)
                 eng.set_active(None)
                 eng.step(dy, -dy, opts, fs.MAX_STRAIN)  # warm (graph capture)
@@ -53,18 +57,18 @@ def main():
                     eng.set_active(None)
                     t = time.perf_counter()
                     _, _, st = eng.step(dy, -dy, opts, fs.MAX_STRAIN)
-                    res[v]["wall_ms"].append(1e3 * (time.perf_counter() - t))
-                    res[v]["ms_step"].append(st.t_assemble_ms + st.t_rhs_ms + st.t_solve_ms + st.t_post_ms)
-                res[v]["iter_us"].append(1e3 * eng.profile_iteration(PC_GAMG, reps=30))
-                res[v]["spmv_us"].append(1e3 * eng.profile_spmv(reps=100))
+                    res[(v, c)]["wall_ms"].append(1e3 * (time.perf_counter() - t))
+                    res[(v, c)]["ms_step"].append(st.t_assemble_ms + st.t_rhs_ms + st.t_solve_ms + st.t_post_ms)
+                res[(v, c)]["iter_us"].append(1e3 * eng.profile_iteration(PC_GAMG, reps=30))
+                res[(v, c)]["spmv_us"].append(1e3 * eng.profile_spmv(reps=100))
                 U = eng.displacement()
                 if U0 is None:
                     U0 = U
-                res[v].update(iters=st.iters, relres=st.relres, setup_ms=st.t_setup_ms,
-                              dU=float(np.linalg.norm(U - U0) / np.linalg.norm(U0)))
-        for v in a.values:
-            r = res[v]
-            print(json.dumps({"config": cfg, a.option: v, "iters": r["iters"], "relres": r["relres"],
+                res[(v, c)].update(iters=st.iters, relres=st.relres, setup_ms=st.t_setup_ms,
+                                   dU=float(np.linalg.norm(U - U0) / np.linalg.norm(U0)))
+        for v, c in runs:
+            r = res[(v, c)]
+            print(json.dumps({"config": cfg, a.option: v, "chunk": c, "iters": r["iters"], "relres": r["relres"],
                               "dU_vs_first": r["dU"], "setup_ms": r["setup_ms"],
                               "wall_ms_med": float(np.median(r["wall_ms"])),
                               "dev_ms_med": float(np.median(r["ms_step"])),

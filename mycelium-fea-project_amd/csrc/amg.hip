@@ -146,21 +146,15 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
 }
 
 
-// P values, one thread per (row, slot k): every slot of a row in flight at
-// once instead of one after another.  Block b = (row block b / wmax, slot
-// b % wmax), numbered XCD-aware: each XCD gets whole row ranges, all slots.
+// P values, one thread per position (slot_wave): every slot of a row in
+// flight at once instead of one after another.
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   const AmgMatD& P = L.P;
-  const int64_t xb = xcd_block();
-  const int k = (int)(xb % P.wmax);
-  const int64_t i = P.rg.lo64() + (xb / P.wmax) * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= P.rg.hi) return;
-  int64_t base;
-  int w;
-  slice_of(P, i, base, w);
-  if (i < P.rg.lo || i >= P.rg.hi || k >= w) return;
-  const int64_t q = base + (int64_t)k * 64;
+  int64_t q, i;
+  int k;
+  if (!slot_wave(P, P.rg.p0 / 64, P.rg.p1 / 64, q, i, k)) return;
+  if (i < P.rg.lo || i >= P.rg.hi) return;
   const int32_t J = P.col[q];
   if (J < 0) return;
   double S[ND * ND], pm[ND * ND], Di[ND * ND];
@@ -213,16 +207,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
   const AmgMatD& T = L.PT;
-  const int64_t xb = xcd_block();
-  const int k = (int)(xb % T.wmax);
-  const int64_t i = (xb / T.wmax) * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= T.n) return;
-  int64_t base;
-  int w;
-  slice_of(T, i, base, w);
-  if (i >= T.n || k >= w) return;
-  const int64_t q = base + (int64_t)k * 64;
-  if (T.col[q] < 0) return;
+  int64_t q, i;
+  int k;
+  if (!slot_wave(T, 0, T.npos / 64, q, i, k) || i >= T.n || T.col[q] < 0) return;
   const int32_t qp = L.pt_p[q];
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
   dinv_load<ND>(L.dinv, L.pt_row[i], Di);
@@ -248,15 +235,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
   const AmgMatD& T = L.RT;
-  const int64_t xb = xcd_block();
-  const int k = (int)(xb % T.wmax);
-  const int64_t J = (xb / T.wmax) * kBlock + threadIdx.x;
-  if (J - (threadIdx.x & 63) >= T.n) return;
-  int64_t base;
-  int w;
-  slice_of(T, J, base, w);
-  if (J >= T.n || k >= w) return;
-  const int64_t q = base + (int64_t)k * 64;
+  int64_t q, J;
+  int k;
+  if (!slot_wave(T, 0, T.npos / 64, q, J, k) || J >= T.n) return;
   const int32_t i = T.col[q];
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
@@ -280,16 +261,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
   const AmgMatD& A = L.A;
-  const int64_t xb = xcd_block();
-  const int k = (int)(xb % A.wmax);
-  const int64_t i = (xb / A.wmax) * kBlock + threadIdx.x;
-  if (i - (threadIdx.x & 63) >= A.n) return;
-  int64_t base;
-  int w;
-  slice_of(A, i, base, w);
-  if (i >= A.n || k >= w) return;
-  const int64_t q = base + (int64_t)k * 64;
-  if (A.col[q] < 0) return;
+  int64_t q, i;
+  int k;
+  if (!slot_wave(A, 0, A.npos / 64, q, i, k) || i >= A.n || A.col[q] < 0) return;
   double Di[ND * ND], m[ND * ND], o[ND * ND];
   dinv_load<ND>(L.dinv, i, Di);
   bload<ND>(A.val, 0, q, m);
@@ -1014,6 +988,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_finish(AmgCg cg, double* __restr
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+static dim3 slot_grid(int64_t npos) {  // one wave per slot row (slot_wave)
+  const int64_t w = kBlock / 64, t = npos / 64;
+  return dim3((unsigned)((t + w - 1) / w > 0 ? (t + w - 1) / w : 1));
+}
 static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock > 0 ? (n + kBlock - 1) / kBlock : 1)); }
 
 // The w kernel writes one partial per block and every wave of the next
@@ -1060,7 +1038,7 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
     hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   if (L.coarsest || !N) return;
   if (stage & kSetupP && L.P.wmax > 0)
-    hipLaunchKernelGGL(k_amg_pvals<ND>, dim3(rows_grid(L.P.rg.span()).x * (unsigned)L.P.wmax), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_pvals<ND>, slot_grid(L.P.rg.npos()), dim3(kBlock), 0, s, L);
   if (stage & kSetupAP) {
     hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
   }
@@ -1077,10 +1055,9 @@ static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev) {
   for (int l = 0; l + 1 < nlev; ++l) {
     const AmgLevD& L = lev[l];
     if (!L.compact || L.PT.wmax <= 0) continue;
-    hipLaunchKernelGGL(k_amg_ptv<ND>, dim3(rows_grid(L.PT.n).x * (unsigned)L.PT.wmax), dim3(kBlock), 0, s, L);
-    hipLaunchKernelGGL(k_amg_rtv<ND>, dim3(rows_grid(L.RT.n).x * (unsigned)L.RT.wmax), dim3(kBlock), 0, s, L,
-                       lev[l + 1]);
-    hipLaunchKernelGGL(k_amg_atv<ND>, dim3(rows_grid(L.A.n).x * (unsigned)L.A.wmax), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_ptv<ND>, slot_grid(L.PT.npos), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_rtv<ND>, slot_grid(L.RT.npos), dim3(kBlock), 0, s, L, lev[l + 1]);
+    hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
   }
 }
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev) {

@@ -195,6 +195,22 @@ __device__ __forceinline__ bool pos_mine(const RowRange& g, int64_t q) {
   return row >= g.lo && row < g.hi;
 }
 
+// One wave per slot row t ∈ [t0, t1) of M's SELL layout (the setup's value
+// kernels: every thread owns one position, none idles — a (row, slot) grid
+// sized by the widest slice left most threads of the wide-tailed P̃ / R̂
+// layouts idle): position q = 64 t + lane, row 64 s + lane of slice
+// s = srow[t], slot k = t − sptr[s].  False past the end (wave-uniform).
+__device__ __forceinline__ bool slot_wave(const AmgMatD& M, int64_t t0, int64_t t1, int64_t& q, int64_t& row,
+                                          int& k) {
+  const int64_t t = t0 + xcd_block() * (kBlock / 64) + (threadIdx.x >> 6);
+  if (t >= t1) return false;
+  const int s = __builtin_amdgcn_readfirstlane(M.srow[t]);
+  k = (int)(t - M.sptr[s]);
+  row = 64 * (int64_t)s + (threadIdx.x & 63);
+  q = t * 64 + (threadIdx.x & 63);
+  return true;
+}
+
 // slot range of the wave's slice (scalar loads, wave-uniform)
 __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
   const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));

@@ -40,6 +40,7 @@ struct AmgMatD {
   int32_t wmax = 0;  // widest slice (host side: launch geometry)
   RowRange rg;       // rows this rank computes
   const int32_t* sptr = nullptr;
+  const int32_t* srow = nullptr;  // slot row → its slice (the setup's one-wave-per-slot-row grids)
   const int32_t* col = nullptr;
   double* val = nullptr;   // [npos][NB2] f64 (setup)
   float* val32 = nullptr;  // [npos][NB2] f32 copy for the V-cycle (levels ≥ 1)

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <deque>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1127,12 +1128,17 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     return p;
   };
   // vals64: f64 values (setup / CG), vals32: the f32 V-cycle copy
+  std::deque<std::vector<int32_t>> srows;  // alive until the copies below have run (the stream sync at the end)
   auto mat = [&](const SellPat& S, bool vals64, bool vals32) {
     AmgMatD m;
     m.n = S.n;
     m.npos = S.n_pos();
     for (size_t k = 0; k + 1 < S.sptr.size(); ++k) m.wmax = std::max(m.wmax, S.sptr[k + 1] - S.sptr[k]);
     m.sptr = I(S.sptr);
+    std::vector<int32_t>& srow = srows.emplace_back(S.sptr.empty() ? 0 : S.sptr.back(), 0);  // slot row → slice
+    for (size_t k = 0; k + 1 < S.sptr.size(); ++k)
+      for (int32_t t = S.sptr[k]; t < S.sptr[k + 1]; ++t) srow[t] = (int32_t)k;
+    m.srow = I(srow);
     m.col = I(S.col);
     m.val = vals64 ? D((size_t)nb2 * m.npos) : nullptr;
     m.val32 = vals32 ? F((size_t)nb2 * m.npos) : nullptr;

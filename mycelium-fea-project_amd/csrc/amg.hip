@@ -276,6 +276,70 @@ __global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
   bstore<ND>(A.at32, 0, q, o);
 }
 
+// the collapsed cycle (amg_collapse.cpp): T = V_{l+1} R̂ (a < 0: the
+// identity, V_coarsest) and V = 2I·[diag] − Ã + Σ P̃·T, one output block per
+// thread, f32 blocks summed in list order (fixed: bitwise reproducible)
+template <int ND>
+__device__ __forceinline__ void fmm_acc(const float* A, const float* B, float* C) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) {
+      float s = C[a * ND + b];
+#pragma unroll
+      for (int k = 0; k < ND; ++k) s = fmaf(A[a * ND + k], B[k * ND + b], s);
+      C[a * ND + b] = s;
+    }
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext) {
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
+  if (q >= L.CT.npos || L.CT.col[q] < 0) return;
+  float C[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
+  for (int t = L.ct_ptr[q]; t < L.ct_ptr[q + 1]; ++t) {
+    const int32_t a = L.ct_a[t], b = L.ct_b[t];
+    float r[ND * ND];
+    bload<ND>(L.RT.val32, 0, b, r);
+    if (a < 0) {
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) C[c] += r[c];
+    } else {
+      float v[ND * ND];
+      bload<ND>(vnext, 0, a, v);
+      fmm_acc<ND>(v, r, C);
+    }
+  }
+  bstore<ND>(L.CT.val32, 0, q, C);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
+  const int64_t q = xcd_block() * kBlock + threadIdx.x;
+  if (q >= L.CV.npos || L.CV.col[q] < 0) return;
+  float C[ND * ND];
+  const int32_t ea = L.cv_ext[q];
+  if (ea >= 0) {
+    bload<ND>(L.A.at32, 0, ea, C);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] = -C[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
+  }
+  if (L.cv_diag[q]) {
+#pragma unroll
+    for (int a = 0; a < ND; ++a) C[a * ND + a] += 2.0f;
+  }
+  for (int t = L.cv_ptr[q]; t < L.cv_ptr[q + 1]; ++t) {
+    float p[ND * ND], tb[ND * ND];
+    bload<ND>(L.PT.val32, 0, L.cv_a[t], p);
+    bload<ND>(L.CT.val32, 0, L.cv_b[t], tb);
+    fmm_acc<ND>(p, tb, C);
+  }
+  bstore<ND>(L.CV.val32, 0, q, C);
+}
+
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
@@ -533,6 +597,29 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
   if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
   else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
   if (a < n && sub == 0 && run) vstore<ND>(e, i, y);
+}
+
+// The collapsed cycle below level kc: e_kc = V x_kc in one sweep (V's rows
+// by length, vrow → the level's row), S lanes per row
+template <int ND, int S>
+__global__ __launch_bounds__(kBlock) void k_amg_vapply(AmgLevD L, const int32_t* gate) {
+  const bool run = gate_open(gate);
+  const AmgMatD& V = L.CV;
+  const int64_t t = xcd_block() * kBlock + threadIdx.x;
+  const int64_t n = V.n;
+  const int64_t a = t / S;
+  const int sub = (int)(t % S);
+  if (a - (threadIdx.x & 63) / S >= n) return;
+  const int64_t aa = a < n ? a : n - 1;
+  int64_t base;
+  int w;
+  slice_of(V, aa, base, w);
+  float y[ND];
+#pragma unroll
+  for (int c = 0; c < ND; ++c) y[c] = 0.0f;
+  if constexpr (S == 1) sell_mac<ND, false, 3>(V.col, V.val32, V.npos, base, w, L.x, y);
+  else sell_mac_sub<ND, S, false>(V.col, V.val32, base, w, sub, L.x, y);
+  if (a < n && sub == 0 && run) vstore<ND>(L.e, L.cv_row[aa], y);
 }
 
 // ---------------------------------------------------------------------------
@@ -1051,7 +1138,7 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 }
 
 template <int ND>
-static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev) {
+static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
   for (int l = 0; l + 1 < nlev; ++l) {
     const AmgLevD& L = lev[l];
     if (!L.compact || L.PT.wmax <= 0) continue;
@@ -1059,10 +1146,18 @@ static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev) {
     hipLaunchKernelGGL(k_amg_rtv<ND>, slot_grid(L.RT.npos), dim3(kBlock), 0, s, L, lev[l + 1]);
     hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
   }
+  if (coll <= 0) return;
+  for (int l = nlev - 2; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
+    const AmgLevD& L = lev[l];
+    if (!L.collapsed) return;
+    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
+    hipLaunchKernelGGL(k_amg_tv<ND>, rows_grid(L.CT.npos), dim3(kBlock), 0, s, L, vnext);
+    hipLaunchKernelGGL(k_amg_vv<ND>, rows_grid(L.CV.npos), dim3(kBlock), 0, s, L);
+  }
 }
-void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev) {
-  if (nd == 2) compact_setup_nd<2>(s, lev, nlev);
-  else compact_setup_nd<3>(s, lev, nlev);
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
+  if (nd == 2) compact_setup_nd<2>(s, lev, nlev, coll);
+  else compact_setup_nd<3>(s, lev, nlev, coll);
 }
 
 // lanes per row: the restriction by R's mean slice width, the f32 operators
@@ -1179,8 +1274,26 @@ static bool ctail_nd(hipStream_t s, const AmgLevD* lev, int nlev, int tail, cons
   return true;
 }
 template <int ND>
+static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
+  const int64_t rows = ((L.CV.n + 63) / 64) * 64;
+  const double mean_w = rows > 0 ? (double)L.CV.npos / (double)rows : 0.0;
+  const int S = mean_w > 12.0 ? 8 : mean_w > 5.0 ? 4 : mean_w > 2.5 ? 2 : 1;
+  const dim3 g(rows_grid(S * L.CV.n));
+  if (S == 8) hipLaunchKernelGGL((k_amg_vapply<ND, 8>), g, dim3(kBlock), 0, s, L, gate);
+  else if (S == 4) hipLaunchKernelGGL((k_amg_vapply<ND, 4>), g, dim3(kBlock), 0, s, L, gate);
+  else if (S == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 2>), g, dim3(kBlock), 0, s, L, gate);
+  else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);
+}
+template <int ND>
 static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, int tail,
                        const int32_t* gate, int l0) {
+  if (cg.coll > l0 && cg.coll < nlev - 1 && lev[cg.coll].collapsed && lev[cg.coll].CV.n > 0) {
+    const int kc = cg.coll;
+    for (int l = l0; l < kc; ++l) down_nd<ND>(s, lev[l], lev[l + 1], gate);
+    vapply_nd<ND>(s, lev[kc], gate);
+    for (int l = kc - 1; l >= l0; --l) up_te<ND, float>(s, lev[l], lev[l + 1], l == 0 ? cg.u : lev[l].e, gate);
+    return;
+  }
   int top = nlev - 1;  // levels [top, nlev) run in the tail launch
   if (tail > l0) {
     // the tail needs its levels' vectors to fit LDS: probe from the requested level down

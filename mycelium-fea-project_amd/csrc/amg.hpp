@@ -213,6 +213,30 @@ std::string build_amg_level0(const AmgPlan& plan, const Pattern& G, const AmgRan
                              const std::vector<int64_t>& node_g, const std::vector<int64_t>& elem_g,
                              const std::vector<uint8_t>& gkey, PosList& a0, std::vector<int32_t>& row0);
 
+// The compact cycle below level kc as one explicit operator (amg_collapse.cpp):
+// V_k = (2I − Ã_k) + P̃_k V_{k+1} R̂_k for k = nlev−2 … kc (V_coarsest = I),
+// through T_k = V_{k+1} R̂_k.  Per level k ≥ kc (lev[k − kc]): the patterns in
+// the plan's device labels and the index lists of the two products.
+struct AmgCollapse {
+  int kc = 0;  // 0: none
+  struct Lev {
+    int k = 0;
+    SellPat T;                   // n_{k+1} × n_k, rows in level k+1 labels
+    PosList tl;                  // per T position: (V_{k+1} position or −1 = identity, R̂ position)
+    SellPat V;                   // n_k × n_k, rows by length (vrow: V row → level row)
+    std::vector<int32_t> vrow;
+    PosList vl;                  // per V position: (P̃ position, T position)
+    std::vector<int32_t> va;     // per V position: the Ã position of the block, or −1
+    std::vector<int32_t> vdiag;  // per V position: 1 on the diagonal (+2I)
+  };
+  std::vector<Lev> lev;
+};
+// kc = the highest level ≥ max(1, min_level) whose V (and every V below it)
+// takes at most max_bytes (f32 blocks + columns) and whose products at most
+// max_pairs list items; none (kc = 0) when not even the deepest fits.
+std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t max_pairs, int min_level,
+                               AmgCollapse& out);
+
 // xsend_rows / xrecv_rows: Pattern rows of the plan's xsend / xrecv nodes
 std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
                            const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,

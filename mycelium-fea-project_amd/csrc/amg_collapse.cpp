@@ -1,0 +1,284 @@
+// amg_collapse.cpp — the compact V-cycle below level kc as ONE explicit
+// operator (amg.hpp AmgCollapse).  Host C++, once per hierarchy.
+//
+// The compact cycle (amg.hip) maps a level's smoothed iterate x_k to its
+// output e_k by  e_k = (2I − Ã_k) x_k + P̃_k e_{k+1},  x_{k+1} = R̂_k x_k, so
+// the whole cycle below level k is the linear map
+//     V_k = (2I − Ã_k) + P̃_k V_{k+1} R̂_k,     V_coarsest = I.
+// On the deep levels V_k stays sparse (C3: 15 blocks per row at level 3, 55
+// at level 2; C2: 50 at level 2) while the launches it replaces — two per
+// level, each ≈ 4.7 µs of latency for kilobytes of data — dominate the
+// iteration.  So the setup forms V_kc (through T_k = V_{k+1} R̂_k for every
+// k ≥ kc, deepest first) and the cycle applies it with one SpMV.
+//
+// Here: the patterns of T_k and V_k in the device labels of the plan and the
+// fixed-order index lists of their products (amg.hip k_amg_tv / k_amg_vv
+// evaluate them every setup: pure gathers, bitwise reproducible).  kc is the
+// highest level whose V fits the byte and product budgets.
+#include <algorithm>
+#include <numeric>
+
+#include "amg.hpp"
+
+namespace mfea {
+
+namespace {
+
+// a SELL pattern read row by row: per row its (column, position) entries in slot order
+struct Rows {
+  std::vector<int64_t> ptr{0};
+  std::vector<int32_t> col, pos;
+};
+Rows rows_of(const SellPat& S, const std::vector<int32_t>* rowmap = nullptr) {
+  const int64_t n = S.n;
+  std::vector<int64_t> cnt(n + 1, 0);
+  for (int64_t r = 0; r < n; ++r) cnt[(rowmap ? (*rowmap)[r] : r) + 1] += S.rlen[r];
+  Rows R;
+  R.ptr.assign(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) R.ptr[i + 1] = R.ptr[i] + cnt[i + 1];
+  R.col.resize(R.ptr[n]);
+  R.pos.resize(R.ptr[n]);
+  std::vector<int64_t> fill(R.ptr.begin(), R.ptr.end() - 1);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t i = rowmap ? (*rowmap)[r] : r;
+    for (int k = 0; k < S.rlen[r]; ++k) {
+      const int64_t q = S.pos(r, k);
+      R.col[fill[i]] = S.col[q];
+      R.pos[fill[i]++] = (int32_t)q;
+    }
+  }
+  return R;
+}
+
+// a product's rows before layout: per row its columns (ascending) and per
+// entry the list of (a, b) operand positions in a fixed order
+struct Prod {
+  int64_t n = 0;
+  std::vector<int64_t> ptr{0};
+  std::vector<int32_t> col;
+  std::vector<int64_t> lptr{0};  // per entry: its pairs [lptr[e], lptr[e+1])
+  std::vector<int32_t> a, b;
+  std::vector<int32_t> extra;    // per entry: Ã position (V only) or -1
+  std::vector<int8_t> diag;      // per entry: on the diagonal (V only)
+};
+
+// SELL-64 of a product with rows relabelled by rperm (new = rperm[old]);
+// epos[e] = position of entry e
+void layout_prod(const Prod& M, const std::vector<int32_t>& rperm, SellPat& S, std::vector<int32_t>& epos) {
+  const int64_t n = M.n;
+  std::vector<int32_t> inv(n);
+  for (int64_t r = 0; r < n; ++r) inv[rperm[r]] = (int32_t)r;
+  S = SellPat();
+  S.n = n;
+  const int64_t ns = (n + 63) / 64;
+  S.sptr.assign(ns + 1, 0);
+  S.rlen.assign(n, 0);
+  int64_t slots = 0;
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t r = 64 * s; r < std::min<int64_t>(n, 64 * s + 64); ++r) {
+      const int64_t len = M.ptr[inv[r] + 1] - M.ptr[inv[r]];
+      S.rlen[r] = (int32_t)len;
+      w = std::max(w, len);
+    }
+    slots += w;
+    S.sptr[s + 1] = (int32_t)slots;
+  }
+  S.col.assign(slots * 64, -1);
+  epos.assign(M.col.size(), -1);
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t o = inv[r];
+    for (int64_t e = M.ptr[o]; e < M.ptr[o + 1]; ++e) {
+      const int64_t q = S.pos(r, (int)(e - M.ptr[o]));
+      S.col[q] = M.col[e];
+      epos[e] = (int32_t)q;
+    }
+  }
+}
+
+// rows sorted by descending length inside 4096-row windows (SELL-C-σ)
+std::vector<int32_t> window_perm(const Prod& M) {
+  const int64_t n = M.n;
+  std::vector<int32_t> order(n), perm(n);
+  std::iota(order.begin(), order.end(), 0);
+  for (int64_t w0 = 0; w0 < n; w0 += 4096) {
+    const int64_t w1 = std::min(n, w0 + 4096);
+    std::stable_sort(order.begin() + w0, order.begin() + w1, [&](int32_t x, int32_t y) {
+      return M.ptr[x + 1] - M.ptr[x] > M.ptr[y + 1] - M.ptr[y];
+    });
+  }
+  for (int64_t k = 0; k < n; ++k) perm[order[k]] = (int32_t)k;
+  return perm;
+}
+
+void to_lists(const Prod& M, const std::vector<int32_t>& epos, int64_t npos, PosList& L) {
+  L = PosList();
+  L.ptr.assign(npos + 1, 0);
+  for (size_t e = 0; e < M.col.size(); ++e) L.ptr[epos[e] + 1] = (int32_t)(M.lptr[e + 1] - M.lptr[e]);
+  for (int64_t q = 0; q < npos; ++q) L.ptr[q + 1] += L.ptr[q];
+  L.a.resize(L.ptr[npos]);
+  L.b.resize(L.ptr[npos]);
+  for (size_t e = 0; e < M.col.size(); ++e) {
+    int64_t d = L.ptr[epos[e]];
+    for (int64_t t = M.lptr[e]; t < M.lptr[e + 1]; ++t, ++d) {
+      L.a[d] = M.a[t];
+      L.b[d] = M.b[t];
+    }
+  }
+}
+
+// C = X · Y over row lists (X rows: entries (col J, pos); Y rows by J): per
+// output (i, j) the pairs (X pos, Y pos) in X-entry order; columns ascending.
+// xid: X is the identity (pairs (-1, Y pos)).  mark: scratch of Y's width.
+void spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C) {
+  C = Prod();
+  C.n = n;
+  std::vector<int32_t> slot(ncols, -1);
+  std::vector<int32_t> cols;
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> acc;
+  for (int64_t i = 0; i < n; ++i) {
+    cols.clear();
+    acc.clear();
+    auto add = [&](int32_t xp, int32_t J) {
+      for (int64_t t = Y.ptr[J]; t < Y.ptr[J + 1]; ++t) {
+        const int32_t j = Y.col[t];
+        if (j < 0) continue;
+        if (slot[j] < 0) {
+          slot[j] = (int32_t)cols.size();
+          cols.push_back(j);
+          acc.emplace_back();
+        }
+        acc[slot[j]].emplace_back(xp, Y.pos[t]);
+      }
+    };
+    if (X) {
+      for (int64_t t = X->ptr[i]; t < X->ptr[i + 1]; ++t)
+        if (X->col[t] >= 0) add(X->pos[t], X->col[t]);
+    } else {
+      add(-1, (int32_t)i);
+    }
+    std::vector<int32_t> ord(cols.size());
+    std::iota(ord.begin(), ord.end(), 0);
+    std::sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cols[x] < cols[y]; });
+    for (int32_t o : ord) {
+      C.col.push_back(cols[o]);
+      for (const auto& pr : acc[o]) {
+        C.a.push_back(pr.first);
+        C.b.push_back(pr.second);
+      }
+      C.lptr.push_back((int64_t)C.a.size());
+      slot[cols[o]] = -1;
+    }
+    C.ptr.push_back((int64_t)C.col.size());
+  }
+}
+
+}  // namespace
+
+std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t max_pairs, int min_level,
+                               AmgCollapse& out) {
+  out = AmgCollapse();
+  const int nlev = (int)plan.lev.size();
+  if (nlev < 2 || plan.n_dist > 0) return "";
+  const int nd = plan.nd;
+  const int64_t bb = 4LL * nd * nd + 4;  // bytes per stored block (f32 + column)
+  // deepest first: V_{c} = I, then V_k for k = c−1, c−2, … while within budget
+  std::vector<AmgCollapse::Lev> levs;
+  Rows vnext;  // V_{k+1} row by row, in level k+1 labels (positions in its SELL layout)
+  bool have_v = false;
+  int kc = 0;
+  for (int k = nlev - 2; k >= std::max(1, min_level); --k) {
+    const AmgLevel& L = plan.lev[k];
+    if (L.PT.n != L.A.n || L.RT.n <= 0) break;  // no compact transfers on this level
+    AmgCollapse::Lev C;
+    C.k = k;
+    // T_k = V_{k+1} R̂_k (rows: level k+1, cols: level k)
+    const Rows RT = rows_of(L.RT);
+    Prod T;
+    spgemm(L.RT.n, have_v ? &vnext : nullptr, RT, L.A.n, T);
+    // V_k = (2I − Ã_k) + P̃_k T_k
+    const Rows PT = rows_of(L.PT, &L.pt_row);
+    Prod V;
+    spgemm(L.A.n, &PT, [&] {
+      Rows TR;
+      TR.ptr = T.ptr;
+      TR.col = T.col;
+      TR.pos.resize(T.col.size());
+      std::iota(TR.pos.begin(), TR.pos.end(), 0);  // T entry index; mapped to positions below
+      return TR;
+    }(), L.A.n, V);
+    // merge A_k's pattern (Ã and the diagonal 2I) into V: A ⊆ V's pattern
+    // in general, but not always (a row with no coarse coupling): add missing
+    const Rows A = rows_of(L.A);
+    {
+      Prod W;
+      W.n = V.n;
+      std::vector<int32_t> apos;
+      for (int64_t i = 0; i < V.n; ++i) {
+        // both sorted ascending in column
+        std::vector<std::pair<int32_t, int32_t>> arow;  // (col, A pos)
+        for (int64_t t = A.ptr[i]; t < A.ptr[i + 1]; ++t)
+          if (A.col[t] >= 0) arow.emplace_back(A.col[t], A.pos[t]);
+        std::sort(arow.begin(), arow.end());
+        size_t u = 0;
+        int64_t e = V.ptr[i];
+        while (e < V.ptr[i + 1] || u < arow.size()) {
+          const int32_t cv = e < V.ptr[i + 1] ? V.col[e] : INT32_MAX;
+          const int32_t ca = u < arow.size() ? arow[u].first : INT32_MAX;
+          const int32_t c = std::min(cv, ca);
+          W.col.push_back(c);
+          W.extra.push_back(ca == c ? arow[u].second : -1);
+          W.diag.push_back(c == i ? 1 : 0);
+          if (cv == c) {
+            for (int64_t t = V.lptr[e]; t < V.lptr[e + 1]; ++t) {
+              W.a.push_back(V.a[t]);
+              W.b.push_back(V.b[t]);
+            }
+            ++e;
+          }
+          if (ca == c) ++u;
+          W.lptr.push_back((int64_t)W.a.size());
+        }
+        W.ptr.push_back((int64_t)W.col.size());
+      }
+      V = std::move(W);
+    }
+    const int64_t vbytes = (int64_t)V.col.size() * bb;
+    const int64_t pairs = (int64_t)V.a.size() + (int64_t)T.a.size();
+    if (!levs.empty() && (vbytes > max_bytes || pairs > max_pairs)) break;
+    if (levs.empty() && (vbytes > max_bytes || pairs > max_pairs)) return "";  // not even the deepest fits
+    // layouts: T in level k+1 order; V by row length inside windows
+    std::vector<int32_t> idT(T.n), eT, eV;
+    std::iota(idT.begin(), idT.end(), 0);
+    layout_prod(T, idT, C.T, eT);
+    const std::vector<int32_t> vperm = window_perm(V);
+    layout_prod(V, vperm, C.V, eV);
+    C.vrow.assign(V.n, 0);
+    for (int64_t i = 0; i < V.n; ++i) C.vrow[vperm[i]] = (int32_t)i;
+    // T's pairs: (V_{k+1} position or -1, R̂ position); V's pairs: (P̃ position, T entry → position)
+    to_lists(T, eT, C.T.n_pos(), C.tl);
+    for (auto& b : V.b) b = eT[b];
+    to_lists(V, eV, C.V.n_pos(), C.vl);
+    C.va.assign(C.V.n_pos(), -1);
+    C.vdiag.assign(C.V.n_pos(), 0);
+    for (size_t e = 0; e < V.col.size(); ++e) {
+      C.va[eV[e]] = V.extra[e];
+      C.vdiag[eV[e]] = V.diag[e] ? 1 : 0;
+    }
+    // V_k row by row (level k labels, SELL positions) for the level above
+    vnext = Rows();
+    vnext.ptr = V.ptr;
+    vnext.col = V.col;
+    vnext.pos.assign(eV.begin(), eV.end());
+    have_v = true;
+    kc = k;
+    levs.push_back(std::move(C));
+  }
+  if (levs.empty()) return "";
+  std::reverse(levs.begin(), levs.end());  // lev[0] = level kc
+  out.kc = kc;
+  out.lev = std::move(levs);
+  return "";
+}
+
+}  // namespace mfea

@@ -93,6 +93,21 @@ struct AmgLevD {
   const int32_t* pt_ap = nullptr;
   const int32_t* pt_p = nullptr;
   const int32_t* rt_pt = nullptr;
+  // the compact cycle collapsed below this level (amg.hpp AmgCollapse, levels
+  // ≥ kc): T = V_{l+1} R̂ (rows: level l+1) and V (rows by length, vrow → level
+  // row), both f32 (val32), with their product lists; V.n > 0 on level kc
+  // makes the cycle apply V there instead of recursing
+  AmgMatD CT, CV;
+  const int32_t* ct_ptr = nullptr;
+  const int32_t* ct_a = nullptr;
+  const int32_t* ct_b = nullptr;
+  const int32_t* cv_row = nullptr;
+  const int32_t* cv_ptr = nullptr;
+  const int32_t* cv_a = nullptr;
+  const int32_t* cv_b = nullptr;
+  const int32_t* cv_ext = nullptr;   // Ã position of the block or −1
+  const int32_t* cv_diag = nullptr;  // 1: + 2I
+  int collapsed = 0;  // 1 on levels ≥ kc that hold CT / CV
 };
 
 // CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
@@ -119,6 +134,7 @@ struct AmgCg {
   // level of the cycle has it (compact set: unsplit levels); 0: four steps
   int cycle = 0;
   int ctail = 0;
+  int coll = 0;  // the compact cycle's collapsed level kc (0: none)
   int nt = 0;  // the SpMV w = A_0 u streams A_0 with non-temporal loads (u stays in L2)  // the compact cycle's single-workgroup LDS tail: its first level (0: none)
 };
 
@@ -151,8 +167,9 @@ constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0,
                             int stage = kSetupAll);
 // the compact cycle's operators of every level (after every level's setup:
-// R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã
-void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev);
+// R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã; then, deepest first, the
+// collapsed operators T, V of levels ≥ kc (coll > 0)
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).

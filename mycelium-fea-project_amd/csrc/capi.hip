@@ -115,6 +115,7 @@ struct Part {
   double* xh_recv = nullptr;
   // SA-AMG preconditioner (amg.hpp): symbolic plan for the active set amg_key
   AmgPlan amg;
+  AmgCollapse amg_coll;  // the compact cycle below level kc as one operator (amg_collapse.cpp)
   bool amg_ok = false;
   std::vector<uint8_t> amg_key;
   int64_t amg_gen = 0;               // bumped on every rebuild (captured graphs hold its pointers)
@@ -210,6 +211,10 @@ struct mfea_handle {
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
+  int opt_amg_collapse = -1;           // GAMG: collapse the compact cycle below the highest level
+                                      // within budget (-1), never (0), or from level ≥ k (k ≥ 1)
+  int64_t opt_amg_collapse_mb = 32;     // … budget: the collapsed operator's bytes
+  int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
                        // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
@@ -1093,6 +1098,12 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
   const int nlev = (int)pl.lev.size();
   hipStream_t s = h->stream;
   size_t ni = 0, ndd = 0, nff = 0;
+  pt.amg_coll = AmgCollapse();
+  if (!rk && h->opt_amg_cycle == 1 && h->opt_amg_collapse != 0) {
+    const std::string cerr = build_amg_collapse(pl, h->opt_amg_collapse_mb << 20, h->opt_amg_collapse_pairs,
+                                                std::max(1, h->opt_amg_collapse), pt.amg_coll);
+    if (!cerr.empty()) return fail(MFEA_EINVAL, cerr);
+  }
   int32_t* ip = nullptr;
   double* dp = nullptr;
   float* fp = nullptr;
@@ -1213,6 +1224,21 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
           d.rt_pt = I(L.rt_pt);
           d.compact = h->opt_amg_cycle;
         }
+        if (pt.amg_coll.kc > 0 && l >= pt.amg_coll.kc) {  // the collapsed operators of this level
+          const AmgCollapse::Lev& C = pt.amg_coll.lev[l - pt.amg_coll.kc];
+          d.CT = mat(C.T, false, true);
+          d.ct_ptr = I(C.tl.ptr);
+          d.ct_a = I(C.tl.a);
+          d.ct_b = I(C.tl.b);
+          d.CV = mat(C.V, false, true);
+          d.cv_row = I(C.vrow);
+          d.cv_ptr = I(C.vl.ptr);
+          d.cv_a = I(C.vl.a);
+          d.cv_b = I(C.vl.b);
+          d.cv_ext = I(C.va);
+          d.cv_diag = I(C.vdiag);
+          d.collapsed = 1;
+        }
       }
     }
     pt.amg_a0_ptr = I(a0 ? a0->ptr : pl.a0.ptr);
@@ -1223,6 +1249,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.hi = rk && nlev ? rk->hi[0] : nf;
     pt.amg_cg.w_block = h->opt_amg_w_block;
     pt.amg_cg.cycle = h->opt_amg_cycle;
+    pt.amg_cg.coll = pt.amg_coll.kc;
     pt.amg_cg.row0 = I(row0 ? *row0 : pl.row0);
     pt.amg_cg.x = D((size_t)nd * nf);
     pt.amg_cg.p = D((size_t)nd * nf);
@@ -1472,7 +1499,7 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   for (int l = 0; l < nlev; ++l)
     launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
-  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev);
+  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.cycle == 1 ? pt.amg_cg.coll : 0);
 }
 
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
@@ -2997,6 +3024,14 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
   }
+  else if (n == "amg_collapse" || n == "amg_collapse_mb" || n == "amg_collapse_pairs") {
+    if (value < -1 || (n == "amg_collapse" && value >= kAmgMaxLevels))
+      return fail(MFEA_EINVAL, n + ": out of range");
+    if (n == "amg_collapse") h->opt_amg_collapse = (int)value;
+    else if (n == "amg_collapse_mb") h->opt_amg_collapse_mb = value;
+    else h->opt_amg_collapse_pairs = value;
+    rebuild = true;
+  }
   else if (n == "amg_spatial") {
     if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_spatial: -1 (by locality), 0 or 1");
     h->opt_amg_spatial = (int)value;
@@ -3194,6 +3229,12 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
+  else if (n == "amg_collapse") *value = h->opt_amg_collapse;
+  else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;
+  else if (n == "amg_collapse_pairs") *value = h->opt_amg_collapse_pairs;
+  else if (n == "amg_collapse_level") {  // read-only: partition 0's collapsed level kc (0: none)
+    *value = h->parts.empty() ? 0 : h->parts[0]->amg_coll.kc;
+  }
   else if (n == "amg_spatial_chosen") {  // read-only: partition 0's plan is in Z-order
     *value = h->parts.empty() ? 0 : (h->parts[0]->amg.spatial ? 1 : 0);
   }

@@ -218,11 +218,65 @@ def vcycle_scaled(levels, r):
         c = 2.0 * x - At @ x
         return c + L["Pt"] @ down_up(l + 1, Rhat @ x)
 
+    if isinstance(r, tuple):  # (level k, x_k): the cycle below level k on its iterate
+        return down_up(*r)
     L0 = levels[0]
     nd = L0["dinv"].shape[1]
     s0 = 1.0 if L0["coarsest"] else L0["omega"]
     x0 = s0 * np.einsum("iab,ib->ia", L0["dinv"], r.reshape(-1, nd)).ravel()
     return down_up(0, x0)
+
+
+def scaled_blocks(levels):
+    """Per level the device's compact operators as SELL position blocks:
+    R̂ (RT positions), P̃ (PT positions, compact_transfers), Ã (A positions)."""
+    for l, L in enumerate(levels[:-1]):
+        N = levels[l + 1]
+        s_n = 1.0 if N["coarsest"] else N["omega"]
+        n, nd = L["n"], L["dinv"].shape[1]
+        D = np.linalg.inv(L["dinv"])
+        jrow, _ = pos_rows(L["RT.sptr"], L["nc"])
+        col = L["RT.col"]
+        ok = (col >= 0) & (jrow >= 0) & (L["rt_pt"] >= 0)
+        Rh = np.zeros((len(col), nd, nd))
+        PtT = np.transpose(L["PTb"][np.maximum(L["rt_pt"], 0)], (0, 2, 1))
+        Rh[ok] = (s_n / L["omega"]) * np.einsum("pab,pbc,pcd->pad", N["dinv"][np.maximum(jrow, 0)], PtT,
+                                                 D[np.maximum(col, 0)])[ok]
+        L["Rhb"] = Rh
+        arow, _ = pos_rows(L["A.sptr"], n)
+        L["Atb"] = L["omega"] * np.einsum("pab,pbc->pac", L["dinv"][np.maximum(arow, 0)], L["Ab"])
+    return levels
+
+
+def collapsed_operator(levels, C, k):
+    """V_k evaluated from the collapse plan's lists (amg.hip k_amg_tv / k_amg_vv
+    in f64): T = V_{k+1} R̂ (identity below the coarsest), V = 2I·diag − Ã + Σ P̃ T.
+    C[k]: dict of the plan arrays of level k.  Returns scipy V_k in level rows."""
+    nd = levels[0]["dinv"].shape[1]
+    vals = {}
+    for kk in sorted(C, reverse=True):
+        L, c = levels[kk], C[kk]
+        Tb = np.zeros((len(c["T.col"]), nd, nd))
+        for q in np.flatnonzero(c["T.col"] >= 0):
+            acc = np.zeros((nd, nd))
+            for t in range(c["tl.ptr"][q], c["tl.ptr"][q + 1]):
+                a, b = c["tl.a"][t], c["tl.b"][t]
+                acc = acc + (L["Rhb"][b] if a < 0 else vals[kk + 1][a] @ L["Rhb"][b])
+            Tb[q] = acc
+        Vb = np.zeros((len(c["V.col"]), nd, nd))
+        for q in np.flatnonzero(c["V.col"] >= 0):
+            acc = 2.0 * np.eye(nd) if c["vdiag"][q] else np.zeros((nd, nd))
+            if c["va"][q] >= 0:
+                acc = acc - L["Atb"][c["va"][q]]
+            for t in range(c["vl.ptr"][q], c["vl.ptr"][q + 1]):
+                acc = acc + L["PTb"][c["vl.a"][t]] @ Tb[c["vl.b"][t]]
+            Vb[q] = acc
+        vals[kk] = Vb
+    c = C[k]
+    n = levels[k]["n"]
+    Va = to_scipy(vals[k], c["V.sptr"], c["V.col"], n, n, nd).tocoo()
+    r = c["vrow"][Va.row // nd] * nd + Va.row % nd
+    return sp.csr_matrix((Va.data, (r, Va.col)), shape=Va.shape)
 
 
 def vcycle(levels, b, l=0):

@@ -36,9 +36,11 @@ def build_host_shim():
     d = os.path.join(REPO, "tests", "native")
     out = os.path.join(d, "libhostshim.so")
     srcs = [os.path.join(d, "host_shim.cpp"), os.path.join(PKG, "csrc", "symbolic.cpp"),
-            os.path.join(PKG, "csrc", "partition.cpp"), os.path.join(PKG, "csrc", "amg_symbolic.cpp"), os.path.join(PKG, "csrc", "amg_dist.cpp")]
+            os.path.join(PKG, "csrc", "partition.cpp"), os.path.join(PKG, "csrc", "amg_symbolic.cpp"), os.path.join(PKG, "csrc", "amg_dist.cpp"),
+            os.path.join(PKG, "csrc", "amg_collapse.cpp")]
     hdrs = glob.glob(os.path.join(PKG, "csrc", "*.hpp"))
-    if not os.path.exists(out) or any(os.path.getmtime(s) > os.path.getmtime(out) for s in srcs + hdrs):
+    deps = srcs + hdrs + [os.path.abspath(__file__)]
+    if not os.path.exists(out) or any(os.path.getmtime(s) > os.path.getmtime(out) for s in deps):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC",
                                "-I" + os.path.join(PKG, "csrc"), *srcs, "-o", out])
     return out

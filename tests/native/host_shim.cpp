@@ -226,6 +226,39 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   return (int64_t)v->size();
 }
 
+// the collapsed compact cycle of the last plan (amg_collapse.cpp): returns kc
+static AmgCollapse g_coll;
+int shim_amg_collapse(int64_t max_bytes, int64_t max_pairs, int min_level, char* err, int errn) {
+  std::string e = build_amg_collapse(g_amg, max_bytes, max_pairs, min_level, g_coll);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return g_coll.kc;
+}
+int64_t shim_coll_array(int k, const char* name, int32_t* out) {
+  const std::string n(name);
+  if (g_coll.kc <= 0 || k < g_coll.kc || k - g_coll.kc >= (int)g_coll.lev.size()) return -1;
+  const AmgCollapse::Lev& C = g_coll.lev[k - g_coll.kc];
+  const std::vector<int32_t>* v = nullptr;
+  if (n == "T.sptr") v = &C.T.sptr;
+  else if (n == "T.col") v = &C.T.col;
+  else if (n == "tl.ptr") v = &C.tl.ptr;
+  else if (n == "tl.a") v = &C.tl.a;
+  else if (n == "tl.b") v = &C.tl.b;
+  else if (n == "V.sptr") v = &C.V.sptr;
+  else if (n == "V.col") v = &C.V.col;
+  else if (n == "vrow") v = &C.vrow;
+  else if (n == "vl.ptr") v = &C.vl.ptr;
+  else if (n == "vl.a") v = &C.vl.a;
+  else if (n == "vl.b") v = &C.vl.b;
+  else if (n == "va") v = &C.va;
+  else if (n == "vdiag") v = &C.vdiag;
+  else return -1;
+  if (out && !v->empty()) std::memcpy(out, v->data(), v->size() * 4);
+  return (int64_t)v->size();
+}
+
 // one rank's share of the last distributed plan (amg_dist.cpp)
 static AmgRank g_rank;
 int shim_amg_rank(int rank, char* err, int errn) {

@@ -219,3 +219,41 @@ def test_spatial_labels_keep_the_hierarchy(shim):
         shim.shim_amg_layout(0)
     assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
     assert np.array_equal(out[0][2], out[1][2])
+
+
+def test_collapsed_cycle_equals_the_recursion(shim):
+    """The compact cycle below level kc as one operator (amg_collapse.cpp): V_kc
+    evaluated from the plan's product lists applies exactly the recursive
+    compact cycle from level kc (2I − Ã, R̂, P̃ of every level below)."""
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    amg_ref.compact_transfers(levels)
+    amg_ref.scaled_blocks(levels)
+    shim.shim_amg_collapse.restype = C.c_int
+    shim.shim_amg_collapse.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_char_p, C.c_int]
+    shim.shim_coll_array.restype = C.c_int64
+    shim.shim_coll_array.argtypes = [C.c_int, C.c_char_p, P]
+    err = C.create_string_buffer(256)
+    nlev = len(levels)
+    for min_level in (nlev - 2, 1):
+        kc = shim.shim_amg_collapse(1 << 40, 1 << 40, min_level, err, 256)
+        assert kc == max(1, min_level), (kc, err.value)
+        plan = {}
+        for k in range(kc, nlev - 1):
+            d = {}
+            for name in ("T.sptr", "T.col", "tl.ptr", "tl.a", "tl.b", "V.sptr", "V.col", "vrow", "vl.ptr",
+                         "vl.a", "vl.b", "va", "vdiag"):
+                m = shim.shim_coll_array(k, name.encode(), None)
+                a = np.zeros(max(m, 0), np.int32)
+                if m > 0:
+                    shim.shim_coll_array(k, name.encode(), a.ctypes.data_as(P))
+                d[name] = a
+            plan[k] = d
+        V = amg_ref.collapsed_operator(levels, plan, kc)
+        rng = np.random.default_rng(kc)
+        for _ in range(2):
+            x = rng.standard_normal(V.shape[0])
+            ref = amg_ref.vcycle_scaled(levels, (kc, x))
+            assert np.linalg.norm(V @ x - ref) <= 1e-12 * np.linalg.norm(ref), kc
+    # a budget no level fits: no collapse
+    assert shim.shim_amg_collapse(16, 1 << 40, 1, err, 256) == 0

@@ -373,3 +373,42 @@ def test_solve_after_layout_rebuild_assembles(engine):
         st = engine.solve(dy, -dy, _opts(1e-13))   # rebuilt by the option, not re-assembled by the caller
         assert st.status == 0 and st.iters > 0
         assert rel(engine.displacement(), Uref) <= 1e-10
+
+
+
+# ---------------------------------------------------------------------------
+# the collapsed compact cycle (amg_collapse: the cycle below level kc as one
+# explicit operator V_kc = (2I − Ã) + P̃ V R̂, formed every setup;
+# tests/test_amg_cpu.py pins V against the recursion): the direct solve's U
+# and the uncollapsed cycle's iteration count, for the automatic level and
+# every forced one
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mesh", ["C2_1x5", "C3_6x8", "C5_2x2", "sim135507_3d"])
+def test_collapsed_cycle_matches_direct(engine, mesh):
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    with engine.options(amg_cycle=1, amg_collapse=0):
+        xyz, e2n, top, bot = _deep_case(engine, mesh)
+        it0 = engine.solve(dy, -dy, _opts(1e-8)).iters
+        nlev = len(engine.amg_info()["rows"])
+        K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+        known, vals = fo.known_dof_map(top, bot, dy, -dy)
+        A, b, free = fo.free_system(K, known, vals)
+        Uref = fo.solve_system(K, known, vals)
+        seen = set()
+        for coll in [-1] + list(range(1, nlev - 1)):
+            engine.set_option("amg_collapse", coll)   # a rebuild: solve re-assembles
+            engine.set_option("amg_collapse_mb", 1 << 20 if coll > 0 else 32)
+            engine.set_option("amg_collapse_pairs", 1 << 40 if coll > 0 else 8000000)
+            it = engine.solve(dy, -dy, _opts(1e-8)).iters
+            kc = engine.get_option("amg_collapse_level")
+            assert kc >= 1 and (coll < 0 or kc == coll), (coll, kc)
+            seen.add(kc)
+            assert abs(it - it0) <= 1, (coll, it, it0)
+            st = engine.solve(dy, -dy, _opts(1e-13))
+            assert st.status == 0
+            U = engine.displacement()
+            assert rel(U, Uref) <= 1e-10, (mesh, coll)
+            assert np.linalg.norm(A @ U[free] - b) <= 1e-12 * np.linalg.norm(b)
+        engine.set_option("amg_collapse_mb", 32)
+        engine.set_option("amg_collapse_pairs", 8000000)
+    assert len(seen) >= 1

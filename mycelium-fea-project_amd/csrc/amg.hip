@@ -149,11 +149,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
 // P values, one thread per position (slot_wave): every slot of a row in
 // flight at once instead of one after another.
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
+__device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& P = L.P;
   int64_t q, i;
   int k;
-  if (!slot_wave(P, P.rg.p0 / 64, P.rg.p1 / 64, q, i, k)) return;
+  if (!slot_wave(P, P.rg.p0 / 64, P.rg.p1 / 64, q, i, k, blk)) return;
   if (i < P.rg.lo || i >= P.rg.hi) return;
   const int32_t J = P.col[q];
   if (J < 0) return;
@@ -176,6 +176,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
   bstore<ND>(P.val, P.npos, q, pm);
   bstore<ND>(P.val32, P.npos, q, pm);
 }
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) { pvals_body<ND>(L, xcd_block()); }
 
 // One output block per thread (every SELL position of the product; pads
 // have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
@@ -205,11 +207,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
 // P̃(i, J) = P(i, J) − ω D_i⁻¹ (A·P)(i, J) on A·P's pattern (f64, stored f32),
 // one thread per (row, slot) as k_amg_pvals
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
+__device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& T = L.PT;
   int64_t q, i;
   int k;
-  if (!slot_wave(T, 0, T.npos / 64, q, i, k) || i >= T.n || T.col[q] < 0) return;
+  if (!slot_wave(T, 0, T.npos / 64, q, i, k, blk) || i >= T.n || T.col[q] < 0) return;
   const int32_t qp = L.pt_p[q];
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
   dinv_load<ND>(L.dinv, L.pt_row[i], Di);
@@ -228,16 +230,18 @@ __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
   bstore<ND>(T.val32, 0, q, pm);
   bstore<ND>(T.val, 0, q, pm);
 }
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) { ptv_body<ND>(L, xcd_block()); }
 // R̂ = s' D'_J⁻¹ P̃ᵀ D_i / ω in RT's own SELL layout, one thread per (row J,
 // slot) as k_amg_pvals: the scalings of x = ω D⁻¹ b on both sides folded in,
 // so the down sweep maps x_l to x_{l+1} directly (D_i: A's diagonal block,
 // slot 0 of row i)
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
+__device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int64_t blk) {
   const AmgMatD& T = L.RT;
   int64_t q, J;
   int k;
-  if (!slot_wave(T, 0, T.npos / 64, q, J, k) || J >= T.n) return;
+  if (!slot_wave(T, 0, T.npos / 64, q, J, k, blk) || J >= T.n) return;
   const int32_t i = T.col[q];
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
@@ -257,13 +261,15 @@ __global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
   for (int c = 0; c < ND * ND; ++c) o[c] *= sc;
   bstore<ND>(T.val32, 0, q, o);
 }
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) { rtv_body<ND>(L, N, xcd_block()); }
 // Ã = ω D_i⁻¹ A_ij (compact cycle), one thread per (row, slot)
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
+__device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& A = L.A;
   int64_t q, i;
   int k;
-  if (!slot_wave(A, 0, A.npos / 64, q, i, k) || i >= A.n || A.col[q] < 0) return;
+  if (!slot_wave(A, 0, A.npos / 64, q, i, k, blk) || i >= A.n || A.col[q] < 0) return;
   double Di[ND * ND], m[ND * ND], o[ND * ND];
   dinv_load<ND>(L.dinv, i, Di);
   bload<ND>(A.val, 0, q, m);
@@ -275,6 +281,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
   for (int c = 0; c < ND * ND; ++c) o[c] *= om;
   bstore<ND>(A.at32, 0, q, o);
 }
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) { atv_body<ND>(L, xcd_block()); }
 
 // the collapsed cycle (amg_collapse.cpp): T = V_{l+1} R̂ (a < 0: the
 // identity, V_coarsest) and V = 2I·[diag] − Ã + Σ P̃·T, one output block per
@@ -342,9 +350,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
-  const int64_t q = L.ac_rg.p0 + xcd_block() * kBlock + threadIdx.x;
+__device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int64_t blk) {
+  const int64_t q = L.ac_rg.p0 + blk * kBlock + threadIdx.x;
   if (q >= L.ac_rg.p1 || Ac.col[q] < 0 || !pos_mine(L.ac_rg, q)) return;
   double C[ND * ND];
 #pragma unroll
@@ -352,6 +359,32 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double
   pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val, L.P.npos, L.apval, L.AP.npos, C);
   bstore<ND>(Ac.val, Ac.npos, q, C);
   bstore<ND>(Ac.val32, Ac.npos, q, C);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
+  ac_body<ND>(L, Ac, xcd_block());
+}
+
+// The compact cycle's operators fused into the Galerkin chain's launches (no
+// launch of their own, no extra dependency): blocks [0, g0) run the chain
+// kernel, the rest the compact parts whose inputs are complete by then —
+// after level l's D⁻¹: P_l values, Ã_l and R̂_{l−1} (it needs D_l⁻¹, ω_l and
+// P̃_{l−1}); after A_l·P_l: A_{l+1} and P̃_l.  Every part keeps its own
+// XCD-contiguous share (sub-ranges of one xcd_block() numbering).
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_fuse_p(AmgLevD L, AmgLevD Lp, int64_t g0, int64_t g1) {
+  const int64_t xb = xcd_block();
+  if (xb < g0) pvals_body<ND>(L, xb);
+  else if (xb < g1) atv_body<ND>(L, xb - g0);
+  else rtv_body<ND>(Lp, L, xb - g1);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, double* omega_next, int64_t g0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;
+  const int64_t xb = xcd_block();
+  if (xb < g0) ac_body<ND>(L, Ac, xb);
+  else ptv_body<ND>(L, xb - g0);
 }
 
 // ---------------------------------------------------------------------------
@@ -923,7 +956,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, co
   vcycle_entry<ND>(L0, cg, i, r);
 }
 
-template <int ND, bool FIRST, int BS, bool DIST>
+template <int ND, bool FIRST, int BS, bool DIST, int KW = 1>
 __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part,
                                                  AmgDist d) {
   // the iteration's gate is tested only before the stores (gate_open)
@@ -941,8 +974,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    if (cg.nt) sell_mac<ND, false, 1, true, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
-    else sell_mac<ND, false, 1, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
+    if (cg.nt) sell_mac<ND, false, KW, true, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
+    else sell_mac<ND, false, KW, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
     if (i < cg.lo || i >= cg.hi) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
@@ -1138,14 +1171,58 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 }
 
 template <int ND>
-static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
-  for (int l = 0; l + 1 < nlev; ++l) {
+static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l) {
+  const AmgLevD& L = lev[l];
+  if (!L.compact || L.PT.wmax <= 0) return;
+  hipLaunchKernelGGL(k_amg_ptv<ND>, slot_grid(L.PT.npos), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_rtv<ND>, slot_grid(L.RT.npos), dim3(kBlock), 0, s, L, lev[l + 1]);
+  hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
+}
+template <int ND>
+static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+  if (coll <= 0) return;
+  for (int l = nlev - 2; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
     const AmgLevD& L = lev[l];
-    if (!L.compact || L.PT.wmax <= 0) continue;
-    hipLaunchKernelGGL(k_amg_ptv<ND>, slot_grid(L.PT.npos), dim3(kBlock), 0, s, L);
-    hipLaunchKernelGGL(k_amg_rtv<ND>, slot_grid(L.RT.npos), dim3(kBlock), 0, s, L, lev[l + 1]);
-    hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
+    if (!L.collapsed) return;
+    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
+    hipLaunchKernelGGL(k_amg_tv<ND>, rows_grid(L.CT.npos), dim3(kBlock), 0, s, L, vnext);
+    hipLaunchKernelGGL(k_amg_vv<ND>, rows_grid(L.CV.npos), dim3(kBlock), 0, s, L);
   }
+}
+// the whole numeric setup of a compact-cycle hierarchy, its compact parts
+// fused into the chain's launches (k_amg_fuse_p / k_amg_fuse_ac): three
+// launches per level (D⁻¹, P values, A·P, A_{l+1}: level 0's D⁻¹ is
+// k_amg_a0's partner) instead of seven
+static int64_t slot_blocks(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
+template <int ND>
+static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+  auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
+  for (int l = 0; l < nlev; ++l) {
+    const AmgLevD& L = lev[l];
+    if (L.A.n <= 0) return;
+    const bool last = L.coarsest || l + 1 >= nlev;
+    if (l > 0)
+      hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+    const int64_t g0 = !last && L.P.wmax > 0 ? slot_blocks(L.P.rg.npos()) : 0;
+    const int64_t g1 = g0 + (compact(l) ? slot_blocks(L.A.npos) : 0);
+    const int64_t g2 = g1 + (l > 0 && compact(l - 1) ? slot_blocks(lev[l - 1].RT.npos) : 0);
+    if (g2 > 0)
+      hipLaunchKernelGGL(k_amg_fuse_p<ND>, dim3((unsigned)g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
+    if (last) break;
+    hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
+    const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
+    const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
+    hipLaunchKernelGGL(k_amg_fuse_ac<ND>, dim3((unsigned)a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
+  }
+  collapse_setup_nd<ND>(s, lev, nlev, coll);
+}
+void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
+  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll);
+  else setup_fused_nd<3>(s, lev, nlev, coll);
+}
+template <int ND>
+static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+  for (int l = 0; l + 1 < nlev; ++l) compact_level_nd<ND>(s, lev, l);
   if (coll <= 0) return;
   for (int l = nlev - 2; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
     const AmgLevD& L = lev[l];
@@ -1409,6 +1486,9 @@ static void w_bs(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgC
   if (d) {
     if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, true>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
     else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS, true>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+  } else if (cg.w_k == 2) {  // slices up to 2U wide in one round trip (wide level-0 rows)
+    if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, false, 2>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
+    else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS, false, 2>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
   } else {
     if (first) hipLaunchKernelGGL((k_amg_cg_w<ND, true, BS, false>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);
     else hipLaunchKernelGGL((k_amg_cg_w<ND, false, BS, false>), g, dim3(BS), 0, s, j, L0, cg, slots, part, dd);

@@ -200,15 +200,20 @@ __device__ __forceinline__ bool pos_mine(const RowRange& g, int64_t q) {
 // sized by the widest slice left most threads of the wide-tailed P̃ / R̂
 // layouts idle): position q = 64 t + lane, row 64 s + lane of slice
 // s = srow[t], slot k = t − sptr[s].  False past the end (wave-uniform).
+// blk: the block's index within its part of a fused grid (xcd_block() alone)
 __device__ __forceinline__ bool slot_wave(const AmgMatD& M, int64_t t0, int64_t t1, int64_t& q, int64_t& row,
-                                          int& k) {
-  const int64_t t = t0 + xcd_block() * (kBlock / 64) + (threadIdx.x >> 6);
+                                          int& k, int64_t blk) {
+  const int64_t t = t0 + blk * (kBlock / 64) + (threadIdx.x >> 6);
   if (t >= t1) return false;
   const int s = __builtin_amdgcn_readfirstlane(M.srow[t]);
   k = (int)(t - M.sptr[s]);
   row = 64 * (int64_t)s + (threadIdx.x & 63);
   q = t * 64 + (threadIdx.x & 63);
   return true;
+}
+__device__ __forceinline__ bool slot_wave(const AmgMatD& M, int64_t t0, int64_t t1, int64_t& q, int64_t& row,
+                                          int& k) {
+  return slot_wave(M, t0, t1, q, row, k, xcd_block());
 }
 
 // slot range of the wave's slice (scalar loads, wave-uniform)

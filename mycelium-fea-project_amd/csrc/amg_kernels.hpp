@@ -116,6 +116,7 @@ struct AmgCg {
   int64_t lo = 0, hi = 0;  // level-0 rows this rank iterates (one partition: [0, n))
   __host__ __device__ int64_t lo64() const { return lo & ~(int64_t)63; }
   int w_block = 0;  // w = A u kernel threads per block (0: by size)
+  int w_k = 1;      // w = A u: 2 — slices up to 2U blocks wide in one round trip (sell_mac's K)
   const int32_t* row0 = nullptr;  // level-0 row → Pattern (row-order) free row
   double* x = nullptr;
   double* p = nullptr;
@@ -170,6 +171,9 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 // R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã; then, deepest first, the
 // collapsed operators T, V of levels ≥ kc (coll > 0)
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0);
+// the levels' setup (after launch_amg_a0) and the compact operators in one
+// sequence, the compact parts fused into the Galerkin chain's launches
+void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).

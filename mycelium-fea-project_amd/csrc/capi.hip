@@ -208,6 +208,7 @@ struct mfea_handle {
   int64_t opt_amg_tail_rows = 2048;  // GAMG: levels of at most this many rows run in one workgroup
   int opt_amg_max_levels = kAmgMaxLevels;  // GAMG: hierarchy depth cap
   int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
+  int opt_amg_w_k = 0;         // GAMG: w = A u step width (0: by level 0's mean slice width, 1, 2)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
@@ -216,6 +217,7 @@ struct mfea_handle {
   int64_t opt_amg_collapse_mb = 32;     // … budget: the collapsed operator's bytes
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
+  int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
                        // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
@@ -1092,6 +1094,17 @@ int set_amg_deep(mfea_handle* h, Part& pt) {
   return 0;
 }
 
+// w = A u's step width: K = 2 (slices up to 2U blocks in one round trip of
+// column loads and gathers, more VGPRs) once level 0's mean slice width
+// passes U = 4 blocks
+static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
+  if (h->opt_amg_w_k > 0) return h->opt_amg_w_k;
+  if (pl.lev.empty() || pl.lev[0].A.sptr.size() < 2) return 1;
+  const auto& sp = pl.lev[0].A.sptr;
+  const double mean = (double)(sp.back() - sp.front()) / (double)(sp.size() - 1);
+  return mean > 4.0 ? 2 : 1;
+}
+
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
                const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
   const int nd = pl.nd, nb2 = nd * nd;
@@ -1248,6 +1261,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.lo = rk && nlev ? rk->lo[0] : 0;
     pt.amg_cg.hi = rk && nlev ? rk->hi[0] : nf;
     pt.amg_cg.w_block = h->opt_amg_w_block;
+    pt.amg_cg.w_k = amg_w_k(h, pl);
     pt.amg_cg.cycle = h->opt_amg_cycle;
     pt.amg_cg.coll = pt.amg_coll.kc;
     pt.amg_cg.row0 = I(row0 ? *row0 : pl.row0);
@@ -1497,9 +1511,14 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   hipStream_t s = h->stream;
   const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
+  if (compact && h->opt_amg_fuse_setup) {
+    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
+    return;
+  }
   for (int l = 0; l < nlev; ++l)
     launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
-  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.cycle == 1 ? pt.amg_cg.coll : 0);
+  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
 }
 
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
@@ -2999,6 +3018,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_max_levels = (int)value;
     rebuild = true;
   }
+  else if (n == "amg_w_k") {
+    if (value < 0 || value > 2) return fail(MFEA_EINVAL, "amg_w_k: 0 (auto), 1 or 2");
+    h->opt_amg_w_k = (int)value;
+    rebuild = true;
+  }
   else if (n == "amg_w_block") {
     if (value != 0 && value != 256 && value != 512 && value != 640 && value != 768 && value != 1024)
       return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 640, 768 or 1024");
@@ -3036,6 +3060,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_spatial: -1 (by locality), 0 or 1");
     h->opt_amg_spatial = (int)value;
     rebuild = true;
+  }
+  else if (n == "amg_fuse_setup") {
+    if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
+    h->opt_amg_fuse_setup = (int)value;
   }
   else if (n == "amg_nt") {
     if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_nt: -1 (by size), 0 or 1");
@@ -3222,12 +3250,14 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_ctail_rows") *value = h->opt_amg_ctail_rows;
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
   else if (n == "amg_w_block") *value = h->opt_amg_w_block;
+  else if (n == "amg_w_k") *value = h->opt_amg_w_k;
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_nt") *value = h->opt_amg_nt;
+  else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;
   else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;

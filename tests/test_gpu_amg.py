@@ -412,3 +412,22 @@ def test_collapsed_cycle_matches_direct(engine, mesh):
         engine.set_option("amg_collapse_mb", 32)
         engine.set_option("amg_collapse_pairs", 8000000)
     assert len(seen) >= 1
+
+
+@pytest.mark.parametrize("mesh", ["C2_1x5", "C3_6x8", "C5_2x2", "sim135507_3d"])
+def test_fused_setup_bitwise_equals_separate_launches(engine, mesh):
+    """The compact operators formed inside the Galerkin chain's launches
+    (k_amg_fuse_p / k_amg_fuse_ac) run the same arithmetic as their own
+    launches: U and the iteration count bit for bit, collapsed or not."""
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    for coll in (0, -1):
+        with engine.options(amg_cycle=1, amg_collapse=coll):
+            _deep_case(engine, mesh)
+            out = {}
+            for v in (0, 1):
+                engine.set_option("amg_fuse_setup", v)
+                st = engine.solve(dy, -dy, _opts(1e-10))
+                assert st.status == 0
+                out[v] = (engine.displacement(), st.iters)
+            engine.set_option("amg_fuse_setup", 1)
+        assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0]), (mesh, coll)

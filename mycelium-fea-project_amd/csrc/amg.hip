@@ -181,7 +181,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) { pvals_body<ND
 
 // One output block per thread (every SELL position of the product; pads
 // have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
-template <int ND>
+// PTV: also the compact cycle's P̃(i, J) = P(i, J) − ω D_i⁻¹ AP(i, J) — P̃ has
+// A·P's layout position for position (amg_symbolic.cpp), so it is formed from
+// the block in registers; its operands are loaded before the pair sum.
+template <int ND, bool PTV = false>
 __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
   const int64_t k = xcd_block() * kBlock + threadIdx.x;
   const int64_t qr = L.R.rg.p0 + k;
@@ -196,11 +199,28 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
   }
   const int64_t q = L.AP.rg.p0 + k;
   if (q >= L.AP.rg.p1 || L.AP.col[q] < 0 || !pos_mine(L.AP.rg, q)) return;
-  double C[ND * ND];
+  double C[ND * ND], Di[ND * ND], pm[ND * ND];
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
+  for (int c = 0; c < ND * ND; ++c) C[c] = pm[c] = 0.0;
+  if constexpr (PTV) {
+    const int64_t r = 64 * (int64_t)L.PT.srow[q >> 6] + (q & 63);  // the A·P / P̃ row
+    dinv_load<ND>(L.dinv, L.pt_row[r], Di);
+    const int32_t qp = L.pt_p[q];
+    if (qp >= 0) bload<ND>(L.P.val, 0, qp, pm);
+  }
   pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val, L.A.npos, L.P.val, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
+  if constexpr (PTV) {
+    double m[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+    mm_acc<ND>(Di, C, m);
+    const double om = amg_omega(L.omega);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);
+    bstore<ND>(L.PT.val32, 0, q, pm);
+    bstore<ND>(L.PT.val, 0, q, pm);
+  }
 }
 
 // The compact cycle's transfers (amg.hpp AmgLevel::PT), after A·P:
@@ -1209,10 +1229,16 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     if (g2 > 0)
       hipLaunchKernelGGL(k_amg_fuse_p<ND>, dim3((unsigned)g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
     if (last) break;
-    hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
-    const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
-    const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
-    hipLaunchKernelGGL(k_amg_fuse_ac<ND>, dim3((unsigned)a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
+    const dim3 gap = rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()));
+    if (compact(l) && L.PT.npos == L.AP.npos) {  // P̃ formed by the A·P kernel
+      hipLaunchKernelGGL((k_amg_ap<ND, true>), gap, dim3(kBlock), 0, s, L);
+      hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega);
+    } else {
+      hipLaunchKernelGGL(k_amg_ap<ND>, gap, dim3(kBlock), 0, s, L);
+      const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
+      const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
+      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, dim3((unsigned)a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
+    }
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);
 }

@@ -130,7 +130,10 @@ void to_lists(const Prod& M, const std::vector<int32_t>& epos, int64_t npos, Pos
 // C = X · Y over row lists (X rows: entries (col J, pos); Y rows by J): per
 // output (i, j) the pairs (X pos, Y pos) in X-entry order; columns ascending.
 // xid: X is the identity (pairs (-1, Y pos)).  mark: scratch of Y's width.
-void spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C) {
+// False (C incomplete) as soon as C holds more than max_pairs pairs or
+// max_cols entries: an over-budget level is rejected without being built.
+bool spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C,
+            int64_t max_pairs = INT64_MAX, int64_t max_cols = INT64_MAX) {
   C = Prod();
   C.n = n;
   std::vector<int32_t> slot(ncols, -1);
@@ -170,7 +173,9 @@ void spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C) {
       slot[cols[o]] = -1;
     }
     C.ptr.push_back((int64_t)C.col.size());
+    if ((int64_t)C.a.size() > max_pairs || (int64_t)C.col.size() > max_cols) return false;
   }
+  return true;
 }
 
 }  // namespace
@@ -195,18 +200,19 @@ std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t m
     // T_k = V_{k+1} R̂_k (rows: level k+1, cols: level k)
     const Rows RT = rows_of(L.RT);
     Prod T;
-    spgemm(L.RT.n, have_v ? &vnext : nullptr, RT, L.A.n, T);
+    if (!spgemm(L.RT.n, have_v ? &vnext : nullptr, RT, L.A.n, T, max_pairs)) break;
     // V_k = (2I − Ã_k) + P̃_k T_k
     const Rows PT = rows_of(L.PT, &L.pt_row);
     Prod V;
-    spgemm(L.A.n, &PT, [&] {
+    const bool fits = spgemm(L.A.n, &PT, [&] {
       Rows TR;
       TR.ptr = T.ptr;
       TR.col = T.col;
       TR.pos.resize(T.col.size());
       std::iota(TR.pos.begin(), TR.pos.end(), 0);  // T entry index; mapped to positions below
       return TR;
-    }(), L.A.n, V);
+    }(), L.A.n, V, max_pairs - (int64_t)T.a.size(), max_bytes / bb);
+    if (!fits) break;  // over budget (V's merged pattern only grows)
     // merge A_k's pattern (Ã and the diagonal 2I) into V: A ⊆ V's pattern
     // in general, but not always (a row with no coarse coupling): add missing
     const Rows A = rows_of(L.A);

@@ -79,10 +79,13 @@ def amg_iteration_bytes(ai, compact=None):
       restrict pb·(B+4) + V·n + (2V + B)·n'        (Pᵀ, t in; b', x' out, D⁻¹')
       prolong  pb·(B+4) + 2V·n + V·n'              (P, x in/out, e' in)
       post     nb·(BA+4) + (2V + B + Vb)·n         (A, x, D⁻¹, b in; e out)
-    The compact cycle (amg_cycle 1; tb blocks of P̃_l = R̃_ᵀ per level):
-      down     tb·(B+4) + nb·(BA+4) + (Vb + 2V + B)·n + (B + 2V)·n'
-               (R̃, A, b once, x, D⁻¹ in; c out; D⁻¹' in, b', x' out)
-      up       tb·(B+4) + 2V·n + V·n'                (P̃, c in, e out; e' in)
+    The compact cycle (amg_cycle 1; tb blocks of P̃_l = of R̂_l per level; its
+    sweeps read the level's f32 iterate x alone and Ã = ω D⁻¹ A as full f32
+    blocks, level 0 included):
+      down     tb·(B+4) + nb·(B+4) + 2V·n + V·n'   (R̂, Ã, x in; c out, x' out)
+      up       tb·(B+4) + 2V·n + V·n'              (P̃, c in, e out; e' in)
+    collapsed below level kc (collapse_level > 0; vb blocks of V): the levels
+    ≥ kc are one sweep  vapply  vb·(B+4) + 2V·n_kc  (V, x in; e out).
     CG: update (9·V8 + V + B + V)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀ out);
         w      nb0·(Bs8+4) + (2·V8 + V)·n0         (A_0, r, u in; w out).
     """
@@ -92,14 +95,18 @@ def amg_iteration_bytes(ai, compact=None):
     rows, blocks, pbl = ai["rows"], ai["blocks"], ai["pblocks"]
     if compact is None:
         compact = ai.get("cycle", 0) == 1
+    kc = ai.get("collapse_level", 0) if compact else 0
     b = 0
     for l in range(ai["levels"] - 1):
         n, nn = rows[l], rows[l + 1]
         Vb = V8 if l == 0 else V
         BA = Bs if l == 0 else B
         if compact:
+            if kc and l == kc:
+                b += ai["collapse_blocks"] * (B + 4) + 2 * V * n
+                break
             tb = ai["ptblocks"][l]
-            b += tb * (B + 4) + blocks[l] * (BA + 4) + (Vb + 2 * V + B) * n + (B + 2 * V) * nn
+            b += tb * (B + 4) + blocks[l] * (B + 4) + 2 * V * n + V * nn
             b += tb * (B + 4) + 2 * V * n + V * nn
             continue
         b += blocks[l] * (BA + 4) + (2 * V + Vb) * n
@@ -415,8 +422,9 @@ def main():
         iter_bytes = amg_iteration_bytes(ai)
         nl = ai["levels"]
         if ai.get("cycle", 0) == 1:  # compact cycle: two sweeps per level
-            launches = 2 + 2 * (nl - 1)
-            form = "compact"
+            kc = ai.get("collapse_level", 0)
+            launches = 2 + (2 * kc + 1 if kc else 2 * (nl - 1))
+            form = f"compact, collapsed below level {kc}" if kc else "compact"
         else:
             # levels from the first one of ≤ 2048 rows (above the coarsest) run
             # in one single-workgroup launch (the engine's default amg_tail_rows)

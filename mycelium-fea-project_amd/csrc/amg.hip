@@ -1332,6 +1332,7 @@ int amg_down_lanes(const AmgLevD& L) {
   if (L.rlanes > 0) return L.rlanes;
   const int64_t rows = ((L.RT.n + 63) / 64) * 64;
   const double mean_w = rows > 0 ? (double)L.RT.npos / (double)rows : 0.0;
+  // (16 lanes past a mean width of 20 measured slower: C5 iteration 854 vs 751 µs)
   return mean_w > 6.0 ? 8 : lanes_for(L.RT, 0, 2.5, 5.0);
 }
 int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, 0, 3.5, 8.0); }
@@ -1340,7 +1341,8 @@ static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int
   const int S = amg_down_lanes(L);
   const int64_t gc = rows_grid(S * L.RT.n).x;
   const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
-  if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);

@@ -16,6 +16,7 @@
 // evaluate them every setup: pure gathers, bitwise reproducible).  kc is the
 // highest level whose V fits the byte and product budgets.
 #include <algorithm>
+#include <array>
 #include <numeric>
 
 #include "amg.hpp"
@@ -132,27 +133,18 @@ void to_lists(const Prod& M, const std::vector<int32_t>& epos, int64_t npos, Pos
 // xid: X is the identity (pairs (-1, Y pos)).  mark: scratch of Y's width.
 // False (C incomplete) as soon as C holds more than max_pairs pairs or
 // max_cols entries: an over-budget level is rejected without being built.
-bool spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C,
+bool spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t /*ncols*/, Prod& C,
             int64_t max_pairs = INT64_MAX, int64_t max_cols = INT64_MAX) {
   C = Prod();
   C.n = n;
-  std::vector<int32_t> slot(ncols, -1);
-  std::vector<int32_t> cols;
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> acc;
+  // a row's products as (column, X pos, Y pos) in X-entry order, then a
+  // stable sort by column: each output's pairs keep that order
+  std::vector<std::array<int32_t, 3>> tr;
   for (int64_t i = 0; i < n; ++i) {
-    cols.clear();
-    acc.clear();
+    tr.clear();
     auto add = [&](int32_t xp, int32_t J) {
-      for (int64_t t = Y.ptr[J]; t < Y.ptr[J + 1]; ++t) {
-        const int32_t j = Y.col[t];
-        if (j < 0) continue;
-        if (slot[j] < 0) {
-          slot[j] = (int32_t)cols.size();
-          cols.push_back(j);
-          acc.emplace_back();
-        }
-        acc[slot[j]].emplace_back(xp, Y.pos[t]);
-      }
+      for (int64_t t = Y.ptr[J]; t < Y.ptr[J + 1]; ++t)
+        if (Y.col[t] >= 0) tr.push_back({Y.col[t], xp, Y.pos[t]});
     };
     if (X) {
       for (int64_t t = X->ptr[i]; t < X->ptr[i + 1]; ++t)
@@ -160,17 +152,16 @@ bool spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t ncols, Prod& C,
     } else {
       add(-1, (int32_t)i);
     }
-    std::vector<int32_t> ord(cols.size());
-    std::iota(ord.begin(), ord.end(), 0);
-    std::sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cols[x] < cols[y]; });
-    for (int32_t o : ord) {
-      C.col.push_back(cols[o]);
-      for (const auto& pr : acc[o]) {
-        C.a.push_back(pr.first);
-        C.b.push_back(pr.second);
+    std::stable_sort(tr.begin(), tr.end(),
+                     [](const std::array<int32_t, 3>& x, const std::array<int32_t, 3>& y) { return x[0] < y[0]; });
+    for (size_t k = 0; k < tr.size();) {
+      const int32_t j = tr[k][0];
+      C.col.push_back(j);
+      for (; k < tr.size() && tr[k][0] == j; ++k) {
+        C.a.push_back(tr[k][1]);
+        C.b.push_back(tr[k][2]);
       }
       C.lptr.push_back((int64_t)C.a.size());
-      slot[cols[o]] = -1;
     }
     C.ptr.push_back((int64_t)C.col.size());
     if ((int64_t)C.a.size() > max_pairs || (int64_t)C.col.size() > max_cols) return false;

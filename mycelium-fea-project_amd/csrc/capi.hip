@@ -1105,6 +1105,12 @@ static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
   return mean > 4.0 ? 2 : 1;
 }
 
+// the collapsed cycle's lowest level when chosen automatically: level 1's V
+// is dense-ish on small networks (the reference network: 80 blocks per row,
+// 0.3 M product pairs, a few ms of host build per rebuild) for one saved
+// launch pair; level 2 is what C2 / C3 choose anyway
+constexpr int kAmgCollapseAutoLevel = 2;
+
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
                const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
   const int nd = pl.nd, nb2 = nd * nd;
@@ -1114,7 +1120,8 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
   pt.amg_coll = AmgCollapse();
   if (!rk && h->opt_amg_cycle == 1 && h->opt_amg_collapse != 0) {
     const std::string cerr = build_amg_collapse(pl, h->opt_amg_collapse_mb << 20, h->opt_amg_collapse_pairs,
-                                                std::max(1, h->opt_amg_collapse), pt.amg_coll);
+                                                h->opt_amg_collapse < 0 ? kAmgCollapseAutoLevel : std::max(1, h->opt_amg_collapse),
+                                                pt.amg_coll);
     if (!cerr.empty()) return fail(MFEA_EINVAL, cerr);
   }
   int32_t* ip = nullptr;
@@ -3030,8 +3037,8 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
   }
   else if (n == "amg_restrict_lanes") {
-    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-      return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2, 4 or 8");
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+      return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2, 4, 8 or 16 (16: the compact down sweep)");
     h->opt_amg_rlanes = (int)value;
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.rlanes = (int)value;
@@ -3264,6 +3271,12 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_collapse_pairs") *value = h->opt_amg_collapse_pairs;
   else if (n == "amg_collapse_level") {  // read-only: partition 0's collapsed level kc (0: none)
     *value = h->parts.empty() ? 0 : h->parts[0]->amg_coll.kc;
+  }
+  else if (n == "amg_collapse_blocks") {  // read-only: stored blocks of the collapsed V at kc
+    int64_t nb = 0;
+    if (!h->parts.empty() && h->parts[0]->amg_coll.kc > 0)
+      for (int32_t c : h->parts[0]->amg_coll.lev[0].V.col) nb += c >= 0;
+    *value = nb;
   }
   else if (n == "amg_spatial_chosen") {  // read-only: partition 0's plan is in Z-order
     *value = h->parts.empty() ? 0 : (h->parts[0]->amg.spatial ? 1 : 0);

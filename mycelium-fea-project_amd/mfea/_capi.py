@@ -471,7 +471,9 @@ class Engine:
         return {"levels": n, "rows": rows[:n].tolist(), "blocks": blocks[:n].tolist(),
                 "pblocks": pblocks[:n].tolist(), "ptblocks": ptblocks[:n].tolist(),
                 "pair_items": items.value, "nd": nd.value, "n_dist": ndist.value,
-                "cycle": self.get_option("amg_cycle")}
+                "cycle": self.get_option("amg_cycle"),
+                "collapse_level": self.get_option("amg_collapse_level"),
+                "collapse_blocks": self.get_option("amg_collapse_blocks")}
 
     def amg_vcycle(self, r):
         """mfea_debug_amg_vcycle: one GAMG V-cycle u = M r (n_nodes × ND, original

@@ -49,14 +49,26 @@ def test_spmv_bytes_are_the_w_kernels_share(bench):
 
 
 def test_amg_iteration_bytes_compact_by_hand(bench):
-    """The compact cycle (two sweeps per level with P̃ / R̃ of tb blocks)."""
+    """The compact cycle (two sweeps per level on the f32 iterate x, with P̃ /
+    R̂ of tb blocks and Ã as full f32 blocks), and the cycle collapsed below
+    level kc (one sweep of V's vb blocks there)."""
     n, nn, nb, tb = 1000, 300, 4000, 2500
     ai = {"nd": 2, "levels": 2, "rows": [n, nn], "blocks": [nb, nn], "pblocks": [1800, 0],
           "ptblocks": [tb, 0], "cycle": 1}
     B, V, V8, Bs, Bs8 = 16, 8, 16, 12, 24
-    down = tb * (B + 4) + nb * (Bs + 4) + (V8 + 2 * V + B) * n + (B + 2 * V) * nn
+    down = tb * (B + 4) + nb * (B + 4) + 2 * V * n + V * nn
     up = tb * (B + 4) + 2 * V * n + V * nn
     update = (9 * V8 + V + B + V) * n
     w = nb * (Bs8 + 4) + (2 * V8 + V) * n
     assert bench.amg_iteration_bytes(ai) == down + up + update + w
     assert bench.amg_iteration_bytes(ai, compact=False) == bench.amg_iteration_bytes(dict(ai, cycle=0))
+    # three levels collapsed below level 1: level 0's sweeps, then V at level 1
+    n2, nb1, tb1, vb = 40, 1500, 900, 2700
+    ai3 = {"nd": 2, "levels": 3, "rows": [n, nn, n2], "blocks": [nb, nb1, n2], "pblocks": [1800, 600, 0],
+           "ptblocks": [tb, tb1, 0], "cycle": 1, "collapse_level": 1, "collapse_blocks": vb}
+    vapply = vb * (B + 4) + 2 * V * nn
+    assert bench.amg_iteration_bytes(ai3) == down + up + vapply + update + w
+    # not collapsed: level 1's two sweeps instead
+    down1 = tb1 * (B + 4) + nb1 * (B + 4) + 2 * V * nn + V * n2
+    up1 = tb1 * (B + 4) + 2 * V * nn + V * n2
+    assert bench.amg_iteration_bytes(dict(ai3, collapse_level=0)) == down + up + down1 + up1 + update + w

@@ -180,7 +180,7 @@ def _variant_solves(engine, option, values, nx=1, ny=5):
     return out, fo.solve_system(K, known, vals)
 
 
-@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8]), ("amg_op_lanes", [1, 2, 4])])
+@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8, 16]), ("amg_op_lanes", [1, 2, 4])])
 def test_vcycle_lane_splits_match_direct(engine, option, values):
     out, Uref = _variant_solves(engine, option, values)
     for v, (U, _) in out.items():

@@ -184,6 +184,10 @@ struct mfea_handle {
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipGraphExec_t graph_big = nullptr;  // GAMG: the planned batch's long chunks
   int graph_big_chunk = 0, graph_big_ell = -1;
+  // GAMG: the numeric setup's launches (≈ 30) as one graph, keyed by a hash
+  // of every argument they take (the level views, the level-0 operator, reg)
+  hipGraphExec_t graph_setup = nullptr;
+  uint64_t graph_setup_key = 0;
   hipEvent_t ev[6] = {};
   hipEvent_t ev_setup = nullptr;
   bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
@@ -1528,6 +1532,46 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
 }
 
+uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) k = (k ^ b[i]) * 1099511628211ULL;
+  return k;
+}
+
+// The numeric setup replayed as one captured graph (single partition): the
+// eager launches cost the host ≈ 5–8 µs each (kernel arguments of 1.5–3 KB),
+// more than the GPU spends on the deep levels' kernels; recaptured whenever
+// anything the launches read changes (the key hashes all of it)
+int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
+  hipStream_t s = h->stream;
+  uint64_t k = 1469598103934665603ULL;
+  k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
+  const SellOp op = sell_op(pt);
+  k = fnv1a(k, &op, sizeof op);
+  const void* ptrs[3] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a};
+  k = fnv1a(k, ptrs, sizeof ptrs);
+  const int ints[4] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll};
+  k = fnv1a(k, ints, sizeof ints);
+  k = fnv1a(k, &reg, sizeof reg);
+  if (!h->graph_setup || h->graph_setup_key != k) {
+    if (h->graph_setup) {
+      HIPC(hipStreamSynchronize(s));  // no replay of the old graph in flight
+      (void)hipGraphExecDestroy(h->graph_setup);
+      h->graph_setup = nullptr;
+    }
+    hipGraph_t g;
+    HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    enqueue_amg_setup(h, pt, reg);
+    HIPC(hipStreamEndCapture(s, &g));
+    const hipError_t e = hipGraphInstantiate(&h->graph_setup, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIPC(e);
+    h->graph_setup_key = k;
+  }
+  HIPC(hipGraphLaunch(h->graph_setup, s));
+  return 0;
+}
+
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
   Part& pt = part0(h);
@@ -1545,7 +1589,8 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
   HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
   HIPC(hipEventRecord(h->ev[2], s));
-  enqueue_amg_setup(h, pt, o->reg);
+  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg));
+  else enqueue_amg_setup(h, pt, o->reg);
   HIPC(hipEventRecord(h->ev_setup, s));
   h->ev_setup_used = true;
   const AmgLevD& L0 = pt.amg_lev[0];
@@ -2432,6 +2477,7 @@ int mfea_destroy(mfea_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   destroy_graph(h);
+  if (h->graph_setup) (void)hipGraphExecDestroy(h->graph_setup);
   h->parts.clear();
   if (h->comm) (void)ncclCommDestroy(h->comm);
   for (auto& ev : h->ev)

@@ -72,11 +72,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const 
 // Block-Jacobi inverse, Gershgorin bound per block.  L0: level 0, whose
 // diagonal block K_ii + reg·I (Pattern row row0[i]) is formed and stored here.
 template <int ND, bool L0>
-__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
-                                                     double reg) {
-  __shared__ double red[kBlock / 64];
+__device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, const int32_t* __restrict__ row0,
+                                           double reg, int64_t i) {
   const AmgMatD& A = L.A;
-  const int64_t i = A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
   double g = 0.0;
   if (i - (threadIdx.x & 63) < A.rg.hi) {
     int64_t base;
@@ -129,6 +127,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
       for (int a = 0; a < ND; ++a) g = fmax(g, rs[a]);
     }
   }
+  return g;
+}
+template <int ND, bool L0>
+__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
+                                                     double reg) {
+  __shared__ double red[kBlock / 64];
+  double g = dinv_row<ND, L0>(L, sop, row0, reg, L.A.rg.lo64() + xcd_block() * kBlock + threadIdx.x);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
@@ -184,9 +189,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) { pvals_body<ND
 // PTV: also the compact cycle's P̃(i, J) = P(i, J) − ω D_i⁻¹ AP(i, J) — P̃ has
 // A·P's layout position for position (amg_symbolic.cpp), so it is formed from
 // the block in registers; its operands are loaded before the pair sum.
-template <int ND, bool PTV = false>
-__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
-  const int64_t k = xcd_block() * kBlock + threadIdx.x;
+template <int ND, bool PTV>
+__device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
+  const int64_t k = blk * kBlock + threadIdx.x;
   const int64_t qr = L.R.rg.p0 + k;
   if (qr < L.R.rg.p1 && L.R.col[qr] >= 0 && pos_mine(L.R.rg, qr)) {  // R = Pᵀ (f32) in R's own SELL layout
     double p[ND * ND], t[ND * ND];
@@ -222,6 +227,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
     bstore<ND>(L.PT.val, 0, q, pm);
   }
 }
+template <int ND, bool PTV = false>
+__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) { ap_body<ND, PTV>(L, xcd_block()); }
 
 // The compact cycle's transfers (amg.hpp AmgLevel::PT), after A·P:
 // P̃(i, J) = P(i, J) − ω D_i⁻¹ (A·P)(i, J) on A·P's pattern (f64, stored f32),
@@ -320,8 +327,8 @@ __device__ __forceinline__ void fmm_acc(const float* A, const float* B, float* C
     }
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext) {
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
+__device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restrict__ vnext, int64_t blk) {
+  const int64_t q = blk * kBlock + threadIdx.x;
   if (q >= L.CT.npos || L.CT.col[q] < 0) return;
   float C[ND * ND];
 #pragma unroll
@@ -342,8 +349,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __res
   bstore<ND>(L.CT.val32, 0, q, C);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
-  const int64_t q = xcd_block() * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext) {
+  tv_body<ND>(L, vnext, xcd_block());
+}
+template <int ND>
+__device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
+  const int64_t q = blk * kBlock + threadIdx.x;
   if (q >= L.CV.npos || L.CV.col[q] < 0) return;
   float C[ND * ND];
   const int32_t ea = L.cv_ext[q];
@@ -367,6 +378,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
   }
   bstore<ND>(L.CV.val32, 0, q, C);
 }
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) { vv_body<ND>(L, xcd_block()); }
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
@@ -405,6 +418,76 @@ __global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, d
   const int64_t xb = xcd_block();
   if (xb < g0) ac_body<ND>(L, Ac, xb);
   else ptv_body<ND>(L, xb - g0);
+}
+
+// The setup of the small levels [l0, nlev) in ONE workgroup (levels of at
+// most a few thousand rows: a launch there is ≈ 5–10 µs of latency for
+// ≈ 1 µs of work).  Each phase runs the same bodies as the launches above,
+// over the same virtual 256-thread blocks, kTailBS / kBlock at a time, the
+// phases separated by workgroup barriers; D⁻¹'s bound is reduced in LDS and
+// stored (no atomics).  Then the collapse products of the levels ≥ l0.
+// lev: the device copy of the level views (Part::amg_levd).
+constexpr int kSetupTailBS = 1024;
+__device__ __forceinline__ int64_t nslot_blk(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
+__device__ __forceinline__ int64_t nrow_blk(int64_t n) { return (n + kBlock - 1) / kBlock; }
+template <int ND>
+__global__ __launch_bounds__(kSetupTailBS) void k_amg_setup_tail(const AmgLevD* __restrict__ lev, int l0, int nlev,
+                                                                 int coll) {
+  __shared__ double red[kSetupTailBS / 64];
+  constexpr int64_t VB = kSetupTailBS / kBlock;
+  auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
+  for (int l = l0; l < nlev; ++l) {
+    const AmgLevD& L = lev[l];
+    const bool last = L.coarsest || l + 1 >= nlev;
+    {  // D⁻¹ and the Gershgorin bound of level l
+      double g = 0.0;
+      for (int64_t r0 = 0; r0 < L.A.n; r0 += kSetupTailBS)
+        g = fmax(g, dinv_row<ND, false>(L, SellOp{}, nullptr, 0.0, r0 + threadIdx.x));
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double m = red[0];
+        for (int k = 1; k < kSetupTailBS / 64; ++k) m = fmax(m, red[k]);
+        L.omega[1] = m;
+      }
+      __syncthreads();
+    }
+    // P_l values, Ã_l, R̂_{l−1}
+    if (!last && L.P.wmax > 0)
+      for (int64_t vb = 0, nb = nslot_blk(L.P.rg.p1 - L.P.rg.p0); vb < nb; vb += VB) pvals_body<ND>(L, vb);
+    if (compact(l))
+      for (int64_t vb = 0, nb = nslot_blk(L.A.npos); vb < nb; vb += VB) atv_body<ND>(L, vb);
+    if (l > 0 && compact(l - 1))
+      for (int64_t vb = 0, nb = nslot_blk(lev[l - 1].RT.npos); vb < nb; vb += VB) rtv_body<ND>(lev[l - 1], L, vb);
+    __syncthreads();
+    if (last) break;
+    // A_l·P_l (with P̃_l when it shares A·P's layout), then A_{l+1} (and P̃_l otherwise)
+    const bool ptv = compact(l) && L.PT.npos == L.AP.npos;
+    {
+      const int64_t nb = nrow_blk(max(L.AP.rg.p1 - L.AP.rg.p0, L.R.rg.p1 - L.R.rg.p0));
+      for (int64_t vb = 0; vb < nb; vb += VB) {
+        if (ptv) ap_body<ND, true>(L, vb);
+        else ap_body<ND, false>(L, vb);
+      }
+    }
+    __syncthreads();
+    for (int64_t vb = 0, nb = nrow_blk(L.ac_rg.p1 - L.ac_rg.p0); vb < nb; vb += VB) ac_body<ND>(L, lev[l + 1].A, vb);
+    if (compact(l) && !ptv)
+      for (int64_t vb = 0, nb = nslot_blk(L.PT.npos); vb < nb; vb += VB) ptv_body<ND>(L, vb);
+    __syncthreads();
+  }
+  if (coll <= 0) return;
+  for (int l = nlev - 2; l >= max(coll, l0); --l) {  // deepest first: T_l needs V_{l+1}
+    const AmgLevD& L = lev[l];
+    if (!L.collapsed) return;
+    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
+    for (int64_t vb = 0, nb = nrow_blk(L.CT.npos); vb < nb; vb += VB) tv_body<ND>(L, vnext, vb);
+    __syncthreads();
+    for (int64_t vb = 0, nb = nrow_blk(L.CV.npos); vb < nb; vb += VB) vv_body<ND>(L, vb);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1199,9 +1282,9 @@ static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l) {
   hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
 }
 template <int ND>
-static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, int below = 1 << 30) {
   if (coll <= 0) return;
-  for (int l = nlev - 2; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
+  for (int l = std::min(nlev - 2, below - 1); l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
     const AmgLevD& L = lev[l];
     if (!L.collapsed) return;
     const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
@@ -1215,11 +1298,16 @@ static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int c
 // k_amg_a0's partner) instead of seven
 static int64_t slot_blocks(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
 template <int ND>
-static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, const AmgLevD* levd, int stail) {
   auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
   for (int l = 0; l < nlev; ++l) {
     const AmgLevD& L = lev[l];
     if (L.A.n <= 0) return;
+    if (l > 0 && l == stail && levd) {  // the small levels (and their collapse products) in one workgroup
+      hipLaunchKernelGGL(k_amg_setup_tail<ND>, dim3(1), dim3(kSetupTailBS), 0, s, levd, l, nlev, coll);
+      collapse_setup_nd<ND>(s, lev, nlev, coll, stail);
+      return;
+    }
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0)
       hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
@@ -1242,9 +1330,10 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);
 }
-void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
-  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll);
-  else setup_fused_nd<3>(s, lev, nlev, coll);
+void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll, const AmgLevD* levd,
+                            int stail) {
+  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll, levd, stail);
+  else setup_fused_nd<3>(s, lev, nlev, coll, levd, stail);
 }
 template <int ND>
 static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {

@@ -124,6 +124,8 @@ struct Part {
   DevBuf<double> amg_d;              // every f64 value / vector array, carved
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
+  DevBuf<AmgLevD> amg_levd;          // … and their device copy (the setup tail reads it)
+  int amg_stail = 0;                 // first level of the one-workgroup setup tail (0: none)
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
   int amg_first = 1;                 // first level the tail / the deep launch may start at (not split)
   DevBuf<unsigned> amg_deep_bar;     // the deep launch's barrier words (amg_deep.hip)
@@ -221,6 +223,7 @@ struct mfea_handle {
   int64_t opt_amg_collapse_mb = 32;     // … budget: the collapsed operator's bytes
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
+  int64_t opt_amg_stail_rows = 0;  // GAMG setup: levels of at most this many rows in one workgroup (0: off; measured slower)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
                        // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
@@ -1297,6 +1300,17 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
   }
   RC(set_amg_deep(h, pt));
   set_amg_nt(h, pt);
+  // the numeric setup's one-workgroup tail: the compact cycle's levels of at
+  // most amg_stail_rows rows (one partition's hierarchy only)
+  pt.amg_stail = 0;
+  if (!rk && h->opt_amg_stail_rows > 0)
+    for (int l = 1; l < nlev; ++l)
+      if (pl.lev[l].A.n <= h->opt_amg_stail_rows) {
+        pt.amg_stail = l;
+        break;
+      }
+  HIPC(pt.amg_levd.alloc(std::max(nlev, 1)));
+  HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -1524,7 +1538,7 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
   if (compact && h->opt_amg_fuse_setup) {
-    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
+    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll, pt.amg_levd.ptr, pt.amg_stail);
     return;
   }
   for (int l = 0; l < nlev; ++l)
@@ -1548,9 +1562,9 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
   const SellOp op = sell_op(pt);
   k = fnv1a(k, &op, sizeof op);
-  const void* ptrs[3] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a};
+  const void* ptrs[4] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, pt.amg_levd.ptr};
   k = fnv1a(k, ptrs, sizeof ptrs);
-  const int ints[4] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll};
+  const int ints[5] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll, pt.amg_stail};
   k = fnv1a(k, ints, sizeof ints);
   k = fnv1a(k, &reg, sizeof reg);
   if (!h->graph_setup || h->graph_setup_key != k) {
@@ -3114,6 +3128,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_spatial = (int)value;
     rebuild = true;
   }
+  else if (n == "amg_stail_rows") {
+    if (value < 0) return fail(MFEA_EINVAL, "amg_stail_rows: >= 0 (0: no one-workgroup setup tail)");
+    h->opt_amg_stail_rows = value;
+    rebuild = true;
+  }
   else if (n == "amg_fuse_setup") {
     if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
     h->opt_amg_fuse_setup = (int)value;
@@ -3135,6 +3154,9 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       pp->amg_cg.cycle = (int)value;
       for (auto& L : pp->amg_lev)
         if (L.PT.n > 0) L.compact = (int)value;
+      if (!pp->amg_lev.empty() && pp->amg_levd.n >= pp->amg_lev.size())
+        HIPC(hipMemcpy(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
+                       hipMemcpyHostToDevice));
     }
   }
   else if (n == "amg_deep" || n == "amg_deep_rows" || n == "amg_deep_wgs") {
@@ -3311,6 +3333,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
+  else if (n == "amg_stail_rows") *value = h->opt_amg_stail_rows;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;
   else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;

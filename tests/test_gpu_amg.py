@@ -431,3 +431,20 @@ def test_fused_setup_bitwise_equals_separate_launches(engine, mesh):
                 out[v] = (engine.displacement(), st.iters)
             engine.set_option("amg_fuse_setup", 1)
         assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0]), (mesh, coll)
+
+
+@pytest.mark.parametrize("mesh", ["C2_1x5", "C3_6x8", "C5_2x2", "sim135507_3d"])
+def test_setup_tail_bitwise_equals_launches(engine, mesh):
+    """The small levels' numeric setup in one workgroup (k_amg_setup_tail)
+    runs the launches' bodies over the same virtual blocks: U and the
+    iteration count bit for bit against the per-level launches."""
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    out = {}
+    for rows in (0, 2048, 1 << 20):
+        with engine.options(amg_cycle=1, amg_stail_rows=rows):
+            _deep_case(engine, mesh)
+            st = engine.solve(dy, -dy, _opts(1e-10))
+            assert st.status == 0
+            out[rows] = (engine.displacement(), st.iters)
+    for rows in (2048, 1 << 20):
+        assert out[rows][1] == out[0][1] and np.array_equal(out[rows][0], out[0][0]), (mesh, rows)

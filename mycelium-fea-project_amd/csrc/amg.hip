@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 // Down: blocks [0, gc) form the next level's x_{l+1} = R̂ x_l (S lanes per
 // coarse row), blocks from gc on the smoothed part c_l = 2 x_l − Ã x_l
 // (= x + ω D⁻¹ (b − A x)), kept in t_l.  Both read only x_l.
-template <int ND, int S>
+template <int ND, int S, int KF = 2>
 __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64_t gc, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t xb = xcd_block();
@@ -700,8 +700,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     vload<ND>(L.x, ii, x);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = x[a] + x[a];
-    if (L.nt) sell_mac<ND, true, 2, false, true>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
-    else sell_mac<ND, true, 2>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    if (L.nt) sell_mac<ND, true, KF, false, true>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    else sell_mac<ND, true, KF>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
     if (i < n && run) vstore<ND>(L.t, i, y);
   }
 }
@@ -1424,12 +1424,25 @@ int amg_down_lanes(const AmgLevD& L) {
   // (16 lanes past a mean width of 20 measured slower: C5 iteration 854 vs 751 µs)
   return mean_w > 6.0 ? 8 : lanes_for(L.RT, 0, 2.5, 5.0);
 }
-int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, 0, 3.5, 8.0); }
+// one lane per P̃ row up to a mean width of 8 (measured: C5 iteration 736 µs
+// at 1 lane against 759 at 2 and 845 at 4, C3 71.9 / 75.2 / 83.6)
+int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, L.ulanes, 8.0, 16.0); }
+// the down sweep's Ã rows in steps of 2U (K = 2); K = 3 (option amg_down_k)
+// measured slower even on C5's 11-block-wide level 1 (iteration 790 vs 760 µs)
+static int down_fine_k(const AmgLevD& L) { return L.dk > 0 ? L.dk : 2; }
 template <int ND>
 static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int S = amg_down_lanes(L);
   const int64_t gc = rows_grid(S * L.RT.n).x;
   const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
+  if (down_fine_k(L) == 3) {
+    if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else hipLaunchKernelGGL((k_amg_down<ND, 1, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    return;
+  }
   if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);

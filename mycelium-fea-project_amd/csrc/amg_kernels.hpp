@@ -67,6 +67,8 @@ struct AmgLevD {
   int rlanes = 0;  // restriction lanes per coarse row (0: by R's mean width)
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
+  int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
+  int dk = 0;        // compact down sweep: Ã step width K (0: by A's mean width)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   const int32_t* agg = nullptr;

@@ -224,6 +224,8 @@ struct mfea_handle {
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int64_t opt_amg_stail_rows = 0;  // GAMG setup: levels of at most this many rows in one workgroup (0: off; measured slower)
+  int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
+  int opt_amg_down_k = 0;    // GAMG compact down sweep: Ã step width K (0: by width, 2, 3)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
                        // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
@@ -1217,6 +1219,8 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.rlanes = h->opt_amg_rlanes;
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
+      d.ulanes = h->opt_amg_up_lanes;
+      d.dk = h->opt_amg_down_k;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, true, true);
@@ -3133,6 +3137,14 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_stail_rows = value;
     rebuild = true;
   }
+  else if (n == "amg_up_lanes" || n == "amg_down_k") {
+    const bool up = n == "amg_up_lanes";
+    if (up ? (value != 0 && value != 1 && value != 2 && value != 4) : (value != 0 && value != 2 && value != 3))
+      return fail(MFEA_EINVAL, up ? "amg_up_lanes: 0 (by width), 1, 2 or 4" : "amg_down_k: 0 (by width), 2 or 3");
+    (up ? h->opt_amg_up_lanes : h->opt_amg_down_k) = (int)value;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) (up ? L.ulanes : L.dk) = (int)value;
+  }
   else if (n == "amg_fuse_setup") {
     if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
     h->opt_amg_fuse_setup = (int)value;
@@ -3333,6 +3345,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
+  else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
+  else if (n == "amg_down_k") *value = h->opt_amg_down_k;
   else if (n == "amg_stail_rows") *value = h->opt_amg_stail_rows;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;

@@ -158,14 +158,14 @@ def test_benchmark_sizes_match_direct(engine, nx, ny, chords):
 # V-cycle kernel variants (csrc/amg.hip): lanes per row of the restriction and
 # of the coarse operators.  Every variant converges to the direct solve.
 # ---------------------------------------------------------------------------
-def _variant_solves(engine, option, values, nx=1, ny=5):
+def _variant_solves(engine, option, values, nx=1, ny=5, cycle=0):
     from mfea import synth
     xyz, e2n = synth.tiled_mesh(nx, ny)
     top, bot = synth.grips(xyz)
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
     out = {}
     # every level in its own kernels; the session engine gets its options back
-    with engine.options(amg_tail_rows=0, amg_deep=0, amg_cycle=0, **{option: values[0]}):
+    with engine.options(amg_tail_rows=0, amg_deep=0, amg_cycle=cycle, amg_collapse=0, **{option: values[0]}):
         engine.set_mesh(xyz, e2n)
         engine.set_bc(top, bot)
         engine.set_active(None)
@@ -180,11 +180,18 @@ def _variant_solves(engine, option, values, nx=1, ny=5):
     return out, fo.solve_system(K, known, vals)
 
 
-@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8, 16]), ("amg_op_lanes", [1, 2, 4])])
+@pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8, 16]), ("amg_op_lanes", [1, 2, 4]),
+                                           ("amg_up_lanes", [1, 2, 4]), ("amg_down_k", [2, 3])])
 def test_vcycle_lane_splits_match_direct(engine, option, values):
-    out, Uref = _variant_solves(engine, option, values)
+    # four-step form and the compact one (every level's sweeps: no collapse)
+    for cycle in (0, 1):
+        _lane_splits(engine, option, values, cycle)
+
+
+def _lane_splits(engine, option, values, cycle):
+    out, Uref = _variant_solves(engine, option, values, cycle=cycle)
     for v, (U, _) in out.items():
-        assert rel(U, Uref) <= 1e-10, (option, v, rel(U, Uref))
+        assert rel(U, Uref) <= 1e-10, (option, cycle, v, rel(U, Uref))
 
 
 def test_tail_lds_and_global_bitwise_equal(engine):

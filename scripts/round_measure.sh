@@ -22,5 +22,5 @@ else
     "c3:400:python bench.py" \
     "c2:200:python bench.py --config C2_100k --no-cpu" \
     "c5:300:python bench.py --config C5_10M_dense --no-cpu --steps 5 --warmup 2" \
-    "prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 bench.py --no-cpu --steps 10 --warmup 3"
+    "prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 bench.py --no-cpu --no-full-run --no-jacobi --steps 10 --warmup 3"
 fi

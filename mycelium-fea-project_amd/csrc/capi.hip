@@ -226,6 +226,7 @@ struct mfea_handle {
   int64_t opt_amg_stail_rows = 0;  // GAMG setup: levels of at most this many rows in one workgroup (0: off; measured slower)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
   int opt_amg_down_k = 0;    // GAMG compact down sweep: Ã step width K (0: by width, 2, 3)
+  int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
                        // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
@@ -271,7 +272,7 @@ struct mfea_handle {
 namespace {
 
 constexpr int kMaxChunk = 64;
-constexpr int kAmgBigChunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
+
 // lane-operator doubles per lane: V 18, D 6, x 3, p 3, r/s/w × 2 18, M 6; plus per
 // compact halo record (ell_vecs): h × 2 18, hM 6
 constexpr int64_t kEllDoubles = 18 + 6 + 3 + 3 + 18 + 6 + 18 + 6;
@@ -1662,7 +1663,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     // the planned batch in long chunks (default solves only: a caller's
     // chunk size is kept as given); measured at C3 / C2: chunks of 8 in the
     // batch 2.24 / 1.15 ms per step against 2.36 / 1.20 with chunks of 2
-    const int big = o->chunk > 0 ? chunk : kAmgBigChunk;
+    const int big = o->chunk > 0 ? chunk : h->opt_amg_big_chunk;
     if (big > chunk && (h->graph_big == nullptr || h->graph_big_chunk != big || h->graph_big_ell != tag)) {
       if (h->graph_big) (void)hipGraphExecDestroy(h->graph_big);
       h->graph_big = nullptr;
@@ -3145,6 +3146,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) (up ? L.ulanes : L.dk) = (int)value;
   }
+  else if (n == "amg_big_chunk") {
+    if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
+    h->opt_amg_big_chunk = (int)value;
+  }
   else if (n == "amg_fuse_setup") {
     if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
     h->opt_amg_fuse_setup = (int)value;
@@ -3345,6 +3350,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
+  else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
   else if (n == "amg_down_k") *value = h->opt_amg_down_k;
   else if (n == "amg_stail_rows") *value = h->opt_amg_stail_rows;

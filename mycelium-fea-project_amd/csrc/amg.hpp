@@ -30,11 +30,29 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "symbolic.hpp"
 
 namespace mfea {
+
+// Stable sort of one row's few entries (the symbolic products sort every row:
+// insertion sort, no temporary buffer per call as std::stable_sort takes)
+template <class It, class Less>
+inline void row_stable_sort(It b, It e, Less less) {
+  if (e - b > 48) {
+    std::stable_sort(b, e, less);
+    return;
+  }
+  for (It i = b + (b != e); i < e; ++i) {
+    auto v = std::move(*i);
+    It j = i;
+    for (; j > b && less(v, *(j - 1)); --j) *j = std::move(*(j - 1));
+    *j = std::move(v);
+  }
+}
+
 
 constexpr int kAmgMaxLevels = 32;
 

@@ -152,7 +152,7 @@ bool spgemm(int64_t n, const Rows* X, const Rows& Y, int64_t /*ncols*/, Prod& C,
     } else {
       add(-1, (int32_t)i);
     }
-    std::stable_sort(tr.begin(), tr.end(),
+    row_stable_sort(tr.begin(), tr.end(),
                      [](const std::array<int32_t, 3>& x, const std::array<int32_t, 3>& y) { return x[0] < y[0]; });
     for (size_t k = 0; k < tr.size();) {
       const int32_t j = tr[k][0];

@@ -117,7 +117,7 @@ std::string coarsen(LevelCsr& L, Csr& An) {
         const int32_t a = L.agg[A.col[k]];
         if (a >= 0) t.emplace_back(a, (int32_t)k);
       }
-      std::stable_sort(t.begin(), t.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      row_stable_sort(t.begin(), t.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       for (size_t k = 0; k < t.size(); ++k) {
         if (k == 0 || t[k].first != t[k - 1].first) {
           L.P.col.push_back(t[k].first);
@@ -159,7 +159,7 @@ std::string coarsen(LevelCsr& L, Csr& An) {
         const int64_t kk = A.col[k];
         for (int64_t q = L.P.ptr[kk]; q < L.P.ptr[kk + 1]; ++q) t.push_back({L.P.col[q], (int32_t)k, (int32_t)q});
       }
-      std::stable_sort(t.begin(), t.end(), [](const T3& x, const T3& y) { return x.J < y.J; });
+      row_stable_sort(t.begin(), t.end(), [](const T3& x, const T3& y) { return x.J < y.J; });
       for (size_t k = 0; k < t.size(); ++k) {
         if (k == 0 || t[k].J != t[k - 1].J) {
           L.AP.col.push_back(t[k].J);
@@ -185,7 +185,7 @@ std::string coarsen(LevelCsr& L, Csr& An) {
         const int64_t i = L.R.col[r];
         for (int64_t k = L.AP.ptr[i]; k < L.AP.ptr[i + 1]; ++k) t.push_back({L.AP.col[k], L.rp[r], (int32_t)k});
       }
-      std::stable_sort(t.begin(), t.end(), [I](const T3& x, const T3& y) {
+      row_stable_sort(t.begin(), t.end(), [I](const T3& x, const T3& y) {
         const bool dx = x.J == I, dy = y.J == I;  // the diagonal block first, then ascending
         return dx != dy ? dx : x.J < y.J;
       });
@@ -393,7 +393,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
         if (j < 0 || j >= nf || e < 0 || !active[e]) continue;
         nb.emplace_back(j, (int32_t)pos);
       }
-      std::stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      row_stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       A.col.push_back((int32_t)i);
       a0.ptr.push_back(a0.ptr.back());
       if (use_strength) w_entry.push_back(0.0);

@@ -91,7 +91,6 @@ struct Part {
   DevBuf<double> cg_part;                            // CG-CG block partials, 2 parities
   DevBuf<int32_t> slice_ptr, row_len, s_col, s_elem, e2n_d;
   DevBuf<uint8_t> active, code, elem_own;
-  DevBuf<uint8_t> active_next;  // mfea_step's early post writes the next activity here
   DevBuf<unsigned> tickets;
   // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
   Ell L;
@@ -195,13 +194,6 @@ struct mfea_handle {
   hipEvent_t ev_setup = nullptr;
   bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
   bool in_step = false;        // mfea_step: the solve's end is waited for by post
-  // mfea_step, one partition, GAMG: post is queued behind every batch of the
-  // solve (it reads `active`, writes `active_next`, so a batch that did not
-  // converge is simply followed by another post) and the solve's wait covers
-  // it — one host round trip per step instead of two
-  int opt_early_post = 0;
-  bool early_post_armed = false, early_post_done = false;
-  double step_max_strain = 0.0;
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
   // host view of the element activity (single partition; keys the AMG plan):
@@ -389,7 +381,6 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
   HIPC(pt.s_elem.alloc(pt.G));
   HIPC(pt.e2n_d.alloc(2 * E));
   HIPC(pt.active.alloc(E));
-  HIPC(pt.active_next.alloc(E));
   HIPC(pt.code.alloc(N));
   HIPC(pt.tickets.alloc(kTicketSets * kTicketStride));
   HIPC(pt.slots.alloc(kMaxChunk + 2));
@@ -954,7 +945,7 @@ void solve_times(mfea_handle* h, mfea_stats* st) {
 // is not waited for here — post's wait covers it and the times are read then
 // (one host round trip less per step).
 int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
-  if (!h->early_post_done) HIPC(hipEventRecord(h->ev[3], h->stream));
+  HIPC(hipEventRecord(h->ev[3], h->stream));
   if (!h->in_step) RC(wait_event(h, h->ev[3]));
   if (st) {
     st->iters = fin.iters;
@@ -1560,8 +1551,6 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
 }
 
-int enqueue_post_single(mfea_handle* h, double max_strain, const uint8_t* act_in, uint8_t* act_out);
-
 uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
   const unsigned char* b = static_cast<const unsigned char*>(p);
   for (size_t i = 0; i < n; ++i) k = (k ^ b[i]) * 1099511628211ULL;
@@ -1642,11 +1631,6 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   auto finish = [&]() -> int {
     launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
     HIPC(hipGetLastError());
-    if (h->early_post_armed) {  // mfea_step: post right behind the batch (see mfea_handle)
-      HIPC(hipEventRecord(h->ev[3], s));
-      RC(enqueue_post_single(h, h->step_max_strain, pt.active.ptr, pt.active_next.ptr));
-      h->early_post_done = true;
-    }
     return 0;
   };
   if (no_graph) {
@@ -2348,34 +2332,10 @@ int assemble_impl(mfea_handle* h, mfea_stats* st) {
   return 0;
 }
 
-// the single partition's post launches with the activity read from act_in
-// and written to act_out (early post: active → active_next), then the copy of
-// (force, #active) to the host and ev[5]
-int enqueue_post_single(mfea_handle* h, double max_strain, const uint8_t* act_in, uint8_t* act_out) {
-  hipStream_t s = h->stream;
-  Part& pt = part0(h);
-  const Pattern& P = pt.P;
-  HIPC(hipEventRecord(h->ev[4], s));
-  launch_reaction(s, P.n_free, P.n_top, P.n_nodes, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr,
-                  pt.val.ptr, pt.diag.ptr, pt.G, pt.x.ptr, pt.partials.ptr, tix(pt, 3), pt.red.ptr + 4);
-  launch_stress(s, P.n_elems, pt.e2n_d.ptr, pt.xyz_d.ptr, pt.x.ptr, h->mat, max_strain, act_out, pt.stress.ptr,
-                pt.partials.ptr, tix(pt, 4), pt.red.ptr + 5, nullptr, act_in);
-  HIPC(hipGetLastError());
-  HIPC(hipMemcpyAsync(h->h_red, pt.red.ptr + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPC(hipEventRecord(h->ev[5], s));
-  return 0;
-}
-
 int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
               mfea_stats* st) {
   hipStream_t s = h->stream;
   const bool dm = partitioned(h);
-  if (h->early_post_done) {  // queued behind the solve's last batch, which the solve waited for
-    RC(wait_event(h, h->ev[5]));
-    Part& p0 = part0(h);
-    std::swap(p0.active.ptr, p0.active_next.ptr);
-    h->early_post_done = false;
-  } else {
   HIPC(hipEventRecord(h->ev[4], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -2398,8 +2358,6 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   }
   HIPC(hipEventRecord(h->ev[5], s));
   RC(wait_event(h, h->ev[5]));
-  }
-  Part& p0 = part0(h);
   if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
@@ -2677,13 +2635,8 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   // a solver failure stops the step loop here, as the reference does
   // (src/fea_petsc.cpp:346-354)
   h->in_step = true;
-  h->step_max_strain = max_strain;
-  h->early_post_armed = h->opt_early_post && h->parts.size() == 1 && !partitioned(h);
-  h->early_post_done = false;
   int rc = solve_any(h, dy_top, dy_bot, &o, st);
-  h->early_post_armed = false;
   if (rc == 0) rc = post_impl(h, max_strain, total_force, n_active, st);
-  h->early_post_done = false;  // a failed solve keeps `active` (the early post wrote active_next)
   h->in_step = false;
   if (rc) {
     (void)sync_stream(h);
@@ -3193,10 +3146,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) (up ? L.ulanes : L.dk) = (int)value;
   }
-  else if (n == "early_post") {
-    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "early_post: 0 or 1");
-    h->opt_early_post = (int)value;
-  }
   else if (n == "amg_big_chunk") {
     if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
     h->opt_amg_big_chunk = (int)value;
@@ -3402,7 +3351,6 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
-  else if (n == "early_post") *value = h->opt_early_post;
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
   else if (n == "amg_down_k") *value = h->opt_amg_down_k;
   else if (n == "amg_stail_rows") *value = h->opt_amg_stail_rows;

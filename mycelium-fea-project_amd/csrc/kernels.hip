@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kBlock) void k_reaction(int64_t row0, int64_t nrows
 __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __restrict__ e2n,
                                                    const double* __restrict__ xyz,
                                                    const double* __restrict__ u, Material m,
-                                                   double max_strain, const uint8_t* act_in, uint8_t* active,
+                                                   double max_strain, uint8_t* __restrict__ active,
                                                    double* __restrict__ stress, double* partials,
                                                    unsigned* ticket, double* red_out,
                                                    const uint8_t* __restrict__ owned) {
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
   double cnt[1] = {0.0};
   if (e < E) {
     const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    uint8_t act = act_in[e];
+    uint8_t act = active[e];
     double sg = 0.0;
     if (act && a >= 0) {
       const double vx = xyz[3 * b] - xyz[3 * a], vy = xyz[3 * b + 1] - xyz[3 * a + 1],
@@ -407,8 +407,8 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
       const double strain = dot / L;
       sg = m.E * strain;
       if (fabs(strain) > max_strain) act = 0;
+      active[e] = act;
     }
-    if (act_in != active || !act) active[e] = act;  // in place: only a failure changes it
     stress[e] = sg;
     cnt[0] = (act && (!owned || owned[e])) ? 1.0 : 0.0;
   }
@@ -562,9 +562,9 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
                    double* stress, double* partials, unsigned* ticket, double* red_out,
-                   const uint8_t* owned, const uint8_t* act_in) {
+                   const uint8_t* owned) {
   hipLaunchKernelGGL(k_stress, MFEA_GRID(grid_rows(E > 0 ? E : 1)), E, e2n, xyz, u, m, max_strain,
-                     act_in ? act_in : active, active, stress, partials, ticket, red_out, owned);
+                     active, stress, partials, ticket, red_out, owned);
 }
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,

@@ -455,33 +455,3 @@ def test_setup_tail_bitwise_equals_launches(engine, mesh):
             out[rows] = (engine.displacement(), st.iters)
     for rows in (2048, 1 << 20):
         assert out[rows][1] == out[0][1] and np.array_equal(out[rows][0], out[0][0]), (mesh, rows)
-
-
-def test_early_post_steps_bitwise_equal(engine):
-    """mfea_step's post queued behind each solve batch (option early_post:
-    reads `active`, writes the next activity aside, committed when the solve
-    is done) against post after the solve's wait: the 40-step driver loop
-    with its failures gives the same forces, activity, stresses and U."""
-    import fea_solver as fs
-    nodes, elems = load_mesh("sim_20251117_181147")
-    xyz = nodes[["x", "y", "z"]].values
-    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 0.5)
-    e2n = elems[["n1", "n2"]].values
-    opts = _opts(1e-8)
-    runs = {}
-    for v in (0, 1):
-        with engine.options(early_post=v):
-            engine.set_mesh(xyz, e2n)
-            engine.set_bc(top, bot)
-            engine.set_active(None)
-            rec = []
-            for step in range(fs.N_STEPS):
-                dy = fs.DISPLACEMENT_MAX * step / (fs.N_STEPS - 1)
-                f, na, st = engine.step(dy, -dy, opts, fs.MAX_STRAIN)
-                rec.append((f, na, st.iters, engine.displacement(), engine.stress(), engine.active()))
-            runs[v] = rec
-    assert runs[0][-1][1] < len(e2n)  # elements fail along the way
-    for a, b in zip(runs[0], runs[1]):
-        assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
-        for x, y in zip(a[3:], b[3:]):
-            assert np.array_equal(x, y)

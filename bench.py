@@ -7,14 +7,22 @@ by default, as the reference's -pc_type gamg sweep) to ‖r‖ ≤ 1e-8‖b‖ (
 timed region; no CSV IO.  Workload (BASELINE.json configs[2]): C3_1M = 6×8
 tiles of results/sim_20251117_181147 (1.06 M DOF).
 
-N > 1 (one process per GPU, launched by torch.distributed.run): the
-partitioned solve over RCCL, one strip of the network per GPU
-(partition.hpp: x-strips whose boundaries follow the gaps between tiles).
+N > 1 (one process per GPU): the partitioned solve over RCCL,
+one part of the network per GPU (partition.hpp: the min-cut px × py grid).
   --scaling weak   (default) the network is (6N)×8 tiles — C3 per GPU;
-  --scaling strong the C3 network itself is cut into N strips.
+  --scaling strong the C3 network itself is cut into N parts.
 `value` is the whole network's DOF/s.  `--mode replicas` runs N independent
 copies of the 1-GPU step instead.  torch.distributed (gloo) only carries the
 RCCL unique id, the barriers and the max-over-ranks time.
+
+Launch: `python bench.py --gpus N` with no WORLD_SIZE in the environment
+starts the N ranks itself (child processes with RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_*; the parent touches no GPU) and exits with the first
+failing rank's code — the reference's `mpirun -np N ./fea_petsc`
+(README.md:18).  Under torch.distributed.run, --gpus must equal WORLD_SIZE
+(or be omitted).  A rank whose partitioned solve fails ends the run with a
+non-zero exit; `--allow-replicas` turns that into N independent copies
+(labelled in `parallelism` and `note`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3_1M] [--scaling weak|strong]
 
@@ -37,9 +45,11 @@ import numpy as np  # noqa: E402,F401
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); default WORLD_SIZE, else 1.  N > 1 without WORLD_SIZE: "
+                         "this process launches the N ranks")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_1M", choices=["C2_100k", "C3_1M", "C5_10M_dense"])
@@ -53,6 +63,9 @@ def parse():
                     help="PMC-derived HBM bytes per SpMV launch (rocprofv3 pass), if present")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
                     help="N > 1: one network cut over the GPUs, or N independent copies")
+    ap.add_argument("--allow-replicas", action="store_true",
+                    help="N > 1 partitioned: if the RCCL solve fails on some rank, run replicas "
+                         "instead of exiting non-zero")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N > 1 partitioned: C3 per GPU (weak) or C3 cut N ways (strong)")
     ap.add_argument("--device", type=int, default=None,
@@ -63,7 +76,7 @@ def parse():
                     help="skip the 40-step run (all load steps, with failures) after the timed steps")
     ap.add_argument("--no-jacobi", action="store_true",
                     help="skip the Jacobi-PCG leg (SURVEY §8d's iteration metric) after the timed steps")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def amg_iteration_bytes(ai, compact=None):
@@ -285,10 +298,81 @@ def cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof):
     out["speedup_vs_direct"] = out["value"] / legs["direct_spsolve"]["value"]
 
 
-def main():
-    a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_plan(n, argv, port, env=None):
+    """The N rank processes `python bench.py --gpus N` starts when no launcher
+    did: (argv, env) per rank — this script with the same arguments, one
+    process per GPU (LOCAL_RANK = the GPU), rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if env is None else env)
+    plan = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GROUP_RANK="0")
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        plan.append(([sys.executable, os.path.abspath(__file__)] + list(argv), e))
+    return plan
+
+
+def run_ranks(plan, poll_s=0.2):
+    """Start every rank, wait; the first rank to fail ends the others (their
+    process groups) and its exit code is the launcher's.  Rank 0's stdout is
+    the launcher's (the JSON line); the other ranks' stdout goes to stderr."""
+    import signal
+    import subprocess
+    procs = []
+    for r, (argv, env) in enumerate(plan):
+        procs.append(subprocess.Popen(argv, env=env, start_new_session=True,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                for q in live:  # the rest would wait for the failed rank forever
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def world_of(a, env=None):
+    """(rank, world, launch): the rank and world size of this process, and
+    whether it must launch the ranks itself.  --gpus ≠ WORLD_SIZE is an error."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if a.gpus is not None and a.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+        return int(env.get("RANK", "0")), world, False
+    n = 1 if a.gpus is None else a.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    return 0, n, n > 1
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    rank, world, launch = world_of(a)
+    if launch:  # no GPU call in this process: the ranks are its children
+        sys.exit(run_ranks(launch_plan(world, argv, free_port())))
     local = int(os.environ.get("LOCAL_RANK", "0")) if a.device is None else a.device
     dist = None
     if world > 1:
@@ -360,7 +444,10 @@ def main():
                 eng.close()
                 eng = None
         if eng is None:
-            note = f"partitioned solve failed on some rank ({errs[-1] if errs else 'peer'}); replicas instead"
+            msg = f"partitioned solve failed on some rank ({errs[-1] if errs else 'peer'})"
+            if not a.allow_replicas:
+                raise SystemExit(f"bench.py rank {rank}: {msg}")
+            note = msg + "; replicas instead (--allow-replicas)"
             mode = "replicas"
             eng, nx, xyz, e2n, top, bot = setup(mode)
     else:

@@ -254,6 +254,7 @@ struct mfea_handle {
   int64_t act_gen = 1;        // bumped whenever the element activity may have changed
   int64_t gamg_act_gen = 0;   // act_gen the hierarchy was built for
   DevBuf<uint8_t> gact;       // RCCL: the global activity, max-all-reduced
+  DevBuf<double> gtime;       // RCCL: a host time, max-all-reduced (amg_dist -1's choice)
   // option "amg_dist" -1: per active set (gamg_plan_gen), the first GAMG
   // solve runs the global hierarchy, the next block Jacobi; the faster
   // (host-timed, plan builds excluded) serves the set's further solves
@@ -2384,6 +2385,15 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
 // 4·levels + 2); the global form wherever the cut couplings matter (the
 // grown networks: 17 iterations instead of 190-310).  A variant that fails
 // (max_it, breakdown) hands the step to the other.
+// RCCL world: *t ← the maximum of *t over the ranks (collective)
+int max_over_ranks(mfea_handle* h, double* t) {
+  HIPC(h->gtime.alloc(1));
+  HIPC(hipMemcpyAsync(h->gtime.ptr, t, sizeof(double), hipMemcpyHostToDevice, h->stream));
+  NCCLC(ncclAllReduce(h->gtime.ptr, h->gtime.ptr, 1, ncclFloat64, ncclMax, h->comm, h->stream));
+  HIPC(hipMemcpyAsync(t, h->gtime.ptr, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  return sync_stream(h);
+}
+
 int solve_amg_part(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o, mfea_stats* st) {
   auto run = [&](int mode) {
     return mode ? solve_gamg_global(h, dy_top, dy_bot, o, st) : solve_amg_dist(h, dy_top, dy_bot, o, st);
@@ -2412,6 +2422,9 @@ int solve_amg_part(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   int rc = run(mode);
   if (rc == 0) rc = sync_stream(h);
   a.t[mode] = rc == 0 ? std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() : 1e300;
+  // RCCL: every rank must pick the same form (the two issue different
+  // exchanges), so each compares the slowest rank's times, not its own
+  if (h->world > 1) RC(max_over_ranks(h, &a.t[mode]));
   if (a.t[0] >= 0 && a.t[1] >= 0) a.choice = a.t[1] <= a.t[0] ? 1 : 0;
   if (rc == MFEA_EMAXIT || rc == MFEA_EBREAKDOWN) {
     a.choice = 1 - mode;
@@ -3121,7 +3134,9 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       for (auto& L : pp->amg_lev) L.tail_lds = (int)(value != 0);
   }
   else if (n == "amg_collapse" || n == "amg_collapse_mb" || n == "amg_collapse_pairs") {
-    if (value < -1 || (n == "amg_collapse" && value >= kAmgMaxLevels))
+    if (n == "amg_collapse" ? (value < -1 || value >= kAmgMaxLevels)
+        : n == "amg_collapse_mb" ? (value < 0 || value > (int64_t(1) << 40 >> 20))
+                                 : (value < 0 || value >= INT32_MAX))
       return fail(MFEA_EINVAL, n + ": out of range");
     if (n == "amg_collapse") h->opt_amg_collapse = (int)value;
     else if (n == "amg_collapse_mb") h->opt_amg_collapse_mb = value;
@@ -3287,6 +3302,11 @@ int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t
   *n = L.A.n;
   const int w = which >= 4 && which != 5 ? nd * nd : nd;  // per-row width
   if (!out) return 0;
+  // the device must hold the plan pl describes (a partitioned handle may hold
+  // the block-Jacobi plans after amg_dist 0 or an automatic choice of it)
+  if (dm)
+    for (auto& pp : h->parts)
+      if (pp->dev_plan != 1) return fail(MFEA_ESTATE, "the device holds the block-Jacobi plans: run amg_vcycle first");
   if (cap < w * L.A.n) return fail(MFEA_EINVAL, "output too small");
   for (auto& pp : h->parts) {
     Part& pt = *pp;

@@ -72,3 +72,56 @@ def test_amg_iteration_bytes_compact_by_hand(bench):
     down1 = tb1 * (B + 4) + nb1 * (B + 4) + 2 * V * nn + V * n2
     up1 = tb1 * (B + 4) + 2 * V * nn + V * n2
     assert bench.amg_iteration_bytes(dict(ai3, collapse_level=0)) == down + up + down1 + up1 + update + w
+
+
+# ---- the multi-GPU launcher (bench.py --gpus N), no GPU -----------------------
+
+def test_launch_plan_one_process_per_rank(bench):
+    argv = ["--gpus", "4", "--steps", "3"]
+    plan = bench.launch_plan(4, argv, 29517, env={"PATH": "/usr/bin"})
+    assert len(plan) == 4
+    for r, (cmd, env) in enumerate(plan):
+        assert cmd[1].endswith("bench.py") and cmd[2:] == argv
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == (str(r), str(r), "4")
+        assert (env["MASTER_ADDR"], env["MASTER_PORT"]) == ("127.0.0.1", "29517")
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/usr/bin"
+
+
+def test_world_of(bench):
+    a = bench.parse(["--gpus", "8"])
+    assert bench.world_of(a, env={}) == (0, 8, True)          # launches its 8 ranks
+    assert bench.world_of(a, env={"WORLD_SIZE": "8", "RANK": "3"}) == (3, 8, False)
+    with pytest.raises(SystemExit):                            # --gpus disagrees with the launcher
+        bench.world_of(a, env={"WORLD_SIZE": "4", "RANK": "0"})
+    assert bench.world_of(bench.parse([]), env={}) == (0, 1, False)
+    assert bench.world_of(bench.parse([]), env={"WORLD_SIZE": "2", "RANK": "1"}) == (1, 2, False)
+    assert bench.world_of(bench.parse(["--gpus", "1"]), env={}) == (0, 1, False)
+    assert not bench.parse([]).allow_replicas                   # the replica fallback is opt-in
+
+
+def test_run_ranks_first_failure_ends_the_rest(bench):
+    import sys
+    import time
+    ok = [sys.executable, "-c", "print('rank0 line')"]
+    bad = [sys.executable, "-c", "import sys; sys.exit(3)"]
+    hang = [sys.executable, "-c", "import time; time.sleep(600)"]
+    env = dict(os.environ)
+    t = time.time()
+    assert bench.run_ranks([(ok, env), (bad, env), (hang, env)], poll_s=0.05) == 3
+    assert time.time() - t < 60
+    assert bench.run_ranks([(ok, env), (ok, env)], poll_s=0.05) == 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_without_gpu_exits_nonzero():
+    """`python bench.py --gpus 2` with no GPU: both ranks start (gloo), the
+    engine cannot be created, and with no --allow-replicas the launcher exits
+    non-zero instead of reporting a number."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0", "--no-cpu"], env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode != 0
+    assert '"metric"' not in r.stdout
+    assert "partitioned solve failed" in r.stderr

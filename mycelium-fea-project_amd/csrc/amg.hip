@@ -178,6 +178,10 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
   }
+  if (L.fmask && L.fmask[i]) {  // a floating row: no coarse correction reaches it
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+  }
   bstore<ND>(P.val, P.npos, q, pm);
   bstore<ND>(P.val32, P.npos, q, pm);
 }

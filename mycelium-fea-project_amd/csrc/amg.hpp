@@ -255,6 +255,12 @@ struct AmgCollapse {
 std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t max_pairs, int min_level,
                                AmgCollapse& out);
 
+// Free rows [0, P.n_free) with no path of active elements to a grip row:
+// out[i] = 1.  A hierarchy kept over element failures (capi.hip ensure_amg)
+// zeroes their rows of P_0, so the preconditioner leaves them at exactly zero
+// — what the direct solve gives an unloaded floating piece.
+void floating_free_rows(const Pattern& P, const std::vector<uint8_t>& active, std::vector<uint8_t>& out);
+
 // xsend_rows / xrecv_rows: Pattern rows of the plan's xsend / xrecv nodes
 std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
                            const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,

@@ -655,4 +655,29 @@ std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active,
   return "";
 }
 
+// Free rows of P with no path of active elements to a grip (known, non-ghost)
+// row: their load is zero, so the direct solve leaves them exactly at zero
+// (src/fea_solver.py:128).  Union-find over the active elements.
+void floating_free_rows(const Pattern& P, const std::vector<uint8_t>& active, std::vector<uint8_t>& out) {
+  const int64_t N = P.n_nodes;
+  std::vector<int32_t> up(N);
+  std::iota(up.begin(), up.end(), 0);
+  auto find = [&](int32_t a) {
+    while (up[a] != a) a = up[a] = up[up[a]];
+    return a;
+  };
+  const int64_t E = P.n_elems;
+  for (int64_t e = 0; e < E; ++e) {
+    if (!active[e]) continue;
+    const int32_t a = P.e2n_perm[2 * e], b = P.e2n_perm[2 * e + 1];
+    if (a < 0 || b < 0) continue;
+    const int32_t ra = find(a), rb = find(b);
+    if (ra != rb) up[std::max(ra, rb)] = std::min(ra, rb);
+  }
+  std::vector<uint8_t> anchored(N, 0);
+  for (int64_t i = P.n_free; i < N - P.n_ghost; ++i) anchored[find((int32_t)i)] = 1;
+  out.assign(P.n_free, 0);
+  for (int64_t i = 0; i < P.n_free; ++i) out[i] = anchored[find((int32_t)i)] ? 0 : 1;
+}
+
 }  // namespace mfea

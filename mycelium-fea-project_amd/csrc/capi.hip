@@ -120,6 +120,14 @@ struct Part {
   std::vector<uint8_t> amg_key;
   int64_t amg_gen = 0;               // bumped on every rebuild (captured graphs hold its pointers)
   int amg_last_iters = 0;            // iterations of the last converged GAMG solve (chunk plan)
+  // a hierarchy kept over element failures (option amg_reuse): the activity
+  // its floating-row mask reflects, the iterations of its first solve, and
+  // whether a later solve degraded enough to rebuild
+  std::vector<uint8_t> amg_mask_key;
+  DevBuf<uint8_t> amg_fmask;         // level-0 rows of floating pieces (amg.hpp floating_free_rows)
+  int amg_build_iters = -1;
+  bool amg_stale = false;
+  bool amg_reused = false;           // the last ensure_amg kept a hierarchy built for another set
   DevBuf<int32_t> amg_i;             // every index array of the plan, carved
   DevBuf<double> amg_d;              // every f64 value / vector array, carved
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
@@ -238,6 +246,11 @@ struct mfea_handle {
   int64_t opt_amg_deep_rows = 262144;  // GAMG: the deep launch starts at the first level of at most this many rows
   int opt_amg_deep_wgs = 128;  // GAMG: workgroups of the deep launch (8..256)
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
+  // GAMG over element failures: 1 keep the hierarchy (floating pieces masked)
+  // until a solve needs more than amg_rebuild_pct % of the iterations of the
+  // hierarchy's first solve (+2), then rebuild; 0 rebuild on every new active set
+  int opt_amg_reuse = 1;
+  int opt_amg_rebuild_pct = 150;
   int opt_amg_dist = -1;          // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block
                                   // Jacobi over per-partition hierarchies, -1 whichever solves faster (measured)
   int64_t opt_amg_rep_rows = 32768;  // distributed V-cycle: levels of at most this many rows are replicated
@@ -1315,6 +1328,12 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         pt.amg_stail = l;
         break;
       }
+  if (!rk && nlev > 1) {  // the floating-row mask (zero until ensure_amg fills it)
+    HIPC(pt.amg_fmask.alloc(std::max<int64_t>(pl.lev[0].A.n, 1)));
+    HIPC(hipMemsetAsync(pt.amg_fmask.ptr, 0, pt.amg_fmask.n, s));
+    pt.amg_lev[0].fmask = pt.amg_fmask.ptr;
+    pt.amg_mask_key.clear();
+  }
   HIPC(pt.amg_levd.alloc(std::max(nlev, 1)));
   HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
   HIPC(hipStreamSynchronize(s));
@@ -1376,6 +1395,22 @@ int upload_amg_halo(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
   return 0;
 }
 
+// The floating-row mask of the active set `key` in level-0 labels (one
+// partition's own hierarchy: a partition cannot tell alone what is floating)
+int upload_fmask(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
+  std::vector<uint8_t> fl;
+  floating_free_rows(pt.P, key, fl);
+  const std::vector<int32_t>& row0 = pt.amg.row0;
+  std::vector<uint8_t> m(row0.size());
+  for (size_t i = 0; i < row0.size(); ++i) m[i] = fl[row0[i]];
+  if (!m.empty()) {
+    HIPC(hipMemcpyAsync(pt.amg_fmask.ptr, m.data(), m.size(), hipMemcpyHostToDevice, h->stream));
+    RC(sync_stream(h));
+  }
+  pt.amg_mask_key = key;
+  return 0;
+}
+
 // (Re)build the hierarchy when the active set differs from the plan's.  One
 // partition: the host view of the activity (downloaded only when a post
 // kernel changed it); partitioned: each partition's own elements, read back.
@@ -1390,6 +1425,16 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
     RC(current_active(h, pt));
   }
   const std::vector<uint8_t>& key = dm ? local : h->act_host;
+  pt.amg_reused = false;
+  if (!dm && pt.amg_ok && pt.amg_lev.size() > 1 &&
+      (pt.amg_key == key || (h->opt_amg_reuse && !pt.amg_stale))) {
+    // keep the hierarchy: the numeric setup re-forms its values from the new
+    // K (failed elements are zero slots); only pieces cut off from both grips
+    // need care — their P_0 rows are zeroed so they stay exactly at zero
+    if (pt.amg_mask_key != key) RC(upload_fmask(h, pt, key));
+    pt.amg_reused = pt.amg_key != key;
+    return 0;
+  }
   if (pt.amg_ok && pt.amg_key == key) {
     if (!dm || pt.dev_plan == 0) return 0;
     destroy_graph(h);  // the device holds the global plan: upload this one again
@@ -1411,6 +1456,9 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
   pt.dev_plan = 0;
   pt.amg_key = key;
   pt.amg_ok = true;
+  pt.amg_stale = false;
+  pt.amg_build_iters = -1;
+  if (!dm && pt.amg_lev.size() > 1) RC(upload_fmask(h, pt, key));
   ++pt.amg_gen;
   *rebuilt = true;
   return 0;
@@ -1681,6 +1729,16 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   }
   if (rc) return rc;
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
+  if (fin.status == 0 && !pt.amg_reused) {
+    pt.amg_build_iters = fin.iters;  // the hierarchy on the set it was built for
+  } else if (pt.amg_reused && pt.amg_build_iters >= 0 &&
+             (fin.status != 0 || fin.iters > (int64_t)pt.amg_build_iters * h->opt_amg_rebuild_pct / 100 + 2)) {
+    pt.amg_stale = true;  // degraded: the next solve rebuilds for its active set
+    if (fin.status != 0) {  // ... this one already: solve again on a fresh hierarchy
+      RC(sync_stream(h));
+      return solve_amg(h, dy_top, dy_bot, o, st);
+    }
+  }
   rc = finish_solve(h, fin, st);
   if (st) {
     st->amg_levels = (int32_t)pt.amg_lev.size();
@@ -3207,6 +3265,15 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       if (!pp->amg_lev.empty()) RC(set_amg_deep(h, *pp));
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
+  else if (n == "amg_reuse") {
+    if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_reuse: 0 (rebuild per active set) or 1");
+    h->opt_amg_reuse = (int)value;
+    for (auto& pp : h->parts) pp->amg_stale = true;  // the next solve builds for its own set
+  }
+  else if (n == "amg_rebuild_pct") {
+    if (value < 100 || value > 100000) return fail(MFEA_EINVAL, "amg_rebuild_pct: 100 .. 100000");
+    h->opt_amg_rebuild_pct = (int)value;
+  }
   else if (n == "amg_dist") {
     if (value < -1 || value > 1)
       return fail(MFEA_EINVAL, "amg_dist: 0 (block Jacobi over partitions), 1 (global hierarchy), -1 (faster)");
@@ -3409,6 +3476,10 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   }
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;
+  else if (n == "amg_reuse") *value = h->opt_amg_reuse;
+  else if (n == "amg_rebuild_pct") *value = h->opt_amg_rebuild_pct;
+  else if (n == "amg_reused") *value = part0(h).amg_reused ? 1 : 0;  // read-only: the last solve kept a hierarchy built for another set
+  else if (n == "amg_build_iters") *value = part0(h).amg_build_iters;  // read-only
   else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);

@@ -101,9 +101,19 @@ def to_scipy(blocks, sptr, col, n_rows, n_cols, nd):
     return sp.csr_matrix((b.ravel(), (rr.ravel(), cc.ravel())), shape=(n_rows * nd, n_cols * nd))
 
 
-def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
+def _binv(D):
+    """Block inverses as amg_dev.hpp binv: a singular (zero) block → zero."""
+    out = np.zeros_like(D)
+    ok = np.abs(np.linalg.det(D)) > 0
+    out[ok] = np.linalg.inv(D[ok])
+    return out
+
+
+def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None):
     """The per-solve numeric setup of amg.hip on the plan: fills A (blocks),
-    dinv, omega, P, AP for every level.  val/diag: the assembled SELL values."""
+    dinv, omega, P, AP for every level.  val/diag: the assembled SELL values.
+    fmask: per level-0 row, 1 = a floating row whose P_0 row is formed as zero
+    (a hierarchy kept over element failures, amg.hip pvals_body)."""
     L0 = levels[0]
     n0 = L0["n"]
     row, k = pos_rows(L0["A.sptr"], n0)
@@ -123,7 +133,7 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
         row, k = pos_rows(L["A.sptr"], n)
         Ab = L["Ab"]
         D = Ab[(k == 0) & (row >= 0)]          # rows in order
-        Dinv = np.linalg.inv(D)
+        Dinv = _binv(D)
         L["dinv"] = Dinv
         ok = (L["A.col"] >= 0) & (row >= 0)
         M = np.abs(np.einsum("pab,pbc->pac", Dinv[row[ok]], Ab[ok])).sum(axis=2)  # [p][a]
@@ -143,6 +153,8 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12):
         Pb[okp] = -L["omega"] * np.einsum("pab,pbc->pac", Dinv[prow[okp]], S[okp])
         ident = okp & (L["P.col"] == np.where(prow >= 0, L["agg"][np.maximum(prow, 0)], -9))
         Pb[ident] += np.eye(nd)
+        if l == 0 and fmask is not None:
+            Pb[okp & (fmask[np.maximum(prow, 0)] != 0)] = 0.0
         L["Pb"] = Pb
         L["P"] = to_scipy(Pb, L["P.sptr"], L["P.col"], n, L["nc"], nd)
         APb = seg_sum(np.einsum("pab,pbc->pac", Ab[L["ap.a"]], Pb[L["ap.b"]]), L["ap.ptr"])

@@ -140,6 +140,15 @@ void shim_amg_strength(double theta, double kb_kax) {
   g_strength.theta = theta;
   g_strength.kb_kax = kb_kax;
 }
+// floating_free_rows (amg.hpp) of the last built pattern: out[n_free] in
+// pattern row order; returns the number of floating rows
+int64_t shim_floating(const uint8_t* active, uint8_t* out) {
+  std::vector<uint8_t> a(active, active + g_P.n_elems), f;
+  floating_free_rows(g_P, a, f);
+  int64_t n = 0;
+  for (size_t i = 0; i < f.size(); ++i) n += (out[i] = f[i]);
+  return n;
+}
 int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   std::vector<uint8_t> a(active, active + g_P.n_elems);
   std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, nullptr, g_strength, g_layout);

@@ -31,6 +31,8 @@ def shim():
     lib.shim_sell_values.argtypes = [P, C.c_double, C.c_double, P, P]
     lib.shim_amg.restype = C.c_int
     lib.shim_amg.argtypes = [P, C.c_int, C.c_char_p, C.c_int]
+    lib.shim_floating.restype = C.c_int64
+    lib.shim_floating.argtypes = [P, P]
     lib.shim_amg_array.restype = C.c_int64
     lib.shim_amg_array.argtypes = [C.c_int, C.c_char_p, P]
     return lib
@@ -171,6 +173,74 @@ def test_aggregates_respect_components_after_failures(shim):
     ref = spsolve(Kff.tocsc(), b)
     x, _ = amg_ref.pcg(Kff, b, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13)
     assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10
+
+
+def test_kept_hierarchy_over_failures(shim):
+    """The hierarchy of the intact network kept over element failures (capi.hip
+    ensure_amg, option amg_reuse): the plan of the intact set, the values of
+    the failed one, and P_0's rows of floating pieces (no path to a grip,
+    floating_free_rows) formed as zero.  The V-cycle stays SPD on the loaded
+    part, PCG reaches the direct solve, and every floating row stays EXACTLY
+    zero, as spsolve leaves it."""
+    xyz, e2n, top, bot = _golden22k()
+    rng = np.random.default_rng(3)
+    active = (rng.random(len(e2n)) > 0.05).astype(np.uint8)
+    # the failed set's K / b in the intact plan's level-0 order
+    levels_f, Kff, b, nodes0 = setup_case(shim, xyz, e2n, top, bot, active, 2)
+    # floating rows: the host routine against scipy's connected components
+    nf = levels_f[0]["n"]
+    fl = np.zeros(nf, np.uint8)
+    n_fl = shim.shim_floating(_ptr(np.ascontiguousarray(active)), _ptr(fl))
+    n = len(xyz)
+    a = e2n[active.astype(bool)]
+    _, lab = connected_components(sp.coo_matrix((np.ones(len(a)), (a[:, 0], a[:, 1])), shape=(n, n)),
+                                  directed=False)
+    anchored = np.zeros(lab.max() + 1, bool)
+    anchored[lab[np.concatenate([top, bot])]] = True
+    perm = np.empty(n, np.int32)
+    _, G_, nsl = _pattern_sizes(shim, xyz, e2n, top, bot)
+    junk = [np.empty(n, np.int32), np.empty(nsl + 1, np.int32), np.empty(G_, np.int32),
+            np.empty(G_, np.int32), np.empty(n, np.uint8)]
+    shim.shim_arrays(_ptr(perm), *[_ptr(j) for j in junk])
+    assert np.array_equal(fl.astype(bool), ~anchored[lab[perm[:nf]]])
+    assert n_fl > 10
+    # the intact set's plan, the failed set's values
+    val = np.zeros(6 * G_)
+    diag = np.zeros(6 * n)
+    shim.shim_sell_values(_ptr(active), EA, EI12, _ptr(val), _ptr(diag))
+    levels = amg_ref.fetch_plan(shim, np.ones(len(e2n), np.uint8), 2)
+    fm = fl[levels[0]["row0"]]
+    amg_ref.numeric_setup(levels, val, diag, G_, n, 2, fmask=fm)
+    # K / b in THIS plan's level-0 order
+    Kf = fo.assemble_global_stiffness(xyz, e2n, active.astype(bool))
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    A3, b3, free = fo.free_system(Kf, known, vals)
+    nodes = perm[:nf][levels[0]["row0"]]
+    dofs = (nodes[:, None].astype(np.int64) * 3 + np.arange(2)).ravel()
+    pos = np.searchsorted(free, dofs)
+    K2, b2 = A3[pos][:, pos].tocsr(), b3[pos]
+    assert _rel(levels[0]["A"], K2) <= 1e-15
+    ref = spsolve(K2.tocsc(), b2)
+    x, it = amg_ref.pcg(K2, b2, lambda r: amg_ref.vcycle(levels, r), rtol=1e-13, max_it=2000)
+    assert np.linalg.norm(x - ref) / np.linalg.norm(ref) <= 1e-10
+    fr = np.repeat(fm.astype(bool), 2)
+    assert np.all(x[fr] == 0.0) and np.all(ref[fr] == 0.0)
+    _, it8 = amg_ref.pcg(K2, b2, lambda r: amg_ref.vcycle(levels, r), rtol=1e-8, max_it=2000)
+    assert it8 <= 60, it8
+    print(f"kept hierarchy: {it8} iterations to 1e-8, {n_fl} floating rows")
+
+
+def _pattern_sizes(shim, xyz, e2n, top, bot):
+    xyz = np.ascontiguousarray(xyz, np.float64)
+    e2n = np.ascontiguousarray(e2n, np.int64)
+    top = np.ascontiguousarray(top, np.int64)
+    bot = np.ascontiguousarray(bot, np.int64)
+    sizes = np.zeros(5, np.int64)
+    err = C.create_string_buffer(256)
+    assert shim.shim_build(len(xyz), _ptr(xyz), len(e2n), _ptr(e2n), 0, len(top), _ptr(top), len(bot),
+                           _ptr(bot), -1, _ptr(sizes), err, 256) == 0
+    return int(sizes[0]), int(sizes[4]), int(sizes[3])
 
 
 def test_compact_cycle_transfers_and_cycle(shim):

@@ -66,24 +66,83 @@ def test_gamg_deterministic_and_no_rebuild(engine):
     assert engine.solve(0.01, -0.01, _opts(1e-10)).amg_rebuilt == 0
 
 
-def test_gamg_rebuilds_after_failures_and_matches_direct(engine):
-    """Steps with element failures: the hierarchy follows the active set, and
-    every step's U matches the direct solve of that step's K."""
+@pytest.mark.parametrize("reuse", [0, 1])
+def test_gamg_rebuilds_after_failures_and_matches_direct(engine, reuse):
+    """Steps with element failures: every step's U matches the direct solve of
+    that step's K.  amg_reuse 0: the hierarchy is rebuilt for every new active
+    set; 1 (default): the intact set's hierarchy is kept (floating pieces
+    masked) unless the iterations degrade."""
     xyz, e2n, top, bot = _sim181147(engine)
     active = np.ones(len(e2n), bool)
-    rebuilt = []
-    for step in (10, 25, 39):
-        dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+    rebuilt, reused = [], []
+    with engine.options(amg_reuse=reuse):
+        for step in (10, 25, 39):
+            dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+            engine.set_active(active)
+            f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
+            rebuilt.append(st.amg_rebuilt)
+            reused.append(engine.get_option("amg_reused"))
+            K = fo.assemble_global_stiffness(xyz, e2n, active)
+            known, vals = fo.known_dof_map(top, bot, dy, -dy)
+            Uref = fo.solve_system(K, known, vals)
+            assert rel(engine.displacement(), Uref) <= 1e-10, step
+            active = engine.active()
+    assert n_act < len(e2n)          # failures happened
+    if reuse:
+        assert reused[-1] == 1 or rebuilt[-1] == 1
+    else:
+        assert sum(rebuilt[1:]) >= 1     # a later step rebuilt the plan
+        assert not any(reused)
+
+
+def _floating_nodes(xyz, e2n, active, top, bot):
+    """Nodes with no path of active elements to a grip node (scipy csgraph)."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import connected_components
+    n = len(xyz)
+    a = e2n[active]
+    g = sp.coo_matrix((np.ones(len(a)), (a[:, 0], a[:, 1])), shape=(n, n))
+    _, lab = connected_components(g, directed=False)
+    anchored = np.zeros(lab.max() + 1, bool)
+    anchored[lab[np.concatenate([top, bot])]] = True
+    return ~anchored[lab]
+
+
+def test_gamg_kept_hierarchy_floating_pieces_exactly_zero(engine):
+    """Knock out 6 % of the elements (seeded): pieces cut off from both grips
+    appear.  The intact set's hierarchy is kept (amg_reuse 1, no rebuild
+    forced): U matches the direct solve and is EXACTLY zero on every floating
+    node, as spsolve gives (zero load there); the kept hierarchy also survives
+    the reverse change back to the intact set."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+        engine.set_active(None)
+        engine.assemble()
+        st0 = engine.solve(dy, -dy, _opts(1e-13))
+        rng = np.random.default_rng(7)
+        active = rng.random(len(e2n)) > 0.06
+        fl = _floating_nodes(xyz, e2n, active, top, bot)
+        free_fl = fl.copy()
+        free_fl[np.concatenate([top, bot])] = False
+        assert free_fl.sum() > 20
         engine.set_active(active)
-        f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
-        rebuilt.append(st.amg_rebuilt)
+        engine.assemble()
+        st = engine.solve(dy, -dy, _opts(1e-13))
+        assert st.amg_rebuilt == 0 and engine.get_option("amg_reused") == 1
+        U = engine.displacement().reshape(-1, 3)
         K = fo.assemble_global_stiffness(xyz, e2n, active)
         known, vals = fo.known_dof_map(top, bot, dy, -dy)
         Uref = fo.solve_system(K, known, vals)
-        assert rel(engine.displacement(), Uref) <= 1e-10, step
-        active = engine.active()
-    assert n_act < len(e2n)          # failures happened
-    assert sum(rebuilt[1:]) >= 1     # and a later step rebuilt the plan
+        assert rel(U.ravel(), Uref) <= 1e-10
+        assert np.all(U[free_fl] == 0.0)
+        assert np.all(Uref.reshape(-1, 3)[free_fl] == 0.0)
+        engine.set_active(None)
+        engine.assemble()
+        st1 = engine.solve(dy, -dy, _opts(1e-13))
+        assert st1.amg_rebuilt == 0 and st1.iters == st0.iters
+        K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+        assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
 
 
 def test_gamg_3d_mesh_matches_direct(engine):

@@ -424,76 +424,6 @@ __global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, d
   else ptv_body<ND>(L, xb - g0);
 }
 
-// The setup of the small levels [l0, nlev) in ONE workgroup (levels of at
-// most a few thousand rows: a launch there is ≈ 5–10 µs of latency for
-// ≈ 1 µs of work).  Each phase runs the same bodies as the launches above,
-// over the same virtual 256-thread blocks, kTailBS / kBlock at a time, the
-// phases separated by workgroup barriers; D⁻¹'s bound is reduced in LDS and
-// stored (no atomics).  Then the collapse products of the levels ≥ l0.
-// lev: the device copy of the level views (Part::amg_levd).
-constexpr int kSetupTailBS = 1024;
-__device__ __forceinline__ int64_t nslot_blk(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
-__device__ __forceinline__ int64_t nrow_blk(int64_t n) { return (n + kBlock - 1) / kBlock; }
-template <int ND>
-__global__ __launch_bounds__(kSetupTailBS) void k_amg_setup_tail(const AmgLevD* __restrict__ lev, int l0, int nlev,
-                                                                 int coll) {
-  __shared__ double red[kSetupTailBS / 64];
-  constexpr int64_t VB = kSetupTailBS / kBlock;
-  auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
-  for (int l = l0; l < nlev; ++l) {
-    const AmgLevD& L = lev[l];
-    const bool last = L.coarsest || l + 1 >= nlev;
-    {  // D⁻¹ and the Gershgorin bound of level l
-      double g = 0.0;
-      for (int64_t r0 = 0; r0 < L.A.n; r0 += kSetupTailBS)
-        g = fmax(g, dinv_row<ND, false>(L, SellOp{}, nullptr, 0.0, r0 + threadIdx.x));
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
-      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double m = red[0];
-        for (int k = 1; k < kSetupTailBS / 64; ++k) m = fmax(m, red[k]);
-        L.omega[1] = m;
-      }
-      __syncthreads();
-    }
-    // P_l values, Ã_l, R̂_{l−1}
-    if (!last && L.P.wmax > 0)
-      for (int64_t vb = 0, nb = nslot_blk(L.P.rg.p1 - L.P.rg.p0); vb < nb; vb += VB) pvals_body<ND>(L, vb);
-    if (compact(l))
-      for (int64_t vb = 0, nb = nslot_blk(L.A.npos); vb < nb; vb += VB) atv_body<ND>(L, vb);
-    if (l > 0 && compact(l - 1))
-      for (int64_t vb = 0, nb = nslot_blk(lev[l - 1].RT.npos); vb < nb; vb += VB) rtv_body<ND>(lev[l - 1], L, vb);
-    __syncthreads();
-    if (last) break;
-    // A_l·P_l (with P̃_l when it shares A·P's layout), then A_{l+1} (and P̃_l otherwise)
-    const bool ptv = compact(l) && L.PT.npos == L.AP.npos;
-    {
-      const int64_t nb = nrow_blk(max(L.AP.rg.p1 - L.AP.rg.p0, L.R.rg.p1 - L.R.rg.p0));
-      for (int64_t vb = 0; vb < nb; vb += VB) {
-        if (ptv) ap_body<ND, true>(L, vb);
-        else ap_body<ND, false>(L, vb);
-      }
-    }
-    __syncthreads();
-    for (int64_t vb = 0, nb = nrow_blk(L.ac_rg.p1 - L.ac_rg.p0); vb < nb; vb += VB) ac_body<ND>(L, lev[l + 1].A, vb);
-    if (compact(l) && !ptv)
-      for (int64_t vb = 0, nb = nslot_blk(L.PT.npos); vb < nb; vb += VB) ptv_body<ND>(L, vb);
-    __syncthreads();
-  }
-  if (coll <= 0) return;
-  for (int l = nlev - 2; l >= max(coll, l0); --l) {  // deepest first: T_l needs V_{l+1}
-    const AmgLevD& L = lev[l];
-    if (!L.collapsed) return;
-    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
-    for (int64_t vb = 0, nb = nrow_blk(L.CT.npos); vb < nb; vb += VB) tv_body<ND>(L, vnext, vb);
-    __syncthreads();
-    for (int64_t vb = 0, nb = nrow_blk(L.CV.npos); vb < nb; vb += VB) vv_body<ND>(L, vb);
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------
 // V-cycle (f32; level 0 reads r and writes u in f64)
 // ---------------------------------------------------------------------------
@@ -704,8 +634,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     vload<ND>(L.x, ii, x);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = x[a] + x[a];
-    if (L.nt) sell_mac<ND, true, KF, false, true>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
-    else sell_mac<ND, true, KF>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
+    sell_mac<ND, true, KF>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
     if (i < n && run) vstore<ND>(L.t, i, y);
   }
 }
@@ -937,94 +866,6 @@ __global__ __launch_bounds__(kTailBS) void k_amg_tail_lds(const TailLevels tl, i
   }
 }
 
-// The compact cycle's tail (k_amg_down / k_amg_up of levels [l0, nlev) in ONE
-// workgroup, their vectors in LDS).  A down phase sweeps the next level's rows
-// (R̂ x) and then this level's (c), a wave never straddling the two.  Up to
-// kCTailLdsMax bytes: MI355X has 160 KB of LDS.
-constexpr int64_t kCTailLdsMax = 160 * 1024;
-template <int ND>
-__device__ __forceinline__ void ctail_down(const AmgLevD& L, const float* x, float* c, float* nx) {
-  const int64_t nc = L.RT.n, nf = L.A.n, nc64 = (nc + 63) & ~(int64_t)63;
-  for (int64_t r0 = 0; r0 < nc64 + nf; r0 += kTailBS) {
-    const int64_t k = r0 + threadIdx.x, wave0 = r0 + (threadIdx.x & ~63);
-    if (wave0 >= nc64 + nf) break;
-    int64_t base;
-    int w;
-    if (wave0 < nc64) {  // coarse row I: x' = R̂ x
-      const int64_t I = k, Ic = I < nc ? I : nc - 1;
-      slice_of(L.RT, Ic, base, w);
-      float xc[ND];
-#pragma unroll
-      for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
-      sell_mac<ND, false, 3>(L.RT.col, L.RT.val32, L.RT.npos, base, w, x, xc);
-      if (I < nc) vstore<ND>(nx, I, xc);
-    } else {  // fine row i: c = 2x − Ã x
-      const int64_t i = k - nc64, ii = i < nf ? i : nf - 1;
-      slice_of(L.A, ii, base, w);
-      float xv[ND], y[ND];
-      vload<ND>(x, ii, xv);
-#pragma unroll
-      for (int a = 0; a < ND; ++a) y[a] = xv[a] + xv[a];
-      sell_mac<ND, true, 3>(L.A.col, L.A.at32, L.A.npos, base, w, x, y);
-      if (i < nf) vstore<ND>(c, i, y);
-    }
-  }
-}
-template <int ND>
-__device__ __forceinline__ void ctail_up(const AmgLevD& L, const float* c, const float* src, float* e) {
-  const int64_t n = L.PT.n;
-  for (int64_t r0 = 0; r0 < n; r0 += kTailBS) {
-    const int64_t a = r0 + threadIdx.x;
-    if (r0 + (threadIdx.x & ~63) >= n) break;
-    const int64_t aa = a < n ? a : n - 1;
-    int64_t base;
-    int w;
-    slice_of(L.PT, aa, base, w);
-    const int64_t i = L.pt_row[aa];
-    float y[ND];
-    vload<ND>(c, i, y);
-    sell_mac<ND, false, 3>(L.PT.col, L.PT.val32, L.PT.npos, base, w, src, y);
-    if (a < n) vstore<ND>(e, i, y);
-  }
-}
-template <int ND>
-__device__ __forceinline__ int64_t ctail_lds_off(const AmgLevD* __restrict__ lev, int l, int l0) {
-  int64_t off = 0;
-  for (int m = l0; m < l; ++m) off += 2 * ND * lev[m].A.n;
-  return off;
-}
-// LDS per level: x then c (a level's output e overwrites its x, dead after
-// its down sweep; the coarsest level's output is its x)
-template <int ND>
-__global__ __launch_bounds__(kTailBS) void k_amg_ctail_lds(const TailLevels tl, int l0, int nlev,
-                                                           const int32_t* gate) {
-  extern __shared__ float sm[];
-  if (gated(gate)) return;
-  const AmgLevD* lev = tl.lev - l0;
-  {
-    const AmgLevD G = lev[l0];
-    for (int64_t k = threadIdx.x; k < ND * G.A.n; k += kTailBS) sm[k] = G.x[k];
-  }
-  __syncthreads();
-  for (int l = l0; l + 1 < nlev; ++l) {
-    const AmgLevD L = lev[l];
-    float* v = sm + ctail_lds_off<ND>(lev, l, l0);  // x c of level l
-    ctail_down<ND>(L, v, v + ND * L.A.n, v + 2 * ND * L.A.n);
-    __syncthreads();
-  }
-  for (int l = nlev - 2; l >= l0; --l) {
-    const AmgLevD L = lev[l];
-    float* v = sm + ctail_lds_off<ND>(lev, l, l0);
-    const float* src = v + 2 * ND * L.A.n;  // level l+1's output, held over its x
-    if (l > l0) {
-      ctail_up<ND>(L, v + ND * L.A.n, src, v);
-      __syncthreads();
-    } else {
-      ctail_up<ND>(L, v + ND * L.A.n, src, L.e);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // CG (f64)
 // ---------------------------------------------------------------------------
@@ -1081,8 +922,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
     vload<ND>(cg.r, ii, r);
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    if (cg.nt) sell_mac<ND, false, KW, true, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
-    else sell_mac<ND, false, KW, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
+    sell_mac<ND, false, KW, true>(L0.A.col, L0.A.sym, L0.A.npos, base, w, cg.u, y);
     if (i < cg.lo || i >= cg.hi) continue;
     if constexpr (DIST) {  // couplings to free rows of other partitions: K_ig u_g
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
@@ -1302,16 +1142,11 @@ static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int c
 // k_amg_a0's partner) instead of seven
 static int64_t slot_blocks(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
 template <int ND>
-static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, const AmgLevD* levd, int stail) {
+static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
   auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
   for (int l = 0; l < nlev; ++l) {
     const AmgLevD& L = lev[l];
     if (L.A.n <= 0) return;
-    if (l > 0 && l == stail && levd) {  // the small levels (and their collapse products) in one workgroup
-      hipLaunchKernelGGL(k_amg_setup_tail<ND>, dim3(1), dim3(kSetupTailBS), 0, s, levd, l, nlev, coll);
-      collapse_setup_nd<ND>(s, lev, nlev, coll, stail);
-      return;
-    }
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0)
       hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
@@ -1334,10 +1169,9 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);
 }
-void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll, const AmgLevD* levd,
-                            int stail) {
-  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll, levd, stail);
-  else setup_fused_nd<3>(s, lev, nlev, coll, levd, stail);
+void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
+  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll);
+  else setup_fused_nd<3>(s, lev, nlev, coll);
 }
 template <int ND>
 static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
@@ -1431,22 +1265,13 @@ int amg_down_lanes(const AmgLevD& L) {
 // one lane per P̃ row up to a mean width of 8 (measured: C5 iteration 736 µs
 // at 1 lane against 759 at 2 and 845 at 4, C3 71.9 / 75.2 / 83.6)
 int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, L.ulanes, 8.0, 16.0); }
-// the down sweep's Ã rows in steps of 2U (K = 2); K = 3 (option amg_down_k)
-// measured slower even on C5's 11-block-wide level 1 (iteration 790 vs 760 µs)
-static int down_fine_k(const AmgLevD& L) { return L.dk > 0 ? L.dk : 2; }
+// the down sweep's Ã rows in steps of 2U (K = 2; K = 3 measured slower even
+// on C5's 11-block-wide level 1: iteration 790 vs 760 µs)
 template <int ND>
 static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int S = amg_down_lanes(L);
   const int64_t gc = rows_grid(S * L.RT.n).x;
   const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
-  if (down_fine_k(L) == 3) {
-    if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-    else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-    else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-    else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-    else hipLaunchKernelGGL((k_amg_down<ND, 1, 3>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-    return;
-  }
   if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
@@ -1461,29 +1286,6 @@ static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, cons
   else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
 }
-// levels [tail, nlev) of the compact cycle in one workgroup (k_amg_ctail_lds)
-// when their vectors fit its LDS; returns whether it was launched
-template <int ND>
-static bool ctail_nd(hipStream_t s, const AmgLevD* lev, int nlev, int tail, const int32_t* gate) {
-  if (tail <= 0 || tail >= nlev - 1 || nlev - tail > kTailMaxLev || !lev[tail].tail_lds) return false;
-  TailLevels tl;
-  int64_t lds = 0;
-  for (int l = tail; l < nlev; ++l) {
-    tl.lev[l - tail] = lev[l];
-    lds += 2 * ND * lev[l].A.n * (int64_t)sizeof(float);
-  }
-  if (lds > kCTailLdsMax) return false;
-  static bool attr = false;  // dynamic LDS above 64 KB must be allowed once per kernel
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_amg_ctail_lds<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kCTailLdsMax);
-    (void)hipFuncSetAttribute((const void*)k_amg_ctail_lds<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kCTailLdsMax);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_amg_ctail_lds<ND>, dim3(1), dim3(kTailBS), (size_t)lds, s, tl, tail, nlev, gate);
-  return true;
-}
 template <int ND>
 static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   const int64_t rows = ((L.CV.n + 63) / 64) * 64;
@@ -1496,8 +1298,7 @@ static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);
 }
 template <int ND>
-static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, int tail,
-                       const int32_t* gate, int l0) {
+static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const int32_t* gate, int l0) {
   if (cg.coll > l0 && cg.coll < nlev - 1 && lev[cg.coll].collapsed && lev[cg.coll].CV.n > 0) {
     const int kc = cg.coll;
     for (int l = l0; l < kc; ++l) down_nd<ND>(s, lev[l], lev[l + 1], gate);
@@ -1505,15 +1306,8 @@ static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg&
     for (int l = kc - 1; l >= l0; --l) up_te<ND, float>(s, lev[l], lev[l + 1], l == 0 ? cg.u : lev[l].e, gate);
     return;
   }
-  int top = nlev - 1;  // levels [top, nlev) run in the tail launch
-  if (tail > l0) {
-    // the tail needs its levels' vectors to fit LDS: probe from the requested level down
-    int64_t lds = 0;
-    for (int l = tail; l < nlev; ++l) lds += 2 * ND * lev[l].A.n * (int64_t)sizeof(float);
-    if (lds <= kCTailLdsMax && tail < nlev - 1 && nlev - tail <= kTailMaxLev && lev[tail].tail_lds) top = tail;
-  }
+  const int top = nlev - 1;  // the coarsest level's output is its x
   for (int l = l0; l < top; ++l) down_nd<ND>(s, lev[l], lev[l + 1], gate);
-  if (top < nlev - 1) ctail_nd<ND>(s, lev, nlev, top, gate);
   for (int l = top - 1; l >= l0; --l) {
     if (l == 0) up_te<ND, float>(s, lev[0], lev[1], cg.u, gate);
     else up_te<ND, float>(s, lev[l], lev[l + 1], lev[l].e, gate);
@@ -1532,21 +1326,7 @@ template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
                       int tail, const int32_t* gate, int l0) {
   if (cg.cycle == 1 && amg_compact_ok(lev, nlev, l0)) {
-    compact_nd<ND>(s, lev, nlev, cg, cg.ctail, gate, l0);
-    return;
-  }
-  // levels [deep, nlev) in the persistent launch (amg_deep.hip), if they fit it
-  const int deep = cg.deep > 0 ? (cg.deep > l0 ? cg.deep : (l0 > 0 ? l0 : 1)) : 0;
-  if (deep > 0 && deep < nlev - 1 && cg.deep_bar && amg_deep_fits(lev, nlev, deep)) {
-    for (int l = l0; l < deep; ++l) {
-      resid_nd<ND>(s, lev, l, cg, gate);
-      launch_restrict<ND>(s, lev[l], lev[l + 1], gate);
-    }
-    launch_amg_deep(s, ND, lev, nlev, deep, cg, gate);
-    for (int l = deep - 1; l >= l0; --l) {
-      prolong_nd<ND>(s, lev, l, gate);
-      post_nd<ND>(s, lev, l, cg, gate);
-    }
+    compact_nd<ND>(s, lev, nlev, cg, gate, l0);
     return;
   }
   if (tail > 0 && tail < l0) tail = l0;

@@ -68,7 +68,6 @@ struct AmgLevD {
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
-  int dk = 0;        // compact down sweep: Ã step width K (0: by A's mean width)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   // level 0 of a hierarchy kept over element failures: rows of floating
@@ -92,7 +91,6 @@ struct AmgLevD {
   // restriction R̂ = s' D'⁻¹ P̃ᵀ D / ω (RT.val32; s' = ω' or 1 on the coarsest
   // level), formed by launch_amg_compact_setup once every level is set up
   int compact = 0;
-  int nt = 0;  // the compact sweeps stream this level's Ã with non-temporal loads
   AmgMatD PT, RT;
   const int32_t* pt_row = nullptr;  // PT row → level row (P̃ has A·P's row order)
   const int32_t* pt_ap = nullptr;
@@ -130,18 +128,10 @@ struct AmgCg {
   double* w = nullptr;
   float* u = nullptr;   // level 0's V-cycle output: the f32 cycle's values, stored
                         // exactly (half the bytes of f64 for every gather of u)
-  // the persistent deep-level V-cycle (amg_deep.hip): levels [deep, nlev) in
-  // ONE launch of deep_wgs workgroups (deep = 0: per-level launches and the
-  // single-workgroup tail); deep_bar: its barrier words (zero between launches)
-  int deep = 0;
-  int deep_wgs = 0;
-  unsigned* deep_bar = nullptr;
   // 1: the compact cycle (two sweeps per level, AmgLevD::PT) where every
   // level of the cycle has it (compact set: unsplit levels); 0: four steps
   int cycle = 0;
-  int ctail = 0;
   int coll = 0;  // the compact cycle's collapsed level kc (0: none)
-  int nt = 0;  // the SpMV w = A_0 u streams A_0 with non-temporal loads (u stays in L2)  // the compact cycle's single-workgroup LDS tail: its first level (0: none)
 };
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered
@@ -178,10 +168,7 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0);
 // the levels' setup (after launch_amg_a0) and the compact operators in one
 // sequence, the compact parts fused into the Galerkin chain's launches
-// levd / stail: the device copy of the level views and the first level whose
-// setup runs in one workgroup (k_amg_setup_tail; 0: none)
-void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll,
-                            const AmgLevD* levd = nullptr, int stail = 0);
+void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).
@@ -213,16 +200,6 @@ int amg_op_lanes(const AmgLevD& L);
 int amg_down_lanes(const AmgLevD& L);
 int amg_up_lanes(const AmgLevD& L);
 bool amg_compact_ok(const AmgLevD* lev, int nlev, int l0);
-// ---- the deep-level V-cycle in one persistent launch (amg_deep.hip) --------
-// levels [l0, nlev) of the cycle on level l0's b, x (output: its e), deep_wgs
-// workgroups synchronised by grid barriers on deep_bar.  False (nothing
-// launched) when the levels do not fit the launch (kDeepMaxLev, row ranges).
-constexpr int kDeepMaxLev = 8;
-constexpr int kDeepBarWords = 320;     // 8 shards + done + timeout, 128 B apart
-constexpr int kDeepTimeoutWord = 288;  // sticky: a barrier wait gave up
-bool amg_deep_fits(const AmgLevD* lev, int nlev, int l0);
-bool launch_amg_deep(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int l0, const AmgCg& cg,
-                     const int32_t* gate);
 // first level l ≥ 1 (above the coarsest) with at most max_rows rows, or 0
 int amg_tail_level(const int64_t* rows, int nlev, int64_t max_rows);
 // ---- CG (single-reduction, as cg.hip) ---------------------------------------

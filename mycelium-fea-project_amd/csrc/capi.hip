@@ -133,10 +133,8 @@ struct Part {
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
   DevBuf<AmgLevD> amg_levd;          // … and their device copy (the setup tail reads it)
-  int amg_stail = 0;                 // first level of the one-workgroup setup tail (0: none)
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
-  int amg_first = 1;                 // first level the tail / the deep launch may start at (not split)
-  DevBuf<unsigned> amg_deep_bar;     // the deep launch's barrier words (amg_deep.hip)
+  int amg_first = 1;                 // first level the four-step tail may start at (not split)
   AmgCg amg_cg;
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
@@ -231,20 +229,11 @@ struct mfea_handle {
   int64_t opt_amg_collapse_mb = 32;     // … budget: the collapsed operator's bytes
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
-  int64_t opt_amg_stail_rows = 0;  // GAMG setup: levels of at most this many rows in one workgroup (0: off; measured slower)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
-  int opt_amg_down_k = 0;    // GAMG compact down sweep: Ã step width K (0: by width, 2, 3)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
-  int opt_amg_nt = 0;  // GAMG: level-0 operators streamed non-temporal (-1: when A_0 outgrows the
-                       // Infinity Cache, 0 never, 1 always); measured slower at C3 and C5: off
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
-  int64_t opt_amg_ctail_rows = 0;  // GAMG compact cycle: levels of at most this many rows in one workgroup
-                                   // (measured slower than their launches at C2 / C3: off)
   int opt_amg_cycle = 1;       // GAMG: 1 the compact V-cycle (two sweeps per level), 0 four steps
-  int opt_amg_deep = 0;        // GAMG: first level of the persistent deep launch (-1: by amg_deep_rows, 0: none)
-  int64_t opt_amg_deep_rows = 262144;  // GAMG: the deep launch starts at the first level of at most this many rows
-  int opt_amg_deep_wgs = 128;  // GAMG: workgroups of the deep launch (8..256)
   double opt_part_slack = 0.35;  // partition boundaries: min-cut search window (fraction of a strip)
   // GAMG over element failures: 1 keep the hierarchy (floating pieces masked)
   // until a solve needs more than amg_rebuild_pct % of the iterations of the
@@ -1081,43 +1070,6 @@ AmgStrength amg_strength(const mfea_handle* h) {
   return st;
 }
 
-// The persistent deep-level launch of the V-cycle (amg_deep.hip): its first
-// level (option amg_deep, or the first unsplit level of at most amg_deep_rows
-// rows), its workgroups and its barrier words (zeroed once; every launch
-// leaves them zero).
-// non-temporal level-0 operator streams (option amg_nt), meant to keep the
-// gathered u / x in the XCD's L2 while A_0 streams past: measured slower at
-// both sizes (SpMV C3 9.7 → 12.8 µs, C5 215 → 244 µs), so off by default
-void set_amg_nt(mfea_handle* h, Part& pt) {
-  if (pt.amg_lev.empty()) return;
-  const AmgLevD& L0 = pt.amg_lev[0];
-  const double a0_bytes = (double)L0.A.npos * (8.0 * pt.amg.nd * (pt.amg.nd + 1) / 2 + 4.0);
-  const int on = h->opt_amg_nt < 0 ? (a0_bytes > 128e6 ? 1 : 0) : h->opt_amg_nt;
-  pt.amg_cg.nt = on;
-  pt.amg_lev[0].nt = on;
-}
-
-int set_amg_deep(mfea_handle* h, Part& pt) {
-  const int nlev = (int)pt.amg_lev.size();
-  int deep = 0;
-  if (h->opt_amg_deep > 0) deep = std::max(pt.amg_first, h->opt_amg_deep);
-  else if (h->opt_amg_deep < 0)
-    for (int l = pt.amg_first; l + 1 < nlev; ++l)
-      if (pt.amg_lev[l].A.n <= h->opt_amg_deep_rows) {
-        deep = l;
-        break;
-      }
-  if (deep >= nlev - 1 || !amg_deep_fits(pt.amg_lev.data(), nlev, deep)) deep = 0;
-  if (deep > 0 && !pt.amg_deep_bar.ptr) {
-    HIPC(pt.amg_deep_bar.alloc(kDeepBarWords));
-    HIPC(hipMemset(pt.amg_deep_bar.ptr, 0, kDeepBarWords * sizeof(unsigned)));
-  }
-  pt.amg_cg.deep = deep;
-  pt.amg_cg.deep_wgs = h->opt_amg_deep_wgs;
-  pt.amg_cg.deep_bar = pt.amg_deep_bar.ptr;
-  return 0;
-}
-
 // w = A u's step width: K = 2 (slices up to 2U blocks in one round trip of
 // column loads and gathers, more VGPRs) once level 0's mean slice width
 // passes U = 4 blocks
@@ -1235,7 +1187,6 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
-      d.dk = h->opt_amg_down_k;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, true, true);
@@ -1314,20 +1265,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_tail = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_tail_rows) : 0;
     if (pt.amg_tail > 0) pt.amg_tail += first - 1;
     pt.amg_first = first;
-    int ct = first < nlev ? amg_tail_level(rows.data() + first - 1, nlev - first + 1, h->opt_amg_ctail_rows) : 0;
-    pt.amg_cg.ctail = ct > 0 ? ct + first - 1 : 0;
   }
-  RC(set_amg_deep(h, pt));
-  set_amg_nt(h, pt);
-  // the numeric setup's one-workgroup tail: the compact cycle's levels of at
-  // most amg_stail_rows rows (one partition's hierarchy only)
-  pt.amg_stail = 0;
-  if (!rk && h->opt_amg_stail_rows > 0)
-    for (int l = 1; l < nlev; ++l)
-      if (pl.lev[l].A.n <= h->opt_amg_stail_rows) {
-        pt.amg_stail = l;
-        break;
-      }
   if (!rk && nlev > 1) {  // the floating-row mask (zero until ensure_amg fills it)
     HIPC(pt.amg_fmask.alloc(std::max<int64_t>(pl.lev[0].A.n, 1)));
     HIPC(hipMemsetAsync(pt.amg_fmask.ptr, 0, pt.amg_fmask.n, s));
@@ -1592,7 +1530,7 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
   const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
   if (compact && h->opt_amg_fuse_setup) {
-    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll, pt.amg_levd.ptr, pt.amg_stail);
+    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
     return;
   }
   for (int l = 0; l < nlev; ++l)
@@ -1618,7 +1556,7 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   k = fnv1a(k, &op, sizeof op);
   const void* ptrs[4] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, pt.amg_levd.ptr};
   k = fnv1a(k, ptrs, sizeof ptrs);
-  const int ints[5] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll, pt.amg_stail};
+  const int ints[4] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll};
   k = fnv1a(k, ints, sizeof ints);
   k = fnv1a(k, &reg, sizeof reg);
   if (!h->graph_setup || h->graph_setup_key != k) {
@@ -3155,7 +3093,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   } else if (n == "ell_maxg") h->opt_ell_maxg = value;
   else if (n == "ell_compact") { h->opt_ell_compact = value != 0; rebuild = true; }
   else if (n == "amg_tail_rows") { h->opt_amg_tail_rows = value; rebuild = true; }
-  else if (n == "amg_ctail_rows") { h->opt_amg_ctail_rows = value; rebuild = true; }
   else if (n == "amg_max_levels") {
     if (value < 1 || value > kAmgMaxLevels) return fail(MFEA_EINVAL, "amg_max_levels: 1..32");
     h->opt_amg_max_levels = (int)value;
@@ -3206,18 +3143,12 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_spatial = (int)value;
     rebuild = true;
   }
-  else if (n == "amg_stail_rows") {
-    if (value < 0) return fail(MFEA_EINVAL, "amg_stail_rows: >= 0 (0: no one-workgroup setup tail)");
-    h->opt_amg_stail_rows = value;
-    rebuild = true;
-  }
-  else if (n == "amg_up_lanes" || n == "amg_down_k") {
-    const bool up = n == "amg_up_lanes";
-    if (up ? (value != 0 && value != 1 && value != 2 && value != 4) : (value != 0 && value != 2 && value != 3))
-      return fail(MFEA_EINVAL, up ? "amg_up_lanes: 0 (by width), 1, 2 or 4" : "amg_down_k: 0 (by width), 2 or 3");
-    (up ? h->opt_amg_up_lanes : h->opt_amg_down_k) = (int)value;
+  else if (n == "amg_up_lanes") {
+    if (value != 0 && value != 1 && value != 2 && value != 4)
+      return fail(MFEA_EINVAL, "amg_up_lanes: 0 (by width), 1, 2 or 4");
+    h->opt_amg_up_lanes = (int)value;
     for (auto& pp : h->parts)
-      for (auto& L : pp->amg_lev) (up ? L.ulanes : L.dk) = (int)value;
+      for (auto& L : pp->amg_lev) L.ulanes = (int)value;
   }
   else if (n == "amg_big_chunk") {
     if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
@@ -3226,11 +3157,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   else if (n == "amg_fuse_setup") {
     if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
     h->opt_amg_fuse_setup = (int)value;
-  }
-  else if (n == "amg_nt") {
-    if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_nt: -1 (by size), 0 or 1");
-    h->opt_amg_nt = (int)value;
-    for (auto& pp : h->parts) set_amg_nt(h, *pp);
   }
   else if (n == "amg_theta_ppm") {
     if (value < 0 || value > 1000000) return fail(MFEA_EINVAL, "amg_theta_ppm: 0..1000000");
@@ -3248,21 +3174,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
         HIPC(hipMemcpy(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
                        hipMemcpyHostToDevice));
     }
-  }
-  else if (n == "amg_deep" || n == "amg_deep_rows" || n == "amg_deep_wgs") {
-    if (n == "amg_deep") {
-      if (value < -1 || value >= kAmgMaxLevels) return fail(MFEA_EINVAL, "amg_deep: -1 (by amg_deep_rows), 0 (none) or a level");
-      h->opt_amg_deep = (int)value;
-    } else if (n == "amg_deep_rows") {
-      if (value < 0) return fail(MFEA_EINVAL, "amg_deep_rows: >= 0");
-      h->opt_amg_deep_rows = value;
-    } else {
-      if (value < 8 || value > 256) return fail(MFEA_EINVAL, "amg_deep_wgs: 8..256");
-      h->opt_amg_deep_wgs = (int)value;
-    }
-    RC(set_device(h));
-    for (auto& pp : h->parts)
-      if (!pp->amg_lev.empty()) RC(set_amg_deep(h, *pp));
   }
   else if (n == "dist_timeout_ms") h->dist_timeout_s = value / 1e3;
   else if (n == "amg_reuse") {
@@ -3426,7 +3337,6 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "ell_maxg") *value = h->opt_ell_maxg;
   else if (n == "ell_compact") *value = h->opt_ell_compact;
   else if (n == "amg_tail_rows") *value = h->opt_amg_tail_rows;
-  else if (n == "amg_ctail_rows") *value = h->opt_amg_ctail_rows;
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
   else if (n == "amg_w_block") *value = h->opt_amg_w_block;
   else if (n == "amg_w_k") *value = h->opt_amg_w_k;
@@ -3435,12 +3345,9 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
-  else if (n == "amg_nt") *value = h->opt_amg_nt;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
-  else if (n == "amg_down_k") *value = h->opt_amg_down_k;
-  else if (n == "amg_stail_rows") *value = h->opt_amg_stail_rows;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;
   else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;
@@ -3456,23 +3363,6 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   }
   else if (n == "amg_spatial_chosen") {  // read-only: partition 0's plan is in Z-order
     *value = h->parts.empty() ? 0 : (h->parts[0]->amg.spatial ? 1 : 0);
-  }
-  else if (n == "amg_deep") *value = h->opt_amg_deep;
-  else if (n == "amg_deep_rows") *value = h->opt_amg_deep_rows;
-  else if (n == "amg_deep_wgs") *value = h->opt_amg_deep_wgs;
-  else if (n == "amg_deep_level") {  // read-only: the first level of partition 0's deep launch (0: none)
-    *value = h->parts.empty() ? 0 : h->parts[0]->amg_cg.deep;
-  }
-  else if (n == "amg_deep_timeouts") {  // read-only: a deep launch gave up a barrier wait (never expected)
-    *value = 0;
-    RC(set_device(h));
-    for (auto& pp : h->parts)
-      if (pp->amg_deep_bar.ptr) {
-        unsigned w[kDeepBarWords];
-        HIPC(hipStreamSynchronize(h->stream));
-        HIPC(hipMemcpy(w, pp->amg_deep_bar.ptr, sizeof w, hipMemcpyDeviceToHost));
-        *value += w[kDeepTimeoutWord] != 0;
-      }
   }
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;

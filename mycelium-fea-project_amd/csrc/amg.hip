@@ -41,34 +41,6 @@ namespace mfea {
 // ---------------------------------------------------------------------------
 // numeric setup (f64, with f32 copies for the V-cycle)
 // ---------------------------------------------------------------------------
-// A_0 off-diagonal blocks, one position per thread: Σ of the listed SELL
-// slots' K_ij (= −S_e) in slot order.  Diagonal and padding positions have
-// empty lists; the diagonal block is written by k_amg_dinv<ND, true>.
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_a0(AmgMatD A, SellOp sop, const int32_t* __restrict__ ptr,
-                                                   const int32_t* __restrict__ lst, double* omega0) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) omega0[1] = 0.0;  // level 0's bound, max'ed by k_amg_dinv
-  const int64_t q = A.rg.p0 + xcd_block() * kBlock + threadIdx.x;
-  if (q >= A.rg.p1 || !pos_mine(A.rg, q)) return;
-  const int t0 = ptr[q], t1 = ptr[q + 1];
-  if (t0 == t1) return;
-  double m[ND * ND];
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
-  for (int t = t0; t < t1; ++t) {
-    double s6[6], e[ND * ND];
-    const int64_t g = lst[t];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) s6[c] = sop.val[(int64_t)c * sop.G + g];
-    sym_to<ND>(s6, e);
-#pragma unroll
-    for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
-  }
-  bstore<ND>(A.val, A.npos, q, m);
-  bstore_sym<ND>(A.sym, q, m);
-  bstore_sym<ND>(A.sym32, q, m);
-}
-
 // Block-Jacobi inverse, Gershgorin bound per block.  L0: level 0, whose
 // diagonal block K_ii + reg·I (Pattern row row0[i]) is formed and stored here.
 template <int ND, bool L0>
@@ -90,18 +62,19 @@ __device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, 
         s6[3] += reg;
         s6[5] += reg;
         sym_to<ND>(s6, D);
-        bstore<ND>(A.val, A.npos, base, D);
+        bstore<ND>(A.val32, A.npos, base, D);
         bstore_sym<ND>(A.sym, base, D);
         bstore_sym<ND>(A.sym32, base, D);
       } else {
-        bload<ND>(A.val, A.npos, base, D);
+        bload<ND>(A.val32, A.npos, base, D);
       }
       binv<ND>(D, Di);
+      if (L.dinv) {  // f64 copy: a one-level hierarchy's exact block solve (k_amg_cg_init)
 #pragma unroll
-      for (int c = 0; c < ND * ND; ++c) {
-        L.dinv[i * (ND * ND) + c] = Di[c];
-        L.dinv32[i * (ND * ND) + c] = (float)Di[c];
+        for (int c = 0; c < ND * ND; ++c) L.dinv[i * (ND * ND) + c] = Di[c];
       }
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) L.dinv32[i * (ND * ND) + c] = (float)Di[c];
       double rs[ND];
 #pragma unroll
       for (int a = 0; a < ND; ++a) rs[a] = 0.0;
@@ -113,7 +86,7 @@ __device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, 
 #pragma unroll
           for (int c = 0; c < ND * ND; ++c) m[c] = D[c];
         } else {
-          bload<ND>(A.val, A.npos, q, m);
+          bload<ND>(A.val32, A.npos, q, m);
         }
 #pragma unroll
         for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
@@ -151,6 +124,110 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
 }
 
 
+// Level 0 in one row-wise pass (replaces k_amg_a0 + k_amg_dinv<ND, true>):
+// per row i, the diagonal K_ii + reg·I from the assembled diagonal, its exact
+// inverse, every off-diagonal block (Σ of the listed SELL slots' K_ij = −S_e,
+// slot order) stored as A_0's f64 symmetric / f32 blocks, and the Gershgorin
+// row sums of |D⁻¹ A_ij| accumulated from the blocks in registers — A_0 is
+// written once and never read back here.  omega0[1] must be zero before the
+// launch (launch_amg_a0 clears it); the blocks' maxima meet by atomic max.
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
+                                                       const int32_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ lst, double reg) {
+  __shared__ double red[kBlock / 64];
+  const AmgMatD& A = L.A;
+  const int64_t i = A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  double g = 0.0;
+  if (i - (threadIdx.x & 63) < A.rg.hi) {
+    int64_t base;
+    int w;
+    slice_of(A, i, base, w);
+    if (i >= A.rg.lo && i < A.rg.hi) {
+      double s6[6], D[ND * ND], Di[ND * ND];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
+      s6[0] += reg;
+      s6[3] += reg;
+      s6[5] += reg;
+      sym_to<ND>(s6, D);
+      bstore<ND>(A.val32, A.npos, base, D);
+      bstore_sym<ND>(A.sym, base, D);
+      bstore_sym<ND>(A.sym32, base, D);
+      binv<ND>(D, Di);
+      if (L.dinv) {  // f64 copy: a one-level hierarchy's exact block solve (k_amg_cg_init)
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) L.dinv[i * (ND * ND) + c] = Di[c];
+      }
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) L.dinv32[i * (ND * ND) + c] = (float)Di[c];
+      double rs[ND];
+      {
+        double pm[ND * ND];
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+        mm_acc<ND>(Di, D, pm);
+#pragma unroll
+        for (int a = 0; a < ND; ++a) {
+          rs[a] = 0.0;
+#pragma unroll
+          for (int b = 0; b < ND; ++b) rs[a] += fabs(pm[a * ND + b]);
+        }
+      }
+      constexpr int U = 4;  // slots whose lists are in flight together
+      for (int k0 = 1; k0 < w; k0 += U) {
+        int32_t t0[U], t1[U];
+        int64_t q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          q[u] = base + (int64_t)(k0 + u < w ? k0 + u : k0) * 64;
+          t0[u] = k0 + u < w ? ptr[q[u]] : 0;
+          t1[u] = k0 + u < w ? ptr[q[u] + 1] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (t0[u] == t1[u]) continue;  // padding (or past the row)
+          double m[ND * ND];
+#pragma unroll
+          for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+          for (int t = t0[u]; t < t1[u]; ++t) {
+            double v6[6], e[ND * ND];
+            const int64_t gs = lst[t];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
+            sym_to<ND>(v6, e);
+#pragma unroll
+            for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+          }
+          bstore<ND>(A.val32, A.npos, q[u], m);
+          bstore_sym<ND>(A.sym, q[u], m);
+          bstore_sym<ND>(A.sym32, q[u], m);
+          double pm[ND * ND];
+#pragma unroll
+          for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+          mm_acc<ND>(Di, m, pm);
+#pragma unroll
+          for (int a = 0; a < ND; ++a)
+#pragma unroll
+            for (int b = 0; b < ND; ++b) rs[a] += fabs(pm[a * ND + b]);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < ND; ++a) g = fmax(g, rs[a]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mx = red[0];
+    for (int k = 1; k < kBlock / 64; ++k) mx = fmax(mx, red[k]);
+    atomicMax(reinterpret_cast<unsigned long long*>(&L.omega[1]),
+              static_cast<unsigned long long>(__double_as_longlong(mx)));
+  }
+}
+
 // P values, one thread per position (slot_wave): every slot of a row in
 // flight at once instead of one after another.
 template <int ND>
@@ -167,9 +244,9 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   for (int c = 0; c < ND * ND; ++c) {
     S[c] = 0.0;
     pm[c] = 0.0;
-    Di[c] = L.dinv[i * (ND * ND) + c];
+    Di[c] = L.dinv32[i * (ND * ND) + c];
   }
-  list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val, L.A.npos, S);
+  list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val32, L.A.npos, S);
   mm_acc<ND>(Di, S, pm);
   const double om = amg_omega(L.omega);
 #pragma unroll
@@ -182,7 +259,6 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
   }
-  bstore<ND>(P.val, P.npos, q, pm);
   bstore<ND>(P.val32, P.npos, q, pm);
 }
 template <int ND>
@@ -199,7 +275,7 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   const int64_t qr = L.R.rg.p0 + k;
   if (qr < L.R.rg.p1 && L.R.col[qr] >= 0 && pos_mine(L.R.rg, qr)) {  // R = Pᵀ (f32) in R's own SELL layout
     double p[ND * ND], t[ND * ND];
-    bload<ND>(L.P.val, L.P.npos, L.rp[qr], p);
+    bload<ND>(L.P.val32, L.P.npos, L.rp[qr], p);
 #pragma unroll
     for (int a = 0; a < ND; ++a)
 #pragma unroll
@@ -213,11 +289,11 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   for (int c = 0; c < ND * ND; ++c) C[c] = pm[c] = 0.0;
   if constexpr (PTV) {
     const int64_t r = 64 * (int64_t)L.PT.srow[q >> 6] + (q & 63);  // the A·P / P̃ row
-    dinv_load<ND>(L.dinv, L.pt_row[r], Di);
+    dinv_load<ND>(L.dinv32, L.pt_row[r], Di);
     const int32_t qp = L.pt_p[q];
-    if (qp >= 0) bload<ND>(L.P.val, 0, qp, pm);
+    if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
   }
-  pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val, L.A.npos, L.P.val, L.P.npos, C);
+  pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val32, L.A.npos, L.P.val32, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
   if constexpr (PTV) {
     double m[ND * ND];
@@ -228,7 +304,6 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);
     bstore<ND>(L.PT.val32, 0, q, pm);
-    bstore<ND>(L.PT.val, 0, q, pm);
   }
 }
 template <int ND, bool PTV = false>
@@ -245,9 +320,9 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   if (!slot_wave(T, 0, T.npos / 64, q, i, k, blk) || i >= T.n || T.col[q] < 0) return;
   const int32_t qp = L.pt_p[q];
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
-  dinv_load<ND>(L.dinv, L.pt_row[i], Di);
+  dinv_load<ND>(L.dinv32, L.pt_row[i], Di);
   bload<ND>(L.apval, 0, L.pt_ap[q], ap);
-  if (qp >= 0) bload<ND>(L.P.val, 0, qp, pm);
+  if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
   else {
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
@@ -259,7 +334,6 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);
   bstore<ND>(T.val32, 0, q, pm);
-  bstore<ND>(T.val, 0, q, pm);
 }
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) { ptv_body<ND>(L, xcd_block()); }
@@ -276,9 +350,9 @@ __device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int
   const int32_t i = T.col[q];
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
-  bload<ND>(L.PT.val, 0, L.rt_pt[q], p);
-  dinv_load<ND>(N.dinv, J, Dn);
-  bload<ND>(L.A.val, 0, (int64_t)L.A.sptr[i >> 6] * 64 + (i & 63), D);
+  bload<ND>(L.PT.val32, 0, L.rt_pt[q], p);
+  dinv_load<ND>(N.dinv32, J, Dn);
+  bload<ND>(L.A.val32, 0, (int64_t)L.A.sptr[i >> 6] * 64 + (i & 63), D);
   const double sc = (N.coarsest ? 1.0 : amg_omega(N.omega)) / amg_omega(L.omega);
 #pragma unroll
   for (int a = 0; a < ND; ++a)
@@ -302,8 +376,8 @@ __device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
   int k;
   if (!slot_wave(A, 0, A.npos / 64, q, i, k, blk) || i >= A.n || A.col[q] < 0) return;
   double Di[ND * ND], m[ND * ND], o[ND * ND];
-  dinv_load<ND>(L.dinv, i, Di);
-  bload<ND>(A.val, 0, q, m);
+  dinv_load<ND>(L.dinv32, i, Di);
+  bload<ND>(A.val32, 0, q, m);
   const double om = amg_omega(L.omega);
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) o[c] = 0.0;
@@ -393,8 +467,7 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-  pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val, L.P.npos, L.apval, L.AP.npos, C);
-  bstore<ND>(Ac.val, Ac.npos, q, C);
+  pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val32, L.P.npos, L.apval, L.AP.npos, C);
   bstore<ND>(Ac.val32, Ac.npos, q, C);
 }
 template <int ND>
@@ -1088,8 +1161,8 @@ template <int ND>
 static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
                   const int32_t* a, double reg) {
   if (L0.A.n <= 0) return;
-  hipLaunchKernelGGL(k_amg_a0<ND>, rows_grid(L0.A.rg.npos()), dim3(kBlock), 0, s, L0.A, sop, p, a, L0.omega);
-  hipLaunchKernelGGL((k_amg_dinv<ND, true>), rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, reg);
+  (void)hipMemsetAsync(L0.omega + 1, 0, sizeof(double), s);  // level 0's bound, max'ed by the blocks
+  hipLaunchKernelGGL(k_amg_a0dinv<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
                    const int32_t* a0_ptr, const int32_t* a0_a, double reg) {

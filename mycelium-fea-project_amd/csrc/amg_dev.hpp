@@ -315,10 +315,10 @@ __device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t 
 // order, U pairs' loads in flight per step (every pair is two dependent hops:
 // index, then blocks).  Lists longer than 4 take steps of 8 (the Galerkin
 // product's lists run ≈ 2–30 pairs).
-template <int ND, bool TX, int U>
+template <int ND, bool TX, int U, class TX_, class TY_>
 __device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __restrict__ la,
-                                           const int32_t* __restrict__ lb, const double* __restrict__ X,
-                                           const double* __restrict__ Y, double* C) {
+                                           const int32_t* __restrict__ lb, const TX_* __restrict__ X,
+                                           const TY_* __restrict__ Y, double* C) {
   for (int t = t0; t < t1; t += U) {
     int32_t ia[U], ib[U];
 #pragma unroll
@@ -341,17 +341,17 @@ __device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __rest
     }
   }
 }
-template <int ND, bool TX>
+template <int ND, bool TX, class TX_, class TY_>
 __device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const int32_t* __restrict__ lb, const double* __restrict__ X,
-                                         int64_t /*nx*/, const double* __restrict__ Y, int64_t /*ny*/, double* C) {
+                                         const int32_t* __restrict__ lb, const TX_* __restrict__ X,
+                                         int64_t /*nx*/, const TY_* __restrict__ Y, int64_t /*ny*/, double* C) {
   if (t1 - t0 > 4) pair_sum_u<ND, TX, 8>(t0, t1, la, lb, X, Y, C);
   else pair_sum_u<ND, TX, 4>(t0, t1, la, lb, X, Y, C);
 }
 // S += Σ_t X[a_t] over one index list, in list order
-template <int ND, int U>
+template <int ND, int U, class TX_>
 __device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __restrict__ la,
-                                           const double* __restrict__ X, double* S) {
+                                           const TX_* __restrict__ X, double* S) {
   for (int t = t0; t < t1; t += U) {
     int32_t ia[U];
 #pragma unroll
@@ -367,9 +367,9 @@ __device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __rest
     }
   }
 }
-template <int ND>
+template <int ND, class TX_>
 __device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
-                                         const double* __restrict__ X, int64_t /*nx*/, double* S) {
+                                         const TX_* __restrict__ X, int64_t /*nx*/, double* S) {
   if (t1 - t0 > 4) list_sum_u<ND, 8>(t0, t1, la, X, S);
   else list_sum_u<ND, 4>(t0, t1, la, X, S);
 }

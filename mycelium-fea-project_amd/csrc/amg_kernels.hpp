@@ -78,7 +78,7 @@ struct AmgLevD {
   const int32_t* pv_a = nullptr;
   AmgMatD R;  // val32 = Pᵀ blocks in R's layout (setup)
   const int32_t* rp = nullptr;
-  double* apval = nullptr;
+  float* apval = nullptr;  // A_l·P_l blocks (f32 storage; the setup computes in f64)
   AmgMatD AP;  // pattern only (sptr, col) + npos; values in apval
   const int32_t* ap_ptr = nullptr;
   const int32_t* ap_a = nullptr;

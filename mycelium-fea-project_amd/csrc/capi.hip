@@ -1134,7 +1134,9 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     fp += amg_al(n);
     return p;
   };
-  // vals64: f64 values (setup / CG), vals32: the f32 V-cycle copy
+  // vals64: f64 values, vals32: f32 values (the numeric setup stores every
+  // hierarchy value in f32 — computing in f64 — and the V-cycle reads them;
+  // only A_0's symmetric blocks for the CG's w = A u stay f64)
   std::deque<std::vector<int32_t>> srows;  // alive until the copies below have run (the stream sync at the end)
   auto mat = [&](const SellPat& S, bool vals64, bool vals32) {
     AmgMatD m;
@@ -1168,14 +1170,14 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       AmgLevD& d = pt.amg_lev[l];
       const int64_t n = L.A.n;
       const int64_t lo = rk ? rk->lo[l] : 0, hi = rk ? rk->hi[l] : n;
-      d.A = mat(L.A, true, l > 0);
+      d.A = mat(L.A, false, true);
       d.A.rg = row_range(L.A, lo, hi);
       if (l == 0) {  // A_0: symmetric blocks for the CG and the level-0 V-cycle kernels
         const size_t ns = (size_t)nd * (nd + 1) / 2;
         d.A.sym = D(ns * d.A.npos);
         d.A.sym32 = F(ns * d.A.npos);
       }
-      d.dinv = D((size_t)nb2 * n);
+      d.dinv = l == 0 && nlev == 1 ? D((size_t)nb2 * n) : nullptr;  // one level: the exact block solve
       d.dinv32 = F((size_t)nb2 * n);
       d.omega = D(2);
       d.b = l ? F((size_t)nd * n) : nullptr;  // level 0 reads the CG's r
@@ -1189,7 +1191,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.ulanes = h->opt_amg_up_lanes;
       if (!L.coarsest) {
         d.agg = I(L.agg);
-        d.P = mat(L.P, true, true);
+        d.P = mat(L.P, false, true);
         d.P.rg = row_range(L.P, lo, hi);
         d.pv_ptr = I(L.pv.ptr);
         d.pv_a = I(L.pv.a);
@@ -1200,7 +1202,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         d.rp = I(L.rp);
         d.AP = mat(L.AP, false, false);
         d.AP.rg = row_range(L.AP, rk ? rk->aplo[l] : 0, rk ? rk->aphi[l] : L.AP.n);
-        d.apval = D((size_t)nb2 * d.AP.npos);
+        d.apval = F((size_t)nb2 * d.AP.npos);
         d.ap_ptr = I(L.ap.ptr);
         d.ap_a = I(L.ap.a);
         d.ap_b = I(L.ap.b);
@@ -1210,7 +1212,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         // the compact cycle's P̃ / R̃ (one partition's hierarchy only: the
         // distributed V-cycle exchanges per four-step step)
         if (!rk && L.PT.n == n) {
-          d.PT = mat(L.PT, true, true);  // f64 P̃ too: R̂ is formed from it
+          d.PT = mat(L.PT, false, true);
           d.A.at32 = F((size_t)nb2 * d.A.npos);
           d.PT.rg = row_range(L.PT, 0, n);
           d.pt_row = I(L.pt_row);
@@ -1931,15 +1933,13 @@ int enqueue_gamg_setup(mfea_handle* h, double reg) {
     RC(stage(kSetupP));
     if (split)
       RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_sp[l]; },
-            [l](Part& p) -> void* { return p.amg_lev[l].P.val; }, nb2, 8));
+            [l](Part& p) -> void* { return p.amg_lev[l].P.val32; }, nb2, 4));
     RC(stage(kSetupAP));
     if (split)
       RC(gx(h, [l](Part& p) -> const Part::XDev& { return p.xd_sap[l]; },
-            [l](Part& p) -> void* { return p.amg_lev[l].apval; }, nb2, 8));
+            [l](Part& p) -> void* { return p.amg_lev[l].apval; }, nb2, 4));
     RC(stage(kSetupAC));
     if (l + 1 == ns && ns < nlev) {  // level ns is replicated: gather its A
-      RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_sg; },
-            [ns](Part& p) -> void* { return p.amg_lev[ns].A.val; }, nb2, 8));
       RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_sg; },
             [ns](Part& p) -> void* { return p.amg_lev[ns].A.val32; }, nb2, 4));
     }
@@ -3291,14 +3291,16 @@ int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t
     const AmgLevD& d = pt.amg_lev[l];
     std::vector<double> v((size_t)w * L.A.n, 0.0);
     if (which == 4) {  // D⁻¹ blocks
-      HIPC(hipMemcpy(v.data(), d.dinv, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+      std::vector<float> f(v.size());
+      HIPC(hipMemcpy(f.data(), d.dinv32, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
     } else if (which == 5) {  // the Gershgorin bound g, every row
       double om[2];
       HIPC(hipMemcpy(om, d.omega, sizeof(om), hipMemcpyDeviceToHost));
       std::fill(v.begin(), v.end(), om[1]);
     } else if (which == 6) {  // diagonal blocks of A (slot 0 of every row)
-      std::vector<double> a((size_t)nd * nd * d.A.npos);
-      HIPC(hipMemcpy(a.data(), d.A.val, a.size() * sizeof(double), hipMemcpyDeviceToHost));
+      std::vector<float> a((size_t)nd * nd * d.A.npos);
+      HIPC(hipMemcpy(a.data(), d.A.val32, a.size() * sizeof(float), hipMemcpyDeviceToHost));
       for (int64_t i = 0; i < L.A.n; ++i)
         for (int c = 0; c < nd * nd; ++c) v[(size_t)nd * nd * i + c] = a[(size_t)nd * nd * L.A.pos(i, 0) + c];
     } else if (l == 0 && (which == 0 || which == 3)) {

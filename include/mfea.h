@@ -54,6 +54,16 @@ extern "C" {
                                    per-partition ones — per active set the faster of the
                                    two, measured (mfea_debug.h option "amg_dist") */
 
+#define MFEA_PC_SOR 3           /* `-pc_type sor`: SSOR (ω = 1, PETSc's default) on the
+                                   node blocks of K_ff + reg·I, block Jacobi over 256-row
+                                   blocks with multicolour sweeps inside each (PETSc's
+                                   SOR is processor-local in parallel); one partition */
+#define MFEA_PC_ICC 4           /* `-pc_type icc` (the reference source's default PCICC,
+                                   src/fea_petsc.cpp:331; also `ilu`, the same factor on
+                                   an SPD matrix): DIC(0) — incomplete block Cholesky
+                                   with A's off-diagonal blocks and a corrected diagonal —
+                                   in the same block / colour layout as MFEA_PC_SOR */
+
 /* stopping norm (mfea_solve_opts.norm) */
 #define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
 #define MFEA_NORM_PRECONDITIONED 1   /* ‖z‖₂ ≤ rtol·‖M⁻¹b‖₂ (PETSc KSPCG default)     */

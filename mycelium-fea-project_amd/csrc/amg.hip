@@ -37,6 +37,16 @@
 
 namespace mfea {
 
+// The numeric setup's block index.  x1 (levels of a few thousand rows,
+// AmgLevD::x1): the launch has 8× the blocks and only those dealt to XCD 0 work
+// (blocks are dealt round-robin over the 8 XCDs) — a small level's chain of
+// launches then reads what the previous launch wrote from the same L2 instead
+// of another XCD's.  Speed only; −1: this block has no work.
+__device__ __forceinline__ int64_t setup_block(int x1) {
+  if (!x1) return xcd_block();
+  return (blockIdx.x & 7) ? -1 : (int64_t)(blockIdx.x >> 3);
+}
+
 
 // ---------------------------------------------------------------------------
 // numeric setup (f64, with f32 copies for the V-cycle)
@@ -63,8 +73,8 @@ __device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, 
         s6[5] += reg;
         sym_to<ND>(s6, D);
         bstore<ND>(A.val32, A.npos, base, D);
-        bstore_sym<ND>(A.sym, base, D);
-        bstore_sym<ND>(A.sym32, base, D);
+        bstore_sym<ND>(A.sym, A.npos, base, D);
+        bstore_sym<ND>(A.sym32, A.npos, base, D);
       } else {
         bload<ND>(A.val32, A.npos, base, D);
       }
@@ -106,7 +116,9 @@ template <int ND, bool L0>
 __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
                                                      double reg) {
   __shared__ double red[kBlock / 64];
-  double g = dinv_row<ND, L0>(L, sop, row0, reg, L.A.rg.lo64() + xcd_block() * kBlock + threadIdx.x);
+  const int64_t xb = setup_block(L.x1);
+  if (xb < 0) return;
+  double g = dinv_row<ND, L0>(L, sop, row0, reg, L.A.rg.lo64() + xb * kBlock + threadIdx.x);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
@@ -152,8 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
       s6[5] += reg;
       sym_to<ND>(s6, D);
       bstore<ND>(A.val32, A.npos, base, D);
-      bstore_sym<ND>(A.sym, base, D);
-      bstore_sym<ND>(A.sym32, base, D);
+      bstore_sym<ND>(A.sym, A.npos, base, D);
+      bstore_sym<ND>(A.sym32, A.npos, base, D);
       binv<ND>(D, Di);
       if (L.dinv) {  // f64 copy: a one-level hierarchy's exact block solve (k_amg_cg_init)
 #pragma unroll
@@ -200,8 +212,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
             for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
           }
           bstore<ND>(A.val32, A.npos, q[u], m);
-          bstore_sym<ND>(A.sym, q[u], m);
-          bstore_sym<ND>(A.sym32, q[u], m);
+          bstore_sym<ND>(A.sym, A.npos, q[u], m);
+          bstore_sym<ND>(A.sym32, A.npos, q[u], m);
           double pm[ND * ND];
 #pragma unroll
           for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
@@ -262,7 +274,10 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   bstore<ND>(P.val32, P.npos, q, pm);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) { pvals_body<ND>(L, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_pvals(AmgLevD L) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) pvals_body<ND>(L, xb);
+}
 
 // One output block per thread (every SELL position of the product; pads
 // have empty lists): AP(i, J) = Σ A[a]·P[b].  The same grid writes R = Pᵀ.
@@ -307,7 +322,10 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   }
 }
 template <int ND, bool PTV = false>
-__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) { ap_body<ND, PTV>(L, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_ap(AmgLevD L) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) ap_body<ND, PTV>(L, xb);
+}
 
 // The compact cycle's transfers (amg.hpp AmgLevel::PT), after A·P:
 // P̃(i, J) = P(i, J) − ω D_i⁻¹ (A·P)(i, J) on A·P's pattern (f64, stored f32),
@@ -336,7 +354,10 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   bstore<ND>(T.val32, 0, q, pm);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) { ptv_body<ND>(L, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_ptv(AmgLevD L) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) ptv_body<ND>(L, xb);
+}
 // R̂ = s' D'_J⁻¹ P̃ᵀ D_i / ω in RT's own SELL layout, one thread per (row J,
 // slot) as k_amg_pvals: the scalings of x = ω D⁻¹ b on both sides folded in,
 // so the down sweep maps x_l to x_{l+1} directly (D_i: A's diagonal block,
@@ -367,7 +388,10 @@ __device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int
   bstore<ND>(T.val32, 0, q, o);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) { rtv_body<ND>(L, N, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_rtv(AmgLevD L, AmgLevD N) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) rtv_body<ND>(L, N, xb);
+}
 // Ã = ω D_i⁻¹ A_ij (compact cycle), one thread per (row, slot)
 template <int ND>
 __device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
@@ -387,7 +411,10 @@ __device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
   bstore<ND>(A.at32, 0, q, o);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) { atv_body<ND>(L, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_atv(AmgLevD L) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) atv_body<ND>(L, xb);
+}
 
 // the collapsed cycle (amg_collapse.cpp): T = V_{l+1} R̂ (a < 0: the
 // identity, V_coarsest) and V = 2I·[diag] − Ã + Σ P̃·T, one output block per
@@ -428,7 +455,8 @@ __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restric
 }
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext) {
-  tv_body<ND>(L, vnext, xcd_block());
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) tv_body<ND>(L, vnext, xb);
 }
 template <int ND>
 __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
@@ -457,7 +485,10 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
   bstore<ND>(L.CV.val32, 0, q, C);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) { vv_body<ND>(L, xcd_block()); }
+__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) vv_body<ND>(L, xb);
+}
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
 template <int ND>
@@ -473,7 +504,8 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
-  ac_body<ND>(L, Ac, xcd_block());
+  const int64_t xb = setup_block(L.x1);
+  if (xb >= 0) ac_body<ND>(L, Ac, xb);
 }
 
 // The compact cycle's operators fused into the Galerkin chain's launches (no
@@ -484,7 +516,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double
 // XCD-contiguous share (sub-ranges of one xcd_block() numbering).
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_fuse_p(AmgLevD L, AmgLevD Lp, int64_t g0, int64_t g1) {
-  const int64_t xb = xcd_block();
+  const int64_t xb = setup_block(L.x1);
+  if (xb < 0) return;
   if (xb < g0) pvals_body<ND>(L, xb);
   else if (xb < g1) atv_body<ND>(L, xb - g0);
   else rtv_body<ND>(Lp, L, xb - g1);
@@ -492,7 +525,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_fuse_p(AmgLevD L, AmgLevD Lp, in
 template <int ND>
 __global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, double* omega_next, int64_t g0) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;
-  const int64_t xb = xcd_block();
+  const int64_t xb = setup_block(L.x1);
+  if (xb < 0) return;
   if (xb < g0) ac_body<ND>(L, Ac, xb);
   else ptv_body<ND>(L, xb - g0);
 }
@@ -947,6 +981,7 @@ __global__ __launch_bounds__(kTailBS) void k_amg_tail_lds(const TailLevels tl, i
 // solve u = D⁻¹ r (f64, rounded to the f32 u) straight into the CG's u
 template <int ND>
 __device__ __forceinline__ void vcycle_entry(const AmgLevD& L0, const AmgCg& cg, int64_t i, const double* r) {
+  if (cg.sweep) return;  // the sweep kernel forms u from r
   if (L0.coarsest) {
     double u[ND];
     dinv_apply<ND>(L0.dinv, L0.A.n, i, 1.0, r, u);
@@ -1170,20 +1205,24 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
   else a0_nd<3>(s, L0, sop, row0, a0_ptr, a0_a, reg);
 }
 
+// the grid of a setup launch over level L (x1: 8× the blocks, setup_block)
+static dim3 xg(const AmgLevD& L, dim3 g) { return dim3(L.x1 ? 8 * g.x : g.x); }
+static dim3 xg(const AmgLevD& L, int64_t blocks) { return xg(L, dim3((unsigned)blocks)); }
+
 template <int ND>
 static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool level0, int stage) {
   if (L.A.n <= 0) return;
   // level 0's k_amg_dinv ran in launch_amg_a0 (it also forms the diagonal)
   if (stage & kSetupDinv && !level0)
-    hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+    hipLaunchKernelGGL((k_amg_dinv<ND, false>), xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
   if (L.coarsest || !N) return;
   if (stage & kSetupP && L.P.wmax > 0)
-    hipLaunchKernelGGL(k_amg_pvals<ND>, slot_grid(L.P.rg.npos()), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_pvals<ND>, xg(L, slot_grid(L.P.rg.npos())), dim3(kBlock), 0, s, L);
   if (stage & kSetupAP) {
-    hipLaunchKernelGGL(k_amg_ap<ND>, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos())), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()))), dim3(kBlock), 0, s, L);
   }
   if (stage & kSetupAC)
-    hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, N->A, N->omega);
+    hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, N->A, N->omega);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0, int stage) {
   if (nd == 2) setup_nd<2>(s, L, next, level0, stage);
@@ -1194,9 +1233,9 @@ template <int ND>
 static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l) {
   const AmgLevD& L = lev[l];
   if (!L.compact || L.PT.wmax <= 0) return;
-  hipLaunchKernelGGL(k_amg_ptv<ND>, slot_grid(L.PT.npos), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_rtv<ND>, slot_grid(L.RT.npos), dim3(kBlock), 0, s, L, lev[l + 1]);
-  hipLaunchKernelGGL(k_amg_atv<ND>, slot_grid(L.A.npos), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_ptv<ND>, xg(L, slot_grid(L.PT.npos)), dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL(k_amg_rtv<ND>, xg(L, slot_grid(L.RT.npos)), dim3(kBlock), 0, s, L, lev[l + 1]);
+  hipLaunchKernelGGL(k_amg_atv<ND>, xg(L, slot_grid(L.A.npos)), dim3(kBlock), 0, s, L);
 }
 template <int ND>
 static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, int below = 1 << 30) {
@@ -1205,8 +1244,8 @@ static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int c
     const AmgLevD& L = lev[l];
     if (!L.collapsed) return;
     const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
-    hipLaunchKernelGGL(k_amg_tv<ND>, rows_grid(L.CT.npos), dim3(kBlock), 0, s, L, vnext);
-    hipLaunchKernelGGL(k_amg_vv<ND>, rows_grid(L.CV.npos), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_tv<ND>, xg(L, rows_grid(L.CT.npos)), dim3(kBlock), 0, s, L, vnext);
+    hipLaunchKernelGGL(k_amg_vv<ND>, xg(L, rows_grid(L.CV.npos)), dim3(kBlock), 0, s, L);
   }
 }
 // the whole numeric setup of a compact-cycle hierarchy, its compact parts
@@ -1222,22 +1261,22 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     if (L.A.n <= 0) return;
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0)
-      hipLaunchKernelGGL((k_amg_dinv<ND, false>), rows_grid(L.A.rg.span()), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+      hipLaunchKernelGGL((k_amg_dinv<ND, false>), xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
     const int64_t g0 = !last && L.P.wmax > 0 ? slot_blocks(L.P.rg.npos()) : 0;
     const int64_t g1 = g0 + (compact(l) ? slot_blocks(L.A.npos) : 0);
     const int64_t g2 = g1 + (l > 0 && compact(l - 1) ? slot_blocks(lev[l - 1].RT.npos) : 0);
     if (g2 > 0)
-      hipLaunchKernelGGL(k_amg_fuse_p<ND>, dim3((unsigned)g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
+      hipLaunchKernelGGL(k_amg_fuse_p<ND>, xg(L, g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
     if (last) break;
     const dim3 gap = rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()));
     if (compact(l) && L.PT.npos == L.AP.npos) {  // P̃ formed by the A·P kernel
-      hipLaunchKernelGGL((k_amg_ap<ND, true>), gap, dim3(kBlock), 0, s, L);
-      hipLaunchKernelGGL(k_amg_ac<ND>, rows_grid(L.ac_rg.npos()), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega);
+      hipLaunchKernelGGL((k_amg_ap<ND, true>), xg(L, gap), dim3(kBlock), 0, s, L);
+      hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega);
     } else {
-      hipLaunchKernelGGL(k_amg_ap<ND>, gap, dim3(kBlock), 0, s, L);
+      hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, gap), dim3(kBlock), 0, s, L);
       const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
       const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
-      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, dim3((unsigned)a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
+      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, xg(L, a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
     }
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);
@@ -1254,8 +1293,8 @@ static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int co
     const AmgLevD& L = lev[l];
     if (!L.collapsed) return;
     const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
-    hipLaunchKernelGGL(k_amg_tv<ND>, rows_grid(L.CT.npos), dim3(kBlock), 0, s, L, vnext);
-    hipLaunchKernelGGL(k_amg_vv<ND>, rows_grid(L.CV.npos), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_amg_tv<ND>, xg(L, rows_grid(L.CT.npos)), dim3(kBlock), 0, s, L, vnext);
+    hipLaunchKernelGGL(k_amg_vv<ND>, xg(L, rows_grid(L.CV.npos)), dim3(kBlock), 0, s, L);
   }
 }
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {

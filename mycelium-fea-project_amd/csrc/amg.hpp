@@ -255,6 +255,23 @@ struct AmgCollapse {
 std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t max_pairs, int min_level,
                                AmgCollapse& out);
 
+// Block-Jacobi multicolour sweeps over A_0 (MFEA_PC_SOR, MFEA_PC_ICC; sweep.hip):
+// level-0 rows in blocks of `rows_per_block` consecutive rows (one workgroup
+// each — the couplings between blocks are dropped, as PETSc's processor-local
+// SOR / ICC drops those between ranks), inside a block a greedy colouring of
+// the rows' in-block couplings (row order), so one colour's rows are
+// independent and the triangular sweeps run colour by colour.  Per row its
+// in-block neighbours of earlier colours (lower) and of later colours (upper):
+// their index in the block and the A_0 position of the coupling block.
+struct SweepPlan {
+  int rows_per_block = 256;
+  int max_colors = 0;
+  std::vector<uint8_t> color;                    // per level-0 row
+  std::vector<int32_t> lo_ptr, lo_loc, lo_pos;   // lower (earlier colours)
+  std::vector<int32_t> up_ptr, up_loc, up_pos;   // upper (later colours)
+};
+std::string build_sweep(const AmgPlan& plan, int rows_per_block, SweepPlan& out);
+
 // Free rows [0, P.n_free) with no path of active elements to a grip row:
 // out[i] = 1.  A hierarchy kept over element failures (capi.hip ensure_amg)
 // zeroes their rows of P_0, so the preconditioner leaves them at exactly zero

@@ -23,15 +23,19 @@ __device__ __forceinline__ void bstore(T* __restrict__ v, int64_t /*npos*/, int6
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) v[q * (ND * ND) + c] = (T)m[c];
 }
-// symmetric blocks stored as their upper triangle (A_0: AmgMatD::sym)
+// symmetric blocks stored as their upper triangle (A_0: AmgMatD::sym, sym32),
+// component-major ([NS][npos]): a SELL slot's 64 lanes read NS runs of 64
+// consecutive values — each load instruction one contiguous 512-B (f64) run,
+// where the block-major form's 24-B lane stride made every one of the three
+// instructions touch all twelve lines of the slot
 template <int ND>
 constexpr int nsym() { return ND * (ND + 1) / 2; }
 template <int ND, class T, class C>
-__device__ __forceinline__ void bload_sym(const T* __restrict__ v, int64_t q, C* m) {
+__device__ __forceinline__ void bload_sym(const T* __restrict__ v, int64_t npos, int64_t q, C* m) {
   constexpr int NS = nsym<ND>();
   C t[NS];
 #pragma unroll
-  for (int c = 0; c < NS; ++c) t[c] = (C)v[q * NS + c];
+  for (int c = 0; c < NS; ++c) t[c] = (C)v[c * npos + q];
   if constexpr (ND == 2) {
     m[0] = t[0]; m[1] = t[1];
     m[2] = t[1]; m[3] = t[2];
@@ -42,34 +46,12 @@ __device__ __forceinline__ void bload_sym(const T* __restrict__ v, int64_t q, C*
   }
 }
 template <int ND, class T, class C>
-__device__ __forceinline__ void bstore_sym(T* __restrict__ v, int64_t q, const C* m) {
+__device__ __forceinline__ void bstore_sym(T* __restrict__ v, int64_t npos, int64_t q, const C* m) {
   if constexpr (ND == 2) {
-    v[q * 3 + 0] = (T)m[0]; v[q * 3 + 1] = (T)m[1]; v[q * 3 + 2] = (T)m[3];
+    v[q] = (T)m[0]; v[npos + q] = (T)m[1]; v[2 * npos + q] = (T)m[3];
   } else {
-    v[q * 6 + 0] = (T)m[0]; v[q * 6 + 1] = (T)m[1]; v[q * 6 + 2] = (T)m[2];
-    v[q * 6 + 3] = (T)m[4]; v[q * 6 + 4] = (T)m[5]; v[q * 6 + 5] = (T)m[8];
-  }
-}
-// non-temporal forms (streamed operator blocks that should not evict the
-// gathered vector from the XCD's L2; MI355X_MICROARCH.md, nt-weights)
-template <int ND, class T, class C>
-__device__ __forceinline__ void bload_nt(const T* __restrict__ v, int64_t q, C* m) {
-#pragma unroll
-  for (int c = 0; c < ND * ND; ++c) m[c] = (C)__builtin_nontemporal_load(&v[q * (ND * ND) + c]);
-}
-template <int ND, class T, class C>
-__device__ __forceinline__ void bload_sym_nt(const T* __restrict__ v, int64_t q, C* m) {
-  constexpr int NS = nsym<ND>();
-  C t[NS];
-#pragma unroll
-  for (int c = 0; c < NS; ++c) t[c] = (C)__builtin_nontemporal_load(&v[q * NS + c]);
-  if constexpr (ND == 2) {
-    m[0] = t[0]; m[1] = t[1];
-    m[2] = t[1]; m[3] = t[2];
-  } else {
-    m[0] = t[0]; m[1] = t[1]; m[2] = t[2];
-    m[3] = t[1]; m[4] = t[3]; m[5] = t[4];
-    m[6] = t[2]; m[7] = t[4]; m[8] = t[5];
+    v[q] = (T)m[0]; v[npos + q] = (T)m[1]; v[2 * npos + q] = (T)m[2];
+    v[3 * npos + q] = (T)m[4]; v[4 * npos + q] = (T)m[5]; v[5 * npos + q] = (T)m[8];
   }
 }
 template <int ND, class T, class C>
@@ -232,7 +214,7 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
 template <int ND>
 constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
 
-template <int ND, int U, bool SUB, bool SYM = false, bool NT = false, class TV, class XP, class C>
+template <int ND, int U, bool SUB, bool SYM = false, class TV, class XP, class C>
 __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                            int64_t npos, int64_t base, int w,
                                            XP x, C* y) {
@@ -242,15 +224,12 @@ __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, cons
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       q[u] = k + u < w ? base + (int64_t)(k + u) * 64 : base;
-      if constexpr (NT) c[u] = k + u < w ? __builtin_nontemporal_load(&col[q[u]]) : -1;
-      else c[u] = k + u < w ? col[q[u]] : -1;
+      c[u] = k + u < w ? col[q[u]] : -1;
     }
     C m[U][ND * ND], xc[U][ND];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (SYM && NT) bload_sym_nt<ND>(val, q[u], m[u]);
-      else if constexpr (SYM) bload_sym<ND>(val, q[u], m[u]);
-      else if constexpr (NT) bload_nt<ND>(val, q[u], m[u]);
+      if constexpr (SYM) bload_sym<ND>(val, npos, q[u], m[u]);
       else bload<ND>(val, npos, q[u], m[u]);
       vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
     }
@@ -276,14 +255,14 @@ __device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, cons
 // for 98 % of the waves, stays at K = 1 (a 2U path put it at 139 VGPRs, one
 // 768-thread block per CU); the streaming level-0 kernels use K = 2; the
 // restrictions and the latency-bound coarse levels K = 3.
-template <int ND, bool SUB, int K = 2, bool SYM = false, bool NT = false, class TV, class XP, class C>
+template <int ND, bool SUB, int K = 2, bool SYM = false, class TV, class XP, class C>
 __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                          int64_t npos, int64_t base, int w,
                                          XP x, C* y) {
   constexpr int U = mac_unroll<ND>();
-  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB, SYM, NT>(col, val, npos, base, w, x, y);
-  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB, SYM, NT>(col, val, npos, base, w, x, y);
-  else sell_mac_u<ND, U, SUB, SYM, NT>(col, val, npos, base, w, x, y);
+  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB, SYM>(col, val, npos, base, w, x, y);
+  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB, SYM>(col, val, npos, base, w, x, y);
+  else sell_mac_u<ND, U, SUB, SYM>(col, val, npos, base, w, x, y);
 }
 
 // o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C).  dinv_load / dinv_mul

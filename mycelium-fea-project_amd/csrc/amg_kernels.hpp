@@ -68,6 +68,7 @@ struct AmgLevD {
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
+  int x1 = 0;        // the numeric setup's launches over this level run on one XCD (amg.hip setup_block)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   // level 0 of a hierarchy kept over element failures: rows of floating
@@ -132,7 +133,27 @@ struct AmgCg {
   // level of the cycle has it (compact set: unsplit levels); 0: four steps
   int cycle = 0;
   int coll = 0;  // the compact cycle's collapsed level kc (0: none)
+  int sweep = 0;  // 1: the preconditioner is a multicolour sweep (sweep.hip): u is its output only
 };
+
+// Block-Jacobi multicolour SSOR / DIC(0) (sweep.hip, amg.hpp SweepPlan): per
+// level-0 row its colour and in-block lower / upper couplings; dt32 the
+// blocks D̃⁻¹ the sweeps apply (SOR: A_0's D⁻¹; ICC: formed by k_sweep_dic)
+struct SweepD {
+  int64_t n = 0;
+  int colors = 0;
+  int dic = 0;
+  const uint8_t* color = nullptr;
+  const int32_t* lo_ptr = nullptr;
+  const int32_t* lo_loc = nullptr;
+  const int32_t* lo_pos = nullptr;
+  const int32_t* up_ptr = nullptr;
+  const int32_t* up_loc = nullptr;
+  const int32_t* up_pos = nullptr;
+  float* dt32 = nullptr;
+};
+void launch_sweep_setup(hipStream_t s, int nd, const SweepD& sw, const AmgLevD& L0);
+void launch_sweep(hipStream_t s, int nd, const SweepD& sw, const AmgLevD& L0, const AmgCg& cg, const int32_t* gate);
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered
 // per-rank partial sums, its ghost couplings and the u halo buffers.

@@ -655,6 +655,49 @@ std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active,
   return "";
 }
 
+std::string build_sweep(const AmgPlan& plan, int rows_per_block, SweepPlan& out) {
+  out = SweepPlan();
+  out.rows_per_block = rows_per_block;
+  if (plan.lev.empty()) return "";
+  const SellPat& A = plan.lev[0].A;
+  const int64_t n = A.n;
+  out.color.assign(n, 0);
+  out.lo_ptr.assign(n + 1, 0);
+  out.up_ptr.assign(n + 1, 0);
+  std::vector<int32_t> nb;
+  std::vector<uint64_t> used;
+  for (int64_t b0 = 0; b0 < n; b0 += rows_per_block) {
+    const int64_t b1 = std::min<int64_t>(n, b0 + rows_per_block);
+    for (int64_t i = b0; i < b1; ++i) {  // greedy colour in row order
+      uint64_t u = 0;
+      const int w = A.rlen[i];
+      for (int k = 1; k < w; ++k) {
+        const int32_t j = A.col[A.pos(i, k)];
+        if (j >= b0 && j < i) u |= uint64_t(1) << out.color[j];
+      }
+      int c = 0;
+      while (c < 63 && (u >> c & 1)) ++c;
+      if (c >= 63) return "sweep colouring: more than 63 colours in a block";
+      out.color[i] = (uint8_t)c;
+      out.max_colors = std::max(out.max_colors, c + 1);
+    }
+    for (int64_t i = b0; i < b1; ++i) {
+      const int w = A.rlen[i];
+      for (int k = 1; k < w; ++k) {
+        const int64_t q = A.pos(i, k);
+        const int32_t j = A.col[q];
+        if (j < b0 || j >= b1) continue;  // another block: dropped
+        const bool lower = out.color[j] < out.color[i];
+        (lower ? out.lo_loc : out.up_loc).push_back((int32_t)(j - b0));
+        (lower ? out.lo_pos : out.up_pos).push_back((int32_t)q);
+      }
+      out.lo_ptr[i + 1] = (int32_t)out.lo_loc.size();
+      out.up_ptr[i + 1] = (int32_t)out.up_loc.size();
+    }
+  }
+  return "";
+}
+
 // Free rows of P with no path of active elements to a grip (known, non-ghost)
 // row: their load is zero, so the direct solve leaves them exactly at zero
 // (src/fea_solver.py:128).  Union-find over the active elements.

@@ -136,6 +136,14 @@ struct Part {
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
   int amg_first = 1;                 // first level the four-step tail may start at (not split)
   AmgCg amg_cg;
+  // the plan's preconditioner kind: MFEA_PC_GAMG (the hierarchy) or a
+  // one-level plan with multicolour sweeps (MFEA_PC_SOR / MFEA_PC_ICC, sweep.hip)
+  int amg_kind = MFEA_PC_GAMG;
+  SweepPlan sweep;
+  SweepD swd;
+  DevBuf<int32_t> sw_i;   // lo/up ptr, loc, pos
+  DevBuf<uint8_t> sw_c;   // colours
+  DevBuf<float> sw_dt;    // ICC: D̃⁻¹ blocks
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
   // partitioned GAMG (amg.hpp AmgHalo): ghost couplings and the u halo
@@ -230,6 +238,7 @@ struct mfea_handle {
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
+  int64_t opt_amg_x1_rows = 8192;  // GAMG setup: levels of at most this many rows run on one XCD (0: never)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
@@ -1189,6 +1198,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
+      d.x1 = !rk && l > 0 && n <= h->opt_amg_x1_rows ? 1 : 0;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, false, true);
@@ -1351,11 +1361,67 @@ int upload_fmask(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
   return 0;
 }
 
+// the multicolour sweep's arrays for a one-level plan (MFEA_PC_SOR / _ICC);
+// a GAMG plan: none (amg_cg.sweep = 0)
+int upload_sweep(mfea_handle* h, Part& pt, int kind) {
+  pt.swd = SweepD{};
+  pt.amg_cg.sweep = 0;
+  if (kind != MFEA_PC_SOR && kind != MFEA_PC_ICC) return 0;
+  const SweepPlan& sp = pt.sweep;
+  const int64_t n = (int64_t)sp.color.size();
+  const size_t a = sp.lo_ptr.size(), b = sp.lo_loc.size(), c = sp.up_ptr.size(), d = sp.up_loc.size();
+  HIPC(pt.sw_i.alloc(a + 2 * b + c + 2 * d + 1));
+  HIPC(pt.sw_c.alloc(std::max<int64_t>(n, 1)));
+  int32_t* ip = pt.sw_i.ptr;
+  hipStream_t s = h->stream;
+  auto put = [&](const std::vector<int32_t>& v) -> const int32_t* {
+    int32_t* p = ip;
+    if (!v.empty()) (void)hipMemcpyAsync(p, v.data(), v.size() * 4, hipMemcpyHostToDevice, s);
+    ip += v.size();
+    return p;
+  };
+  SweepD& w = pt.swd;
+  w.n = n;
+  w.colors = sp.max_colors;
+  w.dic = kind == MFEA_PC_ICC ? 1 : 0;
+  w.lo_ptr = put(sp.lo_ptr);
+  w.lo_loc = put(sp.lo_loc);
+  w.lo_pos = put(sp.lo_pos);
+  w.up_ptr = put(sp.up_ptr);
+  w.up_loc = put(sp.up_loc);
+  w.up_pos = put(sp.up_pos);
+  if (n) HIPC(hipMemcpyAsync(pt.sw_c.ptr, sp.color.data(), n, hipMemcpyHostToDevice, s));
+  w.color = pt.sw_c.ptr;
+  if (w.dic) {
+    HIPC(pt.sw_dt.alloc(std::max<int64_t>(1, n * pt.amg.nd * pt.amg.nd)));
+    w.dt32 = pt.sw_dt.ptr;
+  } else {
+    w.dt32 = pt.amg_lev.empty() ? nullptr : pt.amg_lev[0].dinv32;
+  }
+  pt.amg_cg.sweep = 1;
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// the preconditioner application u = M r of one PCG iteration (gate: its
+// flag; NULL: ungated)
+void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate) {
+  if (pt.amg_cg.sweep) launch_sweep(h->stream, pt.amg.nd, pt.swd, pt.amg_lev[0], pt.amg_cg, gate);
+  else launch_amg_vcycle(h->stream, pt.amg.nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, gate);
+}
+
 // (Re)build the hierarchy when the active set differs from the plan's.  One
 // partition: the host view of the activity (downloaded only when a post
 // kernel changed it); partitioned: each partition's own elements, read back.
-int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
+int upload_sweep(mfea_handle* h, Part& pt, int kind);
+
+int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG) {
   *rebuilt = false;
+  if (pt.amg_ok && pt.amg_kind != kind) {  // another preconditioner's plan
+    pt.amg_ok = false;
+    pt.amg_last_iters = 0;
+  }
   const bool dm = partitioned(h);
   std::vector<uint8_t> local;
   if (dm) {
@@ -1387,11 +1453,15 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt) {
   pt.amg_ok = false;
   AmgLayout lay;
   lay.spatial = h->opt_amg_spatial;
-  const std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, h->opt_amg_max_levels, nullptr,
-                                    amg_strength(h), lay);
+  const bool sweep = kind == MFEA_PC_SOR || kind == MFEA_PC_ICC;
+  std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, sweep ? 1 : h->opt_amg_max_levels, nullptr,
+                              amg_strength(h), lay);
+  if (err.empty() && sweep) err = build_sweep(pt.amg, 256, pt.sweep);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
+  pt.amg_kind = kind;
   RC(upload_amg(h, pt, pt.amg));
+  RC(upload_sweep(h, pt, kind));
   if (dm) RC(upload_amg_halo(h, pt, key));
   pt.dev_plan = 0;
   pt.amg_key = key;
@@ -1409,8 +1479,7 @@ void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_update(s, nd, j, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
-                    pt.amg_tail, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
+  launch_precond(h, pt, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
   launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
 }
 
@@ -1517,8 +1586,7 @@ void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   for (int j = 0; j < chunk; ++j) {
-    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
-                      pt.amg_tail, &pt.slots.ptr[j + 1].flag);
+    launch_precond(h, pt, &pt.slots.ptr[j + 1].flag);
     launch_amg_cg_w(s, nd, j, false, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
     launch_amg_cg_update(s, nd, j + 1, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
   }
@@ -1530,6 +1598,10 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   hipStream_t s = h->stream;
   const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
   launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  if (pt.amg_cg.sweep) {
+    launch_sweep_setup(s, nd, pt.swd, pt.amg_lev[0]);
+    return;
+  }
   const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
   if (compact && h->opt_amg_fuse_setup) {
     launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
@@ -1558,7 +1630,8 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   k = fnv1a(k, &op, sizeof op);
   const void* ptrs[4] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, pt.amg_levd.ptr};
   k = fnv1a(k, ptrs, sizeof ptrs);
-  const int ints[4] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll};
+  const int ints[5] = {pt.amg.nd, h->opt_amg_fuse_setup, pt.amg_cg.cycle, pt.amg_cg.coll, pt.amg_cg.sweep};
+  k = fnv1a(k, &pt.swd, sizeof pt.swd);
   k = fnv1a(k, ints, sizeof ints);
   k = fnv1a(k, &reg, sizeof reg);
   if (!h->graph_setup || h->graph_setup_key != k) {
@@ -1585,9 +1658,9 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   Part& pt = part0(h);
   hipStream_t s = h->stream;
   if (o->norm != MFEA_NORM_UNPRECONDITIONED)
-    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
+    return fail(MFEA_EINVAL, "MFEA_PC_GAMG / SOR / ICC stop on the unpreconditioned residual only");
   bool rebuilt = false;
-  RC(ensure_amg(h, pt, &rebuilt));
+  RC(ensure_amg(h, pt, &rebuilt, o->precond));
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
@@ -2437,6 +2510,10 @@ int solve_any(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     if (!partitioned(h)) return solve_amg(h, dy_top, dy_bot, o, st);
     return solve_amg_part(h, dy_top, dy_bot, o, st);
   }
+  if (o->precond == MFEA_PC_SOR || o->precond == MFEA_PC_ICC) {
+    if (partitioned(h)) return fail(MFEA_EINVAL, "MFEA_PC_SOR / MFEA_PC_ICC: one partition per handle");
+    return solve_amg(h, dy_top, dy_bot, o, st);
+  }
   if (o->precond != MFEA_PC_JACOBI && o->precond != MFEA_PC_BLOCK_JACOBI)
     return fail(MFEA_EINVAL, "unknown preconditioner");
   return partitioned(h) ? solve_dist(h, dy_top, dy_bot, o, st) : solve_impl(h, dy_top, dy_bot, o, st);
@@ -3143,6 +3220,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_spatial = (int)value;
     rebuild = true;
   }
+  else if (n == "amg_x1_rows") {
+    if (value < 0) return fail(MFEA_EINVAL, "amg_x1_rows: >= 0");
+    h->opt_amg_x1_rows = value;
+    rebuild = true;
+  }
   else if (n == "amg_up_lanes") {
     if (value != 0 && value != 1 && value != 2 && value != 4)
       return fail(MFEA_EINVAL, "amg_up_lanes: 0 (by width), 1, 2 or 4");
@@ -3369,6 +3451,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;
   else if (n == "amg_reuse") *value = h->opt_amg_reuse;
+  else if (n == "amg_x1_rows") *value = h->opt_amg_x1_rows;
   else if (n == "amg_rebuild_pct") *value = h->opt_amg_rebuild_pct;
   else if (n == "amg_reused") *value = part0(h).amg_reused ? 1 : 0;  // read-only: the last solve kept a hierarchy built for another set
   else if (n == "amg_build_iters") *value = part0(h).amg_build_iters;  // read-only

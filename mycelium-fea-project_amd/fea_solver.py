@@ -298,7 +298,7 @@ def main(argv=None):
     ap.add_argument("--rtol", type=float, default=RTOL)
     ap.add_argument("--max-it", type=int, default=MAX_IT)
     ap.add_argument("--reg", type=float, default=REG)
-    ap.add_argument("--pc", choices=["gamg", "jacobi", "bjacobi"], default="gamg")
+    ap.add_argument("--pc", choices=["gamg", "jacobi", "bjacobi", "sor", "icc"], default="gamg")
     ap.add_argument("--format", choices=["python", "petsc"], default="python")
     ap.add_argument("--npy", action="store_true", help="also write each record as a .npy sidecar")
     ap.add_argument("--parts", type=int, default=1,
@@ -308,7 +308,7 @@ def main(argv=None):
     N_STEPS, DISPLACEMENT_MAX, MAX_STRAIN, REG = a.n_steps, a.disp_max, a.max_strain, a.reg
     fea_solver(a.results_dir, tol=a.grip_length, rtol=a.rtol, max_it=a.max_it,
                precond={"gamg": _capi.PC_GAMG, "jacobi": _capi.PC_JACOBI,
-                        "bjacobi": _capi.PC_BLOCK_JACOBI}[a.pc],
+                        "bjacobi": _capi.PC_BLOCK_JACOBI, "sor": _capi.PC_SOR, "icc": _capi.PC_ICC}[a.pc],
                out_format=a.format, nparts=a.parts, npy=a.npy)
 
 

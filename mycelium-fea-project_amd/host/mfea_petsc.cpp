@@ -5,7 +5,7 @@
 // the MI355X through libmfea.so (include/mfea.h).  Host C++ only: it reads the
 // CSVs, makes the C-ABI calls and writes the records.
 //
-//   mfea_petsc <results_dir> [-ksp_type cg] [-pc_type jacobi|bjacobi|gamg]
+//   mfea_petsc <results_dir> [-ksp_type cg] [-pc_type icc|ilu|sor|jacobi|bjacobi|gamg]
 //              [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it N]
 //              [-ksp_norm_type preconditioned|unpreconditioned]
 //              [-n_steps N] [-disp_max D] [-grip_length G] [-max_strain S]
@@ -14,15 +14,19 @@
 // Defaults are the reference's: its constants (src/fea_petsc.cpp:23-32) and
 // PETSc's KSP defaults (rtol 1e-5, atol 1e-50, max_it 1e4, the preconditioned
 // residual norm for CG).  The reference builds KSPCG with PCICC in source
-// (src/fea_petsc.cpp:328-331) and PCBJACOBI in its binaries and MPI variant
-// (src/fea_petsc_parallel.cpp:339); here -pc_type bjacobi (the default) is the
-// exact inverse of each node's 3×3 diagonal block and jacobi is PCJACOBI.
-// Documented differences: prescribed DOFs hold exactly their value (PETSc adds
-// the 1e-12 shift to those rows too and returns x/(1+1e-12)); -pc_type gamg
-// (the reference sweep's GAMG, src/fea_petsc_solverAndPC.cpp:330-391) is the
-// engine's SA-AMG V-cycle and stops on the unpreconditioned residual (the
-// default norm under gamg; asking for the preconditioned one is an error);
-// -pc_type icc/ilu/sor and other -ksp_type are rejected.
+// (src/fea_petsc.cpp:328-331) and PCBJACOBI in its MPI variant
+// (src/fea_petsc_parallel.cpp:339): so does this driver — -pc_type icc is the
+// default on one process, bjacobi under a multi-process launch.  icc (and ilu,
+// the same factor of an SPD matrix) is the engine's DIC(0) and sor its SSOR
+// (ω = 1), both block Jacobi over 256-row blocks with multicolour sweeps
+// inside (PETSc's SOR / ICC are processor-local in parallel; sweep.hip);
+// bjacobi is the exact inverse of each node's 3×3 diagonal block and jacobi
+// PCJACOBI.  Documented differences: prescribed DOFs hold exactly their value
+// (PETSc adds the 1e-12 shift to those rows too and returns x/(1+1e-12));
+// -pc_type gamg (the reference sweep's GAMG, src/fea_petsc_solverAndPC.cpp:
+// 330-391) is the engine's SA-AMG V-cycle; gamg, icc, ilu and sor stop on the
+// unpreconditioned residual (their default norm here; asking for the
+// preconditioned one is an error); other -ksp_type are rejected.
 //
 // Multi-GPU: launched as N processes — `mpirun -np N mfea_petsc <dir>` as the
 // reference's `mpirun -np 4 ./fea_petsc_parallel.exe` (README.md:18), or
@@ -59,7 +63,7 @@ struct Options {
   std::string dir;
   double rtol = 1e-5, atol = 1e-50, reg = 1e-12;
   int max_it = 10000;
-  int precond = MFEA_PC_BLOCK_JACOBI;
+  int precond = -1;  // -1: the reference's default (icc; bjacobi on several processes)
   int norm = MFEA_NORM_PRECONDITIONED;
   bool norm_given = false;
   int n_steps = 40;              // src/fea_petsc.cpp:28
@@ -98,7 +102,9 @@ Options parse(int argc, char** argv) {
       if (!std::strcmp(v, "jacobi")) o.precond = MFEA_PC_JACOBI;
       else if (!std::strcmp(v, "bjacobi")) o.precond = MFEA_PC_BLOCK_JACOBI;
       else if (!std::strcmp(v, "gamg")) o.precond = MFEA_PC_GAMG;
-      else die(std::string("-pc_type ") + v + " not supported (jacobi, bjacobi, gamg)");
+      else if (!std::strcmp(v, "icc") || !std::strcmp(v, "ilu")) o.precond = MFEA_PC_ICC;
+      else if (!std::strcmp(v, "sor")) o.precond = MFEA_PC_SOR;
+      else die(std::string("-pc_type ") + v + " not supported (icc, ilu, sor, jacobi, bjacobi, gamg)");
     } else if (a == "-ksp_norm_type") {
       o.norm_given = true;
       if (!std::strcmp(v, "preconditioned")) o.norm = MFEA_NORM_PRECONDITIONED;
@@ -126,13 +132,21 @@ Options parse(int argc, char** argv) {
       die("unknown option " + a);
     }
   }
-  if (o.precond == MFEA_PC_GAMG) {
-    if (o.norm_given && o.norm == MFEA_NORM_PRECONDITIONED)
-      die("-pc_type gamg stops on the unpreconditioned residual (-ksp_norm_type unpreconditioned)");
-    o.norm = MFEA_NORM_UNPRECONDITIONED;
-  }
   if (o.n_steps < 2) die("-n_steps must be at least 2");
   return o;
+}
+
+// the preconditioner default (the reference's PCICC; its MPI variant's
+// PCBJACOBI) and the norm gamg / icc / sor stop on
+void finish_options(Options& o, int world) {
+  if (o.precond < 0) o.precond = world > 1 ? MFEA_PC_BLOCK_JACOBI : MFEA_PC_ICC;
+  if (world > 1 && (o.precond == MFEA_PC_ICC || o.precond == MFEA_PC_SOR))
+    die("-pc_type icc / ilu / sor: one process (use bjacobi, jacobi or gamg under mpirun)");
+  if (o.precond == MFEA_PC_GAMG || o.precond == MFEA_PC_ICC || o.precond == MFEA_PC_SOR) {
+    if (o.norm_given && o.norm == MFEA_NORM_PRECONDITIONED)
+      die("-pc_type gamg / icc / ilu / sor stop on the unpreconditioned residual (-ksp_norm_type unpreconditioned)");
+    o.norm = MFEA_NORM_UNPRECONDITIONED;
+  }
 }
 
 // src/fea_petsc.cpp:42-82: header skipped, empty lines skipped, the first
@@ -243,7 +257,7 @@ int main(int argc, char** argv) {
     std::printf("Usage: %s <results_dir>\n", argv[0]);
     return 1;
   }
-  const Options o = parse(argc, argv);
+  Options o = parse(argc, argv);
   if (o.dir.empty()) {
     std::printf("Usage: %s <results_dir>\n", argv[0]);
     return 1;
@@ -251,6 +265,7 @@ int main(int argc, char** argv) {
   const auto started = std::chrono::system_clock::now();
   const Launch L = launch_env();
   if (L.world < 1 || L.rank < 0 || L.rank >= L.world) die("bad rank / world size in the environment");
+  finish_options(o, L.world);
   const bool root = L.rank == 0;
   const std::string fea_dir = o.dir + "/fea_results";
   struct stat st;
@@ -339,7 +354,9 @@ int main(int argc, char** argv) {
                   "PC Object: type %s\n",
                   L.world, L.world > 1 ? "es" : "", device, stt.iters, stt.relres, o.rtol, o.atol, o.max_it,
                   o.norm == MFEA_NORM_PRECONDITIONED ? "PRECONDITIONED" : "UNPRECONDITIONED",
-                  o.precond == MFEA_PC_JACOBI ? "jacobi" : o.precond == MFEA_PC_GAMG ? "gamg" : "bjacobi (3x3 node blocks)");
+                  o.precond == MFEA_PC_JACOBI ? "jacobi" : o.precond == MFEA_PC_GAMG ? "gamg"
+                  : o.precond == MFEA_PC_ICC ? "icc (DIC(0), 256-row blocks, multicolour)"
+                  : o.precond == MFEA_PC_SOR ? "sor (SSOR, 256-row blocks, multicolour)" : "bjacobi (3x3 node blocks)");
     }
     // the whole mesh's records on rank 0 (collective; one process: a copy)
     check(mfea_gather_results(h, U.data(), E ? S.data() : nullptr, E ? A.data() : nullptr), "mfea_gather_results");

@@ -32,7 +32,7 @@ _lib = C.CDLL(LIB_PATH)
 
 # error codes (mfea.h)
 OK, EINVAL, EDEVICE, ESTATE, EMAXIT, EBREAKDOWN, ENOMEM, ECOMM = 0, -1, -2, -3, -4, -5, -6, -7
-PC_JACOBI, PC_BLOCK_JACOBI, PC_GAMG = 0, 1, 2
+PC_JACOBI, PC_BLOCK_JACOBI, PC_GAMG, PC_SOR, PC_ICC = 0, 1, 2, 3, 4
 NORM_UNPRECONDITIONED, NORM_PRECONDITIONED = 0, 1
 MESH_SKIP_INVALID = 1
 

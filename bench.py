@@ -639,6 +639,19 @@ def main(argv=None):
                           f"fail from mid-run on. ") + fr["note"]
             out["full_run_failures"] = fr
 
+    if not a.no_jacobi and pc == PC_GAMG and mode == "1gpu":
+        # the reference sweep's other preconditioners on the same step
+        # (src/fea_petsc_solverAndPC.cpp:331): SSOR and the source default's
+        # ICC (here DIC(0)), block Jacobi over 256-row blocks (csrc/sweep.hip)
+        from mfea import PC_ICC, PC_SOR
+        for name, code in (("sor", PC_SOR), ("icc", PC_ICC)):
+            eng.set_active(None)
+            eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=code), fs.MAX_STRAIN)  # plan build
+            eng.set_active(None)
+            _, _, sk = eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=code), fs.MAX_STRAIN)
+            out[f"{name}_iters_1e8"] = sk.iters
+            out[f"{name}_step_ms"] = sk.t_assemble_ms + sk.t_rhs_ms + sk.t_solve_ms + sk.t_post_ms
+
     if rank == 0 and not a.no_cpu and world == 1:
         cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof)
 

@@ -311,10 +311,14 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val32, L.A.npos, L.P.val32, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
   if constexpr (PTV) {
-    double m[ND * ND];
+    // from the stored (f32) A·P block, as k_amg_ptv forms it: the same bits
+    double m[ND * ND], Cs[ND * ND];
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
-    mm_acc<ND>(Di, C, m);
+    for (int c = 0; c < ND * ND; ++c) {
+      m[c] = 0.0;
+      Cs[c] = (double)(float)C[c];
+    }
+    mm_acc<ND>(Di, Cs, m);
     const double om = amg_omega(L.omega);
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = fma(-om, m[c], pm[c]);

@@ -128,6 +128,7 @@ struct Part {
   int amg_build_iters = -1;
   bool amg_stale = false;
   bool amg_reused = false;           // the last ensure_amg kept a hierarchy built for another set
+  int64_t amg_seen_gen = -1;         // act_gen at which the plan / mask last matched the activity
   DevBuf<int32_t> amg_i;             // every index array of the plan, carved
   DevBuf<double> amg_d;              // every f64 value / vector array, carved
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
@@ -210,6 +211,7 @@ struct mfea_handle {
   bool in_step = false;        // mfea_step: the solve's end is waited for by post
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
+  bool act_all = false;  // every element is active on the device (set_active(NULL), no failure since)
   // host view of the element activity (single partition; keys the AMG plan):
   // exact after set_active / a build, stale once a post kernel deactivated
   // elements (then downloaded on demand)
@@ -238,7 +240,8 @@ struct mfea_handle {
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
-  int64_t opt_amg_x1_rows = 8192;  // GAMG setup: levels of at most this many rows run on one XCD (0: never)
+  int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
+                                   // C3: levels 4-5 gain 1-2 µs per launch, level 3 at 8192 lost as much)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
@@ -1423,6 +1426,9 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
     pt.amg_last_iters = 0;
   }
   const bool dm = partitioned(h);
+  // no activity change since the plan / mask last matched it: nothing to do
+  // (no O(E) key compares on the hot path)
+  if (!dm && pt.amg_ok && !pt.amg_stale && pt.amg_seen_gen == h->act_gen) return 0;
   std::vector<uint8_t> local;
   if (dm) {
     local.resize(pt.P.n_elems);
@@ -1439,9 +1445,11 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
     // need care — their P_0 rows are zeroed so they stay exactly at zero
     if (pt.amg_mask_key != key) RC(upload_fmask(h, pt, key));
     pt.amg_reused = pt.amg_key != key;
+    pt.amg_seen_gen = h->act_gen;
     return 0;
   }
   if (pt.amg_ok && pt.amg_key == key) {
+    if (!dm) pt.amg_seen_gen = h->act_gen;
     if (!dm || pt.dev_plan == 0) return 0;
     destroy_graph(h);  // the device holds the global plan: upload this one again
     RC(upload_amg(h, pt, pt.amg));
@@ -1468,7 +1476,9 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   pt.amg_ok = true;
   pt.amg_stale = false;
   pt.amg_build_iters = -1;
+  pt.amg_reused = false;
   if (!dm && pt.amg_lev.size() > 1) RC(upload_fmask(h, pt, key));
+  if (!dm) pt.amg_seen_gen = h->act_gen;
   ++pt.amg_gen;
   *rebuilt = true;
   return 0;
@@ -1676,8 +1686,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   h->ev_setup_used = true;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
-  launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
-                    pt.amg_tail, nullptr);
+  launch_precond(h, pt, nullptr);
   launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
   launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
   HIPC(hipGetLastError());
@@ -2432,6 +2441,7 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
   if ((int64_t)h->h_red[1] != h->n_active) ++h->act_gen;  // elements only ever fail here
+  if ((int64_t)h->h_red[1] < h->Ecount) h->act_all = false;
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
   // elements only ever fail here: a changed count means a changed set
@@ -2621,6 +2631,7 @@ int mfea_set_mesh(mfea_handle* h, int64_t n_nodes, const double* xyz, int64_t n_
   h->mesh_flags = flags;
   h->has_mesh = true;
   h->dirty = true;
+  h->act_all = false;
   h->active_host.clear();
   h->planar = true;
   for (int64_t n = 0; n < n_nodes; ++n)
@@ -2658,7 +2669,11 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   if (!h) return fail(MFEA_EINVAL, "NULL handle");
   RC(set_device(h));
   RC(ensure_built(h));
+  // all active already (the benchmark resets every step): nothing changes —
+  // no act_gen bump, so a partitioned handle skips its activity all-reduce
+  if (!active && h->act_all) return 0;
   ++h->act_gen;
+  h->act_all = !active;
   if (h->Ecount == 0) return 0;
   for (auto& pp : h->parts) {
     Part& pt = *pp;

@@ -42,11 +42,11 @@ def test_cli_unreadable_input(tmp_path):
 
 
 def test_cli_without_gpu_fails_cleanly(tmp_path):
+    from mfea import Engine, MfeaError
     try:
-        import torch
-        if torch.cuda.is_available():
-            pytest.skip("GPU present")
-    except ImportError:
+        Engine(0).close()
+        pytest.skip("GPU present")
+    except MfeaError:
         pass
     d = tmp_path / "test_I"
     shutil.copytree(os.path.join(GOLDEN, "meshes", "test_I"), d)

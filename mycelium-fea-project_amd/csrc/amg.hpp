@@ -106,7 +106,8 @@ struct AmgLevel {
   std::vector<int32_t> pt_row; // PT row → the level's row
   std::vector<int32_t> pt_ap;  // PT position → its A·P position
   std::vector<int32_t> pt_p;   // PT position → the P position of the same block, or -1
-  SellPat RT;                  // nc × n
+  SellPat RT;                  // nc × n, rows by RT length inside windows (rt_row)
+  std::vector<int32_t> rt_row; // RT row → the level-(l+1) row
   std::vector<int32_t> rt_pt;  // RT position → PT position (value = PT[rt_pt]ᵀ)
 };
 

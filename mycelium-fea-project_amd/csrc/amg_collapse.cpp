@@ -189,7 +189,7 @@ std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t m
     AmgCollapse::Lev C;
     C.k = k;
     // T_k = V_{k+1} R̂_k (rows: level k+1, cols: level k)
-    const Rows RT = rows_of(L.RT);
+    const Rows RT = rows_of(L.RT, &L.rt_row);
     Prod T;
     if (!spgemm(L.RT.n, have_v ? &vnext : nullptr, RT, L.A.n, T, max_pairs)) break;
     // V_k = (2I − Ã_k) + P̃_k T_k

@@ -97,6 +97,7 @@ struct AmgLevD {
   const int32_t* pt_ap = nullptr;
   const int32_t* pt_p = nullptr;
   const int32_t* rt_pt = nullptr;
+  const int32_t* rt_row = nullptr;  // RT row → level l+1 row (R̂ rows by length)
   // the compact cycle collapsed below this level (amg.hpp AmgCollapse, levels
   // ≥ kc): T = V_{l+1} R̂ (rows: level l+1) and V (rows by length, vrow → level
   // row), both f32 (val32), with their product lists; V.n > 0 on level kc

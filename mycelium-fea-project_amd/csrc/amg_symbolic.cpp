@@ -608,7 +608,18 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
           RT.col[t] = (int32_t)i;
           rt_e[t] = (int32_t)e;
         }
-      if (!(err = layout(RT, perm[l + 1], &perm[l], out.RT, eRT)).empty()) return err;
+      // R̂'s rows are the down sweep's widest (C5 level 0: 30 blocks on average,
+      // 142 at most): their own labelling by R̂ length inside windows, as P̃'s
+      // (in the level's order C5 fills 75 % of the padded positions)
+      std::vector<int32_t> prt;
+      {
+        std::vector<int64_t> key(L.nc);
+        for (int64_t J = 0; J < L.nc; ++J) key[J] = RT.ptr[J + 1] - RT.ptr[J];
+        prt = sort_perm(key, nullptr, world, nullptr, spatial ? &bases[l + 1] : nullptr);
+      }
+      if (!(err = layout(RT, prt, &perm[l], out.RT, eRT)).empty()) return err;
+      out.rt_row.assign(L.nc, 0);
+      for (int64_t J = 0; J < L.nc; ++J) out.rt_row[prt[J]] = perm[l + 1][J];
       out.rt_pt.assign(out.RT.n_pos(), -1);
       for (size_t t = 0; t < rt_e.size(); ++t) out.rt_pt[eRT[t]] = ePT[rt_e[t]];
     }

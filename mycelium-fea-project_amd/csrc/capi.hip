@@ -1234,6 +1234,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
           d.RT = mat(L.RT, false, true);
           d.RT.rg = row_range(L.RT, 0, L.RT.n);
           d.rt_pt = I(L.rt_pt);
+          d.rt_row = I(L.rt_row);
           d.compact = h->opt_amg_cycle;
         }
         if (pt.amg_coll.kc > 0 && l >= pt.amg_coll.kc) {  // the collapsed operators of this level

@@ -8,6 +8,8 @@ set -u
 TAG=$1; CFG=${2:-C3_1M}; REPS=${3:-50}; shift 3 2>/dev/null || shift $#
 SETS=${*:+--set $*}
 export TMPDIR=/tmp
+# one packet per graph node under the tracer (round_measure.sh)
+export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
 D=gpurun_out/prof_$TAG
 mkdir -p $D
 P="python3 tools/amg_profile.py --config $CFG --reps $REPS $SETS"

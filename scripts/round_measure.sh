@@ -6,6 +6,10 @@
 #   gpurun -- bash scripts/round_measure.sh TAG b   the bench lines (C3 default with its
 #             CPU legs, C2, C5) and the rocprofv3 kernel stats of the default bench command
 # Everything lands under gpurun_out/ (TAG_*.log, prof_TAG_*, traffic_*.json) for profiles/.
+# Under rocprofv3 the HIP runtime submits each graph node as its own packet
+# (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0): the tracer's queue interception walks a
+# multi-packet batch past the end of the 1 MiB queue ring when one straddles
+# it — kernel durations are unaffected.
 set -u
 T=${1:-fin}
 PHASE=${2:-a}
@@ -22,5 +26,5 @@ else
     "c3:400:python bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench_C3_1M.json" \
     "c2:200:python bench.py --config C2_100k --no-cpu --steps 20 --warmup 5 > gpurun_out/${T}_bench_C2_100k.json" \
     "c5:300:python bench.py --config C5_10M_dense --no-cpu --steps 5 --warmup 2 > gpurun_out/${T}_bench_C5_10M_dense.json" \
-    "prof:400:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 tools/maps_bench.py --steps 20 --warmup 5"
+    "prof:400:cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_benchprof -o t -- python3 tools/maps_bench.py --steps 20 --warmup 5"
 fi

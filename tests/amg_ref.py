@@ -19,7 +19,7 @@ RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
 
 _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
           "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b",
-          "PT.sptr", "PT.col", "pt_row", "pt_ap", "pt_p", "RT.sptr", "RT.col", "rt_pt")
+          "PT.sptr", "PT.col", "pt_row", "pt_ap", "pt_p", "RT.sptr", "RT.col", "rt_pt", "rt_row")
 
 
 def fetch_plan(shim, active, nd, build=True):
@@ -92,8 +92,10 @@ def _sym(v6, nd):
                      np.stack([v6[..., 2], v6[..., 4], v6[..., 5]], -1)], -2)
 
 
-def to_scipy(blocks, sptr, col, n_rows, n_cols, nd):
+def to_scipy(blocks, sptr, col, n_rows, n_cols, nd, rowmap=None):
     row, _ = pos_rows(sptr, n_rows)
+    if rowmap is not None:  # layout rows → the matrix's rows (R̂: rt_row)
+        row = np.where(row >= 0, np.asarray(rowmap)[np.maximum(row, 0)], -1)
     ok = (col >= 0) & (row >= 0)
     r, c, b = row[ok], col[ok], blocks[ok]
     rr = (r[:, None, None] * nd + np.arange(nd)[None, :, None]) + 0 * np.arange(nd)[None, None, :]
@@ -188,7 +190,7 @@ def compact_transfers(levels):
         rok = L["rt_pt"] >= 0
         RTb = np.zeros((len(L["rt_pt"]), nd, nd))
         RTb[rok] = np.transpose(PTb[L["rt_pt"][rok]], (0, 2, 1))
-        L["Rt"] = to_scipy(RTb, L["RT.sptr"], L["RT.col"], L["nc"], n, nd)
+        L["Rt"] = to_scipy(RTb, L["RT.sptr"], L["RT.col"], L["nc"], n, nd, L["rt_row"])
     return levels
 
 
@@ -248,6 +250,7 @@ def scaled_blocks(levels):
         n, nd = L["n"], L["dinv"].shape[1]
         D = np.linalg.inv(L["dinv"])
         jrow, _ = pos_rows(L["RT.sptr"], L["nc"])
+        jrow = np.where(jrow >= 0, L["rt_row"][np.maximum(jrow, 0)], -1)
         col = L["RT.col"]
         ok = (col >= 0) & (jrow >= 0) & (L["rt_pt"] >= 0)
         Rh = np.zeros((len(col), nd, nd))

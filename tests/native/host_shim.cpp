@@ -227,6 +227,7 @@ int64_t shim_amg_array(int l, const char* name, int32_t* out) {
   else if (n == "RT.sptr") v = &L.RT.sptr;
   else if (n == "RT.col") v = &L.RT.col;
   else if (n == "rt_pt") v = &L.rt_pt;
+  else if (n == "rt_row") v = &L.rt_row;
   else if (n == "row0") v = &g_amg.row0;
   else if (n == "a0.ptr") v = &g_amg.a0.ptr;
   else if (n == "a0.a") v = &g_amg.a0.a;

@@ -51,11 +51,10 @@ __device__ __forceinline__ int64_t setup_block(int x1) {
 // ---------------------------------------------------------------------------
 // numeric setup (f64, with f32 copies for the V-cycle)
 // ---------------------------------------------------------------------------
-// Block-Jacobi inverse, Gershgorin bound per block.  L0: level 0, whose
-// diagonal block K_ii + reg·I (Pattern row row0[i]) is formed and stored here.
-template <int ND, bool L0>
-__device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, const int32_t* __restrict__ row0,
-                                           double reg, int64_t i) {
+// Block-Jacobi inverse and Gershgorin bound per block of a coarse level
+// (level 0's are formed with its blocks, k_amg_a0dinv).
+template <int ND>
+__device__ __forceinline__ double dinv_row(const AmgLevD& L, int64_t i) {
   const AmgMatD& A = L.A;
   double g = 0.0;
   if (i - (threadIdx.x & 63) < A.rg.hi) {
@@ -64,25 +63,8 @@ __device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, 
     slice_of(A, i, base, w);
     if (i >= A.rg.lo && i < A.rg.hi) {
       double D[ND * ND], Di[ND * ND];
-      if (L0) {
-        double s6[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
-        s6[0] += reg;
-        s6[3] += reg;
-        s6[5] += reg;
-        sym_to<ND>(s6, D);
-        bstore<ND>(A.val32, A.npos, base, D);
-        bstore_sym<ND>(A.sym, A.npos, base, D);
-        bstore_sym<ND>(A.sym32, A.npos, base, D);
-      } else {
-        bload<ND>(A.val32, A.npos, base, D);
-      }
+      bload<ND>(A.val32, A.npos, base, D);
       binv<ND>(D, Di);
-      if (L.dinv) {  // f64 copy: a one-level hierarchy's exact block solve (k_amg_cg_init)
-#pragma unroll
-        for (int c = 0; c < ND * ND; ++c) L.dinv[i * (ND * ND) + c] = Di[c];
-      }
 #pragma unroll
       for (int c = 0; c < ND * ND; ++c) L.dinv32[i * (ND * ND) + c] = (float)Di[c];
       double rs[ND];
@@ -112,13 +94,12 @@ __device__ __forceinline__ double dinv_row(const AmgLevD& L, const SellOp& sop, 
   }
   return g;
 }
-template <int ND, bool L0>
-__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
-                                                     double reg) {
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
   __shared__ double red[kBlock / 64];
   const int64_t xb = setup_block(L.x1);
   if (xb < 0) return;
-  double g = dinv_row<ND, L0>(L, sop, row0, reg, L.A.rg.lo64() + xb * kBlock + threadIdx.x);
+  double g = dinv_row<ND>(L, L.A.rg.lo64() + xb * kBlock + threadIdx.x);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
@@ -129,14 +110,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L, SellOp sop, cons
     // the level's bound g = max over blocks: a max is order-free, so one
     // atomic per block gives the same bits as any reduction (m ≥ 0, so its
     // IEEE bits order as unsigned integers); zeroed by the kernel producing
-    // this level's A (k_amg_a0 / k_amg_ac)
+    // this level's A (k_amg_ac / k_amg_fuse_ac)
     atomicMax(reinterpret_cast<unsigned long long*>(&L.omega[1]),
               static_cast<unsigned long long>(__double_as_longlong(m)));
   }
 }
 
-
-// Level 0 in one row-wise pass (replaces k_amg_a0 + k_amg_dinv<ND, true>):
+// Level 0 in one row-wise pass (one launch where a0 and a level-0 D⁻¹ were two):
 // per row i, the diagonal K_ii + reg·I from the assembled diagonal, its exact
 // inverse, every off-diagonal block (Σ of the listed SELL slots' K_ij = −S_e,
 // slot order) stored as A_0's f64 symmetric / f32 blocks, and the Gershgorin
@@ -165,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
       sym_to<ND>(s6, D);
       bstore<ND>(A.val32, A.npos, base, D);
       bstore_sym<ND>(A.sym, A.npos, base, D);
-      bstore_sym<ND>(A.sym32, A.npos, base, D);
+      if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, base, D);  // the four-step cycle's level-0 blocks
       binv<ND>(D, Di);
       if (L.dinv) {  // f64 copy: a one-level hierarchy's exact block solve (k_amg_cg_init)
 #pragma unroll
@@ -213,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
           }
           bstore<ND>(A.val32, A.npos, q[u], m);
           bstore_sym<ND>(A.sym, A.npos, q[u], m);
-          bstore_sym<ND>(A.sym32, A.npos, q[u], m);
+          if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q[u], m);
           double pm[ND * ND];
 #pragma unroll
           for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
@@ -288,7 +268,9 @@ template <int ND, bool PTV>
 __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   const int64_t k = blk * kBlock + threadIdx.x;
   const int64_t qr = L.R.rg.p0 + k;
-  if (qr < L.R.rg.p1 && L.R.col[qr] >= 0 && pos_mine(L.R.rg, qr)) {  // R = Pᵀ (f32) in R's own SELL layout
+  // R = Pᵀ (f32) in R's own SELL layout: the four-step cycle's restriction
+  // (the compact cycle restricts with R̂)
+  if (!L.compact && qr < L.R.rg.p1 && L.R.col[qr] >= 0 && pos_mine(L.R.rg, qr)) {
     double p[ND * ND], t[ND * ND];
     bload<ND>(L.P.val32, L.P.npos, L.rp[qr], p);
 #pragma unroll
@@ -1216,9 +1198,9 @@ static dim3 xg(const AmgLevD& L, int64_t blocks) { return xg(L, dim3((unsigned)b
 template <int ND>
 static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool level0, int stage) {
   if (L.A.n <= 0) return;
-  // level 0's k_amg_dinv ran in launch_amg_a0 (it also forms the diagonal)
+  // level 0's D⁻¹ came with its blocks (k_amg_a0dinv, launch_amg_a0)
   if (stage & kSetupDinv && !level0)
-    hipLaunchKernelGGL((k_amg_dinv<ND, false>), xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+    hipLaunchKernelGGL(k_amg_dinv<ND>, xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L);
   if (L.coarsest || !N) return;
   if (stage & kSetupP && L.P.wmax > 0)
     hipLaunchKernelGGL(k_amg_pvals<ND>, xg(L, slot_grid(L.P.rg.npos())), dim3(kBlock), 0, s, L);
@@ -1265,14 +1247,14 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     if (L.A.n <= 0) return;
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0)
-      hipLaunchKernelGGL((k_amg_dinv<ND, false>), xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L, SellOp{}, nullptr, 0.0);
+      hipLaunchKernelGGL(k_amg_dinv<ND>, xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L);
     const int64_t g0 = !last && L.P.wmax > 0 ? slot_blocks(L.P.rg.npos()) : 0;
     const int64_t g1 = g0 + (compact(l) ? slot_blocks(L.A.npos) : 0);
     const int64_t g2 = g1 + (l > 0 && compact(l - 1) ? slot_blocks(lev[l - 1].RT.npos) : 0);
     if (g2 > 0)
       hipLaunchKernelGGL(k_amg_fuse_p<ND>, xg(L, g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
     if (last) break;
-    const dim3 gap = rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()));
+    const dim3 gap = rows_grid(std::max(L.AP.rg.npos(), L.compact ? 0 : L.R.rg.npos()));
     if (compact(l) && L.PT.npos == L.AP.npos) {  // P̃ formed by the A·P kernel
       hipLaunchKernelGGL((k_amg_ap<ND, true>), xg(L, gap), dim3(kBlock), 0, s, L);
       hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega);

@@ -1165,10 +1165,18 @@ static dim3 rows_grid(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBl
 // vs 170.0 µs at 512 and 169.5 at 1024; C5 1786 vs 1831 vs 1784), 512 / 256
 // below.  Both read the w kernel's partial count, amg_w_grid.  cg.w_block > 0
 // overrides the choice (mfea_set_option "amg_w_block").
+// Round 4: between 512·512 and 768·512 rows the smallest of 576 / 640 / 704 /
+// 768 whose grid fits kCgMaxG blocks in one pass — at C3 704 × 478 blocks
+// instead of 768 × 438: two blocks on every CU carry 1,408 rows instead of
+// 1,536 where 74 CUs got one (the SpMV is one pass of latency-bound rows).
 int amg_w_block(const AmgCg& cg) {
   if (cg.w_block > 0) return cg.w_block;
   const int64_t n = cg.hi > cg.lo ? cg.hi - cg.lo64() : 0;
-  return n > (int64_t)kCgMaxG * 512 ? 768 : n > (int64_t)kCgMaxG * kCgBS ? 512 : kCgBS;
+  if (n <= (int64_t)kCgMaxG * kCgBS) return kCgBS;
+  if (n <= (int64_t)kCgMaxG * 512) return 512;
+  for (int bs : {576, 640, 704})
+    if (n <= (int64_t)kCgMaxG * bs) return bs;
+  return 768;
 }
 int64_t amg_w_grid(const AmgCg& cg) {
   const int64_t n = cg.hi > cg.lo ? cg.hi - cg.lo64() : 0;
@@ -1511,7 +1519,9 @@ static void w_nd(hipStream_t s, int j, bool first, const AmgLevD& L0, const AmgC
                  double* part, const AmgDist* d) {
   switch (amg_w_block(cg)) {
     case 512: w_bs<ND, 512>(s, j, first, L0, cg, slots, part, d); break;
+    case 576: w_bs<ND, 576>(s, j, first, L0, cg, slots, part, d); break;
     case 640: w_bs<ND, 640>(s, j, first, L0, cg, slots, part, d); break;
+    case 704: w_bs<ND, 704>(s, j, first, L0, cg, slots, part, d); break;
     case 768: w_bs<ND, 768>(s, j, first, L0, cg, slots, part, d); break;
     case 1024: w_bs<ND, 1024>(s, j, first, L0, cg, slots, part, d); break;
     default: w_bs<ND, kCgBS>(s, j, first, L0, cg, slots, part, d); break;

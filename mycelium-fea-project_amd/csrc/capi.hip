@@ -3197,8 +3197,9 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     rebuild = true;
   }
   else if (n == "amg_w_block") {
-    if (value != 0 && value != 256 && value != 512 && value != 640 && value != 768 && value != 1024)
-      return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 640, 768 or 1024");
+    if (value != 0 && value != 256 && value != 512 && value != 576 && value != 640 && value != 704 &&
+        value != 768 && value != 1024)
+      return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 576, 640, 704, 768 or 1024");
     h->opt_amg_w_block = (int)value;
     for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
   }

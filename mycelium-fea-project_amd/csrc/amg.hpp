@@ -168,6 +168,10 @@ struct AmgStrength {
 struct AmgLayout {
   int spatial = 0;
   double far_frac = 0.10;
+  // rows of a coarse level sorted by their A length alone (the compact
+  // cycle's sweeps read A and R̂, which has labels of its own); false: by
+  // A + R length (the four-step cycle's resid and restriction)
+  bool by_a = false;
 };
 
 // Builds the hierarchy for the free rows [0, P.n_free) of P with the element

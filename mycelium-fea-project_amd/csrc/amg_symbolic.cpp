@@ -508,7 +508,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   for (int l = 0; l < nlev; ++l) {
     const int64_t n = lv[l].A.n;
     std::vector<int64_t> key(n);
-    for (int64_t i = 0; i < n; ++i) key[i] = lv[l].A.len(i) + (l ? lv[l - 1].R.len(i) : 0);
+    for (int64_t i = 0; i < n; ++i) key[i] = lv[l].A.len(i) + (l && !lay.by_a ? lv[l - 1].R.len(i) : 0);
     // levels [0, n_dist] owner-major (level n_dist: its rows are produced by
     // their rank's restriction, then gathered by every rank)
     const bool om = dist && l <= n_dist && l < (int)own.size();

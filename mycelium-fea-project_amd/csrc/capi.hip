@@ -1462,6 +1462,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   pt.amg_ok = false;
   AmgLayout lay;
   lay.spatial = h->opt_amg_spatial;
+  lay.by_a = h->opt_amg_cycle == 1;
   const bool sweep = kind == MFEA_PC_SOR || kind == MFEA_PC_ICC;
   std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, sweep ? 1 : h->opt_amg_max_levels, nullptr,
                               amg_strength(h), lay);

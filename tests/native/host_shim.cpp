@@ -134,6 +134,7 @@ static AmgStrength g_strength;
 static AmgLayout g_layout;
 // row labels of the next shim_amg (amg.hpp AmgLayout: 0 depth-first, 1 Z-order, -1 by locality)
 void shim_amg_layout(int spatial) { g_layout.spatial = spatial; }
+void shim_amg_layout_by_a(int by_a) { g_layout.by_a = by_a != 0; }
 int shim_amg_spatial() { return g_amg.spatial ? 1 : 0; }
 // strength of connection of the next shim_amg / shim_amg_dist (amg.hpp AmgStrength)
 void shim_amg_strength(double theta, double kb_kax) {

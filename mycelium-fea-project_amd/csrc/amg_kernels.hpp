@@ -140,6 +140,7 @@ struct AmgCg {
 // Block-Jacobi multicolour SSOR / DIC(0) (sweep.hip, amg.hpp SweepPlan): per
 // level-0 row its colour and in-block lower / upper couplings; dt32 the
 // blocks D̃⁻¹ the sweeps apply (SOR: A_0's D⁻¹; ICC: formed by k_sweep_dic)
+constexpr int kSweepRows = 1024;  // rows per block = threads per workgroup (sweep.hip)
 struct SweepD {
   int64_t n = 0;
   int colors = 0;

@@ -1466,7 +1466,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   const bool sweep = kind == MFEA_PC_SOR || kind == MFEA_PC_ICC;
   std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, sweep ? 1 : h->opt_amg_max_levels, nullptr,
                               amg_strength(h), lay);
-  if (err.empty() && sweep) err = build_sweep(pt.amg, 256, pt.sweep);
+  if (err.empty() && sweep) err = build_sweep(pt.amg, kSweepRows, pt.sweep);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   pt.amg_kind = kind;

@@ -694,7 +694,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 // Down: blocks [0, gc) form the next level's x_{l+1} = R̂ x_l (S lanes per
 // coarse row), blocks from gc on the smoothed part c_l = 2 x_l − Ã x_l
 // (= x + ω D⁻¹ (b − A x)), kept in t_l.  Both read only x_l.
-template <int ND, int S, int KF = 2>
+template <int ND, int S, int KF = 2, int K1 = 3>
 __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64_t gc, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t xb = xcd_block();
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     float xc[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
-    if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.x, xc);
+    if constexpr (S == 1) sell_mac<ND, false, K1>(R.col, R.val32, R.npos, base, w, L.x, xc);
     else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.x, xc);
     if (I < n && sub == 0 && run) vstore<ND>(N.x, L.rt_row[I], xc);
   } else {
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
 // Up: e_l = c_l + P̃ e_{l+1} (the coarsest level's output is its x), S lanes
 // per row; level 0 writes the CG's u.  P̃'s rows run in A·P's order: row a is
 // the level's row pt_row[a] (c gathered, e scattered — within 4096-row windows)
-template <int ND, int S, class TE>
+template <int ND, int S, class TE, int K1 = 3>
 __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __restrict__ e, const int32_t* gate) {
   const bool run = gate_open(gate);
   const AmgMatD& T = L.PT;
@@ -756,14 +756,14 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
     for (int a = 0; a < ND; ++a) y[a] = 0.0f;
   }
   const float* src = N.coarsest ? N.x : N.e;
-  if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
+  if constexpr (S == 1) sell_mac<ND, false, K1>(T.col, T.val32, T.npos, base, w, src, y);
   else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
   if (a < n && sub == 0 && run) vstore<ND>(e, i, y);
 }
 
 // The collapsed cycle below level kc: e_kc = V x_kc in one sweep (V's rows
 // by length, vrow → the level's row), S lanes per row
-template <int ND, int S>
+template <int ND, int S, int K1 = 3>
 __global__ __launch_bounds__(kBlock) void k_amg_vapply(AmgLevD L, const int32_t* gate) {
   const bool run = gate_open(gate);
   const AmgMatD& V = L.CV;
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_vapply(AmgLevD L, const int32_t*
   float y[ND];
 #pragma unroll
   for (int c = 0; c < ND; ++c) y[c] = 0.0f;
-  if constexpr (S == 1) sell_mac<ND, false, 3>(V.col, V.val32, V.npos, base, w, L.x, y);
+  if constexpr (S == 1) sell_mac<ND, false, K1>(V.col, V.val32, V.npos, base, w, L.x, y);
   else sell_mac_sub<ND, S, false>(V.col, V.val32, base, w, sub, L.x, y);
   if (a < n && sub == 0 && run) vstore<ND>(L.e, L.cv_row[aa], y);
 }
@@ -1382,6 +1382,7 @@ static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int
   else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_down<ND, 1, 2, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);
 }
 template <int ND, class TE>
@@ -1390,6 +1391,7 @@ static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, cons
   const dim3 g(rows_grid(S * L.PT.n));
   if (S == 4) hipLaunchKernelGGL((k_amg_up<ND, 4, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
+  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_up<ND, 1, TE, 2>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
 }
 template <int ND>
@@ -1401,6 +1403,7 @@ static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   if (S == 8) hipLaunchKernelGGL((k_amg_vapply<ND, 8>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_vapply<ND, 4>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 2>), g, dim3(kBlock), 0, s, L, gate);
+  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 1, 2>), g, dim3(kBlock), 0, s, L, gate);
   else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);
 }
 template <int ND>

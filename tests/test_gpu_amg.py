@@ -240,7 +240,7 @@ def _variant_solves(engine, option, values, nx=1, ny=5, cycle=0):
 
 
 @pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8, 16]), ("amg_op_lanes", [1, 2, 4]),
-                                           ("amg_up_lanes", [1, 2, 4])])
+                                           ("amg_up_lanes", [1, 2, 4]), ("amg_up_k", [2, 3])])
 def test_vcycle_lane_splits_match_direct(engine, option, values):
     # four-step form and the compact one (every level's sweeps: no collapse)
     for cycle in (0, 1):
@@ -441,3 +441,16 @@ def test_fused_setup_bitwise_equals_separate_launches(engine, mesh):
                 out[v] = (engine.displacement(), st.iters)
             engine.set_option("amg_fuse_setup", 1)
         assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0]), (mesh, coll)
+
+
+def test_default_options_table_matches_library():
+    """mfea._capi.DEFAULT_OPTIONS documents the library's option defaults (a
+    fresh handle: the session engine's options are test-scoped)."""
+    from mfea import Engine
+    from mfea._capi import DEFAULT_OPTIONS
+    eng = Engine(0)
+    try:
+        got = {k: eng.get_option(k) for k in DEFAULT_OPTIONS}
+    finally:
+        eng.close()
+    assert got == DEFAULT_OPTIONS

@@ -55,7 +55,7 @@ extern "C" {
                                    two, measured (mfea_debug.h option "amg_dist") */
 
 #define MFEA_PC_SOR 3           /* `-pc_type sor`: SSOR (ω = 1, PETSc's default) on the
-                                   node blocks of K_ff + reg·I, block Jacobi over 1024-row
+                                   node blocks of K_ff + reg·I, block Jacobi over 256-row
                                    blocks with multicolour sweeps inside each (PETSc's
                                    SOR is processor-local in parallel); one partition */
 #define MFEA_PC_ICC 4           /* `-pc_type icc` (the reference source's default PCICC,

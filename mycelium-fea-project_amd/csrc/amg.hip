@@ -137,8 +137,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
     slice_of(A, i, base, w);
     if (i >= A.rg.lo && i < A.rg.hi) {
       double s6[6], D[ND * ND], Di[ND * ND];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
+      sym6_load<ND>(sop.diag, sop.N, row0[i], s6);
       s6[0] += reg;
       s6[3] += reg;
       s6[5] += reg;
@@ -185,8 +184,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
           for (int t = t0[u]; t < t1[u]; ++t) {
             double v6[6], e[ND * ND];
             const int64_t gs = lst[t];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
+            sym6_load<ND>(sop.val, sop.G, gs, v6);
             sym_to<ND>(v6, e);
 #pragma unroll
             for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
@@ -694,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_post(AmgLevD L, const TB* __rest
 // Down: blocks [0, gc) form the next level's x_{l+1} = R̂ x_l (S lanes per
 // coarse row), blocks from gc on the smoothed part c_l = 2 x_l − Ã x_l
 // (= x + ω D⁻¹ (b − A x)), kept in t_l.  Both read only x_l.
-template <int ND, int S, int KF = 2, int K1 = 3>
+template <int ND, int S, int KF = 2>
 __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64_t gc, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t xb = xcd_block();
@@ -712,7 +710,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     float xc[ND];
 #pragma unroll
     for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
-    if constexpr (S == 1) sell_mac<ND, false, K1>(R.col, R.val32, R.npos, base, w, L.x, xc);
+    if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.x, xc);
     else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.x, xc);
     if (I < n && sub == 0 && run) vstore<ND>(N.x, L.rt_row[I], xc);
   } else {
@@ -735,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
 // Up: e_l = c_l + P̃ e_{l+1} (the coarsest level's output is its x), S lanes
 // per row; level 0 writes the CG's u.  P̃'s rows run in A·P's order: row a is
 // the level's row pt_row[a] (c gathered, e scattered — within 4096-row windows)
-template <int ND, int S, class TE, int K1 = 3>
+template <int ND, int S, class TE>
 __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __restrict__ e, const int32_t* gate) {
   const bool run = gate_open(gate);
   const AmgMatD& T = L.PT;
@@ -756,14 +754,14 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
     for (int a = 0; a < ND; ++a) y[a] = 0.0f;
   }
   const float* src = N.coarsest ? N.x : N.e;
-  if constexpr (S == 1) sell_mac<ND, false, K1>(T.col, T.val32, T.npos, base, w, src, y);
+  if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
   else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
   if (a < n && sub == 0 && run) vstore<ND>(e, i, y);
 }
 
 // The collapsed cycle below level kc: e_kc = V x_kc in one sweep (V's rows
 // by length, vrow → the level's row), S lanes per row
-template <int ND, int S, int K1 = 3>
+template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_vapply(AmgLevD L, const int32_t* gate) {
   const bool run = gate_open(gate);
   const AmgMatD& V = L.CV;
@@ -779,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_vapply(AmgLevD L, const int32_t*
   float y[ND];
 #pragma unroll
   for (int c = 0; c < ND; ++c) y[c] = 0.0f;
-  if constexpr (S == 1) sell_mac<ND, false, K1>(V.col, V.val32, V.npos, base, w, L.x, y);
+  if constexpr (S == 1) sell_mac<ND, false, 3>(V.col, V.val32, V.npos, base, w, L.x, y);
   else sell_mac_sub<ND, S, false>(V.col, V.val32, base, w, sub, L.x, y);
   if (a < n && sub == 0 && run) vstore<ND>(L.e, L.cv_row[aa], y);
 }
@@ -1022,8 +1020,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
         const int64_t q = d.gslot[t];
         double s6[6], m[ND * ND], ug[ND];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) s6[c] = d.sval[(int64_t)c * d.G + q];
+        sym6_load<ND>(d.sval, d.G, q, s6);
         sym_to<ND>(s6, m);
         vload<ND>(d.urecv, d.grecv[t], ug);
 #pragma unroll
@@ -1382,7 +1379,6 @@ static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int
   else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_down<ND, 1, 2, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
   else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);
 }
 template <int ND, class TE>
@@ -1391,7 +1387,6 @@ static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, cons
   const dim3 g(rows_grid(S * L.PT.n));
   if (S == 4) hipLaunchKernelGGL((k_amg_up<ND, 4, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
-  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_up<ND, 1, TE, 2>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
 }
 template <int ND>
@@ -1403,7 +1398,6 @@ static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   if (S == 8) hipLaunchKernelGGL((k_amg_vapply<ND, 8>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_vapply<ND, 4>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 2>), g, dim3(kBlock), 0, s, L, gate);
-  else if (L.uk == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 1, 2>), g, dim3(kBlock), 0, s, L, gate);
   else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);
 }
 template <int ND>

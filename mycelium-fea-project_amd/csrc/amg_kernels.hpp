@@ -68,7 +68,6 @@ struct AmgLevD {
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
-  int uk = 3;        // one-lane compact sweeps (S = 1): widest step 4U (3) or 2U (2) slots (sell_mac's K)
   int x1 = 0;        // the numeric setup's launches over this level run on one XCD (amg.hip setup_block)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
@@ -141,7 +140,7 @@ struct AmgCg {
 // Block-Jacobi multicolour SSOR / DIC(0) (sweep.hip, amg.hpp SweepPlan): per
 // level-0 row its colour and in-block lower / upper couplings; dt32 the
 // blocks D̃⁻¹ the sweeps apply (SOR: A_0's D⁻¹; ICC: formed by k_sweep_dic)
-constexpr int kSweepRows = 1024;  // rows per block = threads per workgroup (sweep.hip)
+constexpr int kSweepRows = 256;  // rows per block = threads per workgroup (sweep.hip)
 struct SweepD {
   int64_t n = 0;
   int colors = 0;

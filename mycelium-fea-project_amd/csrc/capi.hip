@@ -240,7 +240,6 @@ struct mfea_handle {
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
-  int opt_amg_up_k = 3;      // GAMG compact sweeps at one lane per row: widest step 2 (2U) or 3 (4U slots)
   int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
                                    // C3: levels 4-5 gain 1-2 µs per launch, level 3 at 8192 lost as much)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
@@ -1202,7 +1201,6 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
-      d.uk = h->opt_amg_up_k;
       d.x1 = !rk && l > 0 && n <= h->opt_amg_x1_rows ? 1 : 0;
       if (!L.coarsest) {
         d.agg = I(L.agg);
@@ -3252,12 +3250,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.ulanes = (int)value;
   }
-  else if (n == "amg_up_k") {
-    if (value != 2 && value != 3) return fail(MFEA_EINVAL, "amg_up_k: 2 or 3");
-    h->opt_amg_up_k = (int)value;
-    for (auto& pp : h->parts)
-      for (auto& L : pp->amg_lev) L.uk = (int)value;
-  }
   else if (n == "amg_big_chunk") {
     if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
     h->opt_amg_big_chunk = (int)value;
@@ -3458,7 +3450,6 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
-  else if (n == "amg_up_k") *value = h->opt_amg_up_k;
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;
   else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;

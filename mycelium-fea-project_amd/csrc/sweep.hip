@@ -6,9 +6,9 @@
 //
 // Layout (amg.hpp SweepPlan): the AMG plan's level-0 rows (node blocks of
 // A_0 = K_ff + reg·I, depth-first order: hyphal chains contiguous) in blocks
-// of 1024 consecutive rows, one workgroup each.  Couplings between blocks are
+// of 256 consecutive rows, one workgroup each.  Couplings between blocks are
 // dropped — PETSc's SOR and ICC are processor-local in parallel, so this is
-// its semantics with a 1024-row "rank" per workgroup — and inside a block the
+// its semantics with a 256-row "rank" per workgroup — and inside a block the
 // rows are coloured (greedy, in row order), so the rows of one colour are
 // independent and each triangular sweep is C workgroup-barrier phases, all in
 // ONE launch per application.  With L / U the in-block couplings to earlier /
@@ -46,7 +46,7 @@ __device__ __forceinline__ bool spd(const double* m) {
 // D̃_i⁻¹ → sw.dt32
 template <int ND>
 __global__ __launch_bounds__(kSweepBS) void k_sweep_dic(SweepD sw, AmgLevD L0) {
-  __shared__ float dti[kSweepBS * ND * ND];  // D̃_j⁻¹ of the block's rows (f32: 36 KB at ND = 3)
+  __shared__ double dti[kSweepBS * ND * ND];  // D̃_j⁻¹ of the block's rows
   const int64_t i = (int64_t)blockIdx.x * kSweepBS + threadIdx.x;
   const bool valid = i < sw.n;
   const int c_i = valid ? sw.color[i] : -1;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kSweepBS) void k_sweep_dic(SweepD sw, AmgLevD L0) {
       }
       binv<ND>(spd<ND>(T) ? T : D, Di);
 #pragma unroll
-      for (int e = 0; e < ND * ND; ++e) dti[threadIdx.x * ND * ND + e] = (float)Di[e];
+      for (int e = 0; e < ND * ND; ++e) dti[threadIdx.x * ND * ND + e] = Di[e];
     }
     __syncthreads();
   }

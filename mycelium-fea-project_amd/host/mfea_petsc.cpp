@@ -18,7 +18,7 @@
 // (src/fea_petsc_parallel.cpp:339): so does this driver — -pc_type icc is the
 // default on one process, bjacobi under a multi-process launch.  icc (and ilu,
 // the same factor of an SPD matrix) is the engine's DIC(0) and sor its SSOR
-// (ω = 1), both block Jacobi over 1024-row blocks with multicolour sweeps
+// (ω = 1), both block Jacobi over 256-row blocks with multicolour sweeps
 // inside (PETSc's SOR / ICC are processor-local in parallel; sweep.hip);
 // bjacobi is the exact inverse of each node's 3×3 diagonal block and jacobi
 // PCJACOBI.  Documented differences: prescribed DOFs hold exactly their value
@@ -355,8 +355,8 @@ int main(int argc, char** argv) {
                   L.world, L.world > 1 ? "es" : "", device, stt.iters, stt.relres, o.rtol, o.atol, o.max_it,
                   o.norm == MFEA_NORM_PRECONDITIONED ? "PRECONDITIONED" : "UNPRECONDITIONED",
                   o.precond == MFEA_PC_JACOBI ? "jacobi" : o.precond == MFEA_PC_GAMG ? "gamg"
-                  : o.precond == MFEA_PC_ICC ? "icc (DIC(0), 1024-row blocks, multicolour)"
-                  : o.precond == MFEA_PC_SOR ? "sor (SSOR, 1024-row blocks, multicolour)" : "bjacobi (3x3 node blocks)");
+                  : o.precond == MFEA_PC_ICC ? "icc (DIC(0), 256-row blocks, multicolour)"
+                  : o.precond == MFEA_PC_SOR ? "sor (SSOR, 256-row blocks, multicolour)" : "bjacobi (3x3 node blocks)");
     }
     // the whole mesh's records on rank 0 (collective; one process: a copy)
     check(mfea_gather_results(h, U.data(), E ? S.data() : nullptr, E ? A.data() : nullptr), "mfea_gather_results");

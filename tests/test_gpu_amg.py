@@ -240,7 +240,7 @@ def _variant_solves(engine, option, values, nx=1, ny=5, cycle=0):
 
 
 @pytest.mark.parametrize("option,values", [("amg_restrict_lanes", [1, 2, 4, 8, 16]), ("amg_op_lanes", [1, 2, 4]),
-                                           ("amg_up_lanes", [1, 2, 4]), ("amg_up_k", [2, 3])])
+                                           ("amg_up_lanes", [1, 2, 4])])
 def test_vcycle_lane_splits_match_direct(engine, option, values):
     # four-step form and the compact one (every level's sweeps: no collapse)
     for cycle in (0, 1):

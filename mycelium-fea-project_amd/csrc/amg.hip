@@ -137,7 +137,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
     slice_of(A, i, base, w);
     if (i >= A.rg.lo && i < A.rg.hi) {
       double s6[6], D[ND * ND], Di[ND * ND];
-      sym6_load<ND>(sop.diag, sop.N, row0[i], s6);
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
       s6[0] += reg;
       s6[3] += reg;
       s6[5] += reg;
@@ -184,7 +185,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
           for (int t = t0[u]; t < t1[u]; ++t) {
             double v6[6], e[ND * ND];
             const int64_t gs = lst[t];
-            sym6_load<ND>(sop.val, sop.G, gs, v6);
+#pragma unroll
+            for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
             sym_to<ND>(v6, e);
 #pragma unroll
             for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
@@ -1020,7 +1022,8 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
       for (int t = d.gptr[i]; t < d.gptr[i + 1]; ++t) {
         const int64_t q = d.gslot[t];
         double s6[6], m[ND * ND], ug[ND];
-        sym6_load<ND>(d.sval, d.G, q, s6);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) s6[c] = d.sval[(int64_t)c * d.G + q];
         sym_to<ND>(s6, m);
         vload<ND>(d.urecv, d.grecv[t], ug);
 #pragma unroll

@@ -131,15 +131,6 @@ __device__ __forceinline__ void sym_to(const double* s6, double* m) {
   }
 }
 
-// the assembled operator's symmetric block [6][stride] at idx; a planar
-// level (ND = 2) reads only xx, xy, yy (the z components would be three more
-// cache lines per gathered block: C5's level-0 pass fetched 2.7 GB)
-template <int ND>
-__device__ __forceinline__ void sym6_load(const double* __restrict__ v, int64_t stride, int64_t idx, double* s6) {
-#pragma unroll
-  for (int c = 0; c < 6; ++c) s6[c] = (ND == 3 || c == 0 || c == 1 || c == 3) ? v[(int64_t)c * stride + idx] : 0.0;
-}
-
 __device__ __forceinline__ bool gated(const int32_t* gate) { return gate && *gate != kRun; }
 // The V-cycle kernels load the gate with their first operands and test it only
 // before their stores: a test at entry puts one more dependent memory round

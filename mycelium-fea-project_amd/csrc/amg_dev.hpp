@@ -356,7 +356,7 @@ constexpr double kRhoSafety = 1.45; // ω·g ≤ (4/3)·1.45 < 2
 
 // the smoother weight ω_l from the level's Gershgorin bound g = omega[1]
 __device__ __forceinline__ double amg_omega(const double* __restrict__ om) {
-  return (4.0 / 3.0) / fmax(kRhoFloor, om[1] / kRhoSafety);
+  return (4.0 / 3.0) / (om[0] > 0.0 ? om[0] : fmax(kRhoFloor, om[1] / kRhoSafety));
 }
 
 // S lanes per row (S = 2, 4) for the SELL operators with wide rows: R's rows

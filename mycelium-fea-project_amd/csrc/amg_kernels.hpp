@@ -57,7 +57,7 @@ struct AmgLevD {
   AmgMatD A;
   double* dinv = nullptr;
   float* dinv32 = nullptr;
-  double* omega = nullptr;  // [2]: [1] = Gershgorin bound g_l (ω_l = amg_omega(omega)); [0] unused
+  double* omega = nullptr;  // [2]: [1] = Gershgorin bound g_l; [0] > 0: ρ̂_l in place of max(2, g_l / 1.45) (ω_l = amg_omega(omega))
   // V-cycle vectors [n][ND], f32 (level 0: b = the CG's r, e = the CG's u, f64)
   float* b = nullptr;
   float* x = nullptr;

@@ -201,6 +201,8 @@ struct mfea_handle {
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipGraphExec_t graph_big = nullptr;  // GAMG: the planned batch's long chunks
   int graph_big_chunk = 0, graph_big_ell = -1;
+  hipGraphExec_t graph_rem = nullptr;  // GAMG: the planned batch's remainder, its exact length
+  int graph_rem_chunk = 0, graph_rem_ell = -1;
   // GAMG: the numeric setup's launches (≈ 30) as one graph, keyed by a hash
   // of every argument they take (the level views, the level-0 operator, reg)
   hipGraphExec_t graph_setup = nullptr;
@@ -240,6 +242,11 @@ struct mfea_handle {
   int64_t opt_amg_collapse_pairs = 8000000;  // … budget: its setup products' list items
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
+  // GAMG: ρ̂ of the levels below 0 in ppm (ω_l = 4 / (3 ρ̂)); 0: max(2, g_l / 1.45), the
+  // Gershgorin-safe value.  One partition only; a solve that fails with it
+  // falls back to the safe value for the handle's lifetime (amg_safe_omega).
+  int64_t opt_amg_coarse_rho_ppm = 1750000;
+  bool amg_safe_omega = false;
   int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
                                    // C3: levels 4-5 gain 1-2 µs per launch, level 3 at 8192 lost as much)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
@@ -310,6 +317,10 @@ void destroy_graph(mfea_handle* h) {
   h->graph_big = nullptr;
   h->graph_big_chunk = 0;
   h->graph_big_ell = -1;
+  if (h->graph_rem) (void)hipGraphExecDestroy(h->graph_rem);
+  h->graph_rem = nullptr;
+  h->graph_rem_chunk = 0;
+  h->graph_rem_ell = -1;
   h->graph = nullptr;
   h->graph_chunk = 0;
   h->graph_precond = -1;
@@ -913,16 +924,22 @@ int drive_planned(mfea_handle* h, int chunk, int max_it, int expected, Enqueue&&
 // one at a time until the device reports done.  enqueue(size) queues one.
 template <class Enqueue, class After = NoEpilogue>
 int drive_sized(mfea_handle* h, int big, int small, int max_it, int expected, Enqueue&& enqueue,
-                SolveState* out, After&& after = After{}) {
+                SolveState* out, After&& after = After{}, bool exact_rem = false) {
   hipStream_t s = h->stream;
   volatile SolveState* hs = h->h_state;
   hs[0].done = 0;
   const int need = std::max(1, expected + 1);  // updates the batch assumes, as drive_planned
   const int nbig = big > small ? need / big : 0;
-  const int nsmall = (need - nbig * big + small - 1) / small;
+  const int rem = need - nbig * big;
+  const int nsmall = (rem + small - 1) / small;
   int64_t done_its = 0;
   for (int k = 0; k < nbig; ++k, done_its += big) RC(enqueue(big));
-  for (int k = 0; k < nsmall; ++k, done_its += small) RC(enqueue(small));
+  if (exact_rem && rem > 0) {  // one chunk of the remainder's own length (drive_rem_chunk)
+    RC(enqueue(rem));
+    done_its += rem;
+  } else {
+    for (int k = 0; k < nsmall; ++k, done_its += small) RC(enqueue(small));
+  }
   RC(after());
   HIPC(hipEventRecord(h->poll[0], s));
   RC(wait_event(h, h->poll[0]));
@@ -1098,6 +1115,12 @@ static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
 // 0.3 M product pairs, a few ms of host build per rebuild) for one saved
 // launch pair; level 2 is what C2 / C3 choose anyway
 constexpr int kAmgCollapseAutoLevel = 2;
+
+// ρ̂ of the levels below 0 (0: the Gershgorin rule): one partition, until a
+// solve has failed with it
+double coarse_rho(const mfea_handle* h) {
+  return partitioned(h) || h->amg_safe_omega ? 0.0 : (double)h->opt_amg_coarse_rho_ppm * 1e-6;
+}
 
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
                const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
@@ -1288,6 +1311,12 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_lev[0].fmask = pt.amg_fmask.ptr;
     pt.amg_mask_key.clear();
   }
+  // ρ̂ of the coarse levels in place of the Gershgorin estimate (omega[0], zeroed above;
+  // DESIGN.md §4.2 "Coarse-level smoothing weight")
+  const double rho_coarse = coarse_rho(h);
+  if (rho_coarse > 0.0)
+    for (int l = 1; l < nlev; ++l)
+      HIPC(hipMemcpyAsync(pt.amg_lev[l].omega, &rho_coarse, sizeof(double), hipMemcpyHostToDevice, s));
   HIPC(pt.amg_levd.alloc(std::max(nlev, 1)));
   HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
   HIPC(hipStreamSynchronize(s));
@@ -1744,14 +1773,39 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
       h->graph_big_chunk = big;
       h->graph_big_ell = tag;
     }
+    // the batch's remainder as ONE chunk of its own length (captured once per
+    // length; the AMG iteration kernels keep no state across chunks that
+    // depends on the chunk's parity): an odd iteration count no longer runs
+    // one gated iteration — which costs as much as a live one — nor two
+    // extra chunk boundaries (C3 at 15 iterations: 8 + 7 instead of 8 + 4×2)
+    const int need = std::max(1, expected + 1);
+    const int rem = big > chunk ? need - (need / big) * big : 0;
+    const bool exact_rem = rem > 0 && rem != chunk;
+    if (exact_rem && (h->graph_rem == nullptr || h->graph_rem_chunk != rem || h->graph_rem_ell != tag)) {
+      if (h->graph_rem) (void)hipGraphExecDestroy(h->graph_rem);
+      h->graph_rem = nullptr;
+      RC(capture(&h->graph_rem, rem));
+      h->graph_rem_chunk = rem;
+      h->graph_rem_ell = tag;
+    }
     rc = drive_sized(h, big, chunk, o->max_it, expected,
                      [&](int n) -> int {
-                       HIPC(hipGraphLaunch(n == chunk ? h->graph : h->graph_big, s));
+                       HIPC(hipGraphLaunch(n == chunk ? h->graph : n == big ? h->graph_big : h->graph_rem, s));
                        return 0;
                      },
-                     &fin, finish);
+                     &fin, finish, exact_rem);
   }
   if (rc) return rc;
+  if (fin.status != 0 && coarse_rho(h) > 0.0 && pt.amg_lev.size() > 1 && pt.amg_kind == MFEA_PC_GAMG) {
+    // the over-relaxed coarse smoothers did not give an SPD cycle on this
+    // operator (ω_l λ_l ≥ 2 somewhere): the Gershgorin-safe weights from now
+    // on, and this solve again (its numeric setup re-forms every ω product)
+    h->amg_safe_omega = true;
+    for (size_t l = 1; l < pt.amg_lev.size(); ++l)
+      HIPC(hipMemsetAsync(pt.amg_lev[l].omega, 0, sizeof(double), s));
+    RC(sync_stream(h));
+    return solve_amg(h, dy_top, dy_bot, o, st);
+  }
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
   if (fin.status == 0 && !pt.amg_reused) {
     pt.amg_build_iters = fin.iters;  // the hierarchy on the set it was built for
@@ -3250,6 +3304,13 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.ulanes = (int)value;
   }
+  else if (n == "amg_coarse_rho_ppm") {
+    if (value != 0 && (value < 100000 || value > 100000000))
+      return fail(MFEA_EINVAL, "amg_coarse_rho_ppm: 0 (Gershgorin) or 1e5 .. 1e8");
+    h->opt_amg_coarse_rho_ppm = value;
+    h->amg_safe_omega = false;
+    rebuild = true;
+  }
   else if (n == "amg_big_chunk") {
     if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
     h->opt_amg_big_chunk = (int)value;
@@ -3450,6 +3511,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
+  else if (n == "amg_coarse_rho_ppm") *value = h->opt_amg_coarse_rho_ppm;
+  else if (n == "amg_safe_omega") *value = h->amg_safe_omega ? 1 : 0;  // read-only
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;
   else if (n == "amg_collapse_mb") *value = h->opt_amg_collapse_mb;

@@ -20,7 +20,7 @@ DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_
                    "amg_rep_rows": 32768, "amg_cycle": 1, "amg_fuse_setup": 1, "amg_big_chunk": 8,
                    "amg_up_lanes": 0, "amg_spatial": -1, "amg_collapse": -1, "amg_collapse_mb": 32,
                    "amg_collapse_pairs": 8000000, "amg_theta_ppm": 0, "amg_reuse": 1, "amg_rebuild_pct": 150,
-                   "amg_x1_rows": 2048}
+                   "amg_x1_rows": 2048, "amg_coarse_rho_ppm": 1750000}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))

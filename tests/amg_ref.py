@@ -16,6 +16,7 @@ import numpy as np
 import scipy.sparse as sp
 
 RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
+RHO_COARSE = 1.75  # capi.hip opt_amg_coarse_rho_ppm: ρ̂ of the levels below 0 (one partition)
 
 _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
           "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b",
@@ -111,11 +112,13 @@ def _binv(D):
     return out
 
 
-def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None):
+def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho=RHO_COARSE):
     """The per-solve numeric setup of amg.hip on the plan: fills A (blocks),
     dinv, omega, P, AP for every level.  val/diag: the assembled SELL values.
     fmask: per level-0 row, 1 = a floating row whose P_0 row is formed as zero
-    (a hierarchy kept over element failures, amg.hip pvals_body)."""
+    (a hierarchy kept over element failures, amg.hip pvals_body).
+    coarse_rho: ρ̂ of the levels below 0 (0: the Gershgorin rule, as level 0
+    and every partitioned hierarchy)."""
     L0 = levels[0]
     n0 = L0["n"]
     row, k = pos_rows(L0["A.sptr"], n0)
@@ -142,7 +145,7 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None):
         rs = np.zeros((n, nd))
         np.add.at(rs, row[ok], M)
         g = rs.max() if n else 0.0
-        rho = max(RHO_FLOOR, g / RHO_SAFETY)
+        rho = coarse_rho if l > 0 and coarse_rho > 0 else max(RHO_FLOOR, g / RHO_SAFETY)
         L["omega"] = (4.0 / 3.0) / rho
         L["g"] = g
         L["A"] = to_scipy(Ab, L["A.sptr"], L["A.col"], n, n, nd)

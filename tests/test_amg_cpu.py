@@ -327,3 +327,36 @@ def test_collapsed_cycle_equals_the_recursion(shim):
             assert np.linalg.norm(V @ x - ref) <= 1e-12 * np.linalg.norm(ref), kc
     # a budget no level fits: no collapse
     assert shim.shim_amg_collapse(16, 1 << 40, 1, err, 256) == 0
+
+
+@pytest.mark.parametrize("mesh", ["golden22k", "C2_1x5", "C5_2x2"])
+def test_coarse_levels_spectral_radius_below_two(shim, mesh):
+    """The coarse smoothers run at ω = 4 / (3 · 1.75) (capi.hip
+    opt_amg_coarse_rho_ppm), over-relaxed against the Gershgorin-safe rule, so
+    the V-cycle stays SPD only while ω·λmax(D_l⁻¹A_l) < 2, i.e. λmax < 2.625.
+    Level 0 has λmax ≤ 2 exactly (A = Σ_e [[S,−S],[−S,S]] ≤ 2 D); the Galerkin
+    levels measure ≤ 2 as well on the reference network, the tiled benchmark
+    recipe and the chord (C5) recipe — 24 % under the limit — while their
+    Gershgorin bounds reach 3.2.  (A solve that fails anyway falls back to the
+    Gershgorin rule, test_gpu_amg.py::test_coarse_overrelaxation_fallback.)"""
+    from mfea import synth
+    if mesh == "golden22k":
+        xyz, e2n, top, bot = _golden22k()
+    else:
+        nx, ny, ch = {"C2_1x5": (1, 5, False), "C5_2x2": (2, 2, True)}[mesh]
+        xyz, e2n = synth.tiled_mesh(nx, ny, chords=ch)
+        top, bot = synth.grips(xyz)
+    levels, _, _, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    rng = np.random.default_rng(3)
+    for l, L in enumerate(levels):
+        if L["coarsest"]:
+            break
+        M = (sp.block_diag(list(L["dinv"]), format="csr") @ L["A"]).tocsr()
+        v = rng.standard_normal(M.shape[0])
+        for _ in range(60):
+            v = M @ v
+            lam = np.linalg.norm(v)
+            v /= lam
+        assert lam <= 2.05, (mesh, l, lam, L["g"])
+        if l > 0:
+            assert L["omega"] * lam < 1.6, (mesh, l, L["omega"], lam)

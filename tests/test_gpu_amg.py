@@ -454,3 +454,23 @@ def test_default_options_table_matches_library():
     finally:
         eng.close()
     assert got == DEFAULT_OPTIONS
+
+
+def test_coarse_overrelaxation_fallback(engine):
+    """The coarse smoothers' over-relaxed weight (amg_coarse_rho_ppm) is
+    measured, not proven, safe (tests/test_amg_cpu.py::
+    test_coarse_levels_spectral_radius_below_two).  A weight that breaks the
+    cycle — here ρ̂ = 0.2, ω = 6.7 — makes the solve fail; the engine then
+    re-forms the hierarchy with the Gershgorin-safe weights and solves again:
+    the same U as the default, and the handle stays on the safe weights."""
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    with engine.options(amg_coarse_rho_ppm=200000):
+        _sim181147(engine)
+        engine.assemble()
+        assert engine.get_option("amg_safe_omega") == 0
+        st = engine.solve(dy, -dy, _opts(1e-13))
+        assert st.status == 0
+        assert engine.get_option("amg_safe_omega") == 1
+        assert rel(engine.displacement(), sysz["U"]) <= 1e-10
+    assert engine.get_option("amg_safe_omega") == 0  # a new weight, a new chance

@@ -17,6 +17,11 @@
 // norm on every level and the V-cycle is symmetric positive definite — the
 // requirement for CG — while ω takes the sharp value 2/3 whenever g < 2.9.
 //
+// Below level 0 the engine by default replaces ρ̂ by 1.75 (omega[0], capi.hip
+// opt_amg_coarse_rho_ppm): the measured λ of the Galerkin levels is ≤ 2.0, so
+// the over-relaxed ω = 0.76 keeps ω·λ ≈ 1.5 — measured, not proven; a solve
+// that fails with it falls back to the rule above.
+//
 // V-cycle (one per PCG iteration, pre- and post-smoothing by one damped
 // block-Jacobi sweep each, exact block-diagonal solve on the coarsest level),
 // in f32 (values and vectors; the CG around it stays f64 — a preconditioner

@@ -243,8 +243,8 @@ struct mfea_handle {
   int opt_amg_spatial = -1;  // GAMG: rows labelled in Z-order (1), depth-first (0), by locality (-1)
   int opt_amg_up_lanes = 0;  // GAMG compact up sweep: lanes per P̃ row (0: by width)
   // GAMG: ρ̂ of the levels below 0 in ppm (ω_l = 4 / (3 ρ̂)); 0: max(2, g_l / 1.45), the
-  // Gershgorin-safe value.  One partition only; a solve that fails with it
-  // falls back to the safe value for the handle's lifetime (amg_safe_omega).
+  // Gershgorin-safe value.  A solve that fails with it falls back to the safe
+  // value for the handle's lifetime (amg_safe_omega, omega_fallback).
   int64_t opt_amg_coarse_rho_ppm = 1750000;
   bool amg_safe_omega = false;
   int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
@@ -1116,10 +1116,24 @@ static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
 // launch pair; level 2 is what C2 / C3 choose anyway
 constexpr int kAmgCollapseAutoLevel = 2;
 
-// ρ̂ of the levels below 0 (0: the Gershgorin rule): one partition, until a
-// solve has failed with it
+// ρ̂ of the levels below 0 (0: the Gershgorin rule), until a solve has failed
+// with it
 double coarse_rho(const mfea_handle* h) {
-  return partitioned(h) || h->amg_safe_omega ? 0.0 : (double)h->opt_amg_coarse_rho_ppm * 1e-6;
+  return h->amg_safe_omega ? 0.0 : (double)h->opt_amg_coarse_rho_ppm * 1e-6;
+}
+
+// A GAMG solve failed (breakdown or max_it) with the over-relaxed coarse
+// smoothers: the Gershgorin-safe weights on every partition's hierarchy from
+// now on (its next numeric setup re-forms every ω product).  Partitioned over
+// RCCL every rank sees the same status (the CG scalars are all-reduced), so
+// every rank takes this path together.  True: the caller solves again.
+bool omega_fallback(mfea_handle* h, int status) {
+  if (status == 0 || coarse_rho(h) <= 0.0) return false;
+  h->amg_safe_omega = true;
+  for (auto& pp : h->parts)
+    for (size_t l = 1; l < pp->amg_lev.size(); ++l)
+      (void)hipMemsetAsync(pp->amg_lev[l].omega, 0, sizeof(double), h->stream);
+  return true;
 }
 
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
@@ -1796,13 +1810,9 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                      &fin, finish, exact_rem);
   }
   if (rc) return rc;
-  if (fin.status != 0 && coarse_rho(h) > 0.0 && pt.amg_lev.size() > 1 && pt.amg_kind == MFEA_PC_GAMG) {
+  if (pt.amg_lev.size() > 1 && pt.amg_kind == MFEA_PC_GAMG && omega_fallback(h, fin.status)) {
     // the over-relaxed coarse smoothers did not give an SPD cycle on this
-    // operator (ω_l λ_l ≥ 2 somewhere): the Gershgorin-safe weights from now
-    // on, and this solve again (its numeric setup re-forms every ω product)
-    h->amg_safe_omega = true;
-    for (size_t l = 1; l < pt.amg_lev.size(); ++l)
-      HIPC(hipMemsetAsync(pt.amg_lev[l].omega, 0, sizeof(double), s));
+    // operator (ω_l λ_l ≥ 2 somewhere): this solve again on the safe weights
     RC(sync_stream(h));
     return solve_amg(h, dy_top, dy_bot, o, st);
   }
@@ -2237,6 +2247,10 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
                      },
                      &fin));
   }
+  if (omega_fallback(h, fin.status)) {
+    RC(sync_stream(h));
+    return solve_gamg_global(h, dy_top, dy_bot, o, st);
+  }
   if (fin.status == 0) p0.amg_last_iters = fin.iters;
   // x to row order, then the displacement halo (ghost rows of the post kernels)
   for (auto& pp : h->parts) {
@@ -2339,6 +2353,10 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
                        return 0;
                      },
                      &fin));
+  }
+  if (omega_fallback(h, fin.status)) {
+    RC(sync_stream(h));
+    return solve_amg_dist(h, dy_top, dy_bot, o, st);
   }
   if (fin.status == 0) p0.amg_last_iters = fin.iters;
   // x to row order, then the displacement halo (ghost rows of the post kernels)

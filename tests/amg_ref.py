@@ -16,7 +16,7 @@ import numpy as np
 import scipy.sparse as sp
 
 RHO_FLOOR, RHO_SAFETY = 2.0, 1.45  # amg.hip kRhoFloor / kRhoSafety
-RHO_COARSE = 1.75  # capi.hip opt_amg_coarse_rho_ppm: ρ̂ of the levels below 0 (one partition)
+RHO_COARSE = 1.75  # capi.hip opt_amg_coarse_rho_ppm: ρ̂ of the levels below 0
 
 _NAMES = ("A.sptr", "A.col", "agg", "P.sptr", "P.col", "pv.ptr", "pv.a", "R.sptr", "R.col", "rp",
           "AP.sptr", "AP.col", "ap.ptr", "ap.a", "ap.b", "ac.ptr", "ac.a", "ac.b",
@@ -118,7 +118,7 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho
     fmask: per level-0 row, 1 = a floating row whose P_0 row is formed as zero
     (a hierarchy kept over element failures, amg.hip pvals_body).
     coarse_rho: ρ̂ of the levels below 0 (0: the Gershgorin rule, as level 0
-    and every partitioned hierarchy)."""
+    and the engine after a failed solve)."""
     L0 = levels[0]
     n0 = L0["n"]
     row, k = pos_rows(L0["A.sptr"], n0)

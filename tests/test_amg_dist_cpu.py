@@ -86,7 +86,7 @@ def _case(shim, xyz, e2n, top, bot, world, rep_rows, nd=2, active=None):
     shim.shim_node_owner(N, _p(xyz), E, _p(e2n), len(top), _p(top), len(bot), _p(bot), world, -1, 0.35, _p(owner))
     assert shim.shim_amg_dist(_p(act), nd, world, _p(owner), rep_rows, err, 256) > 0, err.value
     levels = amg_ref.fetch_plan(shim, act, nd, build=False)
-    amg_ref.numeric_setup(levels, val, diag, G, N, nd, coarse_rho=0.0)  # partitioned: Gershgorin ω
+    amg_ref.numeric_setup(levels, val, diag, G, N, nd)
     n_dist = shim.shim_amg_array(0, b"n_dist", None)
     K = fo.assemble_global_stiffness(xyz, e2n, act.astype(bool))
     known, vals = fo.known_dof_map(top, bot, 0.01, -0.01)

@@ -341,3 +341,20 @@ def test_dropin_partitioned_csvs_match_one_partition(tmp_path):
     Fa, Fb = a["force_displacement.csv"].values, b["force_displacement.csv"].values
     assert np.array_equal(Fa[:, 0], Fb[:, 0])
     assert np.abs(Fb[:, 1] - Fa[:, 1]).max() <= 1e-8 * np.abs(Fa[:, 1]).max()
+
+
+def test_partitioned_coarse_overrelaxation_fallback(peng):
+    """The over-relaxed coarse smoothers' fallback on a partitioned handle
+    (both GAMG forms): a breaking weight (ρ̂ = 0.2) makes the solve fail, every
+    partition re-forms its levels with the Gershgorin-safe weights, and the
+    solve still meets the direct solve."""
+    from mfea import PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    for dist in (1, 0):
+        with peng.options(amg_coarse_rho_ppm=200000, amg_dist=dist):
+            _sim181147(peng, 4, -1)
+            peng.assemble()
+            st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
+            assert st.status == 0 and peng.get_option("amg_safe_omega") == 1, dist
+            assert rel(peng.displacement(), sysz["U"]) <= 1e-10, dist

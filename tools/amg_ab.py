@@ -8,6 +8,7 @@ iteration count, the relative residual, the V-cycle iteration time
 interleaved per round so box drift hits all of them alike.
 
     python tools/amg_ab.py --configs C3_1M C5_10M_dense --option amg_restrict_lanes --values 0 2 4
+    python tools/amg_ab.py --option amg_collapse --values -1 1 --set amg_collapse_mb=1024
 """
 import argparse
 import json
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--values", nargs="+", type=int, default=[0, 2, 4])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--set", nargs="*", default=[], help="name=value options held fixed for every run")
     ap.add_argument("--chunk", type=int, nargs="*", default=[0],
                     help="solve chunk sizes to sweep as well (0: the engine's default)")
     a = ap.parse_args()
@@ -41,6 +43,9 @@ def main():
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
         top, bot = synth.grips(xyz)
         eng = Engine(0)
+        for kv in a.set:
+            k, v = kv.split("=")
+            eng.set_option(k, int(v))
         eng.set_material(fs.E_mod, fs.A, fs.I)
         eng.set_mesh(xyz, e2n)
         eng.set_bc(top, bot)

@@ -288,4 +288,15 @@ std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active,
                            const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,
                            AmgHalo& halo);
 
+// The GAMG form of a partitioned solve chosen automatically (option
+// "amg_dist" −1; capi.hip solve_amg_part): t[0] = the block-Jacobi form's
+// step time, t[1] = the global hierarchy's, seconds, −1 while untimed.  The
+// form to time next (the global one first), −1 once both are timed; then the
+// choice, the faster (ties: the global hierarchy).  Over RCCL every rank
+// passes the MAX over ranks of each time, so every rank returns the same
+// mode: the two forms issue different exchanges, and ranks on different
+// forms would hang (tests/test_amg_cpu.py::test_auto_form_choice_is_collective).
+inline int amg_auto_pending(const double t[2]) { return t[1] < 0 ? 1 : t[0] < 0 ? 0 : -1; }
+inline int amg_auto_choice(const double t[2]) { return t[1] <= t[0] ? 1 : 0; }
+
 }  // namespace mfea

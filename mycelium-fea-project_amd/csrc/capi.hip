@@ -2561,7 +2561,7 @@ int solve_amg_part(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
     a.t[0] = a.t[1] = -1.0;
   }
   if (a.choice >= 0) return run(a.choice);
-  const int mode = a.t[1] < 0 ? 1 : 0;
+  const int mode = amg_auto_pending(a.t);
   if (mode) {
     RC(ensure_gamg(h, &rebuilt));
   } else {
@@ -2578,7 +2578,7 @@ int solve_amg_part(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   // RCCL: every rank must pick the same form (the two issue different
   // exchanges), so each compares the slowest rank's times, not its own
   if (h->world > 1) RC(max_over_ranks(h, &a.t[mode]));
-  if (a.t[0] >= 0 && a.t[1] >= 0) a.choice = a.t[1] <= a.t[0] ? 1 : 0;
+  if (amg_auto_pending(a.t) < 0) a.choice = amg_auto_choice(a.t);
   if (rc == MFEA_EMAXIT || rc == MFEA_EBREAKDOWN) {
     a.choice = 1 - mode;
     rc = run(a.choice);

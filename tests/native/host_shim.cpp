@@ -136,6 +136,9 @@ static AmgLayout g_layout;
 void shim_amg_layout(int spatial) { g_layout.spatial = spatial; }
 void shim_amg_layout_by_a(int by_a) { g_layout.by_a = by_a != 0; }
 int shim_amg_spatial() { return g_amg.spatial ? 1 : 0; }
+// capi.hip solve_amg_part's automatic GAMG form (amg.hpp): t = {block Jacobi, global}
+int shim_amg_auto_pending(double t0, double t1) { const double t[2] = {t0, t1}; return amg_auto_pending(t); }
+int shim_amg_auto_choice(double t0, double t1) { const double t[2] = {t0, t1}; return amg_auto_choice(t); }
 // strength of connection of the next shim_amg / shim_amg_dist (amg.hpp AmgStrength)
 void shim_amg_strength(double theta, double kb_kax) {
   g_strength.theta = theta;

@@ -360,3 +360,27 @@ def test_coarse_levels_spectral_radius_below_two(shim, mesh):
         assert lam <= 2.05, (mesh, l, lam, L["g"])
         if l > 0:
             assert L["omega"] * lam < 1.6, (mesh, l, L["omega"], lam)
+
+
+def test_auto_form_choice_is_collective(shim):
+    """with amg_dist −1 each rank times both GAMG forms of a
+    partitioned solve and picks the faster; ranks on different forms issue
+    different exchanges and hang.  capi.hip max-all-reduces each time over the
+    ranks before the choice (max_over_ranks), so the choice (amg.hpp
+    amg_auto_pending / amg_auto_choice) sees the same inputs everywhere.
+    Two mocked ranks whose own timings disagree: local choices differ, the
+    choices on the reduced timings agree."""
+    shim.shim_amg_auto_pending.restype = C.c_int
+    shim.shim_amg_auto_pending.argtypes = [C.c_double, C.c_double]
+    shim.shim_amg_auto_choice.restype = C.c_int
+    shim.shim_amg_auto_choice.argtypes = [C.c_double, C.c_double]
+    # timing order: the global form first, then block Jacobi, then decide
+    assert shim.shim_amg_auto_pending(-1.0, -1.0) == 1
+    assert shim.shim_amg_auto_pending(-1.0, 2e-3) == 0
+    assert shim.shim_amg_auto_pending(1e-3, 2e-3) == -1
+    ranks = [(0.9e-3, 1.0e-3), (1.1e-3, 1.0e-3)]  # (block Jacobi, global) per rank
+    local = [shim.shim_amg_auto_choice(*t) for t in ranks]
+    assert local[0] != local[1]                     # what a per-rank choice would do
+    tmax = tuple(max(t[k] for t in ranks) for k in range(2))
+    assert [shim.shim_amg_auto_choice(*tmax) for _ in ranks] == [1, 1]
+    assert shim.shim_amg_auto_choice(1e-3, 1e-3) == 1   # ties: the global hierarchy

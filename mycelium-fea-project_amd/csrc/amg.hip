@@ -481,9 +481,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
   if (xb >= 0) vv_body<ND>(L, xb);
 }
 
-// A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread
+// A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread.  dinv_next
+// (level l+1 at a fixed ω, AmgLevD::fixed_omega): the thread of a diagonal
+// block (slot 0 of its row) also stores its inverse — from the stored f32
+// block, the bits k_amg_dinv would form — so level l+1 needs no D⁻¹ launch.
 template <int ND>
-__device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int64_t blk) {
+__device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int64_t blk, float* dinv_next) {
   const int64_t q = L.ac_rg.p0 + blk * kBlock + threadIdx.x;
   if (q >= L.ac_rg.p1 || Ac.col[q] < 0 || !pos_mine(L.ac_rg, q)) return;
   double C[ND * ND];
@@ -491,12 +494,25 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
   pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val32, L.P.npos, L.apval, L.AP.npos, C);
   bstore<ND>(Ac.val32, Ac.npos, q, C);
+  if (dinv_next) {
+    const int64_t t = q >> 6;
+    const int sl = Ac.srow[t];
+    if (t == (int64_t)Ac.sptr[sl]) {  // slot 0: the diagonal block of row 64·sl + lane
+      double D[ND * ND], Di[ND * ND];
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) D[c] = (double)(float)C[c];
+      binv<ND>(D, Di);
+      const int64_t row = 64 * (int64_t)sl + (q & 63);
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) dinv_next[row * (ND * ND) + c] = (float)Di[c];
+    }
+  }
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next) {
+__global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next, float* dinv_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
   const int64_t xb = setup_block(L.x1);
-  if (xb >= 0) ac_body<ND>(L, Ac, xb);
+  if (xb >= 0) ac_body<ND>(L, Ac, xb, dinv_next);
 }
 
 // The compact cycle's operators fused into the Galerkin chain's launches (no
@@ -514,11 +530,12 @@ __global__ __launch_bounds__(kBlock) void k_amg_fuse_p(AmgLevD L, AmgLevD Lp, in
   else rtv_body<ND>(Lp, L, xb - g1);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, double* omega_next, int64_t g0) {
+__global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, double* omega_next, int64_t g0,
+                                                        float* dinv_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;
   const int64_t xb = setup_block(L.x1);
   if (xb < 0) return;
-  if (xb < g0) ac_body<ND>(L, Ac, xb);
+  if (xb < g0) ac_body<ND>(L, Ac, xb, dinv_next);
   else ptv_body<ND>(L, xb - g0);
 }
 
@@ -1221,7 +1238,8 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
     hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()))), dim3(kBlock), 0, s, L);
   }
   if (stage & kSetupAC)
-    hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, N->A, N->omega);
+    hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, N->A, N->omega,
+                       (float*)nullptr);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0, int stage) {
   if (nd == 2) setup_nd<2>(s, L, next, level0, stage);
@@ -1259,7 +1277,7 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     const AmgLevD& L = lev[l];
     if (L.A.n <= 0) return;
     const bool last = L.coarsest || l + 1 >= nlev;
-    if (l > 0)
+    if (l > 0 && !L.fixed_omega)  // (fixed ω: D⁻¹ came with A_l, k_amg_ac)
       hipLaunchKernelGGL(k_amg_dinv<ND>, xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L);
     const int64_t g0 = !last && L.P.wmax > 0 ? slot_blocks(L.P.rg.npos()) : 0;
     const int64_t g1 = g0 + (compact(l) ? slot_blocks(L.A.npos) : 0);
@@ -1268,14 +1286,17 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
       hipLaunchKernelGGL(k_amg_fuse_p<ND>, xg(L, g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);
     if (last) break;
     const dim3 gap = rows_grid(std::max(L.AP.rg.npos(), L.compact ? 0 : L.R.rg.npos()));
+    float* const dnext = lev[l + 1].fixed_omega ? lev[l + 1].dinv32 : nullptr;
     if (compact(l) && L.PT.npos == L.AP.npos) {  // P̃ formed by the A·P kernel
       hipLaunchKernelGGL((k_amg_ap<ND, true>), xg(L, gap), dim3(kBlock), 0, s, L);
-      hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega);
+      hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega,
+                         dnext);
     } else {
       hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, gap), dim3(kBlock), 0, s, L);
       const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
       const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
-      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, xg(L, a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0);
+      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, xg(L, a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0,
+                         dnext);
     }
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);

@@ -69,6 +69,7 @@ struct AmgLevD {
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
   int x1 = 0;        // the numeric setup's launches over this level run on one XCD (amg.hip setup_block)
+  int fixed_omega = 0;  // ω from omega[0] (no Gershgorin bound): the fused setup forms D⁻¹ with A (k_amg_ac)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   // level 0 of a hierarchy kept over element failures: rows of floating

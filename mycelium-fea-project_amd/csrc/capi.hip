@@ -1130,9 +1130,15 @@ double coarse_rho(const mfea_handle* h) {
 bool omega_fallback(mfea_handle* h, int status) {
   if (status == 0 || coarse_rho(h) <= 0.0) return false;
   h->amg_safe_omega = true;
-  for (auto& pp : h->parts)
-    for (size_t l = 1; l < pp->amg_lev.size(); ++l)
+  for (auto& pp : h->parts) {
+    for (size_t l = 1; l < pp->amg_lev.size(); ++l) {
       (void)hipMemsetAsync(pp->amg_lev[l].omega, 0, sizeof(double), h->stream);
+      pp->amg_lev[l].fixed_omega = 0;  // the D⁻¹ launches (and their bounds) again
+    }
+    if (!pp->amg_lev.empty() && pp->amg_levd.n >= pp->amg_lev.size())
+      (void)hipMemcpyAsync(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
+                           hipMemcpyHostToDevice, h->stream);
+  }
   return true;
 }
 
@@ -1239,6 +1245,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
       d.x1 = !rk && l > 0 && n <= h->opt_amg_x1_rows ? 1 : 0;
+      d.fixed_omega = !rk && l > 0 && coarse_rho(h) > 0.0 ? 1 : 0;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, false, true);

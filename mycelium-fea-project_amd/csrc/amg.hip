@@ -225,6 +225,115 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
   }
 }
 
+// Level 0 at a fixed ω (AmgLevD::fixed_omega: ρ̂_0 = 2, the exact level-0
+// bound): k_amg_a0dinv's row pass without the Gershgorin bound, plus — from
+// the same row's blocks — the compact cycle's Ã_0 = ω D⁻¹ A_0 and the row's
+// P_0 values, the work k_amg_fuse_p does for level 0 (the fused setup then
+// skips that launch).  Ã and P from the stored f32 blocks and D⁻¹, as
+// atv_body / pvals_body form them: the same bits.  P reads back A_0 blocks
+// this thread stored (its own row: program order).
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_a0full(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
+                                                       const int32_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ lst, double reg) {
+  const AmgMatD& A = L.A;
+  const int64_t i = A.rg.lo64() + xcd_block() * kBlock + threadIdx.x;
+  if (i - (threadIdx.x & 63) >= A.rg.hi) return;
+  int64_t base;
+  int w;
+  slice_of(A, i, base, w);
+  if (i < A.rg.lo || i >= A.rg.hi) return;
+  const double om = amg_omega(L.omega);
+  double s6[6], D[ND * ND], Di[ND * ND], Dq[ND * ND];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + row0[i]];
+  s6[0] += reg;
+  s6[3] += reg;
+  s6[5] += reg;
+  sym_to<ND>(s6, D);
+  bstore<ND>(A.val32, A.npos, base, D);
+  bstore_sym<ND>(A.sym, A.npos, base, D);
+  if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, base, D);
+  binv<ND>(D, Di);
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) {
+    L.dinv32[i * (ND * ND) + c] = (float)Di[c];
+    Dq[c] = (double)(float)Di[c];  // the f32 D⁻¹ the separate kernels read
+  }
+  auto at_store = [&](int64_t q, const double* m) {  // Ã = ω D⁻¹ A from the f32 block
+    double mf[ND * ND], o[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) {
+      mf[c] = (double)(float)m[c];
+      o[c] = 0.0;
+    }
+    mm_acc<ND>(Dq, mf, o);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) o[c] *= om;
+    bstore<ND>(A.at32, 0, q, o);
+  };
+  if (A.at32) at_store(base, D);
+  constexpr int U = 4;
+  for (int k0 = 1; k0 < w; k0 += U) {
+    int32_t t0[U], t1[U];
+    int64_t q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      q[u] = base + (int64_t)(k0 + u < w ? k0 + u : k0) * 64;
+      t0[u] = k0 + u < w ? ptr[q[u]] : 0;
+      t1[u] = k0 + u < w ? ptr[q[u] + 1] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t0[u] == t1[u]) continue;  // padding (or past the row)
+      double m[ND * ND];
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+      for (int t = t0[u]; t < t1[u]; ++t) {
+        double v6[6], e[ND * ND];
+        const int64_t gs = lst[t];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
+        sym_to<ND>(v6, e);
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+      }
+      bstore<ND>(A.val32, A.npos, q[u], m);
+      bstore_sym<ND>(A.sym, A.npos, q[u], m);
+      if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q[u], m);
+      if (A.at32) at_store(q[u], m);
+    }
+  }
+  const AmgMatD& P = L.P;
+  if (L.coarsest || P.wmax <= 0 || i < P.rg.lo || i >= P.rg.hi) return;
+  int64_t pb;
+  int pw;
+  slice_of(P, i, pb, pw);
+  const int32_t ai = L.agg[i];
+  const bool floating = L.fmask && L.fmask[i];
+  for (int k = 0; k < pw; ++k) {
+    const int64_t q = pb + (int64_t)k * 64;
+    const int32_t J = P.col[q];
+    if (J < 0) continue;
+    double S[ND * ND], pm[ND * ND];
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) S[c] = pm[c] = 0.0;
+    list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, A.val32, A.npos, S);
+    mm_acc<ND>(Dq, S, pm);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
+    if (J == ai) {
+#pragma unroll
+      for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
+    }
+    if (floating) {
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
+    }
+    bstore<ND>(P.val32, P.npos, q, pm);
+  }
+}
+
 // P values, one thread per position (slot_wave): every slot of a row in
 // flight at once instead of one after another.
 template <int ND>
@@ -1210,15 +1319,19 @@ static int pu_of_grid(int64_t g) { return g <= 64 ? 1 : g <= 128 ? 2 : g <= 256 
 
 template <int ND>
 static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int32_t* row0, const int32_t* p,
-                  const int32_t* a, double reg) {
+                  const int32_t* a, double reg, bool full) {
   if (L0.A.n <= 0) return;
+  if (full) {  // fixed ω: Ã_0 and P_0 too, no bound (the fused setup skips level 0's P/Ã launch)
+    hipLaunchKernelGGL(k_amg_a0full<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
+    return;
+  }
   (void)hipMemsetAsync(L0.omega + 1, 0, sizeof(double), s);  // level 0's bound, max'ed by the blocks
   hipLaunchKernelGGL(k_amg_a0dinv<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
-                   const int32_t* a0_ptr, const int32_t* a0_a, double reg) {
-  if (nd == 2) a0_nd<2>(s, L0, sop, row0, a0_ptr, a0_a, reg);
-  else a0_nd<3>(s, L0, sop, row0, a0_ptr, a0_a, reg);
+                   const int32_t* a0_ptr, const int32_t* a0_a, double reg, bool full) {
+  if (nd == 2) a0_nd<2>(s, L0, sop, row0, a0_ptr, a0_a, reg, full);
+  else a0_nd<3>(s, L0, sop, row0, a0_ptr, a0_a, reg, full);
 }
 
 // the grid of a setup launch over level L (x1: 8× the blocks, setup_block)
@@ -1279,8 +1392,10 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0 && !L.fixed_omega)  // (fixed ω: D⁻¹ came with A_l, k_amg_ac)
       hipLaunchKernelGGL(k_amg_dinv<ND>, xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L);
-    const int64_t g0 = !last && L.P.wmax > 0 ? slot_blocks(L.P.rg.npos()) : 0;
-    const int64_t g1 = g0 + (compact(l) ? slot_blocks(L.A.npos) : 0);
+    // (level 0 at a fixed ω: P_0 and Ã_0 came with A_0, k_amg_a0full)
+    const bool a0full = l == 0 && L.a0full;
+    const int64_t g0 = !last && L.P.wmax > 0 && !a0full ? slot_blocks(L.P.rg.npos()) : 0;
+    const int64_t g1 = g0 + (compact(l) && !a0full ? slot_blocks(L.A.npos) : 0);
     const int64_t g2 = g1 + (l > 0 && compact(l - 1) ? slot_blocks(lev[l - 1].RT.npos) : 0);
     if (g2 > 0)
       hipLaunchKernelGGL(k_amg_fuse_p<ND>, xg(L, g2), dim3(kBlock), 0, s, L, l > 0 ? lev[l - 1] : L, g0, g1);

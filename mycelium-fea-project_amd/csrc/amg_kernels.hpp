@@ -70,6 +70,7 @@ struct AmgLevD {
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
   int x1 = 0;        // the numeric setup's launches over this level run on one XCD (amg.hip setup_block)
   int fixed_omega = 0;  // ω from omega[0] (no Gershgorin bound): the fused setup forms D⁻¹ with A (k_amg_ac)
+  int a0full = 0;       // level 0 (fixed ω): A_0, D⁻¹, Ã_0 and P_0 in one row pass (k_amg_a0full)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   // level 0 of a hierarchy kept over element failures: rows of floating
@@ -179,7 +180,7 @@ struct AmgDist {
 // A_0 from the assembled SELL operator: off-diagonal = Σ of the listed slots'
 // K_ij (= −S_e), diagonal = K_ii + reg·I; then level 0's D⁻¹ and bound.
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,
-                   const int32_t* a0_ptr, const int32_t* a0_a, double reg);
+                   const int32_t* a0_ptr, const int32_t* a0_a, double reg, bool full = false);
 // dinv, Gershgorin bound and ω of one level; then P, A·P and A_{l+1}
 // (level0: its D⁻¹ was formed by launch_amg_a0).  stage: which of the four
 // steps (the distributed setup exchanges values between them)

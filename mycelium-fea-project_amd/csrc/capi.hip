@@ -1131,9 +1131,10 @@ bool omega_fallback(mfea_handle* h, int status) {
   if (status == 0 || coarse_rho(h) <= 0.0) return false;
   h->amg_safe_omega = true;
   for (auto& pp : h->parts) {
-    for (size_t l = 1; l < pp->amg_lev.size(); ++l) {
+    for (size_t l = 0; l < pp->amg_lev.size(); ++l) {
       (void)hipMemsetAsync(pp->amg_lev[l].omega, 0, sizeof(double), h->stream);
       pp->amg_lev[l].fixed_omega = 0;  // the D⁻¹ launches (and their bounds) again
+      pp->amg_lev[l].a0full = 0;
     }
     if (!pp->amg_lev.empty() && pp->amg_levd.n >= pp->amg_lev.size())
       (void)hipMemcpyAsync(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
@@ -1338,6 +1339,17 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
   if (rho_coarse > 0.0)
     for (int l = 1; l < nlev; ++l)
       HIPC(hipMemcpyAsync(pt.amg_lev[l].omega, &rho_coarse, sizeof(double), hipMemcpyHostToDevice, s));
+  // level 0 with them: ρ̂_0 = 2, its exact bound (amg.hip header), so level 0
+  // needs no Gershgorin pass either.  Its P_0 / Ã_0 then come with A_0 in one
+  // row pass (k_amg_a0full) where that measured faster: the Z-ordered plans
+  // (C5 setup 4.17 → 3.88 ms); on depth-first ones the per-position launch
+  // stays (C3 0.401 vs 0.408 ms, C2 0.219 vs 0.224)
+  static const double kRho0 = 2.0;
+  if (!rk && nlev > 1 && rho_coarse > 0.0 && pt.amg_lev[0].compact) {
+    pt.amg_lev[0].fixed_omega = 1;
+    pt.amg_lev[0].a0full = pl.spatial ? 1 : 0;
+    HIPC(hipMemcpyAsync(pt.amg_lev[0].omega, &kRho0, sizeof(double), hipMemcpyHostToDevice, s));
+  }
   HIPC(pt.amg_levd.alloc(std::max(nlev, 1)));
   HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
   HIPC(hipStreamSynchronize(s));
@@ -1659,13 +1671,15 @@ void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
 void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   hipStream_t s = h->stream;
   const int nd = pt.amg.nd, nlev = (int)pt.amg_lev.size();
-  launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg);
+  const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
+  const bool fused = compact && h->opt_amg_fuse_setup && !pt.amg_cg.sweep;
+  launch_amg_a0(s, nd, pt.amg_lev[0], sell_op(pt), pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, reg,
+                fused && pt.amg_lev[0].a0full);
   if (pt.amg_cg.sweep) {
     launch_sweep_setup(s, nd, pt.swd, pt.amg_lev[0]);
     return;
   }
-  const bool compact = pt.amg_cg.cycle == 1 && nlev > 1 && pt.amg_lev[0].compact;
-  if (compact && h->opt_amg_fuse_setup) {
+  if (fused) {
     launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
     return;
   }

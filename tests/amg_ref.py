@@ -145,7 +145,12 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho
         rs = np.zeros((n, nd))
         np.add.at(rs, row[ok], M)
         g = rs.max() if n else 0.0
-        rho = coarse_rho if l > 0 and coarse_rho > 0 else max(RHO_FLOOR, g / RHO_SAFETY)
+        # with the over-relaxed coarse levels the engine also fixes level 0 at
+        # its exact bound ρ̂_0 = 2 (capi.hip upload_amg, k_amg_a0full)
+        if coarse_rho > 0:
+            rho = coarse_rho if l > 0 else RHO_FLOOR
+        else:
+            rho = max(RHO_FLOOR, g / RHO_SAFETY)
         L["omega"] = (4.0 / 3.0) / rho
         L["g"] = g
         L["A"] = to_scipy(Ab, L["A.sptr"], L["A.col"], n, n, nd)

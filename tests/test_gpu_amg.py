@@ -430,8 +430,10 @@ def test_fused_setup_bitwise_equals_separate_launches(engine, mesh):
     (k_amg_fuse_p / k_amg_fuse_ac) run the same arithmetic as their own
     launches: U and the iteration count bit for bit, collapsed or not."""
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
-    for coll in (0, -1):
-        with engine.options(amg_cycle=1, amg_collapse=coll):
+    # spatial 1: Z-ordered level 0, whose fused setup forms A_0, D⁻¹, Ã_0 and
+    # P_0 in one row pass (k_amg_a0full) against the separate launches
+    for coll, spatial in ((0, -1), (-1, -1), (-1, 1)):
+        with engine.options(amg_cycle=1, amg_collapse=coll, amg_spatial=spatial):
             _mesh_case(engine, mesh)
             out = {}
             for v in (0, 1):
@@ -440,7 +442,7 @@ def test_fused_setup_bitwise_equals_separate_launches(engine, mesh):
                 assert st.status == 0
                 out[v] = (engine.displacement(), st.iters)
             engine.set_option("amg_fuse_setup", 1)
-        assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0]), (mesh, coll)
+        assert out[0][1] == out[1][1] and np.array_equal(out[0][0], out[1][0]), (mesh, coll, spatial)
 
 
 def test_default_options_table_matches_library():

@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
   for (int off = 32; off > 0; off >>= 1) g = fmax(g, __shfl_xor(g, off, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = g;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !L.fixed_omega) {
     double mx = red[0];
     for (int k = 1; k < kBlock / 64; ++k) mx = fmax(mx, red[k]);
     atomicMax(reinterpret_cast<unsigned long long*>(&L.omega[1]),
@@ -1325,7 +1325,8 @@ static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int
     hipLaunchKernelGGL(k_amg_a0full<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
     return;
   }
-  (void)hipMemsetAsync(L0.omega + 1, 0, sizeof(double), s);  // level 0's bound, max'ed by the blocks
+  // level 0's bound, max'ed by the blocks (not at a fixed ω: nothing reads it)
+  if (!L0.fixed_omega) (void)hipMemsetAsync(L0.omega + 1, 0, sizeof(double), s);
   hipLaunchKernelGGL(k_amg_a0dinv<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
 }
 void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, const int32_t* row0,

@@ -46,6 +46,15 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *                        the distributed V-cycle of one global hierarchy (1), or per
  *                        active set whichever of the two solved faster (-1)
  *   "amg_rep_rows" n     distributed V-cycle: levels of at most n rows replicated (32768)
+ *   "amg_reuse" 0|1      GAMG: keep the hierarchy over element failures, floating pieces
+ *                        masked (1), or rebuild it for every new active set (0)
+ *   "amg_rebuild_pct" n  GAMG: a kept hierarchy is rebuilt once a solve needs more than
+ *                        n % of the iterations it took on its own set (150)
+ *   "amg_x1_rows" n      GAMG setup: levels of ≤ n rows launched on one XCD (2048)
+ *   "amg_coarse_rho_ppm" n  GAMG: ρ̂ of the levels below 0, ppm (1750000: ω = 0.76, level 0
+ *                        then at its exact ρ̂ = 2); 0: the Gershgorin rule max(2, g / 1.45)
+ *                        everywhere.  A solve failing with it falls back to 0 for the
+ *                        handle's lifetime (read-only "amg_safe_omega" = 1)
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 

@@ -77,20 +77,42 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __
   const int len = row_len[row];
   const double xi = xyz[3 * row], yi = xyz[3 * row + 1], zi = xyz[3 * row + 2];
   double d[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = 0; k < len; ++k) {
-    const int64_t idx = base + (int64_t)k * 64;
-    const int32_t e = s_elem[idx];
-    const int32_t j = s_col[idx];
-    double S[6] = {0, 0, 0, 0, 0, 0};
-    if (active[e]) {
-      // v = p2 − p1 with the row as either endpoint: the sign of v does not
-      // change any product n_a n_b, so S is bitwise endpoint-symmetric.
-      bar_block(xyz[3 * j] - xi, xyz[3 * j + 1] - yi, xyz[3 * j + 2] - zi, m, S, nullptr);
+  // slots in batches of U, each batch's loads issued together (slot → element
+  // and column, then activity and coordinates): two dependent round trips per
+  // batch instead of two per slot; the sums stay in slot order
+  constexpr int U = 4;
+  for (int k0 = 0; k0 < len; k0 += U) {
+    int64_t idx[U];
+    int32_t e[U], j[U];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) d[c] += S[c];
+    for (int u = 0; u < U; ++u) {
+      const bool ok = k0 + u < len;
+      idx[u] = base + (int64_t)(ok ? k0 + u : k0) * 64;
+      e[u] = ok ? s_elem[idx[u]] : 0;
+      j[u] = ok ? s_col[idx[u]] : (int32_t)row;
+    }
+    uint8_t act[U];
+    double pj[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      act[u] = k0 + u < len ? active[e[u]] : 0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) pj[u][a] = xyz[3 * (int64_t)j[u] + a];
     }
 #pragma unroll
-    for (int c = 0; c < 6; ++c) val[(int64_t)c * G + idx] = -S[c];
+    for (int u = 0; u < U; ++u) {
+      if (k0 + u >= len) break;
+      double S[6] = {0, 0, 0, 0, 0, 0};
+      if (act[u]) {
+        // v = p2 − p1 with the row as either endpoint: the sign of v does not
+        // change any product n_a n_b, so S is bitwise endpoint-symmetric.
+        bar_block(pj[u][0] - xi, pj[u][1] - yi, pj[u][2] - zi, m, S, nullptr);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) d[c] += S[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) val[(int64_t)c * G + idx[u]] = -S[c];
+    }
   }
 #pragma unroll
   for (int c = 0; c < 6; ++c) diag[(int64_t)c * N + row] = d[c];

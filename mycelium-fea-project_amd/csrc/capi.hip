@@ -1742,7 +1742,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const CgVecs v = cg_vecs(pt);
   const int nd = pt.amg.nd;
   HIPC(hipEventRecord(h->ev[1], s));
-  launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 0, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
+  launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
   HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
   HIPC(hipEventRecord(h->ev[2], s));
@@ -2210,7 +2210,7 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
   HIPC(hipEventRecord(h->ev[1], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
-    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 0, cg_vecs(pt), pt.partials.ptr, tix(pt, 0),
+    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 2, cg_vecs(pt), pt.partials.ptr, tix(pt, 0),
                   pt.red.ptr);
   }
   RC(gather4(h, 0));
@@ -2311,7 +2311,7 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   HIPC(hipEventRecord(h->ev[1], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
-    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 0, cg_vecs(pt), pt.partials.ptr,
+    launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 2, cg_vecs(pt), pt.partials.ptr,
                   tix(pt, 0), pt.red.ptr);
   }
   RC(gather4(h, 0));

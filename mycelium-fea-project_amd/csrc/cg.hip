@@ -139,6 +139,56 @@ __global__ __launch_bounds__(kBlock) void k_cg_rhs(SellOp op, const uint8_t* __r
   block_publish<2>(acc, partials, ticket, red_out);
 }
 
+// The GAMG solves' RHS (precond 2 of launch_cg_rhs): only what they read —
+// b = 0 − K_fk x_k of the free rows (the CG's r₀ source, k_amg_cg_init) and
+// the prescribed x of the known and ghost rows (reactions, stress); no
+// Jacobi M⁻¹ and no Krylov vectors (the AMG CG keeps its own), ‖M⁻¹b‖² = 0
+// (GAMG stops on the unpreconditioned residual).  A row's slots in batches of
+// four: columns, then their codes, then the known couplings.  b's terms in
+// slot order, as k_cg_rhs.
+__global__ __launch_bounds__(kBlock) void k_amg_rhs(SellOp op, const uint8_t* __restrict__ code,
+                                                    double dy_top, double dy_bot, CgVecs v,
+                                                    double* partials, unsigned* ticket, double* red_out) {
+  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double acc[2] = {0.0, 0.0};
+  if (row < op.nf) {
+    const int64_t base = (int64_t)op.slice_ptr[row >> 6] * 64 + (row & 63);
+    const int len = op.row_len[row];
+    const int64_t G = op.G;
+    double kx = 0.0, ky = 0.0, kz = 0.0;
+    constexpr int U = 4;
+    for (int k0 = 0; k0 < len; k0 += U) {
+      int64_t idx[U];
+      int32_t j[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        idx[u] = base + (int64_t)(k0 + u < len ? k0 + u : k0) * 64;
+        j[u] = k0 + u < len ? op.s_col[idx[u]] : 0;
+      }
+      uint8_t c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) c[u] = k0 + u < len && j[u] >= op.nf ? code[j[u]] : 3;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (c[u] != 3) {  // a known neighbour (3: free or ghost free row, x₀ = 0)
+          const double dy = c[u] == 2 ? dy_bot : dy_top;
+          kx = fma(op.val[1 * G + idx[u]], dy, kx);
+          ky = fma(op.val[3 * G + idx[u]], dy, ky);
+          kz = fma(op.val[4 * G + idx[u]], dy, kz);
+        }
+      }
+    }
+    const double b[3] = {0.0 - kx, 0.0 - ky, 0.0 - kz};
+    store3(v.r[0], row, b);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) acc[0] = fma(b[a], b[a], acc[0]);
+  } else if (row < op.N) {
+    const double xk[3] = {0.0, code[row] == 3 ? 0.0 : (code[row] == 2 ? dy_bot : dy_top), 0.0};
+    store3(v.x, row, xk);
+  }
+  block_publish<2>(acc, partials, ticket, red_out);
+}
+
 // k_cg_init_finalize: stopping threshold from the reduced (‖b‖², ‖M⁻¹b‖²).
 __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, int norm,
                                    int max_it, double reg, SolveState* st) {
@@ -437,7 +487,10 @@ void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double 
                    double dy_bot, double reg, int precond, const CgVecs& v, double* partials,
                    unsigned* ticket, double* red_out) {
   const dim3 grid((unsigned)grid_rows(op.N > 0 ? op.N : 1));
-  if (precond == 1)
+  if (precond == 2)
+    hipLaunchKernelGGL(k_amg_rhs, grid, dim3(kBlock), 0, s, op, code, dy_top, dy_bot, v, partials, ticket,
+                       red_out);
+  else if (precond == 1)
     hipLaunchKernelGGL(k_cg_rhs<true>, grid, dim3(kBlock), 0, s, op, code, dy_top, dy_bot, reg, v,
                        partials, ticket, red_out);
   else

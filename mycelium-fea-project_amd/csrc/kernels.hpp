@@ -130,6 +130,8 @@ void launch_spmv_csr(hipStream_t s, int j, int64_t n, const int64_t* indptr,
 
 // ---- single-reduction CG on the SELL operator (one kernel per iteration) ----
 // k_cg_rhs: b, M⁻¹, x, r₀ = b, p = s = w = 0; reduces (b·b, u₀·u₀) into red[0..1].
+// precond 0 Jacobi, 1 block Jacobi, 2 the GAMG solves (k_amg_rhs: b and the
+// known rows' x only, u₀·u₀ = 0).
 void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double dy_top,
                    double dy_bot, double reg, int precond, const CgVecs& v, double* partials,
                    unsigned* ticket, double* red_out);

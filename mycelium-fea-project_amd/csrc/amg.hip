@@ -1212,10 +1212,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_pack_u(AmgCg cg, AmgDist d) {
 
 template <int ND, int PU, int BS, bool DIST>
 __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg cg, Slot* slots,
-                                                      const SolveState* st, double* part, AmgDist d) {
+                                                      SolveState* st, double* part, AmgDist d) {
   const int f0 = __builtin_nontemporal_load(&slots[j].flag);
   const double g0 = slots[j].v[0], a0 = slots[j].alpha;
-  const double tol2 = st->tol2;
+  double tol2 = st->tol2;
   const int base_it = st->base, max_it = st->max_it, norm = st->norm;
   double S[4];
   if constexpr (DIST) {  // the gathered rank sums, rank order (rows ≥ world are 0)
@@ -1240,6 +1240,16 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
     vload<ND>(cg.s, k, s);
     vload<ND>(cg.x, k, x);
     vload<ND>(cg.r, k, r);
+  }
+  if (norm == 1 && f0 == kInit) {
+    // PETSc's preconditioned norm (KSP_NORM_PRECONDITIONED, src/fea_petsc.cpp:336-341):
+    // ‖M⁻¹r‖ ≤ rtol‖M⁻¹b‖ with x₀ = 0 — the reference is this first ‖u₀‖²,
+    // known only now (every block forms the same value; block 0 keeps it)
+    tol2 = fmax(st->rtol2 * S[3], st->atol2);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      st->tol2 = tol2;
+      st->res0 = S[3];
+    }
   }
   const CgScalars cs = cg_scalars(S, f0, g0, a0, tol2, base_it + j, max_it, norm);
   cg_record(slots, j, S, cs);
@@ -1693,7 +1703,7 @@ void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d)
 
 template <int ND, int BS, bool DIST>
 static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                   const SolveState* st, double* part, const AmgDist& d) {
+                   SolveState* st, double* part, const AmgDist& d) {
   const int64_t gw = amg_w_grid(cg);  // partials to reduce = the w kernel's blocks
   int64_t gu = (cg.hi - cg.lo + BS - 1) / BS;
   gu = gu < 1 ? 1 : (gu > kCgMaxG ? kCgMaxG : gu);
@@ -1707,12 +1717,12 @@ static void upd_bs(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slo
 }
 template <int ND>
 static void upd_nd(hipStream_t s, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                   const SolveState* st, double* part, const AmgDist* d) {
+                   SolveState* st, double* part, const AmgDist* d) {
   if (d) upd_bs<ND, kCgBS, true>(s, j, L0, cg, slots, st, part, *d);
   else upd_bs<ND, kCgBS, false>(s, j, L0, cg, slots, st, part, AmgDist{});
 }
 void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg, Slot* slots,
-                          const SolveState* st, double* part, const AmgDist* d) {
+                          SolveState* st, double* part, const AmgDist* d) {
   if (nd == 2) upd_nd<2>(s, j, L0, cg, slots, st, part, d);
   else upd_nd<3>(s, j, L0, cg, slots, st, part, d);
 }

@@ -139,25 +139,39 @@ struct AmgCg {
   int sweep = 0;  // 1: the preconditioner is a multicolour sweep (sweep.hip): u is its output only
 };
 
-// Block-Jacobi multicolour SSOR / DIC(0) (sweep.hip, amg.hpp SweepPlan): per
-// level-0 row its colour and in-block lower / upper couplings; dt32 the
-// blocks D̃⁻¹ the sweeps apply (SOR: A_0's D⁻¹; ICC: formed by k_sweep_dic)
-constexpr int kSweepRows = 256;  // rows per block = threads per workgroup (sweep.hip)
+// Whole-matrix SSOR / IC(0) in the chain-piece multicolour order (sweep.hip,
+// amg.hpp SweepPlan): the plan's entry arrays and the per-solve values the
+// setup launch(es) form from A_0 — the predecessor blocks pv, the cross
+// blocks lov / upv (f32, [item][ND²]), D̃⁻¹ (f32 upper triangles: SOR D⁻¹,
+// ICC the DIC(0) pivots formed in f64) — and the sweeps' f64 iterate y.
+constexpr int kSweepPieceLen = 16;   // rows per piece (tools/icc_lab.py)
+constexpr int kSweepMaxColors = 32;
+constexpr int kSweepBS = 256;        // threads per workgroup (4 waves = 4 × 64 pieces)
 struct SweepD {
-  int64_t n = 0;
+  int64_t n = 0;   // level-0 rows
+  int64_t ne = 0;  // entries
   int colors = 0;
   int dic = 0;
-  const uint8_t* color = nullptr;
+  int32_t cw[kSweepMaxColors + 1] = {};  // colour → first wave
+  const int32_t* wbase = nullptr;
+  const int32_t* wlen = nullptr;
+  const int32_t* row = nullptr;
+  const int32_t* ppos = nullptr;
+  const int32_t* dpos = nullptr;
   const int32_t* lo_ptr = nullptr;
-  const int32_t* lo_loc = nullptr;
+  const int32_t* lo_ent = nullptr;
   const int32_t* lo_pos = nullptr;
   const int32_t* up_ptr = nullptr;
-  const int32_t* up_loc = nullptr;
+  const int32_t* up_ent = nullptr;
   const int32_t* up_pos = nullptr;
-  float* dt32 = nullptr;
+  float* pv = nullptr;
+  float* dt = nullptr;
+  float* lov = nullptr;
+  float* upv = nullptr;
+  double* y = nullptr;
 };
 void launch_sweep_setup(hipStream_t s, int nd, const SweepD& sw, const AmgLevD& L0);
-void launch_sweep(hipStream_t s, int nd, const SweepD& sw, const AmgLevD& L0, const AmgCg& cg, const int32_t* gate);
+void launch_sweep(hipStream_t s, int nd, const SweepD& sw, const AmgCg& cg, const int32_t* gate);
 
 // Partitioned solve (amg.hpp AmgHalo): this partition's rank, the gathered
 // per-rank partial sums, its ghost couplings and the u halo buffers.
@@ -241,7 +255,7 @@ void launch_amg_pack_u(hipStream_t s, int nd, const AmgCg& cg, const AmgDist& d)
 // iteration j: α, β from the partials (d: from the gathered rank sums), p s x
 // r update, level-0 x = ω D⁻¹ r
 void launch_amg_cg_update(hipStream_t s, int nd, int j, const AmgLevD& L0, const AmgCg& cg,
-                          Slot* slots, const SolveState* st, double* part,
+                          Slot* slots, SolveState* st, double* part,
                           const AmgDist* d = nullptr);
 // x (level-0 order, ND per row) → row-order x[3·row + c]
 void launch_amg_finish(hipStream_t s, int nd, const AmgCg& cg, double* x_row);

@@ -134,6 +134,8 @@ struct Part {
   DevBuf<float> amg_f;               // the f32 V-cycle copies and vectors, carved
   std::vector<AmgLevD> amg_lev;      // device views
   DevBuf<AmgLevD> amg_levd;          // … and their device copy (the setup tail reads it)
+  bool amg_om_own = false;           // the hierarchy is this partition's own (not a split global one)
+  bool amg_om_spatial = false;       // ... on Z-ordered labels (level 0's one-pass setup)
   int amg_tail = 0;                  // first level of the single-workgroup tail (0: none)
   int amg_first = 1;                 // first level the four-step tail may start at (not split)
   AmgCg amg_cg;
@@ -142,9 +144,9 @@ struct Part {
   int amg_kind = MFEA_PC_GAMG;
   SweepPlan sweep;
   SweepD swd;
-  DevBuf<int32_t> sw_i;   // lo/up ptr, loc, pos
-  DevBuf<uint8_t> sw_c;   // colours
-  DevBuf<float> sw_dt;    // ICC: D̃⁻¹ blocks
+  DevBuf<int32_t> sw_i;   // the plan's entry arrays and cross lists
+  DevBuf<float> sw_f;     // pv | D̃⁻¹ | lov | upv (formed per solve)
+  DevBuf<double> sw_y;    // the sweeps' iterate
   const int32_t* amg_a0_ptr = nullptr;
   const int32_t* amg_a0_a = nullptr;
   // partitioned GAMG (amg.hpp AmgHalo): ghost couplings and the u halo
@@ -250,6 +252,7 @@ struct mfea_handle {
   int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
                                    // C3: levels 4-5 gain 1-2 µs per launch, level 3 at 8192 lost as much)
   int opt_amg_big_chunk = 8;  // GAMG: iterations per chunk of a planned batch (drive_sized)
+  int opt_sweep_piece = kSweepPieceLen;  // SOR / ICC: rows per chain piece (amg.hpp SweepPlan)
   int opt_amg_fuse_setup = 1;  // GAMG setup: the compact operators fused into the Galerkin chain's launches
   int64_t opt_amg_theta_ppm = 0;  // GAMG: strength threshold θ·10⁶ of the level-0 aggregation (0: all strong)
   int opt_amg_cycle = 1;       // GAMG: 1 the compact V-cycle (two sweeps per level), 0 four steps
@@ -1122,25 +1125,69 @@ double coarse_rho(const mfea_handle* h) {
   return h->amg_safe_omega ? 0.0 : (double)h->opt_amg_coarse_rho_ppm * 1e-6;
 }
 
-// A GAMG solve failed (breakdown or max_it) with the over-relaxed coarse
-// smoothers: the Gershgorin-safe weights on every partition's hierarchy from
-// now on (its next numeric setup re-forms every ω product).  Partitioned over
-// RCCL every rank sees the same status (the CG scalars are all-reduced), so
-// every rank takes this path together.  True: the caller solves again.
-bool omega_fallback(mfea_handle* h, int status) {
-  if (status == 0 || coarse_rho(h) <= 0.0) return false;
-  h->amg_safe_omega = true;
-  for (auto& pp : h->parts) {
-    for (size_t l = 0; l < pp->amg_lev.size(); ++l) {
-      (void)hipMemsetAsync(pp->amg_lev[l].omega, 0, sizeof(double), h->stream);
-      pp->amg_lev[l].fixed_omega = 0;  // the D⁻¹ launches (and their bounds) again
-      pp->amg_lev[l].a0full = 0;
-    }
-    if (!pp->amg_lev.empty() && pp->amg_levd.n >= pp->amg_lev.size())
-      (void)hipMemcpyAsync(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
-                           hipMemcpyHostToDevice, h->stream);
+// The smoothing weights of a partition's hierarchy for the handle's current
+// mode (DESIGN.md §4.2 "Coarse-level smoothing weight"): over-relaxed — ρ̂_l
+// fixed at coarse_rho below level 0 and at 2 (its exact bound) on level 0,
+// so no Gershgorin pass and, on an own hierarchy, no coarse D⁻¹ launches
+// (fixed_omega) — or, after a fallback, the Gershgorin-safe rule (omega[0] =
+// 0: the setup estimates ρ̂_l).  Called at upload and whenever the mode
+// changes; the next numeric setup re-forms every ω product.
+int apply_coarse_omega(mfea_handle* h, Part& pt) {
+  hipStream_t s = h->stream;
+  const int nlev = (int)pt.amg_lev.size();
+  const double rho = coarse_rho(h);
+  static const double kRho0 = 2.0;
+  for (int l = 0; l < nlev; ++l) {
+    AmgLevD& d = pt.amg_lev[l];
+    d.fixed_omega = pt.amg_om_own && l > 0 && rho > 0.0 ? 1 : 0;
+    d.a0full = 0;
+    HIPC(hipMemsetAsync(d.omega, 0, sizeof(double), s));
+    if (l > 0 && rho > 0.0) HIPC(hipMemcpyAsync(d.omega, &rho, sizeof(double), hipMemcpyHostToDevice, s));
   }
-  return true;
+  // level 0: its P_0 / Ã_0 then come with A_0 in one row pass (k_amg_a0full)
+  // where that measured faster: the Z-ordered plans (C5 setup 4.17 → 3.88
+  // ms); on depth-first ones the per-position launch stays (C3 0.401 vs
+  // 0.408 ms, C2 0.219 vs 0.224)
+  if (pt.amg_om_own && nlev > 1 && rho > 0.0 && pt.amg_lev[0].compact) {
+    pt.amg_lev[0].fixed_omega = 1;
+    pt.amg_lev[0].a0full = pt.amg_om_spatial ? 1 : 0;
+    HIPC(hipMemcpyAsync(pt.amg_lev[0].omega, &kRho0, sizeof(double), hipMemcpyHostToDevice, s));
+  }
+  if (nlev) {
+    HIPC(pt.amg_levd.alloc(nlev));
+    HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
+  }
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+// A GAMG solve that failed with the over-relaxed coarse smoothers may have
+// met an operator on which they do not give an SPD cycle (ω_l λ_l ≥ 2).  A
+// breakdown suggests that; max_it only when the caller's limit is far above
+// what this hierarchy needs (`typical` iterations) — a deliberately small
+// max_it is not ω's fault.
+bool omega_suspect(const mfea_handle* h, int status, int max_it, int typical) {
+  if (status == 0 || coarse_rho(h) <= 0.0) return false;
+  if (status == -5) return true;
+  return status == -4 && max_it > 4 * std::max(typical, 16);
+}
+
+// ... then the solve runs once more on the Gershgorin-safe weights, which stay
+// for the handle's lifetime only if that solve converges; otherwise the
+// over-relaxed ones come back and the retry's failure is returned.
+// Partitioned over RCCL every rank sees the same status (the CG scalars are
+// all-reduced), so every rank takes this path together.
+template <class F>
+int omega_retry(mfea_handle* h, F&& again) {
+  RC(sync_stream(h));
+  h->amg_safe_omega = true;
+  for (auto& pp : h->parts) RC(apply_coarse_omega(h, *pp));
+  const int rc = again();
+  if (rc == MFEA_EMAXIT || rc == MFEA_EBREAKDOWN) {
+    h->amg_safe_omega = false;
+    for (auto& pp : h->parts) RC(apply_coarse_omega(h, *pp));
+  }
+  return rc;
 }
 
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
@@ -1246,7 +1293,6 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
       d.x1 = !rk && l > 0 && n <= h->opt_amg_x1_rows ? 1 : 0;
-      d.fixed_omega = !rk && l > 0 && coarse_rho(h) > 0.0 ? 1 : 0;
       if (!L.coarsest) {
         d.agg = I(L.agg);
         d.P = mat(L.P, false, true);
@@ -1333,27 +1379,11 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_lev[0].fmask = pt.amg_fmask.ptr;
     pt.amg_mask_key.clear();
   }
-  // ρ̂ of the coarse levels in place of the Gershgorin estimate (omega[0], zeroed above;
-  // DESIGN.md §4.2 "Coarse-level smoothing weight")
-  const double rho_coarse = coarse_rho(h);
-  if (rho_coarse > 0.0)
-    for (int l = 1; l < nlev; ++l)
-      HIPC(hipMemcpyAsync(pt.amg_lev[l].omega, &rho_coarse, sizeof(double), hipMemcpyHostToDevice, s));
-  // level 0 with them: ρ̂_0 = 2, its exact bound (amg.hip header), so level 0
-  // needs no Gershgorin pass either.  Its P_0 / Ã_0 then come with A_0 in one
-  // row pass (k_amg_a0full) where that measured faster: the Z-ordered plans
-  // (C5 setup 4.17 → 3.88 ms); on depth-first ones the per-position launch
-  // stays (C3 0.401 vs 0.408 ms, C2 0.219 vs 0.224)
-  static const double kRho0 = 2.0;
-  if (!rk && nlev > 1 && rho_coarse > 0.0 && pt.amg_lev[0].compact) {
-    pt.amg_lev[0].fixed_omega = 1;
-    pt.amg_lev[0].a0full = pl.spatial ? 1 : 0;
-    HIPC(hipMemcpyAsync(pt.amg_lev[0].omega, &kRho0, sizeof(double), hipMemcpyHostToDevice, s));
-  }
+  // the smoothing weights (ρ̂ per level in place of the Gershgorin estimate)
+  pt.amg_om_own = !rk;
+  pt.amg_om_spatial = pl.spatial;
   HIPC(pt.amg_levd.alloc(std::max(nlev, 1)));
-  HIPC(hipMemcpyAsync(pt.amg_levd.ptr, pt.amg_lev.data(), nlev * sizeof(AmgLevD), hipMemcpyHostToDevice, s));
-  HIPC(hipStreamSynchronize(s));
-  return 0;
+  return apply_coarse_omega(h, pt);
 }
 
 // The element activity of the handle's single partition, on the host.
@@ -1434,10 +1464,17 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
   pt.amg_cg.sweep = 0;
   if (kind != MFEA_PC_SOR && kind != MFEA_PC_ICC) return 0;
   const SweepPlan& sp = pt.sweep;
-  const int64_t n = (int64_t)sp.color.size();
-  const size_t a = sp.lo_ptr.size(), b = sp.lo_loc.size(), c = sp.up_ptr.size(), d = sp.up_loc.size();
-  HIPC(pt.sw_i.alloc(a + 2 * b + c + 2 * d + 1));
-  HIPC(pt.sw_c.alloc(std::max<int64_t>(n, 1)));
+  if (sp.colors > kSweepMaxColors) return fail(MFEA_EINVAL, "sweep plan: too many colours");
+  const int nd = pt.amg.nd, nb2 = nd * nd, ns = nd * (nd + 1) / 2;
+  const int64_t ne = sp.n_entries();
+  const std::vector<int32_t>* iv[] = {&sp.wbase, &sp.wlen, &sp.row, &sp.ppos, &sp.dpos, &sp.lo_ptr,
+                                      &sp.lo_ent, &sp.lo_pos, &sp.up_ptr, &sp.up_ent, &sp.up_pos};
+  size_t ni = 1;
+  for (auto* v : iv) ni += v->size();
+  HIPC(pt.sw_i.alloc(ni));
+  const size_t nlo = sp.lo_ent.size(), nup = sp.up_ent.size();
+  HIPC(pt.sw_f.alloc((size_t)ne * (nb2 + ns) + (nlo + nup) * nb2 + 1));
+  HIPC(pt.sw_y.alloc((size_t)ne * nd + 1));
   int32_t* ip = pt.sw_i.ptr;
   hipStream_t s = h->stream;
   auto put = [&](const std::vector<int32_t>& v) -> const int32_t* {
@@ -1447,23 +1484,31 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
     return p;
   };
   SweepD& w = pt.swd;
-  w.n = n;
-  w.colors = sp.max_colors;
+  w.n = sp.n;
+  w.ne = ne;
+  w.colors = sp.colors;
   w.dic = kind == MFEA_PC_ICC ? 1 : 0;
+  for (int c = 0; c <= sp.colors; ++c) w.cw[c] = sp.cwave[c];
+  w.wbase = put(sp.wbase);
+  w.wlen = put(sp.wlen);
+  w.row = put(sp.row);
+  w.ppos = put(sp.ppos);
+  w.dpos = put(sp.dpos);
   w.lo_ptr = put(sp.lo_ptr);
-  w.lo_loc = put(sp.lo_loc);
+  w.lo_ent = put(sp.lo_ent);
   w.lo_pos = put(sp.lo_pos);
   w.up_ptr = put(sp.up_ptr);
-  w.up_loc = put(sp.up_loc);
+  w.up_ent = put(sp.up_ent);
   w.up_pos = put(sp.up_pos);
-  if (n) HIPC(hipMemcpyAsync(pt.sw_c.ptr, sp.color.data(), n, hipMemcpyHostToDevice, s));
-  w.color = pt.sw_c.ptr;
-  if (w.dic) {
-    HIPC(pt.sw_dt.alloc(std::max<int64_t>(1, n * pt.amg.nd * pt.amg.nd)));
-    w.dt32 = pt.sw_dt.ptr;
-  } else {
-    w.dt32 = pt.amg_lev.empty() ? nullptr : pt.amg_lev[0].dinv32;
-  }
+  float* fp = pt.sw_f.ptr;
+  w.pv = fp;
+  w.dt = fp + (size_t)ne * nb2;
+  w.lov = w.dt + (size_t)ne * ns;
+  w.upv = w.lov + nlo * nb2;
+  // pads and first steps are never written by the setup: zero them once
+  HIPC(hipMemsetAsync(fp, 0, pt.sw_f.n * sizeof(float), s));
+  w.y = pt.sw_y.ptr;
+  HIPC(hipMemsetAsync(w.y, 0, pt.sw_y.n * sizeof(double), s));
   pt.amg_cg.sweep = 1;
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(s));
@@ -1473,7 +1518,7 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
 // the preconditioner application u = M r of one PCG iteration (gate: its
 // flag; NULL: ungated)
 void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate) {
-  if (pt.amg_cg.sweep) launch_sweep(h->stream, pt.amg.nd, pt.swd, pt.amg_lev[0], pt.amg_cg, gate);
+  if (pt.amg_cg.sweep) launch_sweep(h->stream, pt.amg.nd, pt.swd, pt.amg_cg, gate);
   else launch_amg_vcycle(h->stream, pt.amg.nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, gate);
 }
 
@@ -1481,6 +1526,28 @@ void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate) {
 // partition: the host view of the activity (downloaded only when a post
 // kernel changed it); partitioned: each partition's own elements, read back.
 int upload_sweep(mfea_handle* h, Part& pt, int kind);
+
+// every element active in `a` is active in `b`: a hierarchy built for b is
+// kept for a only then — A_0's slot lists hold b's elements alone, so an
+// element that came back since would be missing from the CG's w = A u
+// (its couplings absent while the diagonal has them)
+static bool active_subset(const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t e = 0; e < a.size(); ++e)
+    if (a[e] && !b[e]) return false;
+  return true;
+}
+
+// the chain-piece plan with at most kSweepMaxColors colours: shorter pieces
+// (fewer couplings per piece) until it fits — pieces of one row are a point
+// colouring, max degree + 1 colours at most
+std::string build_sweep_bounded(const AmgPlan& plan, int piece_len, SweepPlan& sp) {
+  for (int m = piece_len;; m = std::max(1, m / 2)) {
+    const std::string err = build_sweep(plan, m, sp);
+    if (!err.empty() || sp.colors <= kSweepMaxColors) return err;
+    if (m == 1) return "sweep plan: more than 32 colours";
+  }
+}
 
 int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG) {
   *rebuilt = false;
@@ -1502,7 +1569,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   const std::vector<uint8_t>& key = dm ? local : h->act_host;
   pt.amg_reused = false;
   if (!dm && pt.amg_ok && pt.amg_lev.size() > 1 &&
-      (pt.amg_key == key || (h->opt_amg_reuse && !pt.amg_stale))) {
+      (pt.amg_key == key || (h->opt_amg_reuse && !pt.amg_stale && active_subset(key, pt.amg_key)))) {
     // keep the hierarchy: the numeric setup re-forms its values from the new
     // K (failed elements are zero slots); only pieces cut off from both grips
     // need care — their P_0 rows are zeroed so they stay exactly at zero
@@ -1528,7 +1595,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   const bool sweep = kind == MFEA_PC_SOR || kind == MFEA_PC_ICC;
   std::string err = build_amg(pt.P, key, lane_dofs(h), pt.amg, sweep ? 1 : h->opt_amg_max_levels, nullptr,
                               amg_strength(h), lay);
-  if (err.empty() && sweep) err = build_sweep(pt.amg, kSweepRows, pt.sweep);
+  if (err.empty() && sweep) err = build_sweep_bounded(pt.amg, h->opt_sweep_piece, pt.sweep);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
   destroy_graph(h);
   pt.amg_kind = kind;
@@ -1733,8 +1800,6 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
               mfea_stats* st) {
   Part& pt = part0(h);
   hipStream_t s = h->stream;
-  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
-    return fail(MFEA_EINVAL, "MFEA_PC_GAMG / SOR / ICC stop on the unpreconditioned residual only");
   bool rebuilt = false;
   RC(ensure_amg(h, pt, &rebuilt, o->precond));
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
@@ -1831,22 +1896,23 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                      &fin, finish, exact_rem);
   }
   if (rc) return rc;
-  if (pt.amg_lev.size() > 1 && pt.amg_kind == MFEA_PC_GAMG && omega_fallback(h, fin.status)) {
-    // the over-relaxed coarse smoothers did not give an SPD cycle on this
-    // operator (ω_l λ_l ≥ 2 somewhere): this solve again on the safe weights
+  if (fin.status != 0 && pt.amg_reused) {
+    // a hierarchy kept from another active set failed: rebuild for this one
+    // before anything else is blamed (the ω retry below would otherwise run
+    // on the kept hierarchy)
+    pt.amg_stale = true;
     RC(sync_stream(h));
     return solve_amg(h, dy_top, dy_bot, o, st);
   }
+  if (pt.amg_lev.size() > 1 && pt.amg_kind == MFEA_PC_GAMG &&
+      omega_suspect(h, fin.status, o->max_it, std::max(pt.amg_build_iters, pt.amg_last_iters)))
+    return omega_retry(h, [&]() { return solve_amg(h, dy_top, dy_bot, o, st); });
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
   if (fin.status == 0 && !pt.amg_reused) {
     pt.amg_build_iters = fin.iters;  // the hierarchy on the set it was built for
   } else if (pt.amg_reused && pt.amg_build_iters >= 0 &&
-             (fin.status != 0 || fin.iters > (int64_t)pt.amg_build_iters * h->opt_amg_rebuild_pct / 100 + 2)) {
+             fin.iters > (int64_t)pt.amg_build_iters * h->opt_amg_rebuild_pct / 100 + 2) {
     pt.amg_stale = true;  // degraded: the next solve rebuilds for its active set
-    if (fin.status != 0) {  // ... this one already: solve again on a fresh hierarchy
-      RC(sync_stream(h));
-      return solve_amg(h, dy_top, dy_bot, o, st);
-    }
   }
   rc = finish_solve(h, fin, st);
   if (st) {
@@ -2200,8 +2266,6 @@ int enqueue_gamg_chunk(mfea_handle* h, int chunk) {
 
 int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o, mfea_stats* st) {
   hipStream_t s = h->stream;
-  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
-    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
   bool rebuilt = false;
   RC(ensure_gamg(h, &rebuilt));
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
@@ -2268,10 +2332,8 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
                      },
                      &fin));
   }
-  if (omega_fallback(h, fin.status)) {
-    RC(sync_stream(h));
-    return solve_gamg_global(h, dy_top, dy_bot, o, st);
-  }
+  if (omega_suspect(h, fin.status, o->max_it, p0.amg_last_iters))
+    return omega_retry(h, [&]() { return solve_gamg_global(h, dy_top, dy_bot, o, st); });
   if (fin.status == 0) p0.amg_last_iters = fin.iters;
   // x to row order, then the displacement halo (ghost rows of the post kernels)
   for (auto& pp : h->parts) {
@@ -2298,8 +2360,6 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
 int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
                    mfea_stats* st) {
   hipStream_t s = h->stream;
-  if (o->norm != MFEA_NORM_UNPRECONDITIONED)
-    return fail(MFEA_EINVAL, "MFEA_PC_GAMG stops on the unpreconditioned residual only");
   bool rebuilt = false;
   for (auto& pp : h->parts) {
     bool rb = false;
@@ -2375,10 +2435,8 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
                      },
                      &fin));
   }
-  if (omega_fallback(h, fin.status)) {
-    RC(sync_stream(h));
-    return solve_amg_dist(h, dy_top, dy_bot, o, st);
-  }
+  if (omega_suspect(h, fin.status, o->max_it, p0.amg_last_iters))
+    return omega_retry(h, [&]() { return solve_amg_dist(h, dy_top, dy_bot, o, st); });
   if (fin.status == 0) p0.amg_last_iters = fin.iters;
   // x to row order, then the displacement halo (ghost rows of the post kernels)
   for (auto& pp : h->parts) {
@@ -3354,6 +3412,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
     h->opt_amg_big_chunk = (int)value;
   }
+  else if (n == "sweep_piece") {
+    if (value < 1 || value > 1024) return fail(MFEA_EINVAL, "sweep_piece: 1..1024");
+    h->opt_sweep_piece = (int)value;
+    rebuild = true;
+  }
   else if (n == "amg_fuse_setup") {
     if (value < 0 || value > 1) return fail(MFEA_EINVAL, "amg_fuse_setup: 0 or 1");
     h->opt_amg_fuse_setup = (int)value;
@@ -3549,6 +3612,9 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
   else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
+  else if (n == "sweep_piece") *value = h->opt_sweep_piece;
+  else if (n == "sweep_colors") *value = part0(h).sweep.colors;  // read-only
+  else if (n == "sweep_pieces") *value = part0(h).sweep.n_pieces;  // read-only
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
   else if (n == "amg_coarse_rho_ppm") *value = h->opt_amg_coarse_rho_ppm;
   else if (n == "amg_safe_omega") *value = h->amg_safe_omega ? 1 : 0;  // read-only

@@ -197,6 +197,8 @@ __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, 
   const double ref = norm == 1 ? zz : bb;
   const double t = rtol * rtol * ref, a2 = atol * atol;
   st->tol2 = t > a2 ? t : a2;
+  st->rtol2 = rtol * rtol;
+  st->atol2 = a2;
   st->reg = reg;
   st->bb0 = bb;
   st->res0 = ref;

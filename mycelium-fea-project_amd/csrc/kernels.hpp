@@ -68,6 +68,8 @@ struct SolveState {
   int32_t status;  // 0 converged, -4 maxit, -5 breakdown
   int32_t pad[2];
   double res0;     // initial value of the chosen norm² (‖b‖² or ‖M⁻¹b‖²)
+  double rtol2;    // rtol², atol²: the AMG / sweep CG forms tol2 for the preconditioned
+  double atol2;    // norm from its first ‖u₀‖² = ‖M⁻¹b‖² (k_amg_cg_update)
 };
 
 struct Material {

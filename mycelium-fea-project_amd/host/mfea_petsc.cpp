@@ -17,16 +17,16 @@
 // (src/fea_petsc.cpp:328-331) and PCBJACOBI in its MPI variant
 // (src/fea_petsc_parallel.cpp:339): so does this driver — -pc_type icc is the
 // default on one process, bjacobi under a multi-process launch.  icc (and ilu,
-// the same factor of an SPD matrix) is the engine's DIC(0) and sor its SSOR
-// (ω = 1), both block Jacobi over 256-row blocks with multicolour sweeps
-// inside (PETSc's SOR / ICC are processor-local in parallel; sweep.hip);
-// bjacobi is the exact inverse of each node's 3×3 diagonal block and jacobi
-// PCJACOBI.  Documented differences: prescribed DOFs hold exactly their value
-// (PETSc adds the 1e-12 shift to those rows too and returns x/(1+1e-12));
-// -pc_type gamg (the reference sweep's GAMG, src/fea_petsc_solverAndPC.cpp:
-// 330-391) is the engine's SA-AMG V-cycle; gamg, icc, ilu and sor stop on the
-// unpreconditioned residual (their default norm here; asking for the
-// preconditioned one is an error); other -ksp_type are rejected.
+// the same factor of an SPD matrix) is the engine's IC(0) of the whole free
+// system and sor its SSOR (ω = 1), both in a chain-piece multicolour order
+// (sweep.hip; PETSc runs them in the natural order); bjacobi is the exact
+// inverse of each node's 3×3 diagonal block and jacobi PCJACOBI.  Every
+// preconditioner stops on PETSc's default CG norm, the preconditioned one,
+// unless -ksp_norm_type unpreconditioned.  Documented differences: prescribed
+// DOFs hold exactly their value (PETSc adds the 1e-12 shift to those rows too
+// and returns x/(1+1e-12)); -pc_type gamg (the reference sweep's GAMG,
+// src/fea_petsc_solverAndPC.cpp:330-391) is the engine's SA-AMG V-cycle;
+// other -ksp_type are rejected.
 //
 // Multi-GPU: launched as N processes — `mpirun -np N mfea_petsc <dir>` as the
 // reference's `mpirun -np 4 ./fea_petsc_parallel.exe` (README.md:18), or
@@ -137,16 +137,13 @@ Options parse(int argc, char** argv) {
 }
 
 // the preconditioner default (the reference's PCICC; its MPI variant's
-// PCBJACOBI) and the norm gamg / icc / sor stop on
+// PCBJACOBI).  Every preconditioner stops on PETSc's default KSPCG norm, the
+// preconditioned one, unless -ksp_norm_type says otherwise
+// (src/fea_petsc.cpp:336-341).
 void finish_options(Options& o, int world) {
   if (o.precond < 0) o.precond = world > 1 ? MFEA_PC_BLOCK_JACOBI : MFEA_PC_ICC;
   if (world > 1 && (o.precond == MFEA_PC_ICC || o.precond == MFEA_PC_SOR))
     die("-pc_type icc / ilu / sor: one process (use bjacobi, jacobi or gamg under mpirun)");
-  if (o.precond == MFEA_PC_GAMG || o.precond == MFEA_PC_ICC || o.precond == MFEA_PC_SOR) {
-    if (o.norm_given && o.norm == MFEA_NORM_PRECONDITIONED)
-      die("-pc_type gamg / icc / ilu / sor stop on the unpreconditioned residual (-ksp_norm_type unpreconditioned)");
-    o.norm = MFEA_NORM_UNPRECONDITIONED;
-  }
 }
 
 // src/fea_petsc.cpp:42-82: header skipped, empty lines skipped, the first

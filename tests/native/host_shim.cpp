@@ -457,4 +457,47 @@ void shim_part_arrays(int64_t* node_g, uint8_t* ghost, int64_t* elem_g, uint8_t*
   cp(xrecv_node, p.xrecv_node);
 }
 
+// a plan capped at max_levels (1: the one-level plan of MFEA_PC_SOR / _ICC)
+int shim_amg_levels(const uint8_t* active, int nd, int max_levels, char* err, int errn) {
+  std::vector<uint8_t> a(active, active + g_P.n_elems);
+  std::string e = build_amg(g_P, a, nd, g_amg, max_levels, nullptr, g_strength, g_layout);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return (int)g_amg.lev.size();
+}
+
+// the chain-piece sweep plan of the last plan's level 0 (amg.hpp SweepPlan):
+// returns its colour count (−1: error)
+static SweepPlan g_sweep;
+int shim_sweep(int piece_len, char* err, int errn) {
+  std::string e = build_sweep(g_amg, piece_len, g_sweep);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return g_sweep.colors;
+}
+int64_t shim_sweep_array(const char* name, int32_t* out) {
+  const std::string n(name);
+  if (n == "n_pieces") return g_sweep.n_pieces;
+  const std::vector<int32_t>* v = nullptr;
+  if (n == "cwave") v = &g_sweep.cwave;
+  else if (n == "wbase") v = &g_sweep.wbase;
+  else if (n == "wlen") v = &g_sweep.wlen;
+  else if (n == "row") v = &g_sweep.row;
+  else if (n == "ppos") v = &g_sweep.ppos;
+  else if (n == "dpos") v = &g_sweep.dpos;
+  else if (n == "lo_ptr") v = &g_sweep.lo_ptr;
+  else if (n == "lo_ent") v = &g_sweep.lo_ent;
+  else if (n == "lo_pos") v = &g_sweep.lo_pos;
+  else if (n == "up_ptr") v = &g_sweep.up_ptr;
+  else if (n == "up_ent") v = &g_sweep.up_ent;
+  else if (n == "up_pos") v = &g_sweep.up_pos;
+  else return -1;
+  if (out && !v->empty()) std::memcpy(out, v->data(), v->size() * 4);
+  return (int64_t)v->size();
+}
+
 }  // extern "C"

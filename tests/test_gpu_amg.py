@@ -145,6 +145,44 @@ def test_gamg_kept_hierarchy_floating_pieces_exactly_zero(engine):
         assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
 
 
+def test_gamg_hierarchy_not_kept_for_a_superset(engine):
+    """A hierarchy built on a REDUCED active set holds only that set's
+    elements in A_0's slot lists; elements coming back (set_active(None))
+    must rebuild it — a kept one would solve a system missing their
+    couplings.  U then matches the direct solve of the intact K."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    known, vals = fo.known_dof_map(top, bot, dy, -dy)
+    rng = np.random.default_rng(11)
+    active = rng.random(len(e2n)) > 0.03
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+        engine.set_active(active)
+        engine.assemble()
+        assert engine.solve(dy, -dy, _opts(1e-13)).status == 0
+        engine.set_active(None)
+        engine.assemble()
+        st = engine.solve(dy, -dy, _opts(1e-13))
+        assert st.status == 0 and st.amg_rebuilt == 1
+        assert engine.get_option("amg_reused") == 0
+        K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+        assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
+
+
+def test_small_max_it_keeps_overrelaxed_weights(engine):
+    """A caller's deliberately small max_it is not the coarse weights' fault:
+    the solve reports EMAXIT (LinAlgError in the drop-in) and the handle keeps
+    the over-relaxed smoothers for the next solve."""
+    from mfea import PC_GAMG, make_opts
+    _sim181147(engine)
+    engine.assemble()
+    assert engine.get_option("amg_safe_omega") == 0
+    with pytest.raises(np.linalg.LinAlgError):
+        engine.solve(0.01, -0.01, make_opts(rtol=1e-13, max_it=3, precond=PC_GAMG))
+    assert engine.get_option("amg_safe_omega") == 0
+    assert engine.solve(0.01, -0.01, _opts(1e-13)).status == 0
+    assert engine.get_option("amg_safe_omega") == 0
+
+
 def test_gamg_3d_mesh_matches_direct(engine):
     nodes, elems = load_mesh("sim_20251115_135507")
     xyz = nodes[["x", "y", "z"]].values
@@ -159,14 +197,6 @@ def test_gamg_3d_mesh_matches_direct(engine):
     K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
     known, vals = fo.known_dof_map(top, bot, 0.01, -0.01)
     assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
-
-
-def test_gamg_rejects_preconditioned_norm(engine):
-    from mfea import MfeaError, NORM_PRECONDITIONED
-    _sim181147(engine)
-    engine.assemble()
-    with pytest.raises(MfeaError):
-        engine.solve(0.01, -0.01, _opts(1e-8, norm=NORM_PRECONDITIONED))
 
 
 def test_gamg_profile_iteration(engine):

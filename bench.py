@@ -657,6 +657,9 @@ def main(argv=None):
             _, _, sk = eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=code), fs.MAX_STRAIN)
             out[f"{name}_iters_1e8"] = sk.iters
             out[f"{name}_step_ms"] = sk.t_assemble_ms + sk.t_rhs_ms + sk.t_solve_ms + sk.t_post_ms
+            out[f"{name}_plan"] = {"colours": eng.get_option("sweep_colors"),
+                                   "pieces": eng.get_option("sweep_pieces"),
+                                   "iteration_us": 1e3 * eng.profile_iteration(code, reps=50)}
 
     if rank == 0 and not a.no_cpu and world == 1:
         cpu_legs(a, out, xyz, e2n, top, bot, dy, n_dof)

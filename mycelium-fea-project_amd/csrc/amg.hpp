@@ -270,29 +270,29 @@ std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t m
 // their index in the block and the A_0 position of the coupling block.
 // Whole-matrix SSOR / IC(0) in a chain-piece multicolour order (sweep.hip,
 // MFEA_PC_SOR / MFEA_PC_ICC).  The level-0 rows are cut into
-// PIECES: runs of at most `piece_len` rows along a depth-first path of A_0's
-// graph, each row coupled to its predecessor and to no other row of its
-// piece.  The pieces are coloured (greedy: no two coupled pieces share a
-// colour) and the matrix is factorised in the order colour → piece → step,
-// so one lane walks one piece (its rows in path order: a hyphal chain keeps
-// its natural-order factorisation) and the pieces of one colour are
-// independent.  Every coupling of A_0 is kept: in-piece couplings are the
-// predecessor links, the others ("cross" couplings) join pieces of different
-// colours and are lower / upper by colour.
+// PIECES: runs of at most `piece_len` (≤ 64) rows along a depth-first path of
+// A_0's graph, each row coupled to its predecessor and to no other row of
+// its piece.  The pieces are coloured (greedy: no two coupled pieces share a
+// colour) and the matrix is factorised in the order colour → piece → row, so
+// the pieces of one colour are independent and a hyphal chain keeps its
+// natural-order factorisation.  Every coupling of A_0 is kept: in-piece
+// couplings are the predecessor links, the others ("cross" couplings) join
+// pieces of different colours and are lower / upper by colour.
 //
-// Entries: the pieces of a colour, sorted by length (longest first), go 64 to
-// a WAVE (one lane each); wave w's entries are [wbase[w], wbase[w] + 64·wlen[w])
-// step-major (entry = wbase + step·64 + lane), so a step's loads are
-// coalesced.  Steps past a piece's end are padding (row −1).
+// Entries: a colour's pieces, in depth-first order, packed into the 64 lanes
+// of consecutive waves (entry = 64·wave + lane; a piece's rows on
+// consecutive lanes, never across two waves; the rest of a wave that cannot
+// take the next piece is padding, row −1).  A sweep solves a piece's
+// recurrence by a scan across its lanes: wsteps[w] = ⌈log₂(longest piece)⌉.
 struct SweepPlan {
-  int piece_len = 16;
+  int piece_len = 64;
   int colors = 0;
   int64_t n = 0;                         // level-0 rows
   int64_t n_pieces = 0;
   std::vector<int32_t> cwave;            // per colour: first wave (+ end)
-  std::vector<int32_t> wbase, wlen;      // per wave
+  std::vector<int32_t> wsteps;           // per wave: scan steps
   std::vector<int32_t> row;              // per entry: level-0 row (−1: padding)
-  std::vector<int32_t> ppos;             // per entry: A_0 position of (row, predecessor) (−1: first step)
+  std::vector<int32_t> ppos;             // per entry: A_0 position of (row, predecessor) (−1: a piece's first row)
   std::vector<int32_t> dpos;             // per entry: A_0 position of the diagonal block (−1: padding)
   // cross couplings per entry: to earlier colours (lo) / later colours (up):
   // the neighbour's entry and the A_0 position of (row, neighbour)

@@ -144,17 +144,16 @@ struct AmgCg {
 // setup launch(es) form from A_0 — the predecessor blocks pv, the cross
 // blocks lov / upv (f32, [item][ND²]), D̃⁻¹ (f32 upper triangles: SOR D⁻¹,
 // ICC the DIC(0) pivots formed in f64) — and the sweeps' f64 iterate y.
-constexpr int kSweepPieceLen = 16;   // rows per piece (tools/icc_lab.py)
+constexpr int kSweepPieceLen = 64;   // rows per piece at most (one wave)
 constexpr int kSweepMaxColors = 32;
-constexpr int kSweepBS = 256;        // threads per workgroup (4 waves = 4 × 64 pieces)
+constexpr int kSweepBS = 256;        // threads per workgroup
 struct SweepD {
   int64_t n = 0;   // level-0 rows
-  int64_t ne = 0;  // entries
+  int64_t ne = 0;  // entries (64 per wave)
   int colors = 0;
   int dic = 0;
   int32_t cw[kSweepMaxColors + 1] = {};  // colour → first wave
-  const int32_t* wbase = nullptr;
-  const int32_t* wlen = nullptr;
+  const int32_t* wsteps = nullptr;
   const int32_t* row = nullptr;
   const int32_t* ppos = nullptr;
   const int32_t* dpos = nullptr;

@@ -673,13 +673,13 @@ std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active,
 // pieces keep it where a GPU can: tools/icc_lab.py measured IC(0) to rtol 1e-8
 // on the reference network at 395 iterations in the natural order, 392–410 in
 // this order with 8–128-row pieces, 639 in a point red-black order (Jacobi:
-// 1,262 block / 1,644 point).
+// 1,262 block / 1,644 point).  Pieces hold at most 64 rows (one wave: the
+// sweeps scan a piece across its lanes, sweep.hip).
 std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
   out = SweepPlan();
-  piece_len = std::max(1, piece_len);
+  piece_len = std::min(64, std::max(1, piece_len));
   out.piece_len = piece_len;
   out.cwave.assign(1, 0);
-  out.wbase.assign(1, 0);
   out.lo_ptr.assign(1, 0);
   out.up_ptr.assign(1, 0);
   if (plan.lev.empty()) return "";
@@ -687,6 +687,9 @@ std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
   const int64_t n = A.n;
   out.n = n;
   if (n == 0) return "";
+  std::vector<int32_t> nat(n);
+  if ((int64_t)plan.lev[0].nat.size() == n) nat = plan.lev[0].nat;
+  else std::iota(nat.begin(), nat.end(), 0);
   // A_0's off-diagonal couplings per row, ascending neighbour
   std::vector<int64_t> aptr(n + 1, 0);
   std::vector<std::pair<int32_t, int32_t>> adj;  // (neighbour, A position)
@@ -698,15 +701,19 @@ std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
       if (j < 0 || j == i) continue;
       adj.emplace_back(j, (int32_t)q);
     }
-    std::sort(adj.begin() + a0, adj.end());
+    // neighbours in natural (aggregation / depth-first) order, so the pieces
+    // do not depend on the level's device labels
+    std::sort(adj.begin() + a0, adj.end(), [&](const auto& x, const auto& y) { return nat[x.first] < nat[y.first]; });
     aptr[i + 1] = (int64_t)adj.size();
   }
+  std::vector<int32_t> roots(n);
+  for (int64_t i = 0; i < n; ++i) roots[nat[i]] = (int32_t)i;
   // depth-first order and tree parents
   std::vector<int32_t> order, parent(n, -1);
   order.reserve(n);
   std::vector<uint8_t> seen(n, 0);
   std::vector<std::pair<int32_t, int64_t>> st;
-  for (int64_t root = 0; root < n; ++root) {
+  for (const int32_t root : roots) {
     if (seen[root]) continue;
     seen[root] = 1;
     order.push_back((int32_t)root);
@@ -765,36 +772,60 @@ std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
     pcol[p] = c;
     out.colors = std::max(out.colors, c + 1);
   }
-  // waves: a colour's pieces by length (longest first), 64 to a wave
-  std::vector<int64_t> ent0(np);  // entry of a piece's first step (lane offset included)
+  // waves: a colour's pieces packed into the 64 lanes of its waves by
+  // best-fit decreasing (longest piece first, into the open wave with the
+  // least room that holds it; ties in depth-first order) — a piece's rows on
+  // consecutive lanes, never across two waves; the lanes left over are
+  // padding.  Depth-first first-fit left C3's colour 1 at 68 % of its lanes.
+  std::vector<int64_t> ent0(np);  // entry of a piece's first row
+  int64_t ne = 0;
   for (int c = 0; c < out.colors; ++c) {
     std::vector<int32_t> ps;
     for (int64_t p = 0; p < np; ++p)
       if (pcol[p] == c) ps.push_back((int32_t)p);
     std::stable_sort(ps.begin(), ps.end(), [&](int32_t a, int32_t b) { return plen[a] > plen[b]; });
-    for (size_t k = 0; k < ps.size(); k += 64) {
-      const int32_t len = plen[ps[k]];
-      out.wlen.push_back(len);
-      for (size_t l = k; l < std::min(ps.size(), k + 64); ++l) {
-        ent0[ps[l]] = (int64_t)out.wbase.back() + (int64_t)(l - k);
+    const int64_t w0 = ne / 64;
+    std::vector<int32_t> room, wmax;            // per wave of this colour
+    std::vector<std::vector<int32_t>> by_room(65);  // open waves by lanes left
+    for (const int32_t p : ps) {
+      int32_t w = -1;
+      for (int r = plen[p]; r <= 64 && w < 0; ++r) {
+        auto& b = by_room[r];
+        while (!b.empty() && room[b.back()] != r) b.pop_back();  // stale entries
+        if (!b.empty()) {
+          w = b.back();
+          b.pop_back();
+        }
       }
-      const int64_t next = (int64_t)out.wbase.back() + 64 * (int64_t)len;
-      if (next > INT32_MAX) return "sweep plan: too many entries";
-      out.wbase.push_back((int32_t)next);
+      if (w < 0) {
+        w = (int32_t)room.size();
+        room.push_back(64);
+        wmax.push_back(0);
+      }
+      ent0[p] = 64 * (w0 + w) + (64 - room[w]);
+      room[w] -= plen[p];
+      wmax[w] = std::max(wmax[w], plen[p]);
+      by_room[room[w]].push_back(w);
     }
-    out.cwave.push_back((int32_t)out.wlen.size());
+    for (size_t w = 0; w < room.size(); ++w) {
+      int st = 0;
+      while ((1 << st) < wmax[w]) ++st;
+      out.wsteps.push_back(st);
+    }
+    ne += 64 * (int64_t)room.size();
+    out.cwave.push_back((int32_t)(ne / 64));
+    if (ne > INT32_MAX) return "sweep plan: too many entries";
   }
-  const int64_t ne = out.wbase.back();
   out.row.assign(ne, -1);
   out.ppos.assign(ne, -1);
   out.dpos.assign(ne, -1);
   std::vector<int32_t> ent(n);
   for (int64_t p = 0; p < np; ++p)
-    for (int32_t s = 0; s < plen[p]; ++s) ent[order[pstart[p] + s]] = (int32_t)(ent0[p] + 64 * (int64_t)s);
+    for (int32_t s = 0; s < plen[p]; ++s) ent[order[pstart[p] + s]] = (int32_t)(ent0[p] + s);
   auto pos_of = [&](int32_t v, int32_t j) -> int32_t {
-    const auto b = adj.begin() + aptr[v], e = adj.begin() + aptr[v + 1];
-    const auto it = std::lower_bound(b, e, std::make_pair(j, INT32_MIN));
-    return it != e && it->first == j ? it->second : -1;
+    for (int64_t k = aptr[v]; k < aptr[v + 1]; ++k)
+      if (adj[k].first == j) return adj[k].second;
+    return -1;
   };
   for (int64_t p = 0; p < np; ++p)
     for (int32_t s = 0; s < plen[p]; ++s) {
@@ -814,7 +845,7 @@ std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
     const int32_t v = out.row[e];
     if (v >= 0) {
       const int32_t p = piece[v];
-      const int32_t s = (int32_t)((e - ent0[p]) / 64);
+      const int32_t s = (int32_t)(e - ent0[p]);
       const int32_t prev = s > 0 ? order[pstart[p] + s - 1] : -1;
       const int32_t next = s + 1 < plen[p] ? order[pstart[p] + s + 1] : -1;
       for (int64_t k = aptr[v]; k < aptr[v + 1]; ++k) {

@@ -1467,7 +1467,7 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
   if (sp.colors > kSweepMaxColors) return fail(MFEA_EINVAL, "sweep plan: too many colours");
   const int nd = pt.amg.nd, nb2 = nd * nd, ns = nd * (nd + 1) / 2;
   const int64_t ne = sp.n_entries();
-  const std::vector<int32_t>* iv[] = {&sp.wbase, &sp.wlen, &sp.row, &sp.ppos, &sp.dpos, &sp.lo_ptr,
+  const std::vector<int32_t>* iv[] = {&sp.wsteps, &sp.row, &sp.ppos, &sp.dpos, &sp.lo_ptr,
                                       &sp.lo_ent, &sp.lo_pos, &sp.up_ptr, &sp.up_ent, &sp.up_pos};
   size_t ni = 1;
   for (auto* v : iv) ni += v->size();
@@ -1489,8 +1489,7 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
   w.colors = sp.colors;
   w.dic = kind == MFEA_PC_ICC ? 1 : 0;
   for (int c = 0; c <= sp.colors; ++c) w.cw[c] = sp.cwave[c];
-  w.wbase = put(sp.wbase);
-  w.wlen = put(sp.wlen);
+  w.wsteps = put(sp.wsteps);
   w.row = put(sp.row);
   w.ppos = put(sp.ppos);
   w.dpos = put(sp.dpos);
@@ -3206,8 +3205,9 @@ int mfea_profile_iteration(mfea_handle* h, int precond, int reps, double* avg_ms
   RC(ensure_built(h));
   Part& pt = part0(h);
   hipStream_t s = h->stream;
-  if (precond == MFEA_PC_GAMG) {
-    if (!pt.amg_ok) return fail(MFEA_ESTATE, "profile GAMG after a GAMG solve");
+  if (precond == MFEA_PC_GAMG || precond == MFEA_PC_SOR || precond == MFEA_PC_ICC) {
+    if (!pt.amg_ok || pt.amg_kind != precond)
+      return fail(MFEA_ESTATE, "profile GAMG / SOR / ICC after a solve with that preconditioner");
     // Running state: slots[0] = INIT and real partials from an ungated first
     // w kernel; every rep is update + V-cycle + w(first) — the full work of
     // one PCG iteration, all stores included.

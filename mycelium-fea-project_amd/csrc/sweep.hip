@@ -17,18 +17,22 @@
 // on the reference and the tiled networks); a pivot that is not positive
 // definite falls back to D_i (PETSc shifts such pivots), so M stays SPD.
 //
-// One lane walks one piece: its rows are coupled in a chain (each to its
-// predecessor), so the step-to-step dependence is one block product held in
-// registers; the pieces of a colour are independent, one launch per colour
-// and sweep direction (the last colour's backward sweep rides in its forward
-// launch: 2C − 1 launches per application).  A step's entry arrays are
-// step-major over the wave's 64 pieces (coalesced); the few cross couplings
-// (piece ends, branch and fusion points) are short per-entry lists.
+// One lane per row: a piece's rows sit on consecutive lanes of one wave, so
+// its chain recurrence — forward y_l = g_l + G_l y_{l−1} with
+// g_l = D̃_l⁻¹(r_l − Σ_lo A y), G_l = −D̃_l⁻¹ A_{l,l−1}; backward
+// z_l = h_l + H_l z_{l+1} with H_l = −D̃_l⁻¹ A_{l+1,l}ᵀ — is an inclusive scan
+// of affine maps across the lanes (⌈log₂ piece⌉ shuffle steps; G = 0 at a
+// piece's first row, H = 0 at its last, so pieces do not mix).  The pieces of
+// a colour are independent: one launch per colour and direction, the last
+// colour's backward scan in its forward launch (2C − 1 launches per
+// application), every load coalesced except the r / u gathers and the few
+// cross couplings (piece ends, branch and fusion points).
 //
 // Arithmetic in f64 throughout (the iterate y / z is stored f64); the
 // operator values are f32 (pv, lov, upv, D̃⁻¹), the SAME stored values in
-// both sweeps, so M⁻¹ is applied as a fixed symmetric operator up to f64
-// rounding — what keeps a CG of thousands of iterations at the 1e-10 bar.
+// both sweeps and the scan's G / H formed from them in f64 registers, so
+// M⁻¹ is applied as a fixed symmetric operator up to f64 rounding — what
+// keeps a CG of thousands of iterations at the 1e-10 bar.
 #include "amg_dev.hpp"
 
 namespace mfea {
@@ -92,171 +96,238 @@ __device__ __forceinline__ void sub_xdxt(const double* X, const double* D, doubl
     }
 }
 
+// G = −D X (D symmetric ND×ND, X full); TR: G = −D Xᵀ
+template <int ND, bool TR>
+__device__ __forceinline__ void neg_dx(const double* D, const double* X, double* G) {
+#pragma unroll
+  for (int a = 0; a < ND; ++a)
+#pragma unroll
+    for (int b = 0; b < ND; ++b) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < ND; ++k) s = fma(D[a * ND + k], TR ? X[b * ND + k] : X[k * ND + b], s);
+      G[a * ND + b] = -s;
+    }
+}
+
 // Per solve, after A_0's values: the sweeps' operator values from A_0's f64
-// blocks — pv (predecessor), lov / upv (cross), D̃⁻¹.  ICC: one launch per
-// colour (a pivot reads the pivots of earlier colours' cross neighbours);
-// SOR: every colour in one launch.
+// blocks — pv (predecessor), lov / upv (cross), D̃⁻¹.  SOR: every row in
+// parallel, every colour in one launch.  ICC: one launch per colour (a pivot
+// reads the pivots of earlier colours' cross neighbours), the lane of a
+// piece's first row walking the piece's chain of pivots
+// D̃_l = D_l − A_{l,l−1} D̃_{l−1}⁻¹ A_{l,l−1}ᵀ − Σ_lo X D̃_j⁻¹ Xᵀ (f64).
 template <int ND>
 __global__ __launch_bounds__(kSweepBS) void k_sweep_setup(SweepD sw, AmgMatD A, int c0, int c1) {
   const int32_t w = sweep_wave(sw, c0, c1);
   if (w < 0) return;
   const int lane = threadIdx.x & 63;
-  const int64_t e0 = sw.wbase[w] + lane;
-  const int len = sw.wlen[w];
+  const int64_t e = 64 * (int64_t)w + lane;
+  if (sw.row[e] < 0) return;
+  if (sw.ppos[e] >= 0) {
+    double P[ND * ND];
+    bload_sym<ND>(A.sym, 0, sw.ppos[e], P);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) sw.pv[e * (ND * ND) + c] = (float)P[c];
+  }
+  for (int t = sw.lo_ptr[e]; t < sw.lo_ptr[e + 1]; ++t) {
+    double X[ND * ND];
+    bload_sym<ND>(A.sym, 0, sw.lo_pos[t], X);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) sw.lov[(int64_t)t * (ND * ND) + c] = (float)X[c];
+  }
+  for (int t = sw.up_ptr[e]; t < sw.up_ptr[e + 1]; ++t) {
+    double X[ND * ND];
+    bload_sym<ND>(A.sym, 0, sw.up_pos[t], X);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) sw.upv[(int64_t)t * (ND * ND) + c] = (float)X[c];
+  }
+  if (!sw.dic) {
+    double D[ND * ND], Di[ND * ND];
+    bload_sym<ND>(A.sym, 0, sw.dpos[e], D);
+    binv<ND>(D, Di);
+    bstore_sym<ND>(sw.dt, 0, e, Di);
+    return;
+  }
+  if (sw.ppos[e] >= 0) return;  // not a piece's first row: its first row's lane walks it
   double Dprev[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) Dprev[c] = 0.0;
-  for (int s = 0; s < len; ++s) {
-    const int64_t e = e0 + 64 * (int64_t)s;
-    if (sw.row[e] < 0) break;  // past this piece's end
+  const int64_t wend = 64 * (int64_t)w + 64;
+  for (int64_t k = e; k < wend; ++k) {
+    if (k > e && sw.ppos[k] < 0) break;  // the next piece (or padding)
     double D[ND * ND], T[ND * ND], Di[ND * ND];
-    bload_sym<ND>(A.sym, 0, sw.dpos[e], D);
+    bload_sym<ND>(A.sym, 0, sw.dpos[k], D);
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) T[c] = D[c];
-    if (s > 0) {
+    if (k > e) {
       double P[ND * ND];
-      bload_sym<ND>(A.sym, 0, sw.ppos[e], P);
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) sw.pv[e * (ND * ND) + c] = (float)P[c];
-      if (sw.dic) sub_xdxt<ND>(P, Dprev, T);
+      bload_sym<ND>(A.sym, 0, sw.ppos[k], P);
+      sub_xdxt<ND>(P, Dprev, T);
     }
-    for (int t = sw.lo_ptr[e]; t < sw.lo_ptr[e + 1]; ++t) {
-      double X[ND * ND];
+    for (int t = sw.lo_ptr[k]; t < sw.lo_ptr[k + 1]; ++t) {
+      double X[ND * ND], Dj[ND * ND];
       bload_sym<ND>(A.sym, 0, sw.lo_pos[t], X);
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) sw.lov[(int64_t)t * (ND * ND) + c] = (float)X[c];
-      if (sw.dic) {
-        double Dj[ND * ND];
-        load_dt<ND>(sw.dt, sw.lo_ent[t], Dj);
-        sub_xdxt<ND>(X, Dj, T);
-      }
+      load_dt<ND>(sw.dt, sw.lo_ent[t], Dj);
+      sub_xdxt<ND>(X, Dj, T);
     }
-    for (int t = sw.up_ptr[e]; t < sw.up_ptr[e + 1]; ++t) {
-      double X[ND * ND];
-      bload_sym<ND>(A.sym, 0, sw.up_pos[t], X);
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) sw.upv[(int64_t)t * (ND * ND) + c] = (float)X[c];
-    }
-    binv<ND>(sw.dic && spd<ND>(T) ? T : D, Di);
-    bstore_sym<ND>(sw.dt, 0, e, Di);
+    binv<ND>(spd<ND>(T) ? T : D, Di);
+    bstore_sym<ND>(sw.dt, 0, k, Di);
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) Dprev[c] = Di[c];
   }
 }
 
-// backward sweep of one lane's piece, steps len−1 … 0 (the lane's y holds
-// the forward iterate; z overwrites it); u = z for the CG (gated store)
-template <int ND>
-__device__ __forceinline__ void piece_backward(const SweepD& sw, const AmgCg& cg, int64_t e0, int len, bool run) {
-  double zn[ND], Pn[ND * ND];
+// acc ∓= Σ_t X_t y[ent_t] over one entry's cross list [t0, t1): the items'
+// loads issued together, four at a time (a branch row has 2–4 crosses; one
+// at a time they were four dependent round trips each)
+template <int ND, bool SUB>
+__device__ __forceinline__ void cross_sum(int t0, int t1, const int32_t* __restrict__ ent,
+                                          const float* __restrict__ xv, const double* __restrict__ y, double* acc) {
+  constexpr int U = 4;
+  for (int t = t0; t < t1; t += U) {
+    int32_t j[U];
 #pragma unroll
-  for (int a = 0; a < ND; ++a) zn[a] = 0.0;
+    for (int u = 0; u < U; ++u) j[u] = ent[t + u < t1 ? t + u : t0];
+    double X[U][ND * ND], yj[U][ND];
 #pragma unroll
-  for (int c = 0; c < ND * ND; ++c) Pn[c] = 0.0;
-  for (int s = len - 1; s >= 0; --s) {
-    const int64_t e = e0 + 64 * (int64_t)s;
-    const int32_t v = sw.row[e];
-    if (v < 0) continue;  // padding past the piece's end: z = 0, no coupling
-    double y[ND], Dt[ND * ND], acc[ND], P[ND * ND];
-    vload<ND>(sw.y, e, y);
-    load_dt<ND>(sw.dt, e, Dt);
-    if (s > 0) load_blk<ND>(sw.pv, e, P);
-#pragma unroll
-    for (int a = 0; a < ND; ++a) acc[a] = 0.0;
-    bmv<ND, true, false>(Pn, zn, acc);  // A_{i,next} z_next = (A_{next,i})ᵀ z_next
-    for (int t = sw.up_ptr[e]; t < sw.up_ptr[e + 1]; ++t) {
-      double X[ND * ND], zj[ND];
-      load_blk<ND>(sw.upv, t, X);
-      vload<ND>(sw.y, sw.up_ent[t], zj);
-      bmv<ND, false, false>(X, zj, acc);
+    for (int u = 0; u < U; ++u) {
+      load_blk<ND>(xv, t + u < t1 ? t + u : t0, X[u]);
+      vload<ND>(y, j[u], yj[u]);
     }
-    double z[ND];
 #pragma unroll
-    for (int a = 0; a < ND; ++a) z[a] = y[a];
-    bmv<ND, false, true>(Dt, acc, z);
-    vstore<ND>(sw.y, e, z);
-    if (run) vstore<ND>(cg.u, v, z);
+    for (int u = 0; u < U; ++u)
+      if (t + u < t1) bmv<ND, false, SUB>(X[u], yj[u], acc);
+  }
+}
+
+// the affine-map scan across the wave's lanes: x_l = a_l + M_l x_{l∓1}
+// composed over `steps` doubling steps (UP: predecessors are lower lanes)
+template <int ND, bool UP>
+__device__ __forceinline__ void lane_scan(double* a, double* M, int steps) {
+  const int lane = threadIdx.x & 63;
+  for (int k = 0; k < steps; ++k) {
+    const int d = 1 << k;
+    double as[ND], Ms[ND * ND];
 #pragma unroll
-    for (int a = 0; a < ND; ++a) zn[a] = z[a];
-    if (s > 0) {
+    for (int i = 0; i < ND; ++i) as[i] = UP ? __shfl_up(a[i], d, 64) : __shfl_down(a[i], d, 64);
 #pragma unroll
-      for (int c = 0; c < ND * ND; ++c) Pn[c] = P[c];
+    for (int i = 0; i < ND * ND; ++i) Ms[i] = UP ? __shfl_up(M[i], d, 64) : __shfl_down(M[i], d, 64);
+    if (UP ? lane >= d : lane + d < 64) {
+      bmv<ND, false, false>(M, as, a);
+      double N[ND * ND];
+#pragma unroll
+      for (int i = 0; i < ND * ND; ++i) N[i] = 0.0;
+      mm_acc<ND>(M, Ms, N);
+#pragma unroll
+      for (int i = 0; i < ND * ND; ++i) M[i] = N[i];
     }
   }
 }
 
-// forward sweep of colour c: y over its pieces; LAST (the last colour): the
-// backward sweep of the same pieces follows in the same lane
+// backward sweep of the lane's row: z = y − D̃⁻¹(A_{l,l+1} z_{l+1} + Σ_up X z_j)
+// as a suffix scan; P: the lane's own predecessor block (0 on a first row),
+// y: its forward iterate.  Stores z (sw.y) and u = z (gated).
+template <int ND>
+__device__ __forceinline__ void lane_backward(const SweepD& sw, const AmgCg& cg, int64_t e, int32_t v,
+                                              const double* Dt, const double* P, bool hasP, double* y,
+                                              int steps, bool run, bool cross) {
+  double acc[ND];
+#pragma unroll
+  for (int a = 0; a < ND; ++a) acc[a] = 0.0;
+  if (cross && v >= 0) cross_sum<ND, false>(sw.up_ptr[e], sw.up_ptr[e + 1], sw.up_ent, sw.upv, sw.y, acc);
+  bmv<ND, false, true>(Dt, acc, y);  // h = y − D̃⁻¹ acc
+  // H = −D̃⁻¹ (A_{l+1,l})ᵀ where the next lane continues this piece
+  double Pn[ND * ND], H[ND * ND];
+#pragma unroll
+  for (int i = 0; i < ND * ND; ++i) Pn[i] = __shfl_down(P[i], 1, 64);
+  const bool next = __shfl_down(hasP ? 1 : 0, 1, 64) && (threadIdx.x & 63) < 63;
+  if (next) neg_dx<ND, true>(Dt, Pn, H);
+  else {
+#pragma unroll
+    for (int i = 0; i < ND * ND; ++i) H[i] = 0.0;
+  }
+  lane_scan<ND, false>(y, H, steps);
+  if (v >= 0) {
+    vstore<ND>(sw.y, e, y);
+    if (run) vstore<ND>(cg.u, v, y);
+  }
+}
+
+// forward sweep of wave w (one lane per entry); LAST (the last colour, no
+// upper couplings): its backward scan follows in registers
+template <int ND, bool LAST>
+__device__ __forceinline__ void fwd_wave(const SweepD& sw, const AmgCg& cg, int32_t w, bool run) {
+  const int64_t e = 64 * (int64_t)w + (threadIdx.x & 63);
+  const int32_t v = sw.row[e];
+  const int steps = sw.wsteps[w];
+  double g[ND], G[ND * ND], Dt[ND * ND], P[ND * ND];
+  bool hasP = false;
+#pragma unroll
+  for (int i = 0; i < ND; ++i) g[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < ND * ND; ++i) {
+    G[i] = 0.0;
+    P[i] = 0.0;
+    Dt[i] = 0.0;
+  }
+  if (v >= 0) {
+    double t[ND];
+    vload<ND>(cg.r, v, t);
+    load_dt<ND>(sw.dt, e, Dt);
+    hasP = sw.ppos[e] >= 0;
+    if (hasP) load_blk<ND>(sw.pv, e, P);
+    cross_sum<ND, true>(sw.lo_ptr[e], sw.lo_ptr[e + 1], sw.lo_ent, sw.lov, sw.y, t);
+    bmv<ND, false, false>(Dt, t, g);
+    if (hasP) neg_dx<ND, false>(Dt, P, G);
+  }
+  lane_scan<ND, true>(g, G, steps);
+  if constexpr (LAST) {
+    lane_backward<ND>(sw, cg, e, v, Dt, P, hasP, g, steps, run, false);
+  } else if (v >= 0) {
+    vstore<ND>(sw.y, e, g);
+  }
+}
+
+template <int ND>
+__device__ __forceinline__ void bwd_wave(const SweepD& sw, const AmgCg& cg, int32_t w, bool run) {
+  const int64_t e = 64 * (int64_t)w + (threadIdx.x & 63);
+  const int32_t v = sw.row[e];
+  double y[ND], Dt[ND * ND], P[ND * ND];
+  bool hasP = false;
+#pragma unroll
+  for (int i = 0; i < ND; ++i) y[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < ND * ND; ++i) {
+    P[i] = 0.0;
+    Dt[i] = 0.0;
+  }
+  if (v >= 0) {
+    vload<ND>(sw.y, e, y);
+    load_dt<ND>(sw.dt, e, Dt);
+    hasP = sw.ppos[e] >= 0;
+    if (hasP) load_blk<ND>(sw.pv, e, P);
+  }
+  lane_backward<ND>(sw, cg, e, v, Dt, P, hasP, y, sw.wsteps[w], run, true);
+}
+
 template <int ND, bool LAST>
 __global__ __launch_bounds__(kSweepBS) void k_sweep_fwd(SweepD sw, AmgCg cg, int c, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int32_t w = sweep_wave(sw, c, c + 1);
-  if (w < 0) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t e0 = sw.wbase[w] + lane;
-  const int len = sw.wlen[w];
-  double yp[ND];
-#pragma unroll
-  for (int a = 0; a < ND; ++a) yp[a] = 0.0;
-  int n = 0;  // the lane's piece length
-  // one step of look-ahead: the next step's operands are loaded before this
-  // step's products (only yp chains the steps)
-  int32_t v = sw.row[e0];
-  double rn[ND], Pn[ND * ND], Dn[ND * ND];
-  if (v >= 0) {
-    vload<ND>(cg.r, v, rn);
-    load_dt<ND>(sw.dt, e0, Dn);
-  }
-  for (int s = 0; s < len && v >= 0; ++s) {
-    const int64_t e = e0 + 64 * (int64_t)s;
-    double t[ND], Dt[ND * ND], P[ND * ND];
-#pragma unroll
-    for (int a = 0; a < ND; ++a) t[a] = rn[a];
-#pragma unroll
-    for (int k = 0; k < ND * ND; ++k) Dt[k] = Dn[k];
-    if (s > 0) {
-#pragma unroll
-      for (int k = 0; k < ND * ND; ++k) P[k] = Pn[k];
-    }
-    const int32_t vn = s + 1 < len ? sw.row[e + 64] : -1;
-    if (vn >= 0) {
-      vload<ND>(cg.r, vn, rn);
-      load_dt<ND>(sw.dt, e + 64, Dn);
-      load_blk<ND>(sw.pv, e + 64, Pn);
-    }
-    if (s > 0) bmv<ND, false, true>(P, yp, t);
-    for (int k = sw.lo_ptr[e]; k < sw.lo_ptr[e + 1]; ++k) {
-      double X[ND * ND], yj[ND];
-      load_blk<ND>(sw.lov, k, X);
-      vload<ND>(sw.y, sw.lo_ent[k], yj);
-      bmv<ND, false, true>(X, yj, t);
-    }
-    double y[ND];
-#pragma unroll
-    for (int a = 0; a < ND; ++a) y[a] = 0.0;
-    bmv<ND, false, false>(Dt, t, y);
-    vstore<ND>(sw.y, e, y);
-#pragma unroll
-    for (int a = 0; a < ND; ++a) yp[a] = y[a];
-    ++n;
-    v = vn;
-  }
-  if constexpr (LAST) piece_backward<ND>(sw, cg, e0, n, run);
+  if (w >= 0) fwd_wave<ND, LAST>(sw, cg, w, run);
 }
 
 template <int ND>
 __global__ __launch_bounds__(kSweepBS) void k_sweep_bwd(SweepD sw, AmgCg cg, int c, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int32_t w = sweep_wave(sw, c, c + 1);
-  if (w < 0) return;
-  piece_backward<ND>(sw, cg, sw.wbase[w] + (threadIdx.x & 63), sw.wlen[w], run);
+  if (w >= 0) bwd_wave<ND>(sw, cg, w, run);
 }
 
 static dim3 sweep_grid(const SweepD& sw, int c0, int c1) {
   const int64_t waves = sw.cw[c1] - sw.cw[c0];
   return dim3((unsigned)std::max<int64_t>(1, (waves + kSweepBS / 64 - 1) / (kSweepBS / 64)));
 }
-
 template <int ND>
 static void setup_nd(hipStream_t s, const SweepD& sw, const AmgLevD& L0) {
   if (sw.dic) {

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
 D=gpurun_out/prof_$TAG
 mkdir -p $D
-P="python3 tools/amg_profile.py --config $CFG --reps $REPS $SETS"
+P="python3 tools/amg_profile.py --config $CFG --reps $REPS --precond ${PRECOND:-gamg} $SETS"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o t -- $P > $D/trace.log 2>&1 || exit $?
 if [ "${TRACE_ONLY:-0}" = 1 ]; then python3 tools/amg_pmc_summary.py $D $REPS $D/summary.json; exit $?; fi
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o f -- $P > $D/fetch.log 2>&1 || exit $?

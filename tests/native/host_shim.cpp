@@ -484,8 +484,7 @@ int64_t shim_sweep_array(const char* name, int32_t* out) {
   if (n == "n_pieces") return g_sweep.n_pieces;
   const std::vector<int32_t>* v = nullptr;
   if (n == "cwave") v = &g_sweep.cwave;
-  else if (n == "wbase") v = &g_sweep.wbase;
-  else if (n == "wlen") v = &g_sweep.wlen;
+  else if (n == "wsteps") v = &g_sweep.wsteps;
   else if (n == "row") v = &g_sweep.row;
   else if (n == "ppos") v = &g_sweep.ppos;
   else if (n == "dpos") v = &g_sweep.dpos;

@@ -1,9 +1,9 @@
 """NumPy restatement of the whole-matrix SSOR / IC(0) preconditioners
 (csrc/sweep.hip, amg.hpp SweepPlan) — test infrastructure only.
 
-The engine factorises A_0 in the plan's entry order (colour → wave → step →
-lane; the pieces of a colour are independent, so this is a valid elimination
-order of the whole matrix).  Here the same order is applied to the oracle's
+The engine factorises A_0 in the plan's entry order (colour → wave → lane,
+a piece's rows on consecutive lanes; the pieces of a colour are independent,
+so this is a valid elimination order of the whole matrix).  Here the same order is applied to the oracle's
 K_ff, the block factor M = (D̃ + L) D̃⁻¹ (D̃ + Lᵀ) is formed with SciPy, and a
 SciPy-semantics PCG runs with it.  PETSc's own ICC runs in the natural node
 order (src/fea_petsc.cpp:331); `natural_order` gives that one for comparison.
@@ -15,7 +15,7 @@ import scipy.sparse as sp
 from scipy.sparse.linalg import splu
 
 P = C.c_void_p
-NAMES = ("cwave", "wbase", "wlen", "row", "ppos", "dpos", "lo_ptr", "lo_ent", "lo_pos", "up_ptr",
+NAMES = ("cwave", "wsteps", "row", "ppos", "dpos", "lo_ptr", "lo_ent", "lo_pos", "up_ptr",
          "up_ent", "up_pos")
 
 
@@ -34,8 +34,7 @@ def fetch_sweep(shim):
 
 def entry_colour(sw):
     """colour of every entry"""
-    ne = len(sw["row"])
-    wave = np.searchsorted(sw["wbase"], np.arange(ne), side="right") - 1
+    wave = np.arange(len(sw["row"])) // 64
     return np.searchsorted(sw["cwave"], wave, side="right") - 1
 
 

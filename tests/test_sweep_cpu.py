@@ -97,7 +97,7 @@ def _cases():
 
 
 @pytest.mark.parametrize("case", ["sim181147", "sim181147_failed", "C5_2x2"])
-@pytest.mark.parametrize("piece_len", [1, 16])
+@pytest.mark.parametrize("piece_len", [1, 16, 64])
 def test_plan_covers_every_coupling_once(shim, case, piece_len):
     name, xyz, e2n, top, bot, active = next(c for c in _cases() if c[0] == case)
     sw, ncol, K, b, _ = one_level_case(shim, xyz, e2n, top, bot, active, 2, piece_len)
@@ -110,10 +110,10 @@ def test_plan_covers_every_coupling_once(shim, case, piece_len):
     ent[row[valid]] = np.nonzero(valid)[0]
     colour = sweep_ref.entry_colour(sw)
     assert colour.max() + 1 == ncol <= 32
-    # wave layout: steps past a piece's end are padding at the END of a lane
-    for w in range(len(sw["wlen"])):
-        r = row[sw["wbase"][w]:sw["wbase"][w + 1]].reshape(sw["wlen"][w], 64)
-        assert np.all(np.diff((r >= 0).astype(int), axis=0) <= 0)
+    # wave layout: pieces packed from lane 0, padding only at a wave's end
+    r = row.reshape(-1, 64)
+    assert np.all(np.diff((r >= 0).astype(int), axis=1) <= 0)
+    assert len(sw["wsteps"]) == len(r)
     pos_row = lambda q: 64 * np.searchsorted(sptr, q // 64, side="right") - 64 + q % 64  # noqa: E731
     for i in range(n):
         e = ent[i]
@@ -123,13 +123,11 @@ def test_plan_covers_every_coupling_once(shim, case, piece_len):
         nb = {int(col[q]): int(q) for q in qs[1:] if col[q] >= 0 and col[q] != i}
         assert sw["dpos"][e] == base and col[base] == i
         got = {}
-        if sw["ppos"][e] >= 0:   # predecessor: the entry one step back in the lane
-            assert row[e - 64] >= 0
-            got[int(row[e - 64])] = int(sw["ppos"][e])
-        w = np.searchsorted(sw["wbase"], e, side="right") - 1
-        if e + 64 < sw["wbase"][w + 1] and row[e + 64] >= 0:
-            assert sw["ppos"][e + 64] >= 0      # successor: the next step of the lane
-            got[int(row[e + 64])] = -1
+        if sw["ppos"][e] >= 0:   # predecessor: the previous lane of the wave
+            assert e % 64 > 0 and row[e - 1] >= 0
+            got[int(row[e - 1])] = int(sw["ppos"][e])
+        if e % 64 < 63 and row[e + 1] >= 0 and sw["ppos"][e + 1] >= 0:
+            got[int(row[e + 1])] = -1        # successor: its block is the successor's ppos
         for lst, cmp in (("lo", np.less), ("up", np.greater)):
             a, z = sw[lst + "_ptr"][e], sw[lst + "_ptr"][e + 1]
             for t in range(a, z):
@@ -146,6 +144,13 @@ def test_plan_covers_every_coupling_once(shim, case, piece_len):
     # colour order; pieces of one row each make a point colouring
     if piece_len == 1:
         assert np.all(sw["ppos"] < 0)
+    # scan steps cover every piece: ⌈log₂ length⌉ of the wave's longest
+    starts = (row >= 0) & (sw["ppos"] < 0)
+    pid = np.cumsum(starts) - 1
+    lens = np.bincount(pid[row >= 0])
+    wave_of = np.nonzero(starts)[0] // 64
+    for wv, L in zip(wave_of, lens):
+        assert (1 << sw["wsteps"][wv]) >= L
 
 
 @pytest.mark.parametrize("case", ["sim181147", "C5_2x2"])
@@ -153,7 +158,7 @@ def test_icc_order_as_strong_as_natural(shim, case):
     """IC(0) / SSOR in the plan's order against the natural order (PETSc's),
     block Jacobi and point Jacobi, PCG to rtol 1e-8 on the same system."""
     name, xyz, e2n, top, bot, active = next(c for c in _cases() if c[0] == case)
-    sw, ncol, K, b, nodes0 = one_level_case(shim, xyz, e2n, top, bot, active, 2)
+    sw, ncol, K, b, nodes0 = one_level_case(shim, xyz, e2n, top, bot, active, 2, 64)
     order = sweep_ref.elimination_order(sw)
     p = sweep_ref.block_perm(order, 2)
     Kp, bp = K[p][:, p].tocsr(), b[p]

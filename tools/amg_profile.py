@@ -21,9 +21,10 @@ def main():
     ap.add_argument("--config", default="C3_1M")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--set", nargs="*", default=[], help="engine options name=value (mfea_set_option)")
+    ap.add_argument("--precond", default="gamg", choices=["gamg", "icc", "sor"])
     a = ap.parse_args()
     import fea_solver as fs
-    from mfea import PC_GAMG, Engine, make_opts, synth
+    from mfea import PC_GAMG, PC_ICC, PC_SOR, Engine, make_opts, synth
     from mfea.synth import CONFIGS
     nx, ny = CONFIGS[a.config]
     xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
@@ -37,10 +38,11 @@ def main():
     eng.set_bc(top, bot)
     eng.set_active(None)
     dy = fs.DISPLACEMENT_MAX * 20 / (fs.N_STEPS - 1)
-    _, _, st = eng.step(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG), fs.MAX_STRAIN)
-    ms = eng.profile_iteration(PC_GAMG, reps=a.reps)
+    pc = {"gamg": PC_GAMG, "icc": PC_ICC, "sor": PC_SOR}[a.precond]
+    _, _, st = eng.step(dy, -dy, make_opts(rtol=1e-8, max_it=200000, precond=pc), fs.MAX_STRAIN)
+    ms = eng.profile_iteration(pc, reps=a.reps)
     print(json.dumps({"config": a.config, "reps": a.reps, "iter_us_hip_events": ms * 1e3,
-                      "cg_iters": st.iters, "amg": eng.amg_info()}))
+                      "precond": a.precond, "cg_iters": st.iters, "amg": eng.amg_info()}))
     eng.close()
 
 

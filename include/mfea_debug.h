@@ -41,7 +41,6 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *   "part_slack_pct" n   partition boundaries move ≤ n % of a strip to the
  *                        fewest crossing elements (35; 0 = equal free-node counts)
  *   "amg_max_levels" 1..32  GAMG: hierarchy depth cap (32)
- *   "amg_w_block" 0|256..1024  GAMG: threads per block of w = A u (0: by size)
  *   "amg_dist" -1|0|1    partitioned GAMG: block Jacobi over per-partition hierarchies (0),
  *                        the distributed V-cycle of one global hierarchy (1), or per
  *                        active set whichever of the two solved faster (-1)
@@ -50,11 +49,20 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  *                        masked (1), or rebuild it for every new active set (0)
  *   "amg_rebuild_pct" n  GAMG: a kept hierarchy is rebuilt once a solve needs more than
  *                        n % of the iterations it took on its own set (150)
- *   "amg_x1_rows" n      GAMG setup: levels of ≤ n rows launched on one XCD (2048)
  *   "amg_coarse_rho_ppm" n  GAMG: ρ̂ of the levels below 0, ppm (1750000: ω = 0.76, level 0
  *                        then at its exact ρ̂ = 2); 0: the Gershgorin rule max(2, g / 1.45)
  *                        everywhere.  A solve failing with it falls back to 0 for the
  *                        handle's lifetime (read-only "amg_safe_omega" = 1)
+ *   "amg_cycle" 0|1      GAMG: four-step V(1,1) levels (0) or the compact two-sweep form (1)
+ *   "amg_collapse" -1|0|k  compact cycle: collapse the levels below k into one operator
+ *                        (-1: the highest level whose operator fits the budget below; 0 off)
+ *   "amg_collapse_mb" n, "amg_collapse_pairs" n  that budget: MB of blocks (32), product pairs (8e6)
+ *   "amg_spatial" -1|0|1 GAMG labels in Z-order: by locality (-1), off, on
+ *   "amg_up_lanes" 0|1|2|4  compact up sweep: lanes per P̃ row (0: by width)
+ *   "amg_fuse_setup" 0|1 GAMG numeric setup: compact operators in the Galerkin launches (1)
+ *   "amg_theta_ppm" n    GAMG strength threshold θ in ppm (PETSc -pc_gamg_threshold; 0)
+ *   "sweep_piece" 1..64  SOR / ICC: rows per chain piece at most (64; sweep.hip)
+ * Read-only: "sweep_colors", "sweep_pieces" (the last SOR / ICC plan).
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 

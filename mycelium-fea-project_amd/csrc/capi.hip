@@ -203,8 +203,11 @@ struct mfea_handle {
   int graph_chunk = 0, graph_precond = -1, graph_ell = -1;
   hipGraphExec_t graph_big = nullptr;  // GAMG: the planned batch's long chunks
   int graph_big_chunk = 0, graph_big_ell = -1;
-  hipGraphExec_t graph_rem = nullptr;  // GAMG: the planned batch's remainder, its exact length
-  int graph_rem_chunk = 0, graph_rem_ell = -1;
+  // GAMG: the planned batch's remainder at its exact length, one graph per
+  // length (the expected count moves between solves: failures, rebuilds)
+  static constexpr int kRemGraphs = 64;
+  hipGraphExec_t graph_rem[kRemGraphs] = {};
+  int graph_rem_ell = -1;
   // GAMG: the numeric setup's launches (≈ 30) as one graph, keyed by a hash
   // of every argument they take (the level views, the level-0 operator, reg)
   hipGraphExec_t graph_setup = nullptr;
@@ -320,9 +323,10 @@ void destroy_graph(mfea_handle* h) {
   h->graph_big = nullptr;
   h->graph_big_chunk = 0;
   h->graph_big_ell = -1;
-  if (h->graph_rem) (void)hipGraphExecDestroy(h->graph_rem);
-  h->graph_rem = nullptr;
-  h->graph_rem_chunk = 0;
+  for (auto& g : h->graph_rem) {
+    if (g) (void)hipGraphExecDestroy(g);
+    g = nullptr;
+  }
   h->graph_rem_ell = -1;
   h->graph = nullptr;
   h->graph_chunk = 0;
@@ -1879,17 +1883,18 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     // extra chunk boundaries (C3 at 15 iterations: 8 + 7 instead of 8 + 4×2)
     const int need = std::max(1, expected + 1);
     const int rem = big > chunk ? need - (need / big) * big : 0;
-    const bool exact_rem = rem > 0 && rem != chunk;
-    if (exact_rem && (h->graph_rem == nullptr || h->graph_rem_chunk != rem || h->graph_rem_ell != tag)) {
-      if (h->graph_rem) (void)hipGraphExecDestroy(h->graph_rem);
-      h->graph_rem = nullptr;
-      RC(capture(&h->graph_rem, rem));
-      h->graph_rem_chunk = rem;
+    const bool exact_rem = rem > 0 && rem != chunk && rem < mfea_handle::kRemGraphs;
+    if (h->graph_rem_ell != tag) {  // another plan: the cached lengths hold its pointers
+      for (auto& g : h->graph_rem) {
+        if (g) (void)hipGraphExecDestroy(g);
+        g = nullptr;
+      }
       h->graph_rem_ell = tag;
     }
+    if (exact_rem && h->graph_rem[rem] == nullptr) RC(capture(&h->graph_rem[rem], rem));
     rc = drive_sized(h, big, chunk, o->max_it, expected,
                      [&](int n) -> int {
-                       HIPC(hipGraphLaunch(n == chunk ? h->graph : n == big ? h->graph_big : h->graph_rem, s));
+                       HIPC(hipGraphLaunch(n == chunk ? h->graph : n == big ? h->graph_big : h->graph_rem[n], s));
                        return 0;
                      },
                      &fin, finish, exact_rem);
@@ -3343,18 +3348,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_max_levels = (int)value;
     rebuild = true;
   }
-  else if (n == "amg_w_k") {
-    if (value < 0 || value > 2) return fail(MFEA_EINVAL, "amg_w_k: 0 (auto), 1 or 2");
-    h->opt_amg_w_k = (int)value;
-    rebuild = true;
-  }
-  else if (n == "amg_w_block") {
-    if (value != 0 && value != 256 && value != 512 && value != 576 && value != 640 && value != 704 &&
-        value != 768 && value != 1024)
-      return fail(MFEA_EINVAL, "amg_w_block: 0 (auto), 256, 512, 576, 640, 704, 768 or 1024");
-    h->opt_amg_w_block = (int)value;
-    for (auto& pp : h->parts) pp->amg_cg.w_block = (int)value;
-  }
   else if (n == "amg_restrict_lanes") {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
       return fail(MFEA_EINVAL, "amg_restrict_lanes: 0 (by width), 1, 2, 4, 8 or 16 (16: the compact down sweep)");
@@ -3389,11 +3382,6 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_spatial = (int)value;
     rebuild = true;
   }
-  else if (n == "amg_x1_rows") {
-    if (value < 0) return fail(MFEA_EINVAL, "amg_x1_rows: >= 0");
-    h->opt_amg_x1_rows = value;
-    rebuild = true;
-  }
   else if (n == "amg_up_lanes") {
     if (value != 0 && value != 1 && value != 2 && value != 4)
       return fail(MFEA_EINVAL, "amg_up_lanes: 0 (by width), 1, 2 or 4");
@@ -3408,12 +3396,8 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->amg_safe_omega = false;
     rebuild = true;
   }
-  else if (n == "amg_big_chunk") {
-    if (value < 2 || value > 64) return fail(MFEA_EINVAL, "amg_big_chunk: 2..64");
-    h->opt_amg_big_chunk = (int)value;
-  }
   else if (n == "sweep_piece") {
-    if (value < 1 || value > 1024) return fail(MFEA_EINVAL, "sweep_piece: 1..1024");
+    if (value < 1 || value > 64) return fail(MFEA_EINVAL, "sweep_piece: 1..64");
     h->opt_sweep_piece = (int)value;
     rebuild = true;
   }
@@ -3603,15 +3587,12 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "ell_compact") *value = h->opt_ell_compact;
   else if (n == "amg_tail_rows") *value = h->opt_amg_tail_rows;
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
-  else if (n == "amg_w_block") *value = h->opt_amg_w_block;
-  else if (n == "amg_w_k") *value = h->opt_amg_w_k;
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;
   else if (n == "amg_theta_ppm") *value = h->opt_amg_theta_ppm;
   else if (n == "amg_fuse_setup") *value = h->opt_amg_fuse_setup;
-  else if (n == "amg_big_chunk") *value = h->opt_amg_big_chunk;
   else if (n == "sweep_piece") *value = h->opt_sweep_piece;
   else if (n == "sweep_colors") *value = part0(h).sweep.colors;  // read-only
   else if (n == "sweep_pieces") *value = part0(h).sweep.n_pieces;  // read-only
@@ -3637,7 +3618,6 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "dist_timeout_ms") *value = (int64_t)std::llround(h->dist_timeout_s * 1e3);
   else if (n == "amg_dist") *value = h->opt_amg_dist;
   else if (n == "amg_reuse") *value = h->opt_amg_reuse;
-  else if (n == "amg_x1_rows") *value = h->opt_amg_x1_rows;
   else if (n == "amg_rebuild_pct") *value = h->opt_amg_rebuild_pct;
   else if (n == "amg_reused") *value = part0(h).amg_reused ? 1 : 0;  // read-only: the last solve kept a hierarchy built for another set
   else if (n == "amg_build_iters") *value = part0(h).amg_build_iters;  // read-only

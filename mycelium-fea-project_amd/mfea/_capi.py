@@ -15,12 +15,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # mfea_set_option defaults (include/mfea_debug.h)
 DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
-                   "amg_max_levels": 32, "amg_w_block": 0, "amg_w_k": 0, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
+                   "amg_max_levels": 32, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
                    "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,
-                   "amg_rep_rows": 32768, "amg_cycle": 1, "amg_fuse_setup": 1, "amg_big_chunk": 8,
+                   "amg_rep_rows": 32768, "amg_cycle": 1, "amg_fuse_setup": 1,
                    "amg_up_lanes": 0, "amg_spatial": -1, "amg_collapse": -1, "amg_collapse_mb": 32,
                    "amg_collapse_pairs": 8000000, "amg_theta_ppm": 0, "amg_reuse": 1, "amg_rebuild_pct": 150,
-                   "amg_x1_rows": 2048, "amg_coarse_rho_ppm": 1750000}
+                   "amg_coarse_rho_ppm": 1750000, "sweep_piece": 64}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))

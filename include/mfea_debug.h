@@ -23,6 +23,12 @@ int mfea_debug_trace_iteration(mfea_handle* h, int precond, uint64_t* out, int64
  * multi-GPU path on one GPU).  axis as mfea_set_partition_axis. */
 int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
 
+/* The host's global element activity (E bytes, original order) as the
+ * partitioned GAMG plan reads it (capi.hip global_active: kept current by
+ * mfea_set_active and the failed-element ids each post exchanges; a rebuild
+ * gathers it afresh).  One partition: the device activity. */
+int mfea_debug_global_active(mfea_handle* h, uint8_t* out);
+
 /* Tuning options of a handle (experiments and tests; the defaults are the
  * measured best; the library reads no environment variables).  Names:
  *   "graph" 0|1          single-partition CG chunks as hipGraph replays (1)

@@ -91,6 +91,8 @@ struct Part {
   DevBuf<double> cg_part;                            // CG-CG block partials, 2 parities
   DevBuf<int32_t> slice_ptr, row_len, s_col, s_elem, e2n_d;
   DevBuf<uint8_t> active, code, elem_own;
+  DevBuf<int32_t> fail_list;  // partitioned: owned elements failed in the last post (any order)
+  DevBuf<unsigned> fail_cnt;
   DevBuf<unsigned> tickets;
   // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
   Ell L;
@@ -275,6 +277,12 @@ struct mfea_handle {
   std::vector<int32_t> gowner;
   AmgPlan gamg;
   std::vector<uint8_t> gamg_key;  // the global activity gamg was built for
+  // partitioned: the global element activity on the host, exact at act_gen
+  // gkey_gen (set by mfea_set_active, moved by the failed-element ids every
+  // post exchanges — global_active)
+  std::vector<uint8_t> gkey;
+  int64_t gkey_gen = -1;
+  DevBuf<int32_t> gfail;  // RCCL: failed-id all-gather buffers
   bool gamg_ok = false;
   int64_t gamg_gen = 0;       // bumped on every upload (captured graphs hold its pointers)
   int64_t gamg_plan_gen = 0;  // bumped on every host rebuild (a new active set)
@@ -515,6 +523,8 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(up(pt.xrecv_rows.ptr, rr.data(), nr * sizeof(int32_t)));
     HIPC(pt.elem_own.alloc(E));
     HIPC(up(pt.elem_own.ptr, pl.elem_own.data(), E));
+    HIPC(pt.fail_list.alloc(std::max<int64_t>(E, 1)));
+    HIPC(pt.fail_cnt.alloc(1));
   }
   HIPC(hipStreamSynchronize(s));
   return 0;
@@ -526,6 +536,7 @@ int ensure_built(mfea_handle* h) {
   if (!h->dirty) return 0;
   destroy_graph(h);
   h->assembled = false;
+  h->gkey_gen = -1;
   const bool dm = h->world > 1 || h->nparts > 1;
   const int np = h->world > 1 ? 1 : h->nparts;
   const bool skip = (h->mesh_flags & MFEA_MESH_SKIP_INVALID) != 0;
@@ -1939,6 +1950,10 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
 // each partition's own elements; RCCL: a max-all-reduce of E bytes (a rank
 // contributes the elements it reports, 0 elsewhere).
 int global_active(mfea_handle* h, std::vector<uint8_t>& key) {
+  if (h->gkey_gen == h->act_gen && (int64_t)h->gkey.size() == h->Ecount) {
+    key = h->gkey;  // kept current by mfea_set_active and the failed-id exchange
+    return 0;
+  }
   key.assign(h->Ecount, 0);
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -1955,6 +1970,8 @@ int global_active(mfea_handle* h, std::vector<uint8_t>& key) {
     HIPC(hipMemcpyAsync(key.data(), h->gact.ptr, h->Ecount, hipMemcpyDeviceToHost, h->stream));
     RC(sync_stream(h));
   }
+  h->gkey = key;
+  h->gkey_gen = h->act_gen;
   return 0;
 }
 
@@ -2568,6 +2585,56 @@ int assemble_impl(mfea_handle* h, mfea_stats* st) {
   return 0;
 }
 
+// Partitioned: the owned elements that failed in the last post (every
+// partition's device list), as global ids, gathered from every rank, cleared
+// in the host's global activity.  Over RCCL two all-gathers — the counts,
+// then the lists padded to the longest — instead of the E-byte max-reduction
+// of the whole activity (C5: 7 MB per failure step per rank).
+int apply_failures(mfea_handle* h) {
+  std::vector<int32_t> ids;
+  for (auto& pp : h->parts) {
+    Part& pt = *pp;
+    unsigned c = 0;
+    HIPC(hipMemcpy(&c, pt.fail_cnt.ptr, sizeof c, hipMemcpyDeviceToHost));
+    if (c > (unsigned)pt.P.n_elems) return fail(MFEA_EINVAL, "internal: failed-element list overflow");
+    std::vector<int32_t> l(c);
+    if (c) HIPC(hipMemcpy(l.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (int32_t le : l) ids.push_back((int32_t)pt.plan.elem_g[le]);
+  }
+  if (h->world > 1) {
+    hipStream_t s = h->stream;
+    const int W = h->world;
+    HIPC(h->gfail.alloc(2 * (size_t)W));
+    int32_t n = (int32_t)ids.size();
+    HIPC(hipMemcpyAsync(h->gfail.ptr + h->rank, &n, sizeof n, hipMemcpyHostToDevice, s));
+    NCCLC(ncclAllGather(h->gfail.ptr + h->rank, h->gfail.ptr + W, 1, ncclInt32, h->comm, s));
+    std::vector<int32_t> cnt(W);
+    HIPC(hipMemcpyAsync(cnt.data(), h->gfail.ptr + W, W * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    RC(sync_stream(h));
+    const int32_t mx = *std::max_element(cnt.begin(), cnt.end());
+    if (mx > 0) {
+      HIPC(h->gfail.alloc((size_t)(W + 1) * mx));
+      std::vector<int32_t> mine(mx, -1);
+      std::copy(ids.begin(), ids.end(), mine.begin());
+      HIPC(hipMemcpyAsync(h->gfail.ptr, mine.data(), mx * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      NCCLC(ncclAllGather(h->gfail.ptr, h->gfail.ptr + mx, (size_t)mx, ncclInt32, h->comm, s));
+      std::vector<int32_t> all((size_t)W * mx);
+      HIPC(hipMemcpyAsync(all.data(), h->gfail.ptr + mx, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      RC(sync_stream(h));
+      ids.clear();
+      for (int r = 0; r < W; ++r)
+        for (int32_t k = 0; k < cnt[r]; ++k) ids.push_back(all[(size_t)r * mx + k]);
+    } else {
+      ids.clear();
+    }
+  }
+  for (int32_t g : ids) {
+    if (g < 0 || g >= h->Ecount) return fail(MFEA_EINVAL, "internal: failed element id out of range");
+    h->gkey[g] = 0;
+  }
+  return 0;
+}
+
 int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
               mfea_stats* st) {
   hipStream_t s = h->stream;
@@ -2579,9 +2646,11 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
     launch_reaction(s, P.n_free, P.n_top, P.n_nodes, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr,
                     pt.val.ptr, pt.diag.ptr, pt.G, pt.x.ptr, pt.partials.ptr, tix(pt, 3),
                     pt.red.ptr + 4);
+    if (dm) HIPC(hipMemsetAsync(pt.fail_cnt.ptr, 0, sizeof(unsigned), s));
     launch_stress(s, P.n_elems, pt.e2n_d.ptr, pt.xyz_d.ptr, pt.x.ptr, h->mat, max_strain,
                   pt.active.ptr, pt.stress.ptr, pt.partials.ptr, tix(pt, 4), pt.red.ptr + 5,
-                  dm ? pt.elem_own.ptr : nullptr);
+                  dm ? pt.elem_own.ptr : nullptr, dm ? pt.fail_list.ptr : nullptr,
+                  dm ? pt.fail_cnt.ptr : nullptr);
   }
   HIPC(hipGetLastError());
   Part& p0 = part0(h);
@@ -2597,7 +2666,14 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
-  if ((int64_t)h->h_red[1] != h->n_active) ++h->act_gen;  // elements only ever fail here
+  if ((int64_t)h->h_red[1] != h->n_active) {  // elements only ever fail here
+    // every rank sees the same global count, so every rank exchanges
+    if (dm && h->gkey_gen == h->act_gen) {
+      RC(apply_failures(h));
+      h->gkey_gen = h->act_gen + 1;
+    }
+    ++h->act_gen;
+  }
   if ((int64_t)h->h_red[1] < h->Ecount) h->act_all = false;
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
@@ -2831,6 +2907,12 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   if (!active && h->act_all) return 0;
   ++h->act_gen;
   h->act_all = !active;
+  if (partitioned(h)) {  // the global activity is known here: no exchange needed for it
+    h->gkey.assign(h->Ecount, 1);
+    if (active)
+      for (int64_t e = 0; e < h->Ecount; ++e) h->gkey[e] = active[e] ? 1 : 0;
+    h->gkey_gen = h->act_gen;
+  }
   if (h->Ecount == 0) return 0;
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -3625,6 +3707,17 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);
+  return 0;
+}
+
+int mfea_debug_global_active(mfea_handle* h, uint8_t* out) {
+  if (!h || !out) return fail(MFEA_EINVAL, "bad argument");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  std::vector<uint8_t> key;
+  if (partitioned(h)) RC(global_active(h, key));
+  else RC(gather_active(h, key));
+  std::copy(key.begin(), key.end(), out);
   return 0;
 }
 

@@ -410,12 +410,14 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
                                                    double max_strain, uint8_t* __restrict__ active,
                                                    double* __restrict__ stress, double* partials,
                                                    unsigned* ticket, double* red_out,
-                                                   const uint8_t* __restrict__ owned) {
+                                                   const uint8_t* __restrict__ owned,
+                                                   int32_t* __restrict__ fail_list, unsigned* fail_cnt) {
   const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double cnt[1] = {0.0};
   if (e < E) {
     const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    uint8_t act = active[e];
+    const uint8_t act0 = active[e];
+    uint8_t act = act0;
     double sg = 0.0;
     if (act && a >= 0) {
       const double vx = xyz[3 * b] - xyz[3 * a], vy = xyz[3 * b + 1] - xyz[3 * a + 1],
@@ -433,6 +435,10 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
     }
     stress[e] = sg;
     cnt[0] = (act && (!owned || owned[e])) ? 1.0 : 0.0;
+    // partitioned: an owned element failing now joins this rank's list (any
+    // order; the host sorts it) — the global activity then moves by these ids
+    // instead of an E-byte reduction (capi.hip post_impl)
+    if (fail_list && act0 && !act && owned[e]) fail_list[atomicAdd(fail_cnt, 1u)] = (int32_t)e;
   }
   block_publish<1>(cnt, partials, ticket, red_out);
 }
@@ -584,9 +590,9 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
                    double* stress, double* partials, unsigned* ticket, double* red_out,
-                   const uint8_t* owned) {
+                   const uint8_t* owned, int32_t* fail_list, unsigned* fail_cnt) {
   hipLaunchKernelGGL(k_stress, MFEA_GRID(grid_rows(E > 0 ? E : 1)), E, e2n, xyz, u, m, max_strain,
-                     active, stress, partials, ticket, red_out, owned);
+                     active, stress, partials, ticket, red_out, owned, fail_list, fail_cnt);
 }
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,

@@ -115,7 +115,7 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
                    double* stress, double* partials, unsigned* ticket, double* red_out,
-                   const uint8_t* owned = nullptr);
+                   const uint8_t* owned = nullptr, int32_t* fail_list = nullptr, unsigned* fail_cnt = nullptr);
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,
                               Material m, double* Ke, double* L);

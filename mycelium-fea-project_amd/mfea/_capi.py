@@ -124,6 +124,7 @@ _sig = {
     # include/mfea_debug.h
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
+    "mfea_debug_global_active": (C.c_int, [_P, C.c_void_p]),
     "mfea_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "mfea_get_option": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
     "mfea_debug_amg_vcycle": (C.c_int, [_P, _P, _P]),
@@ -314,6 +315,13 @@ class Engine:
 
     def set_partition_axis(self, axis: int = -1):
         _check(_lib.mfea_set_partition_axis(self._h, int(axis)))
+
+    def global_active(self) -> np.ndarray:
+        """The host's global element activity the partitioned plan reads
+        (mfea_debug_global_active)."""
+        out = np.zeros(self.n_elems, np.uint8)
+        _check(_lib.mfea_debug_global_active(self._h, out.ctypes.data_as(C.c_void_p)))
+        return out.astype(bool)
 
     def set_parts(self, nparts: int, axis: int = -1):
         """nparts partitions of the multi-GPU solve held by this handle on one

@@ -232,6 +232,28 @@ def test_partitioned_gamg_step_with_failures(peng):
     assert n_act < len(e2n)
 
 
+def test_partitioned_global_activity_follows_failures(peng):
+    """The global activity the partitioned GAMG plan reads moves by the
+    failed-element ids each post exchanges (no E-byte reduction): after steps
+    with failures and no mfea_set_active in between it equals the gathered
+    device activity, and the solves still match the direct solve."""
+    from mfea import PC_GAMG, make_opts
+    xyz, e2n, top, bot = _sim181147(peng, 4)
+    peng.set_active(None)
+    active = np.ones(len(e2n), bool)
+    seen_failures = False
+    for step in (20, 30, 39):
+        dy = fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+        f, n_act, st = peng.step(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG), fo.MAX_STRAIN)
+        K = fo.assemble_global_stiffness(xyz, e2n, active)
+        known, vals = fo.known_dof_map(top, bot, dy, -dy)
+        assert rel(peng.displacement(), fo.solve_system(K, known, vals)) <= 1e-10, step
+        active = peng.active()
+        seen_failures |= n_act < len(e2n)
+        assert np.array_equal(peng.global_active(), active), step
+    assert seen_failures
+
+
 def test_partitioned_solve_deterministic(peng):
     from mfea import make_opts
     _sim181147(peng, 3)

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <numeric>
+#include <thread>
 
 #include "amg.hpp"
 
@@ -100,6 +101,109 @@ int64_t aggregate(const Csr& A, std::vector<int32_t>& agg, const std::vector<uin
   return na;
 }
 
+// ---- host threads: the symbolic phase's row loops run over contiguous
+// chunks of rows on up to kBuildThreads threads; every output is assembled in
+// row order, so the plan is the same bits for any thread count (C5's build
+// was 4.9 s on one thread).
+constexpr int kBuildThreads = 16;
+constexpr int64_t kChunkRows = 8192;
+
+int build_threads() {
+  const unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min<unsigned>(h ? h : 1, kBuildThreads));
+}
+
+// chunk boundaries of [0, n): T + 1 values
+std::vector<int64_t> chunks(int64_t n) {
+  const int64_t T = std::max<int64_t>(1, std::min<int64_t>(build_threads(), (n + kChunkRows - 1) / kChunkRows));
+  std::vector<int64_t> b(T + 1);
+  for (int64_t t = 0; t <= T; ++t) b[t] = n * t / T;
+  return b;
+}
+
+// f(lo, hi, t) over the chunks of [0, n), one thread each
+template <class F>
+void par_for(int64_t n, F&& f) {
+  const std::vector<int64_t> b = chunks(n);
+  const int T = (int)b.size() - 1;
+  if (T == 1) {
+    f(b[0], b[1], 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; ++t) th.emplace_back([&, t] { f(b[t], b[t + 1], t); });
+  f(b[0], b[1], 0);
+  for (auto& x : th) x.join();
+}
+
+// One chunk's rows of a CSR with per-entry item lists (P + pv, A·P + ap,
+// A_{l+1} + ac, A_0 + a0): entry(c) opens an entry of the current row,
+// item(a[, b]) appends to the last entry's list.
+struct RowSink {
+  std::vector<int64_t> rlen;
+  std::vector<int32_t> col, icnt, a, b;
+  void begin_row() { rlen.push_back(0); }
+  void entry(int32_t c) {
+    col.push_back(c);
+    icnt.push_back(0);
+    ++rlen.back();
+  }
+  void item(int32_t x) {
+    a.push_back(x);
+    ++icnt.back();
+  }
+  void item(int32_t x, int32_t y) {
+    a.push_back(x);
+    b.push_back(y);
+    ++icnt.back();
+  }
+};
+
+// M (n rows) and its lists from emit(i, sink) per row, rows in parallel
+// chunks, merged in row order
+template <class Emit>
+void produce_rows(int64_t n, Csr& M, Lists& Ls, bool pair, Emit&& emit) {
+  const std::vector<int64_t> b = chunks(n);
+  const int T = (int)b.size() - 1;
+  std::vector<RowSink> sk(T);
+  par_for(n, [&](int64_t lo, int64_t hi, int t) {
+    RowSink& s = sk[t];
+    s.rlen.reserve(hi - lo);
+    for (int64_t i = lo; i < hi; ++i) {
+      s.begin_row();
+      emit(i, s);
+    }
+  });
+  std::vector<int64_t> eoff(T + 1, 0), ioff(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    eoff[t + 1] = eoff[t] + (int64_t)sk[t].col.size();
+    ioff[t + 1] = ioff[t] + (int64_t)sk[t].a.size();
+  }
+  M.n = n;
+  M.ptr.assign(n + 1, 0);
+  M.col.resize(eoff[T]);
+  Ls.ptr.assign(eoff[T] + 1, 0);
+  Ls.a.resize(ioff[T]);
+  Ls.b.resize(pair ? ioff[T] : 0);
+  par_for(n, [&](int64_t lo, int64_t hi, int t) {
+    const RowSink& s = sk[t];
+    int64_t e = eoff[t];
+    for (int64_t i = lo; i < hi; ++i) {
+      e += s.rlen[i - lo];
+      M.ptr[i + 1] = e;
+    }
+    std::copy(s.col.begin(), s.col.end(), M.col.begin() + eoff[t]);
+    int64_t q = ioff[t];
+    for (size_t k = 0; k < s.icnt.size(); ++k) {
+      q += s.icnt[k];
+      Ls.ptr[eoff[t] + (int64_t)k + 1] = q;
+    }
+    std::copy(s.a.begin(), s.a.end(), Ls.a.begin() + ioff[t]);
+    if (pair) std::copy(s.b.begin(), s.b.end(), Ls.b.begin() + ioff[t]);
+  });
+}
+
 std::string check32(int64_t v, const char* what) {
   return v > INT32_MAX ? std::string("AMG ") + what + " too large for int32 indices" : std::string();
 }
@@ -109,27 +213,19 @@ std::string coarsen(LevelCsr& L, Csr& An) {
   const Csr& A = L.A;
   const int64_t n = A.n, nc = L.nc;
   // ---- P: row i → the aggregates of {i} ∪ nbrs(i), ascending; value lists
-  {
-    std::vector<std::pair<int32_t, int32_t>> t;  // (aggregate, A entry)
-    for (int64_t i = 0; i < n; ++i) {
-      t.clear();
-      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
-        const int32_t a = L.agg[A.col[k]];
-        if (a >= 0) t.emplace_back(a, (int32_t)k);
-      }
-      row_stable_sort(t.begin(), t.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-      for (size_t k = 0; k < t.size(); ++k) {
-        if (k == 0 || t[k].first != t[k - 1].first) {
-          L.P.col.push_back(t[k].first);
-          L.pv.ptr.push_back(L.pv.ptr.back());
-        }
-        L.pv.a.push_back(t[k].second);
-        ++L.pv.ptr.back();
-      }
-      L.P.ptr.push_back((int64_t)L.P.col.size());
+  produce_rows(n, L.P, L.pv, false, [&](int64_t i, RowSink& s) {
+    thread_local std::vector<std::pair<int32_t, int32_t>> t;  // (aggregate, A entry)
+    t.clear();
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
+      const int32_t a = L.agg[A.col[k]];
+      if (a >= 0) t.emplace_back(a, (int32_t)k);
     }
-    L.P.n = n;
-  }
+    row_stable_sort(t.begin(), t.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (size_t k = 0; k < t.size(); ++k) {
+      if (k == 0 || t[k].first != t[k - 1].first) s.entry(t[k].first);
+      s.item(t[k].second);
+    }
+  });
   std::string err;
   if (!(err = check32((int64_t)L.P.col.size(), "prolongator")).empty()) return err;
   // ---- R = Pᵀ: coarse row J → (fine row i ascending, P entry)
@@ -151,9 +247,8 @@ std::string coarsen(LevelCsr& L, Csr& An) {
   // ---- AP = A·P: per row, (J, A entry, P entry) triples, stable-sorted by J
   {
     struct T3 { int32_t J, a, p; };
-    std::vector<T3> t;
-    L.AP.n = n;
-    for (int64_t i = 0; i < n; ++i) {
+    produce_rows(n, L.AP, L.ap, true, [&](int64_t i, RowSink& s) {
+      thread_local std::vector<T3> t;
       t.clear();
       for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
         const int64_t kk = A.col[k];
@@ -161,25 +256,18 @@ std::string coarsen(LevelCsr& L, Csr& An) {
       }
       row_stable_sort(t.begin(), t.end(), [](const T3& x, const T3& y) { return x.J < y.J; });
       for (size_t k = 0; k < t.size(); ++k) {
-        if (k == 0 || t[k].J != t[k - 1].J) {
-          L.AP.col.push_back(t[k].J);
-          L.ap.ptr.push_back(L.ap.ptr.back());
-        }
-        L.ap.a.push_back(t[k].a);
-        L.ap.b.push_back(t[k].p);
-        ++L.ap.ptr.back();
+        if (k == 0 || t[k].J != t[k - 1].J) s.entry(t[k].J);
+        s.item(t[k].a, t[k].p);
       }
-      L.AP.ptr.push_back((int64_t)L.AP.col.size());
-    }
+    });
   }
   if (!(err = check32((int64_t)L.AP.col.size(), "A·P")).empty()) return err;
   // ---- A_{l+1} = Pᵀ (AP): coarse row I over R row I, diagonal first
   {
     struct T3 { int32_t J, p, m; };
-    std::vector<T3> t;
     An = Csr();
-    An.n = nc;
-    for (int64_t I = 0; I < nc; ++I) {
+    produce_rows(nc, An, L.ac, true, [&](int64_t I, RowSink& s) {
+      thread_local std::vector<T3> t;
       t.clear();
       for (int64_t r = L.R.ptr[I]; r < L.R.ptr[I + 1]; ++r) {
         const int64_t i = L.R.col[r];
@@ -190,16 +278,10 @@ std::string coarsen(LevelCsr& L, Csr& An) {
         return dx != dy ? dx : x.J < y.J;
       });
       for (size_t k = 0; k < t.size(); ++k) {
-        if (k == 0 || t[k].J != t[k - 1].J) {
-          An.col.push_back(t[k].J);
-          L.ac.ptr.push_back(L.ac.ptr.back());
-        }
-        L.ac.a.push_back(t[k].p);
-        L.ac.b.push_back(t[k].m);
-        ++L.ac.ptr.back();
+        if (k == 0 || t[k].J != t[k - 1].J) s.entry(t[k].J);
+        s.item(t[k].p, t[k].m);
       }
-      An.ptr.push_back((int64_t)An.col.size());
-    }
+    });
   }
   return check32((int64_t)An.col.size(), "coarse operator");
 }
@@ -223,12 +305,15 @@ std::vector<int32_t> sort_perm(const std::vector<int64_t>& key, const std::vecto
     for (int64_t i = 0; i < n; ++i) seg[(*own)[i] + 1]++;
     for (int r = 0; r < world; ++r) seg[r + 1] += seg[r];
   }
+  std::vector<std::pair<int64_t, int64_t>> win;  // the sorting windows, independent
   for (size_t g = 0; g + 1 < seg.size(); ++g)
-    for (int64_t w0 = seg[g]; w0 < seg[g + 1]; w0 += kSortWindow) {
-      const int64_t w1 = std::min(seg[g + 1], w0 + kSortWindow);
-      std::stable_sort(order.begin() + w0, order.begin() + w1,
+    for (int64_t w0 = seg[g]; w0 < seg[g + 1]; w0 += kSortWindow) win.emplace_back(w0, std::min(seg[g + 1], w0 + kSortWindow));
+  par_for((int64_t)win.size() * kChunkRows / 16, [&](int64_t lo, int64_t hi, int) {
+    const int64_t a = lo * 16 / kChunkRows, b = hi * 16 / kChunkRows;
+    for (int64_t k = a; k < b && k < (int64_t)win.size(); ++k)
+      std::stable_sort(order.begin() + win[k].first, order.begin() + win[k].second,
                        [&](int32_t x, int32_t y) { return key[x] > key[y]; });
-    }
+  });
   for (int64_t k = 0; k < n; ++k) perm[order[k]] = (int32_t)k;
   if (bounds) *bounds = seg;
   return perm;
@@ -271,7 +356,9 @@ std::string layout(const Csr& M, const std::vector<int32_t>& rperm, const std::v
                    SellPat& S, std::vector<int32_t>& epos) {
   const int64_t n = M.n;
   std::vector<int32_t> inv(n);
-  for (int64_t r = 0; r < n; ++r) inv[rperm[r]] = (int32_t)r;
+  par_for(n, [&](int64_t lo, int64_t hi, int) {
+    for (int64_t r = lo; r < hi; ++r) inv[rperm[r]] = (int32_t)r;
+  });
   S = SellPat();
   S.n = n;
   const int64_t ns = (n + 63) / 64;
@@ -291,14 +378,16 @@ std::string layout(const Csr& M, const std::vector<int32_t>& rperm, const std::v
   }
   S.col.assign(slots * 64, -1);
   epos.assign(M.col.size(), -1);
-  for (int64_t r = 0; r < n; ++r) {
-    const int64_t o = inv[r];
-    for (int64_t k = M.ptr[o]; k < M.ptr[o + 1]; ++k) {
-      const int64_t q = S.pos(r, (int)(k - M.ptr[o]));
-      S.col[q] = cperm ? (*cperm)[M.col[k]] : M.col[k];
-      epos[k] = (int32_t)q;
+  par_for(n, [&](int64_t lo, int64_t hi, int) {  // every row writes its own positions
+    for (int64_t r = lo; r < hi; ++r) {
+      const int64_t o = inv[r];
+      for (int64_t k = M.ptr[o]; k < M.ptr[o + 1]; ++k) {
+        const int64_t q = S.pos(r, (int)(k - M.ptr[o]));
+        S.col[q] = cperm ? (*cperm)[M.col[k]] : M.col[k];
+        epos[k] = (int32_t)q;
+      }
     }
-  }
+  });
   return "";
 }
 
@@ -309,7 +398,9 @@ std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npo
   out = PosList();
   out.ptr.assign(npos + 1, 0);
   const int64_t ne = (int64_t)L.ptr.size() - 1;
-  for (int64_t e = 0; e < ne; ++e) out.ptr[epos[e] + 1] = (int32_t)(L.ptr[e + 1] - L.ptr[e]);
+  par_for(ne, [&](int64_t lo, int64_t hi, int) {
+    for (int64_t e = lo; e < hi; ++e) out.ptr[epos[e] + 1] = (int32_t)(L.ptr[e + 1] - L.ptr[e]);
+  });
   int64_t run = 0;
   for (int64_t q = 0; q < npos; ++q) {
     run += out.ptr[q + 1];
@@ -319,13 +410,15 @@ std::string to_pos(const Lists& L, const std::vector<int32_t>& epos, int64_t npo
   items += run;
   out.a.resize(run);
   if (pair) out.b.resize(run);
-  for (int64_t e = 0; e < ne; ++e) {
-    int64_t d = out.ptr[epos[e]];
-    for (int64_t t = L.ptr[e]; t < L.ptr[e + 1]; ++t, ++d) {
-      out.a[d] = ta ? (*ta)[L.a[t]] : L.a[t];
-      if (pair) out.b[d] = tb ? (*tb)[L.b[t]] : L.b[t];
+  par_for(ne, [&](int64_t lo, int64_t hi, int) {  // every entry fills its own position's list
+    for (int64_t e = lo; e < hi; ++e) {
+      int64_t d = out.ptr[epos[e]];
+      for (int64_t t = L.ptr[e]; t < L.ptr[e + 1]; ++t, ++d) {
+        out.a[d] = ta ? (*ta)[L.a[t]] : L.a[t];
+        if (pair) out.b[d] = tb ? (*tb)[L.b[t]] : L.b[t];
+      }
     }
-  }
+  });
   return "";
 }
 
@@ -380,35 +473,44 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   // slice) and Cuthill–McKee (C3 21 iterations instead of 16, C5 49 instead
   // of 43 — the greedy aggregation follows the row order — for no gain per
   // iteration).
-  {
+  auto level0_row = [&](int64_t i, RowSink& s, std::vector<double>* w) {
+    thread_local std::vector<std::pair<int32_t, int32_t>> nb;  // (neighbour, SELL position)
+    nb.clear();
+    const int64_t base = (int64_t)P.slice_ptr[i >> 6] * 64 + (i & 63);
+    for (int t = 0; t < P.row_len[i]; ++t) {
+      const int64_t pos = base + (int64_t)t * 64;
+      const int32_t j = P.s_col[pos], e = P.s_elem[pos];
+      if (j < 0 || j >= nf || e < 0 || !active[e]) continue;
+      nb.emplace_back(j, (int32_t)pos);
+    }
+    row_stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    s.entry((int32_t)i);
+    if (w) w->push_back(0.0);
+    for (size_t t = 0; t < nb.size(); ++t) {
+      if (t == 0 || nb[t].first != nb[t - 1].first) {
+        s.entry(nb[t].first);
+        if (w) w->push_back(0.0);
+      }
+      s.item(nb[t].second);
+      if (w) w->back() += enorm(i, nb[t].first);
+    }
+  };
+  if (!use_strength) {
+    produce_rows(nf, lv[0].A, a0, false, [&](int64_t i, RowSink& s) { level0_row(i, s, nullptr); });
+  } else {  // the strength weights in row order: one thread
+    RowSink s;
+    for (int64_t i = 0; i < nf; ++i) {
+      s.begin_row();
+      level0_row(i, s, &w_entry);
+    }
     Csr& A = lv[0].A;
     A.n = nf;
-    std::vector<std::pair<int32_t, int32_t>> nb;  // (neighbour, SELL position)
-    for (int64_t i = 0; i < nf; ++i) {
-      nb.clear();
-      const int64_t base = (int64_t)P.slice_ptr[i >> 6] * 64 + (i & 63);
-      for (int t = 0; t < P.row_len[i]; ++t) {
-        const int64_t pos = base + (int64_t)t * 64;
-        const int32_t j = P.s_col[pos], e = P.s_elem[pos];
-        if (j < 0 || j >= nf || e < 0 || !active[e]) continue;
-        nb.emplace_back(j, (int32_t)pos);
-      }
-      row_stable_sort(nb.begin(), nb.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-      A.col.push_back((int32_t)i);
-      a0.ptr.push_back(a0.ptr.back());
-      if (use_strength) w_entry.push_back(0.0);
-      for (size_t t = 0; t < nb.size(); ++t) {
-        if (t == 0 || nb[t].first != nb[t - 1].first) {
-          A.col.push_back(nb[t].first);
-          a0.ptr.push_back(a0.ptr.back());
-          if (use_strength) w_entry.push_back(0.0);
-        }
-        a0.a.push_back(nb[t].second);
-        ++a0.ptr.back();
-        if (use_strength) w_entry.back() += enorm(i, nb[t].first);
-      }
-      A.ptr.push_back((int64_t)A.col.size());
-    }
+    A.ptr.assign(nf + 1, 0);
+    for (int64_t i = 0; i < nf; ++i) A.ptr[i + 1] = A.ptr[i] + s.rlen[i];
+    A.col = std::move(s.col);
+    a0.ptr.assign(A.col.size() + 1, 0);
+    for (size_t k = 0; k < s.icnt.size(); ++k) a0.ptr[k + 1] = a0.ptr[k] + s.icnt[k];
+    a0.a = std::move(s.a);
   }
   // ---- coarsen until every row is isolated (the coarsest level is then
   // block diagonal and its block-Jacobi inverse is exact).  The aggregation
@@ -580,20 +682,23 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     // length: C3 level 0 fills 88 % of its positions, 48 % in the level's own
     // row order), pt_row naming each row's level row; R̃ = P̃ᵀ
     {
-      std::vector<int32_t> ePT, eRT;
-      if (!(err = layout(L.AP, pap, &perm[l + 1], out.PT, ePT)).empty()) return err;
+      std::vector<int32_t> eRT;
+      out.PT = out.AP;  // the same pattern and labels as A·P's layout
+      const std::vector<int32_t>& ePT = eAP;
       out.pt_row.assign(L.A.n, 0);
       for (int64_t i = 0; i < L.A.n; ++i) out.pt_row[pap[i]] = perm[l][i];
       out.pt_ap.assign(out.PT.n_pos(), -1);
       out.pt_p.assign(out.PT.n_pos(), -1);
-      for (int64_t i = 0; i < L.A.n; ++i) {  // both rows ascending in J: merge
-        int64_t k = L.P.ptr[i];
-        for (int64_t e = L.AP.ptr[i]; e < L.AP.ptr[i + 1]; ++e) {
-          out.pt_ap[ePT[e]] = eAP[e];
-          while (k < L.P.ptr[i + 1] && L.P.col[k] < L.AP.col[e]) ++k;
-          if (k < L.P.ptr[i + 1] && L.P.col[k] == L.AP.col[e]) out.pt_p[ePT[e]] = eP[k];
+      par_for(L.A.n, [&](int64_t lo, int64_t hi, int) {
+        for (int64_t i = lo; i < hi; ++i) {  // both rows ascending in J: merge
+          int64_t k = L.P.ptr[i];
+          for (int64_t e = L.AP.ptr[i]; e < L.AP.ptr[i + 1]; ++e) {
+            out.pt_ap[ePT[e]] = eAP[e];
+            while (k < L.P.ptr[i + 1] && L.P.col[k] < L.AP.col[e]) ++k;
+            if (k < L.P.ptr[i + 1] && L.P.col[k] == L.AP.col[e]) out.pt_p[ePT[e]] = eP[k];
+          }
         }
-      }
+      });
       Csr RT;  // transpose of A·P: coarse row J → fine rows ascending
       std::vector<int32_t> rt_e(L.AP.col.size());
       RT.n = L.nc;
@@ -621,12 +726,16 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       out.rt_row.assign(L.nc, 0);
       for (int64_t J = 0; J < L.nc; ++J) out.rt_row[prt[J]] = perm[l + 1][J];
       out.rt_pt.assign(out.RT.n_pos(), -1);
-      for (size_t t = 0; t < rt_e.size(); ++t) out.rt_pt[eRT[t]] = ePT[rt_e[t]];
+      par_for((int64_t)rt_e.size(), [&](int64_t lo, int64_t hi, int) {
+        for (int64_t t = lo; t < hi; ++t) out.rt_pt[eRT[t]] = ePT[rt_e[t]];
+      });
     }
     if (!(err = to_pos(L.pv, eP, out.P.n_pos(), &eA[l], nullptr, false, out.pv, plan.pair_items)).empty())
       return err;
     out.rp.assign(out.R.n_pos(), -1);
-    for (size_t e = 0; e < L.rp.size(); ++e) out.rp[eR[e]] = eP[L.rp[e]];
+    par_for((int64_t)L.rp.size(), [&](int64_t lo, int64_t hi, int) {
+      for (int64_t e = lo; e < hi; ++e) out.rp[eR[e]] = eP[L.rp[e]];
+    });
     if (!(err = to_pos(L.ap, eAP, out.AP.n_pos(), &eA[l], &eP, true, out.ap, plan.pair_items)).empty())
       return err;
     if (!(err = to_pos(L.ac, eA[l + 1], plan.lev[l + 1].A.n_pos(), &eP, &eAP, true, out.ac, plan.pair_items))

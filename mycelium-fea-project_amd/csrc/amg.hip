@@ -1528,13 +1528,21 @@ int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, L.ulanes, 8.0, 16.0)
 template <int ND>
 static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int S = amg_down_lanes(L);
-  const int64_t gc = rows_grid(S * L.RT.n).x;
-  const dim3 g((unsigned)(gc + rows_grid(L.A.n).x));
-  if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-  else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-  else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-  else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
-  else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  const int64_t gr = rows_grid(S * L.RT.n).x, ga = rows_grid(L.A.n).x;
+  auto go = [&](int64_t gc, int64_t blocks) {
+    const dim3 g((unsigned)blocks);
+    if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 8) hipLaunchKernelGGL((k_amg_down<ND, 8>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 4) hipLaunchKernelGGL((k_amg_down<ND, 4>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else if (S == 2) hipLaunchKernelGGL((k_amg_down<ND, 2>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+    else hipLaunchKernelGGL((k_amg_down<ND, 1>), g, dim3(kBlock), 0, s, L, N, gc, gate);
+  };
+  if (L.dsplit) {  // R̂ rows, then Ã rows (experiment: each row set's own time)
+    go(gr, gr);
+    go(0, ga);
+  } else {
+    go(gr, gr + ga);
+  }
 }
 template <int ND, class TE>
 static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, const int32_t* gate) {

@@ -65,6 +65,7 @@ struct AmgLevD {
   float* e = nullptr;
   int coarsest = 0;
   int rlanes = 0;  // restriction lanes per coarse row (0: by R's mean width)
+  int dsplit = 0;  // compact down sweep: its two row sets as two launches
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)

@@ -241,6 +241,7 @@ struct mfea_handle {
   int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
   int opt_amg_w_k = 0;         // GAMG: w = A u step width (0: by level 0's mean slice width, 1, 2)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
+  int opt_amg_down_split = 0;  // GAMG compact down sweep: R̂ and Ã rows as two launches (experiment)
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
   int opt_amg_collapse = -1;           // GAMG: collapse the compact cycle below the highest level
@@ -1304,6 +1305,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.e = l ? F((size_t)nd * n) : nullptr;  // level 0 writes the CG's u
       d.coarsest = L.coarsest ? 1 : 0;
       d.rlanes = h->opt_amg_rlanes;
+      d.dsplit = h->opt_amg_down_split;
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
@@ -3437,6 +3439,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.rlanes = (int)value;
   }
+  else if (n == "amg_down_split") {
+    h->opt_amg_down_split = value != 0;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.dsplit = (int)(value != 0);
+  }
   else if (n == "amg_op_lanes") {
     if (value != 0 && value != 1 && value != 2 && value != 4)
       return fail(MFEA_EINVAL, "amg_op_lanes: 0 (by width), 1, 2 or 4");
@@ -3670,6 +3677,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_tail_rows") *value = h->opt_amg_tail_rows;
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
+  else if (n == "amg_down_split") *value = h->opt_amg_down_split;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;

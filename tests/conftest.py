@@ -41,7 +41,7 @@ def build_host_shim():
     hdrs = glob.glob(os.path.join(PKG, "csrc", "*.hpp"))
     deps = srcs + hdrs + [os.path.abspath(__file__)]
     if not os.path.exists(out) or any(os.path.getmtime(s) > os.path.getmtime(out) for s in deps):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC",
+        subprocess.check_call(["g++", "-O3", "-std=c++17", "-shared", "-fPIC",
                                "-I" + os.path.join(PKG, "csrc"), *srcs, "-o", out])
     return out
 

@@ -1132,8 +1132,6 @@ __global__ __launch_bounds__(kBlock) void k_amg_cg_init(AmgLevD L0, AmgCg cg, co
 template <int ND, bool FIRST, int BS, bool DIST, int KW = 1>
 __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Slot* slots, double* part,
                                                  AmgDist d) {
-  // the iteration's gate is tested only before the stores (gate_open)
-  const bool run = FIRST || flag_load(&slots[j + 1].flag) == kRun;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int lane = threadIdx.x & 63;
@@ -1163,7 +1161,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
           for (int b = 0; b < ND; ++b) y[a] = fma(m[a * ND + b], ug[b], y[a]);
       }
     }
-    if (run) vstore<ND>(cg.w, i, y);
+    vstore<ND>(cg.w, i, y);
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
       acc[0] = fma(r[a], u[a], acc[0]);
@@ -1172,7 +1170,6 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
       acc[3] = fma(u[a], u[a], acc[3]);
     }
   }
-  if (!run) return;  // grid-uniform
   store_block_partial<BS>(acc, part_buf(part, FIRST ? 0 : ((j & 1) ^ 1)));
   if (FIRST && blockIdx.x == 0 && threadIdx.x == 0) {
     Slot s0;

@@ -148,11 +148,13 @@ __device__ __forceinline__ int flag_load(const int32_t* p) {
   return __hip_atomic_load((__attribute__((address_space(1))) int*)p + z, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
-// (no branch on gate == NULL: a branch makes the compiler settle the flag's
-// value — and wait for its load — where the paths join, at the top)
-__device__ const int32_t kRunWord = kRun;
+// gate == NULL: no flag at all (the solve's chunks pass none, capi.hip
+// enqueue_amg_chunk: every gated kernel is a pure function of the CG state
+// the update kernel freezes once the solve stops, so running it past the stop
+// rewrites the same values; the flag load only put its ≈ 1 µs miss — the
+// flag is written on another XCD — in front of each launch's first wait)
 __device__ __forceinline__ bool gate_open(const int32_t* gate) {
-  return flag_load(gate ? gate : &kRunWord) == kRun;
+  return gate == nullptr || flag_load(gate) == kRun;
 }
 
 // XCD-aware block order for the gathering kernels.  Blocks are dealt
@@ -205,62 +207,83 @@ __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t&
 }
 
 // y ±= Σ_k M_k x_{col_k} over every SELL slot of one row (the diagonal
-// included).  U slots per step with all their loads issued before the first
-// FMA: a row costs ⌈w/U⌉ dependent memory round trips instead of w (the
-// per-thread chain col → value, x is what bounds the small levels).  Slots
-// past the row's width or padded (col < 0) contribute exact zeros.
+// included), in slot order.  Slot k of lane `sub` (S lanes per row, adjacent)
+// is the row's slot k·S + sub; a step issues the column loads of U slots, then
+// all their value and gather loads, then the FMAs: a row costs one dependent
+// round trip (column, then gathers) per step.  Slots past the lane's count ws
+// or padded (col < 0) contribute exact zeros.
 template <int ND>
 constexpr int mac_unroll() { return ND == 2 ? 4 : 2; }
 
-template <int ND, int U, bool SUB, bool SYM = false, class TV, class XP, class C>
-__device__ __forceinline__ void sell_mac_u(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                           int64_t npos, int64_t base, int w,
-                                           XP x, C* y) {
-  for (int k = 0; k < w; k += U) {
-    int32_t c[U];
-    int64_t q[U];
+template <int ND, int U, int S, bool SUB, bool SYM, class TV, class XP, class C>
+__device__ __forceinline__ void sell_step(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                          int64_t base, int k, int ws, int sub, XP x, C* y) {
+  int32_t c[U];
+  int64_t q[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = k + u < w ? base + (int64_t)(k + u) * 64 : base;
-      c[u] = k + u < w ? col[q[u]] : -1;
-    }
-    C m[U][ND * ND], xc[U][ND];
+  for (int u = 0; u < U; ++u) {
+    q[u] = k + u < ws ? base + (int64_t)((k + u) * S + sub) * 64 : base;
+    c[u] = k + u < ws ? col[q[u]] : -1;
+  }
+  C m[U][ND * ND], xc[U][ND];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (SYM) bload_sym<ND>(val, npos, q[u], m[u]);
-      else bload<ND>(val, npos, q[u], m[u]);
-      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
-    }
+  for (int u = 0; u < U; ++u) {
+    if constexpr (SYM) bload_sym<ND>(val, 0, q[u], m[u]);
+    else bload<ND>(val, 0, q[u], m[u]);
+    vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
+  }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+  for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
+    for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
 #pragma unroll
-      for (int a = 0; a < ND; ++a)
+    for (int a = 0; a < ND; ++a)
 #pragma unroll
-        for (int b = 0; b < ND; ++b)
-          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
+      for (int b = 0; b < ND; ++b)
+        y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
+  }
+}
+// The steps over a wave's slice: wu steps per lane (uniform over the wave —
+// the slice's width), each step the smallest of 1, 2, 4, … UMAX slots that
+// covers what is left, so a row of up to UMAX slots per lane is one round
+// trip and no step issues more than twice the loads it needs.  (Steps of a
+// fixed U = 8 issued 8 loads per lane for the ≈ 1–2 slots each of the 8
+// lanes of a C3 R̂ row holds: the down sweep's vector-memory instructions
+// were three quarters padding.)  The branches are wave-uniform.
+template <int ND, int UMAX, int S, bool SUB, bool SYM, class TV, class XP, class C>
+__device__ __forceinline__ void sell_steps(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                           int64_t base, int wu, int ws, int sub, XP x, C* y) {
+  for (int k = 0; k < wu;) {
+    const int rem = wu - k;
+    if (UMAX >= 16 && rem > 8) {
+      sell_step<ND, (UMAX >= 16 ? 16 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+      k += 16;
+    } else if (UMAX >= 8 && rem > 4) {
+      sell_step<ND, (UMAX >= 8 ? 8 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+      k += 8;
+    } else if (UMAX >= 4 && rem > 2) {
+      sell_step<ND, (UMAX >= 4 ? 4 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+      k += 4;
+    } else if (rem > 1) {
+      sell_step<ND, 2, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+      k += 2;
+    } else {
+      sell_step<ND, 1, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+      k += 1;
     }
   }
 }
-// Slices wider than U (the restriction's rows hold ≈ 7 blocks, the coarse
-// A rows 4–5) take one step of 2U loads instead of two dependent steps of U,
-// and with K = 3 slices wider than 2U (the restrictions reach 15–29 blocks on
-// every level) one step of 4U: every slice up to the step's width costs one
-// round trip of column loads and one of gathers.  The width is slice-uniform,
-// so the branches are too.  Each step costs registers, and a kernel's VGPR
-// count is its widest path's: the f64 SpMV, whose level-0 slices are ≤ 4 wide
-// for 98 % of the waves, stays at K = 1 (a 2U path put it at 139 VGPRs, one
-// 768-thread block per CU); the streaming level-0 kernels use K = 2; the
-// restrictions and the latency-bound coarse levels K = 3.
+// One lane per row.  K bounds the widest step (the kernel's VGPR count is its
+// widest path's): U·2^(K−1) slots with U = mac_unroll — the f64 SpMV, whose
+// level-0 slices are ≤ 4 wide for 98 % of the waves, stays at K = 1 (a 2U path
+// put it at 139 VGPRs, one 768-thread block per CU); the streaming level-0
+// kernels use K = 2; the restrictions and the latency-bound coarse levels K = 3.
 template <int ND, bool SUB, int K = 2, bool SYM = false, class TV, class XP, class C>
 __device__ __forceinline__ void sell_mac(const int32_t* __restrict__ col, const TV* __restrict__ val,
-                                         int64_t npos, int64_t base, int w,
+                                         int64_t /*npos*/, int64_t base, int w,
                                          XP x, C* y) {
-  constexpr int U = mac_unroll<ND>();
-  if (K >= 3 && w > 2 * U) sell_mac_u<ND, 4 * U, SUB, SYM>(col, val, npos, base, w, x, y);
-  else if (K >= 2 && w > U) sell_mac_u<ND, 2 * U, SUB, SYM>(col, val, npos, base, w, x, y);
-  else sell_mac_u<ND, U, SUB, SYM>(col, val, npos, base, w, x, y);
+  constexpr int UMAX = mac_unroll<ND>() << (K - 1);
+  sell_steps<ND, UMAX, 1, SUB, SYM>(col, val, base, w, w, 0, x, y);
 }
 
 // o = s · D⁻¹ v  (D⁻¹ [n][NB2], storage TD, compute C).  dinv_load / dinv_mul
@@ -372,31 +395,7 @@ __device__ __forceinline__ void sell_mac_sub(const int32_t* __restrict__ col, co
   constexpr int U = 2 * mac_unroll<ND>();  // (U = 4: C2 62.4 vs 60.8 µs per iteration)
   const int wu = (w + S - 1) / S;  // steps: the slice's, uniform
   const int ws = w > sub ? (w - sub + S - 1) / S : 0;
-  for (int k = 0; k < wu; k += U) {
-    int32_t c[U];
-    int64_t q[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = k + u < ws ? base + (int64_t)((k + u) * S + sub) * 64 : base;
-      c[u] = k + u < ws ? col[q[u]] : -1;
-    }
-    C m[U][ND * ND], xc[U][ND];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      bload<ND>(val, 0, q[u], m[u]);
-      vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int b = 0; b < ND; ++b) xc[u][b] = c[u] >= 0 ? xc[u][b] : (C)0;
-#pragma unroll
-      for (int a = 0; a < ND; ++a)
-#pragma unroll
-        for (int b = 0; b < ND; ++b)
-          y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
-    }
-  }
+  sell_steps<ND, U, S, SUB, false>(col, val, base, wu, ws, sub, x, y);
 #pragma unroll
   for (int o = 1; o < S; o <<= 1)
 #pragma unroll

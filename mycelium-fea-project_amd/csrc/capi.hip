@@ -1636,7 +1636,8 @@ void enqueue_amg_iteration(mfea_handle* h, Part& pt, int j, bool profile) {
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_update(s, nd, j, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
-  launch_precond(h, pt, profile ? nullptr : &pt.slots.ptr[j + 1].flag);
+  (void)profile;
+  launch_precond(h, pt, nullptr);
   launch_amg_cg_w(s, nd, j, profile, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
 }
 
@@ -1709,8 +1710,7 @@ int enqueue_amg_dist_iteration(mfea_handle* h, int j) {
     const int nd = pt.amg.nd;
     launch_amg_cg_update(s, nd, j, pt.amg_lev[0], pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr,
                          &pt.amg_dist);
-    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg,
-                      pt.amg_tail, &pt.slots.ptr[j + 1].flag);
+    launch_amg_vcycle(s, nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, nullptr);
     launch_amg_pack_u(s, nd, pt.amg_cg, pt.amg_dist);
   }
   HIPC(hipGetLastError());
@@ -1742,8 +1742,14 @@ void enqueue_amg_chunk(mfea_handle* h, Part& pt, int chunk) {
   hipStream_t s = h->stream;
   const int nd = pt.amg.nd;
   const AmgLevD& L0 = pt.amg_lev[0];
+  // The preconditioner and w = A u launches carry no gate: once the update
+  // kernel stops the solve (converged, max_it, breakdown) it leaves x, r, p,
+  // s and level 0's x unchanged, and every later V-cycle / sweep / w launch
+  // is a pure function of those — it rewrites the values it wrote before.  A
+  // gate flag cost each launch a load from another XCD's L2 ahead of its
+  // first wait (vector loads complete in order), ≈ 1 µs per launch.
   for (int j = 0; j < chunk; ++j) {
-    launch_precond(h, pt, &pt.slots.ptr[j + 1].flag);
+    launch_precond(h, pt, nullptr);
     launch_amg_cg_w(s, nd, j, false, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
     launch_amg_cg_update(s, nd, j + 1, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);
   }
@@ -2213,7 +2219,8 @@ int enqueue_gamg_vcycle(mfea_handle* h, int j) {
   const int nd = pl.nd, nlev = (int)pl.lev.size(), ns = pl.n_dist;
   if (nlev <= 1) return 0;  // the update's vcycle_entry solved the only level
   const int top = std::min(ns, nlev - 1);  // split levels with a level below
-  auto gate = [j](Part& pt) -> const int32_t* { return j < 0 ? nullptr : &pt.slots.ptr[j + 1].flag; };
+  (void)j;  // no gate (enqueue_amg_chunk): past the stop every launch rewrites the same values
+  auto gate = [](Part&) -> const int32_t* { return nullptr; };
   auto steps = [&](int l, int step) {
     for (auto& pp : h->parts) {
       Part& pt = *pp;

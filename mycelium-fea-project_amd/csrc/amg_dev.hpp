@@ -198,10 +198,18 @@ __device__ __forceinline__ bool slot_wave(const AmgMatD& M, int64_t t0, int64_t 
   return slot_wave(M, t0, t1, q, row, k, xcd_block());
 }
 
+// a wave-uniform load of read-only plan data through the constant address
+// space: a scalar load (s_load, counted by lgkmcnt).  Through a global
+// pointer the compiler issues a vector load with a uniform address, and
+// vector loads complete in order: the slice bounds then waited behind every
+// load issued before them.
+__device__ __forceinline__ int32_t uniform_load(const int32_t* p, int64_t i) {
+  return ((const __attribute__((address_space(4))) int32_t*)p)[i];
+}
 // slot range of the wave's slice (scalar loads, wave-uniform)
 __device__ __forceinline__ void slice_of(const AmgMatD& M, int64_t row, int64_t& base, int& width) {
   const int s = __builtin_amdgcn_readfirstlane((int)(row >> 6));
-  const int a = M.sptr[s], b = M.sptr[s + 1];
+  const int a = uniform_load(M.sptr, s), b = uniform_load(M.sptr, s + 1);
   base = (int64_t)a * 64 + (row & 63);
   width = b - a;
 }
@@ -243,6 +251,29 @@ __device__ __forceinline__ void sell_step(const int32_t* __restrict__ col, const
         y[a] = fma(SUB ? -m[u][a * ND + b] : m[u][a * ND + b], xc[u][b], y[a]);
   }
 }
+// one step of the smallest of 1, 2, 4, … UMAX slots covering rem (> 0)
+template <int ND, int UMAX, int S, bool SUB, bool SYM, class TV, class XP, class C>
+__device__ __forceinline__ int sell_step_by(const int32_t* __restrict__ col, const TV* __restrict__ val,
+                                            int64_t base, int k, int rem, int ws, int sub, XP x, C* y) {
+  if (UMAX >= 16 && rem > 8) {
+    sell_step<ND, (UMAX >= 16 ? 16 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+    return 16;
+  }
+  if (UMAX >= 8 && rem > 4) {
+    sell_step<ND, (UMAX >= 8 ? 8 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+    return 8;
+  }
+  if (UMAX >= 4 && rem > 2) {
+    sell_step<ND, (UMAX >= 4 ? 4 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+    return 4;
+  }
+  if (rem > 1) {
+    sell_step<ND, 2, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+    return 2;
+  }
+  sell_step<ND, 1, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
+  return 1;
+}
 // The steps over a wave's slice: wu steps per lane (uniform over the wave —
 // the slice's width), each step the smallest of 1, 2, 4, … UMAX slots that
 // covers what is left, so a row of up to UMAX slots per lane is one round
@@ -253,25 +284,7 @@ __device__ __forceinline__ void sell_step(const int32_t* __restrict__ col, const
 template <int ND, int UMAX, int S, bool SUB, bool SYM, class TV, class XP, class C>
 __device__ __forceinline__ void sell_steps(const int32_t* __restrict__ col, const TV* __restrict__ val,
                                            int64_t base, int wu, int ws, int sub, XP x, C* y) {
-  for (int k = 0; k < wu;) {
-    const int rem = wu - k;
-    if (UMAX >= 16 && rem > 8) {
-      sell_step<ND, (UMAX >= 16 ? 16 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
-      k += 16;
-    } else if (UMAX >= 8 && rem > 4) {
-      sell_step<ND, (UMAX >= 8 ? 8 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
-      k += 8;
-    } else if (UMAX >= 4 && rem > 2) {
-      sell_step<ND, (UMAX >= 4 ? 4 : 1), S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
-      k += 4;
-    } else if (rem > 1) {
-      sell_step<ND, 2, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
-      k += 2;
-    } else {
-      sell_step<ND, 1, S, SUB, SYM>(col, val, base, k, ws, sub, x, y);
-      k += 1;
-    }
-  }
+  for (int k = 0; k < wu;) k += sell_step_by<ND, UMAX, S, SUB, SYM>(col, val, base, k, wu - k, ws, sub, x, y);
 }
 // One lane per row.  K bounds the widest step (the kernel's VGPR count is its
 // widest path's): U·2^(K−1) slots with U = mac_unroll — the f64 SpMV, whose

@@ -9,7 +9,7 @@ OUT=$1; TMO=$2; CMD=$3; N=${4:-6}
 for i in $(seq 1 "$N"); do
   timeout $((TMO + 900)) /usr/local/graft/bin/gpurun --timeout "$TMO" -- "$CMD" > "$OUT" 2>&1
   rc=$?
-  if grep -q "stopped responding while being prepared\|backing off\|no box\|status=transient rc=None" "$OUT" && ! grep -q "merged" "$OUT"; then
+  if grep -q "stopped responding while being prepared\|backing off\|no box\|no free box\|are busy\|status=transient rc=None" "$OUT" && ! grep -q "merged" "$OUT"; then
     echo "attempt $i: no box (rc=$rc); retrying in 150 s" >> "$OUT.attempts"
     sleep 150
     continue

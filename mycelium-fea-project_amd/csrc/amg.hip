@@ -538,17 +538,31 @@ __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restric
   float C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
-  for (int t = L.ct_ptr[q]; t < L.ct_ptr[q + 1]; ++t) {
-    const int32_t a = L.ct_a[t], b = L.ct_b[t];
-    float r[ND * ND];
-    bload<ND>(L.RT.val32, 0, b, r);
-    if (a < 0) {
+  const int t0 = L.ct_ptr[q], t1 = L.ct_ptr[q + 1];
+  constexpr int U = 4;  // items in flight (list order kept: the same sums)
+  for (int t = t0; t < t1; t += U) {
+    int32_t a[U], b[U];
 #pragma unroll
-      for (int c = 0; c < ND * ND; ++c) C[c] += r[c];
-    } else {
-      float v[ND * ND];
-      bload<ND>(vnext, 0, a, v);
-      fmm_acc<ND>(v, r, C);
+    for (int u = 0; u < U; ++u) {
+      const int tt = t + u < t1 ? t + u : t;
+      a[u] = L.ct_a[tt];
+      b[u] = L.ct_b[tt];
+    }
+    float r[U][ND * ND], v[U][ND * ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(L.RT.val32, 0, b[u], r[u]);
+      bload<ND>(vnext ? vnext : L.RT.val32, 0, a[u] >= 0 ? a[u] : 0, v[u]);  // (no V below: a < 0, a dummy read)
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t + u >= t1) break;
+      if (a[u] < 0) {
+#pragma unroll
+        for (int c = 0; c < ND * ND; ++c) C[c] += r[u][c];
+      } else {
+        fmm_acc<ND>(v[u], r[u], C);
+      }
     }
   }
   bstore<ND>(L.CT.val32, 0, q, C);
@@ -576,11 +590,27 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) C[a * ND + a] += 2.0f;
   }
-  for (int t = L.cv_ptr[q]; t < L.cv_ptr[q + 1]; ++t) {
-    float p[ND * ND], tb[ND * ND];
-    bload<ND>(L.PT.val32, 0, L.cv_a[t], p);
-    bload<ND>(L.CT.val32, 0, L.cv_b[t], tb);
-    fmm_acc<ND>(p, tb, C);
+  const int t0 = L.cv_ptr[q], t1 = L.cv_ptr[q + 1];
+  constexpr int U = 4;  // items in flight (list order kept: the same sums)
+  for (int t = t0; t < t1; t += U) {
+    int32_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tt = t + u < t1 ? t + u : t;
+      a[u] = L.cv_a[tt];
+      b[u] = L.cv_b[tt];
+    }
+    float p[U][ND * ND], tb[U][ND * ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(L.PT.val32, 0, a[u], p[u]);
+      bload<ND>(L.CT.val32, 0, b[u], tb[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t + u >= t1) break;
+      fmm_acc<ND>(p[u], tb[u], C);
+    }
   }
   bstore<ND>(L.CV.val32, 0, q, C);
 }
@@ -590,23 +620,56 @@ __global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
   if (xb >= 0) vv_body<ND>(L, xb);
 }
 
-// A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], one output block per thread.  dinv_next
-// (level l+1 at a fixed ω, AmgLevD::fixed_omega): the thread of a diagonal
-// block (slot 0 of its row) also stores its inverse — from the stored f32
-// block, the bits k_amg_dinv would form — so level l+1 needs no D⁻¹ launch.
-template <int ND>
+// A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], S lanes per output block (AmgLevD::ac_lanes):
+// the lists hold 5–40 pairs (C3 level 0 ≈ 30), and one lane walking them in
+// steps of 8 chained four dependent index → block round trips; lane `sub`
+// takes items sub, sub + S, … (a fixed order) and the S partial sums meet by
+// a fixed butterfly — bitwise reproducible.  dinv_next (level l+1 at a fixed
+// ω, AmgLevD::fixed_omega): the group of a diagonal block (slot 0 of its row)
+// also stores its inverse — from the stored f32 block, the bits k_amg_dinv
+// would form — so level l+1 needs no D⁻¹ launch.
+template <int ND, int S>
 __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int64_t blk, float* dinv_next) {
-  const int64_t q = L.ac_rg.p0 + blk * kBlock + threadIdx.x;
+  const int64_t t = blk * kBlock + threadIdx.x;
+  const int64_t q = L.ac_rg.p0 + t / S;
+  const int sub = (int)(t % S);
+  // (the S lanes of a block share q: they leave together)
   if (q >= L.ac_rg.p1 || Ac.col[q] < 0 || !pos_mine(L.ac_rg, q)) return;
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-  pair_sum<ND, true>(L.ac_ptr[q], L.ac_ptr[q + 1], L.ac_a, L.ac_b, L.P.val32, L.P.npos, L.apval, L.AP.npos, C);
+  const int t0 = L.ac_ptr[q], t1 = L.ac_ptr[q + 1];
+  constexpr int U = 4;
+  for (int k = t0 + sub; k < t1; k += U * S) {  // U of this lane's pairs in flight
+    int32_t ia[U], ib[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tt = k + u * S < t1 ? k + u * S : k;
+      ia[u] = L.ac_a[tt];
+      ib[u] = L.ac_b[tt];
+    }
+    double x[U][ND * ND], y[U][ND * ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(L.P.val32, 0, ia[u], x[u]);
+      bload<ND>(L.apval, 0, ib[u], y[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u * S < t1) mtm_acc<ND>(x[u], y[u], C);
+  }
+  if constexpr (S > 1) {
+#pragma unroll
+    for (int o = 1; o < S; o <<= 1)
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) C[c] += __shfl_xor(C[c], o, 64);
+  }
+  if (sub != 0) return;
   bstore<ND>(Ac.val32, Ac.npos, q, C);
   if (dinv_next) {
-    const int64_t t = q >> 6;
-    const int sl = Ac.srow[t];
-    if (t == (int64_t)Ac.sptr[sl]) {  // slot 0: the diagonal block of row 64·sl + lane
+    const int64_t ts = q >> 6;
+    const int sl = Ac.srow[ts];
+    if (ts == (int64_t)Ac.sptr[sl]) {  // slot 0: the diagonal block of row 64·sl + lane
       double D[ND * ND], Di[ND * ND];
 #pragma unroll
       for (int c = 0; c < ND * ND; ++c) D[c] = (double)(float)C[c];
@@ -617,11 +680,16 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
     }
   }
 }
-template <int ND>
+template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_ac(AmgLevD L, AmgMatD Ac, double* omega_next, float* dinv_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;  // level l+1's bound, max'ed by its k_amg_dinv
   const int64_t xb = setup_block(L.x1);
-  if (xb >= 0) ac_body<ND>(L, Ac, xb, dinv_next);
+  if (xb >= 0) ac_body<ND, S>(L, Ac, xb, dinv_next);
+}
+// launch helper: the grid of S lanes per output block
+static int64_t ac_blocks(const AmgLevD& L) {
+  const int64_t n = L.ac_rg.npos() * L.ac_lanes;
+  return (n + kBlock - 1) / kBlock > 0 ? (n + kBlock - 1) / kBlock : 1;
 }
 
 // The compact cycle's operators fused into the Galerkin chain's launches (no
@@ -638,14 +706,30 @@ __global__ __launch_bounds__(kBlock) void k_amg_fuse_p(AmgLevD L, AmgLevD Lp, in
   else if (xb < g1) atv_body<ND>(L, xb - g0);
   else rtv_body<ND>(Lp, L, xb - g1);
 }
-template <int ND>
+template <int ND, int S>
 __global__ __launch_bounds__(kBlock) void k_amg_fuse_ac(AmgLevD L, AmgMatD Ac, double* omega_next, int64_t g0,
                                                         float* dinv_next) {
   if (blockIdx.x == 0 && threadIdx.x == 0) omega_next[1] = 0.0;
   const int64_t xb = setup_block(L.x1);
   if (xb < 0) return;
-  if (xb < g0) ac_body<ND>(L, Ac, xb, dinv_next);
+  if (xb < g0) ac_body<ND, S>(L, Ac, xb, dinv_next);
   else ptv_body<ND>(L, xb - g0);
+}
+// the Galerkin product's launch (fuse: + P̃ from block g0 on) at its lanes
+template <int ND>
+static void launch_ac(hipStream_t s, const AmgLevD& L, const AmgMatD& Ac, double* omega_next, float* dnext,
+                      int64_t blocks, int64_t g0, bool fuse) {
+  const dim3 g(L.x1 ? 8 * (unsigned)blocks : (unsigned)blocks), b(kBlock);
+#define MFEA_AC(S)                                                                                          \
+  if (fuse) hipLaunchKernelGGL((k_amg_fuse_ac<ND, S>), g, b, 0, s, L, Ac, omega_next, g0, dnext); \
+  else hipLaunchKernelGGL((k_amg_ac<ND, S>), g, b, 0, s, L, Ac, omega_next, dnext)
+  switch (L.ac_lanes) {
+    case 8: MFEA_AC(8); break;
+    case 4: MFEA_AC(4); break;
+    case 2: MFEA_AC(2); break;
+    default: MFEA_AC(1); break;
+  }
+#undef MFEA_AC
 }
 
 // ---------------------------------------------------------------------------
@@ -1358,9 +1442,7 @@ static void setup_nd(hipStream_t s, const AmgLevD& L, const AmgLevD* N, bool lev
   if (stage & kSetupAP) {
     hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, rows_grid(std::max(L.AP.rg.npos(), L.R.rg.npos()))), dim3(kBlock), 0, s, L);
   }
-  if (stage & kSetupAC)
-    hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, N->A, N->omega,
-                       (float*)nullptr);
+  if (stage & kSetupAC) launch_ac<ND>(s, L, N->A, N->omega, nullptr, ac_blocks(L), 0, false);
 }
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0, int stage) {
   if (nd == 2) setup_nd<2>(s, L, next, level0, stage);
@@ -1412,14 +1494,12 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
     float* const dnext = lev[l + 1].fixed_omega ? lev[l + 1].dinv32 : nullptr;
     if (compact(l) && L.PT.npos == L.AP.npos) {  // P̃ formed by the A·P kernel
       hipLaunchKernelGGL((k_amg_ap<ND, true>), xg(L, gap), dim3(kBlock), 0, s, L);
-      hipLaunchKernelGGL(k_amg_ac<ND>, xg(L, rows_grid(L.ac_rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega,
-                         dnext);
+      launch_ac<ND>(s, L, lev[l + 1].A, lev[l + 1].omega, dnext, ac_blocks(L), 0, false);
     } else {
       hipLaunchKernelGGL(k_amg_ap<ND>, xg(L, gap), dim3(kBlock), 0, s, L);
-      const int64_t a0 = rows_grid(L.ac_rg.npos()).x;
+      const int64_t a0 = ac_blocks(L);
       const int64_t a1 = a0 + (compact(l) ? slot_blocks(L.PT.npos) : 0);
-      hipLaunchKernelGGL(k_amg_fuse_ac<ND>, xg(L, a1), dim3(kBlock), 0, s, L, lev[l + 1].A, lev[l + 1].omega, a0,
-                         dnext);
+      launch_ac<ND>(s, L, lev[l + 1].A, lev[l + 1].omega, dnext, a1, a0, true);
     }
   }
   collapse_setup_nd<ND>(s, lev, nlev, coll);

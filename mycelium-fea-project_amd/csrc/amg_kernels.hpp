@@ -91,6 +91,7 @@ struct AmgLevD {
   const int32_t* ac_a = nullptr;
   const int32_t* ac_b = nullptr;
   RowRange ac_rg;  // level l+1's A rows this rank's Galerkin product forms (= R's rows)
+  int ac_lanes = 1;  // lanes per output block of the Galerkin product (by its lists' mean length)
   // the compact cycle (amg.hpp AmgLevel::PT): P̃ (f32, PT.val32) and the scaled
   // restriction R̂ = s' D'⁻¹ P̃ᵀ D / ω (RT.val32; s' = ω' or 1 on the coarsest
   // level), formed by launch_amg_compact_setup once every level is set up

@@ -1330,6 +1330,11 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
         d.ac_ptr = I(L.ac.ptr);
         d.ac_a = I(L.ac.a);
         d.ac_b = I(L.ac.b);
+        {  // the Galerkin product's lanes per block: its lists run 5–40 pairs (amg.hip ac_body)
+          const int64_t np = std::max<int64_t>(1, pl.lev[l + 1].A.n_pos());
+          const double mean = L.ac.ptr.empty() ? 0.0 : (double)L.ac.ptr.back() / (double)np;
+          d.ac_lanes = mean > 24.0 ? 8 : mean > 12.0 ? 4 : mean > 6.0 ? 2 : 1;
+        }
         // the compact cycle's P̃ / R̃ (one partition's hierarchy only: the
         // distributed V-cycle exchanges per four-step step)
         if (!rk && L.PT.n == n) {

@@ -1594,8 +1594,10 @@ int amg_down_lanes(const AmgLevD& L) {
   if (L.rlanes > 0) return L.rlanes;
   const int64_t rows = ((L.RT.n + 63) / 64) * 64;
   const double mean_w = rows > 0 ? (double)L.RT.npos / (double)rows : 0.0;
-  // (16 lanes past a mean width of 20 measured slower: C5 iteration 854 vs 751 µs)
-  return mean_w > 6.0 ? 8 : lanes_for(L.RT, 0, 2.5, 5.0);
+  // (16 lanes past a mean width of 20 measured slower on C5's level 0:
+  // iteration 854 vs 751 µs; a small level's launch, one chain long, may gain)
+  const int wide = L.small_lanes > 0 && 8 * L.RT.n < L.small_lanes && mean_w > 12.0 ? 16 : 8;
+  return mean_w > 6.0 ? wide : lanes_for(L.RT, 0, 2.5, 5.0);
 }
 // one lane per P̃ row up to a mean width of 8 (measured: C5 iteration 736 µs
 // at 1 lane against 759 at 2 and 845 at 4, C3 71.9 / 75.2 / 83.6)
@@ -1633,9 +1635,15 @@ template <int ND>
 static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   const int64_t rows = ((L.CV.n + 63) / 64) * 64;
   const double mean_w = rows > 0 ? (double)L.CV.npos / (double)rows : 0.0;
-  const int S = mean_w > 12.0 ? 8 : mean_w > 5.0 ? 4 : mean_w > 2.5 ? 2 : 1;
+  // a V of a few thousand rows cannot fill the GPU at 8 lanes per row: its
+  // launch is one dependent chain long, so 16 lanes shorten the chain
+  // (C2: 2.4 k rows × 50 blocks, iteration 29.1 → 27.7 µs; C5 703 → 695;
+  // C3's 24 k rows stay at 8: 67.1 vs 68.8 at 16)
+  const int wide = L.small_lanes > 0 && 8 * L.CV.n < L.small_lanes ? 16 : 8;
+  const int S = L.vlanes > 0 ? L.vlanes : mean_w > 12.0 ? wide : mean_w > 5.0 ? 4 : mean_w > 2.5 ? 2 : 1;
   const dim3 g(rows_grid(S * L.CV.n));
-  if (S == 8) hipLaunchKernelGGL((k_amg_vapply<ND, 8>), g, dim3(kBlock), 0, s, L, gate);
+  if (S == 16) hipLaunchKernelGGL((k_amg_vapply<ND, 16>), g, dim3(kBlock), 0, s, L, gate);
+  else if (S == 8) hipLaunchKernelGGL((k_amg_vapply<ND, 8>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 4) hipLaunchKernelGGL((k_amg_vapply<ND, 4>), g, dim3(kBlock), 0, s, L, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 2>), g, dim3(kBlock), 0, s, L, gate);
   else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);

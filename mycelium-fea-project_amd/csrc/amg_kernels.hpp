@@ -66,6 +66,8 @@ struct AmgLevD {
   int coarsest = 0;
   int rlanes = 0;  // restriction lanes per coarse row (0: by R's mean width)
   int dsplit = 0;  // compact down sweep: its two row sets as two launches
+  int vlanes = 0;  // collapsed cycle: lanes per V row (0: by V's mean width)
+  int small_lanes = 65536;  // wide rows of a level under this many threads at 8 lanes take 16 (0: never)
   int alanes = 0;  // lanes per row of the f32 operator below level 0 (0: by A's)
   int tail_lds = 1;  // the tail starting at this level keeps its vectors in LDS (if they fit)
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)

@@ -242,6 +242,8 @@ struct mfea_handle {
   int opt_amg_w_k = 0;         // GAMG: w = A u step width (0: by level 0's mean slice width, 1, 2)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_down_split = 0;  // GAMG compact down sweep: R̂ and Ã rows as two launches (experiment)
+  int opt_amg_v_lanes = 0;     // GAMG collapsed cycle: lanes per V row (0: by width; 1, 2, 4, 8, 16)
+  int64_t opt_amg_small_lanes = 65536;  // GAMG: wide rows of small levels at 16 lanes below this many threads
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
   int opt_amg_tail_lds = 1;    // GAMG: the single-workgroup tail keeps its vectors in LDS
   int opt_amg_collapse = -1;           // GAMG: collapse the compact cycle below the highest level
@@ -1306,6 +1308,8 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       d.coarsest = L.coarsest ? 1 : 0;
       d.rlanes = h->opt_amg_rlanes;
       d.dsplit = h->opt_amg_down_split;
+      d.vlanes = h->opt_amg_v_lanes;
+      d.small_lanes = h->opt_amg_small_lanes;
       d.alanes = h->opt_amg_alanes;
       d.tail_lds = h->opt_amg_tail_lds;
       d.ulanes = h->opt_amg_up_lanes;
@@ -3451,6 +3455,19 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.rlanes = (int)value;
   }
+  else if (n == "amg_v_lanes") {
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+      return fail(MFEA_EINVAL, "amg_v_lanes: 0 (by width), 1, 2, 4, 8 or 16");
+    h->opt_amg_v_lanes = (int)value;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.vlanes = (int)value;
+  }
+  else if (n == "amg_small_lanes") {
+    if (value < 0 || value > (int64_t(1) << 30)) return fail(MFEA_EINVAL, "amg_small_lanes: 0 .. 2^30");
+    h->opt_amg_small_lanes = value;
+    for (auto& pp : h->parts)
+      for (auto& L : pp->amg_lev) L.small_lanes = value;
+  }
   else if (n == "amg_down_split") {
     h->opt_amg_down_split = value != 0;
     for (auto& pp : h->parts)
@@ -3690,6 +3707,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_max_levels") *value = h->opt_amg_max_levels;
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_down_split") *value = h->opt_amg_down_split;
+  else if (n == "amg_v_lanes") *value = h->opt_amg_v_lanes;
+  else if (n == "amg_small_lanes") *value = h->opt_amg_small_lanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;
   else if (n == "amg_cycle") *value = h->opt_amg_cycle;

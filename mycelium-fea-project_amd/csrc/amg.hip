@@ -620,6 +620,67 @@ __global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
   if (xb >= 0) vv_body<ND>(L, xb);
 }
 
+// the merged levels' operators (AmgMergeD), one output block per thread, f32
+// in list order (bitwise reproducible): DQ's c_1 rows 2 R̂_0 − Σ Ã_1·R̂_0, its
+// x_2 rows Σ R̂_1·R̂_0; U = P̃_0 (ext) + Σ P̃_0·P̃_1
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_mprod(AmgMergeD m, const float* __restrict__ at1,
+                                                      const float* __restrict__ r0, const float* __restrict__ r1,
+                                                      const float* __restrict__ p0, const float* __restrict__ p1,
+                                                      int64_t gdq) {
+  const int64_t xb = xcd_block();
+  const bool dq = xb < gdq;
+  const AmgMatD& M = dq ? m.DQ : m.U;
+  const int64_t q = (dq ? xb : xb - gdq) * kBlock + threadIdx.x;
+  if (q >= M.npos || M.col[q] < 0) return;
+  const bool c1 = dq && q < m.dq_split;
+  const int32_t* ext = dq ? m.dq_ext : m.u_ext;
+  const int32_t* lp = dq ? m.dq_ptr : m.u_ptr;
+  const int32_t* la = dq ? m.dq_a : m.u_a;
+  const int32_t* lb = dq ? m.dq_b : m.u_b;
+  const float* X = dq ? (c1 ? at1 : r1) : p0;
+  const float* Y = dq ? r0 : p1;
+  float S[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) S[c] = 0.0f;
+  const int t0 = lp[q], t1 = lp[q + 1];
+  constexpr int U = 4;
+  for (int t = t0; t < t1; t += U) {
+    int32_t a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int tt = t + u < t1 ? t + u : t;
+      a[u] = la[tt];
+      b[u] = lb[tt];
+    }
+    float x[U][ND * ND], y[U][ND * ND];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bload<ND>(X, 0, a[u], x[u]);
+      bload<ND>(Y, 0, b[u], y[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (t + u >= t1) break;
+      fmm_acc<ND>(x[u], y[u], S);
+    }
+  }
+  float C[ND * ND];
+  const int32_t e = ext[q];
+  if (e >= 0) {
+    bload<ND>(dq ? r0 : p0, 0, e, C);
+    const float f = dq ? 2.0f : 1.0f;
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] *= f;
+  } else {
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
+  }
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) C[c] = c1 ? C[c] - S[c] : C[c] + S[c];
+  bstore<ND>(M.val32, 0, q, C);
+}
+
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], S lanes per output block (AmgLevD::ac_lanes):
 // the lists hold 5–40 pairs (C3 level 0 ≈ 30), and one lane walking them in
 // steps of 8 chained four dependent index → block round trips; lane `sub`
@@ -1648,6 +1709,20 @@ static void vapply_nd(hipStream_t s, const AmgLevD& L, const int32_t* gate) {
   else if (S == 2) hipLaunchKernelGGL((k_amg_vapply<ND, 2>), g, dim3(kBlock), 0, s, L, gate);
   else hipLaunchKernelGGL((k_amg_vapply<ND, 1>), g, dim3(kBlock), 0, s, L, gate);
 }
+// levels 0 and 1 merged (AmgMergeD): one down launch over DQ's rows and Ã_0's,
+// V_2, one up launch over U's rows into the CG's u
+template <int ND>
+static void merged_nd(hipStream_t s, const AmgLevD* lev, const AmgCg& cg, const AmgMergeD& m, const int32_t* gate) {
+  AmgLevD Ld = lev[0], Nd{}, Lu = lev[0], Nu{};
+  Ld.RT = m.DQ;
+  Ld.rt_row = m.dq_dst;
+  Nd.x = m.B;
+  Lu.PT = m.U;
+  Nu.e = m.B;
+  down_nd<ND>(s, Ld, Nd, gate);
+  vapply_nd<ND>(s, lev[2], gate);
+  up_te<ND, float>(s, Lu, Nu, cg.u, gate);
+}
 template <int ND>
 static void compact_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg, const int32_t* gate, int l0) {
   if (cg.coll > l0 && cg.coll < nlev - 1 && lev[cg.coll].collapsed && lev[cg.coll].CV.n > 0) {
@@ -1675,7 +1750,11 @@ bool amg_compact_ok(const AmgLevD* lev, int nlev, int l0) {
 // x = ω D⁻¹ b), leaving level l0's output in its e (level 0: the CG's u).
 template <int ND>
 static void vcycle_nd(hipStream_t s, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                      int tail, const int32_t* gate, int l0) {
+                      int tail, const int32_t* gate, int l0, const AmgMergeD* mg) {
+  if (mg && mg->on && l0 == 0 && cg.cycle == 1 && cg.coll == 2 && nlev >= 4) {
+    merged_nd<ND>(s, lev, cg, *mg, gate);
+    return;
+  }
   if (cg.cycle == 1 && amg_compact_ok(lev, nlev, l0)) {
     compact_nd<ND>(s, lev, nlev, cg, gate, l0);
     return;
@@ -1709,12 +1788,23 @@ static int clamp_tail(int tail, int nlev) {
   return tail;
 }
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       int tail, const int32_t* gate, int l0) {
+                       int tail, const int32_t* gate, int l0, const AmgMergeD* mg) {
   // one level: the coarsest solve u = D⁻¹ r is done by the producer of r
   if (nlev <= 1 || lev[0].A.n <= 0 || l0 >= nlev - 1) return;
   tail = clamp_tail(tail, nlev);
-  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, tail, gate, l0);
-  else vcycle_nd<3>(s, lev, nlev, cg, tail, gate, l0);
+  if (nd == 2) vcycle_nd<2>(s, lev, nlev, cg, tail, gate, l0, mg);
+  else vcycle_nd<3>(s, lev, nlev, cg, tail, gate, l0, mg);
+}
+void launch_amg_merge_setup(hipStream_t s, int nd, const AmgLevD* lev, const AmgMergeD& m) {
+  if (!m.on) return;
+  const int64_t gdq = rows_grid(m.DQ.npos).x, gu = rows_grid(m.U.npos).x;
+  const dim3 g((unsigned)(gdq + gu));
+  if (nd == 2)
+    hipLaunchKernelGGL(k_amg_mprod<2>, g, dim3(kBlock), 0, s, m, lev[1].A.at32, lev[0].RT.val32, lev[1].RT.val32,
+                       lev[0].PT.val32, lev[1].PT.val32, gdq);
+  else
+    hipLaunchKernelGGL(k_amg_mprod<3>, g, dim3(kBlock), 0, s, m, lev[1].A.at32, lev[0].RT.val32, lev[1].RT.val32,
+                       lev[0].PT.val32, lev[1].PT.val32, gdq);
 }
 void launch_amg_vstep(hipStream_t s, int nd, const AmgLevD* lev, int l, const AmgCg& cg, int step,
                       const int32_t* gate) {

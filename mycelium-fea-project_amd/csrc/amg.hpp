@@ -260,6 +260,31 @@ struct AmgCollapse {
 std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t max_pairs, int min_level,
                                AmgCollapse& out);
 
+// Levels 0 and 1 merged around a cycle collapsed at level 2 (amg_collapse.cpp
+// build_amg_merge; C2-sized networks, whose launches are latency-bound).
+// With x_0 the level-0 iterate the compact cycle computes
+//   c_0 = (2I − Ã_0) x_0,  c_1 = (2I − Ã_1) R̂_0 x_0,  x_2 = R̂_1 R̂_0 x_0,
+//   e_2 = V_2 x_2,  u = c_0 + P̃_0 (c_1 + P̃_1 e_2),
+// so with  DQ = [2R̂_0 − Ã_1 R̂_0 ; R̂_1 R̂_0]  (rows: level 1, then level 2)
+// and  U = [P̃_0 | P̃_0 P̃_1]  the cycle is one down launch (DQ rows + Ã_0
+// rows), V_2, and one up launch: 3 launches where the two-level form takes 5.
+// The vectors live in one buffer B = [c_1 (n1) | x_2 (n2) | e_2 (n2) | scratch].
+struct AmgMerge {
+  bool on = false;
+  int64_t n0 = 0, n1 = 0, n2 = 0;
+  SellPat DQ;                   // rows: c_1's (padded to 64) then x_2's; cols: level-0 rows
+  std::vector<int32_t> dq_dst;  // DQ row → its index in B
+  int64_t dq_split = 0;         // positions below: c_1 rows (Ã_1 × R̂_0 pairs + 2 R̂_0); above: R̂_1 × R̂_0
+  std::vector<int32_t> dq_ext;  // per DQ position: the R̂_0 position of the block (× 2), or −1
+  PosList dq_l;                 // per DQ position: (Ã_1 or R̂_1 position, R̂_0 position) pairs
+  SellPat U;                    // rows: P̃_0's SELL rows (pt_row of level 0); cols: indices in B
+  std::vector<int32_t> u_ext;   // per U position: the P̃_0 position of the block, or −1
+  PosList u_l;                  // per U position: (P̃_0 position, P̃_1 position) pairs
+};
+// on = false (nothing built) unless the plan's cycle collapses at level 2
+// (coll.kc == 2) on one partition.
+std::string build_amg_merge(const AmgPlan& plan, const AmgCollapse& coll, AmgMerge& out);
+
 // Block-Jacobi multicolour sweeps over A_0 (MFEA_PC_SOR, MFEA_PC_ICC; sweep.hip):
 // level-0 rows in blocks of `rows_per_block` consecutive rows (one workgroup
 // each — the couplings between blocks are dropped, as PETSc's processor-local

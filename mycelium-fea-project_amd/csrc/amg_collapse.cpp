@@ -278,4 +278,123 @@ std::string build_amg_collapse(const AmgPlan& plan, int64_t max_bytes, int64_t m
   return "";
 }
 
+// ---- levels 0 and 1 merged (amg.hpp AmgMerge) --------------------------------
+namespace {
+// Prod M plus, per row, the entries of E (an ext term) merged in by column:
+// entries only in E get no pairs; extra[e] = E's position or -1
+Prod merge_ext(const Prod& M, const Rows& E) {
+  Prod W;
+  W.n = M.n;
+  for (int64_t i = 0; i < M.n; ++i) {
+    std::vector<std::pair<int32_t, int32_t>> er;  // (col, E pos)
+    for (int64_t t = E.ptr[i]; t < E.ptr[i + 1]; ++t)
+      if (E.col[t] >= 0) er.emplace_back(E.col[t], E.pos[t]);
+    std::sort(er.begin(), er.end());
+    size_t u = 0;
+    int64_t e = M.ptr[i];
+    while (e < M.ptr[i + 1] || u < er.size()) {
+      const int32_t cm = e < M.ptr[i + 1] ? M.col[e] : INT32_MAX;
+      const int32_t ce = u < er.size() ? er[u].first : INT32_MAX;
+      const int32_t c = std::min(cm, ce);
+      W.col.push_back(c);
+      W.extra.push_back(ce == c ? er[u].second : -1);
+      if (cm == c) {
+        for (int64_t t = M.lptr[e]; t < M.lptr[e + 1]; ++t) {
+          W.a.push_back(M.a[t]);
+          W.b.push_back(M.b[t]);
+        }
+        ++e;
+      }
+      if (ce == c) ++u;
+      W.lptr.push_back((int64_t)W.a.size());
+    }
+    W.ptr.push_back((int64_t)W.col.size());
+  }
+  return W;
+}
+}  // namespace
+
+std::string build_amg_merge(const AmgPlan& plan, const AmgCollapse& coll, AmgMerge& out) {
+  out = AmgMerge();
+  const int nlev = (int)plan.lev.size();
+  if (coll.kc != 2 || nlev < 4 || plan.n_dist > 0) return "";
+  const AmgLevel &L0 = plan.lev[0], &L1 = plan.lev[1];
+  if (L0.PT.n != L0.A.n || L1.PT.n != L1.A.n || L0.RT.n <= 0 || L1.RT.n <= 0) return "";
+  const int64_t n0 = L0.A.n, n1 = L1.A.n, n2 = plan.lev[2].A.n;
+  const Rows R0 = rows_of(L0.RT, &L0.rt_row);  // level-1 rows → (level-0 col, R̂_0 position)
+  const Rows A1 = rows_of(L1.A);               // level-1 rows → (level-1 col, Ã_1 position)
+  const Rows R1 = rows_of(L1.RT, &L1.rt_row);  // level-2 rows → (level-1 col, R̂_1 position)
+  const Rows P0 = rows_of(L0.PT, &L0.pt_row);  // level-0 rows → (level-1 col, P̃_0 position)
+  const Rows P1 = rows_of(L1.PT, &L1.pt_row);  // level-1 rows → (level-2 col, P̃_1 position)
+  // c_1 rows: 2 R̂_0 − Ã_1 R̂_0; x_2 rows: R̂_1 R̂_0; U: P̃_0 ∪ P̃_0 P̃_1
+  Prod C1, Q, W;
+  spgemm(n1, &A1, R0, n0, C1);
+  C1 = merge_ext(C1, R0);
+  spgemm(n2, &R1, R0, n0, Q);
+  Q.extra.assign(Q.col.size(), -1);
+  spgemm(n0, &P0, P1, n2, W);
+  // U's columns are B indices: c_1 at [0, n1), e_2 at [n1 + n2, n1 + 2 n2)
+  for (auto& c : W.col) c += (int32_t)(n1 + n2);
+  Prod Uc = merge_ext(W, P0);  // (P̃_0's columns < n1 sort before W's)
+  // layouts: c_1 rows and x_2 rows each by length inside windows, the c_1
+  // part padded to whole slices (the setup tells the two by position)
+  SellPat S1, S2;
+  std::vector<int32_t> e1, e2;
+  const std::vector<int32_t> p1 = window_perm(C1), p2 = window_perm(Q);
+  layout_prod(C1, p1, S1, e1);
+  layout_prod(Q, p2, S2, e2);
+  const int64_t n1p = (n1 + 63) / 64 * 64, scratch = n1 + 2 * n2;
+  SellPat& DQ = out.DQ;
+  DQ.n = n1p + n2;
+  DQ.sptr = S1.sptr;
+  for (size_t k = 1; k < S2.sptr.size(); ++k) DQ.sptr.push_back(S1.sptr.back() + S2.sptr[k]);
+  DQ.col = S1.col;
+  DQ.col.insert(DQ.col.end(), S2.col.begin(), S2.col.end());
+  DQ.rlen.assign(DQ.n, 0);
+  for (int64_t r = 0; r < n1; ++r) DQ.rlen[r] = S1.rlen[r];
+  for (int64_t r = 0; r < n2; ++r) DQ.rlen[n1p + r] = S2.rlen[r];
+  if (DQ.n_pos() > INT32_MAX) return "";
+  out.dq_split = S1.n_pos();
+  out.dq_dst.assign(DQ.n, (int32_t)scratch);
+  for (int64_t J = 0; J < n1; ++J) out.dq_dst[p1[J]] = (int32_t)J;
+  for (int64_t J = 0; J < n2; ++J) out.dq_dst[n1p + p2[J]] = (int32_t)(n1 + J);
+  for (auto& e : e2) e += (int32_t)out.dq_split;
+  // one list set over DQ's positions (C_1's then Q's)
+  {
+    Prod M;  // C1 and Q as one product for to_lists (rows n1 + n2, entry order kept)
+    M.n = n1 + n2;
+    M.ptr = C1.ptr;
+    for (size_t k = 1; k < Q.ptr.size(); ++k) M.ptr.push_back(C1.ptr.back() + Q.ptr[k]);
+    M.col = C1.col;
+    M.col.insert(M.col.end(), Q.col.begin(), Q.col.end());
+    M.lptr = C1.lptr;
+    for (size_t k = 1; k < Q.lptr.size(); ++k) M.lptr.push_back(C1.lptr.back() + Q.lptr[k]);
+    M.a = C1.a;
+    M.a.insert(M.a.end(), Q.a.begin(), Q.a.end());
+    M.b = C1.b;
+    M.b.insert(M.b.end(), Q.b.begin(), Q.b.end());
+    std::vector<int32_t> ep = e1;
+    ep.insert(ep.end(), e2.begin(), e2.end());
+    to_lists(M, ep, DQ.n_pos(), out.dq_l);
+    out.dq_ext.assign(DQ.n_pos(), -1);
+    for (size_t e = 0; e < C1.col.size(); ++e) out.dq_ext[e1[e]] = C1.extra[e];
+  }
+  // U in P̃_0's row order: SELL row r holds level-0 row pt_row[r]
+  {
+    std::vector<int32_t> uperm(n0);
+    for (int64_t r = 0; r < n0; ++r) uperm[L0.pt_row[r]] = (int32_t)r;
+    std::vector<int32_t> eu;
+    layout_prod(Uc, uperm, out.U, eu);
+    if (out.U.n_pos() > INT32_MAX) return "";
+    to_lists(Uc, eu, out.U.n_pos(), out.u_l);
+    out.u_ext.assign(out.U.n_pos(), -1);
+    for (size_t e = 0; e < Uc.col.size(); ++e) out.u_ext[eu[e]] = Uc.extra[e];
+  }
+  out.n0 = n0;
+  out.n1 = n1;
+  out.n2 = n2;
+  out.on = true;
+  return "";
+}
+
 }  // namespace mfea

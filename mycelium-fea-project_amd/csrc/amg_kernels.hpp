@@ -121,6 +121,29 @@ struct AmgLevD {
   int collapsed = 0;  // 1 on levels ≥ kc that hold CT / CV
 };
 
+// Levels 0 and 1 merged around a cycle collapsed at level 2 (amg.hpp AmgMerge):
+// DQ (rows: c_1's, then x_2's; dq_dst: their index in B) and U = [P̃_0 | P̃_0 P̃_1]
+// (P̃_0's row order), f32 values formed every setup from the lists; B the
+// cycle's vectors [c_1 | x_2 | e_2 | scratch] (level 2's x and e point into it).
+struct AmgMergeD {
+  int on = 0;
+  int64_t n1 = 0, n2 = 0;
+  AmgMatD DQ, U;
+  const int32_t* dq_dst = nullptr;
+  int64_t dq_split = 0;
+  const int32_t* dq_ext = nullptr;
+  const int32_t* dq_ptr = nullptr;
+  const int32_t* dq_a = nullptr;
+  const int32_t* dq_b = nullptr;
+  const int32_t* u_ext = nullptr;
+  const int32_t* u_ptr = nullptr;
+  const int32_t* u_a = nullptr;
+  const int32_t* u_b = nullptr;
+  float* B = nullptr;
+};
+// the merged operators' values (after the levels' setup and the collapse)
+void launch_amg_merge_setup(hipStream_t s, int nd, const AmgLevD* lev, const AmgMergeD& m);
+
 // CG vectors of the AMG path (f64): free rows in level-0 order, ND per row
 struct AmgCg {
   int64_t n = 0;
@@ -216,7 +239,7 @@ void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev,
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).
 // l0 > 0: only levels [l0, nlev), on level l0's b and x (its output: e).
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
-                       int tail, const int32_t* gate, int l0 = 0);
+                       int tail, const int32_t* gate, int l0 = 0, const AmgMergeD* mg = nullptr);
 // one step of the V-cycle on level l (the distributed schedule interleaves
 // exchanges): t = b − A x, restriction into level l+1, x += P e_{l+1}, post-smoothing
 constexpr int kStepResid = 0, kStepRestrict = 1, kStepProlong = 2, kStepPost = 3;

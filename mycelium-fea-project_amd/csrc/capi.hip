@@ -118,6 +118,10 @@ struct Part {
   // SA-AMG preconditioner (amg.hpp): symbolic plan for the active set amg_key
   AmgPlan amg;
   AmgCollapse amg_coll;  // the compact cycle below level kc as one operator (amg_collapse.cpp)
+  AmgMerge amg_mplan;    // levels 0 and 1 merged around the collapsed cycle (amg.hpp AmgMerge)
+  AmgMergeD amg_mg;
+  float* amg_x2 = nullptr;  // level 2's own x / e (the merged cycle points them into amg_mg.B)
+  float* amg_e2 = nullptr;
   bool amg_ok = false;
   std::vector<uint8_t> amg_key;
   int64_t amg_gen = 0;               // bumped on every rebuild (captured graphs hold its pointers)
@@ -242,6 +246,7 @@ struct mfea_handle {
   int opt_amg_w_k = 0;         // GAMG: w = A u step width (0: by level 0's mean slice width, 1, 2)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_down_split = 0;  // GAMG compact down sweep: R̂ and Ã rows as two launches (experiment)
+  int opt_amg_merge = -1;      // GAMG: levels 0 and 1 merged around a level-2 collapse (-1: small networks, 0 off, 1 on)
   int opt_amg_v_lanes = 0;     // GAMG collapsed cycle: lanes per V row (0: by width; 1, 2, 4, 8, 16)
   int64_t opt_amg_small_lanes = 65536;  // GAMG: wide rows of small levels at 16 lanes below this many threads
   int opt_amg_alanes = 0;      // GAMG: operator lanes per row below level 0 (0: by width)
@@ -1136,6 +1141,7 @@ static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
 // 0.3 M product pairs, a few ms of host build per rebuild) for one saved
 // launch pair; level 2 is what C2 / C3 choose anyway
 constexpr int kAmgCollapseAutoLevel = 2;
+constexpr int64_t kMergeRows = 131072;  // amg_merge -1: level-0 rows up to which levels 0 and 1 merge
 
 // ρ̂ of the levels below 0 (0: the Gershgorin rule), until a solve has failed
 // with it
@@ -1208,6 +1214,19 @@ int omega_retry(mfea_handle* h, F&& again) {
   return rc;
 }
 
+// the merged cycle on or off (built plans only): level 2's x / e point into
+// the merged vector buffer while on
+void set_merge(mfea_handle* h, Part& pt) {
+  const bool on = pt.amg_mplan.on && h->opt_amg_merge != 0 && pt.amg_lev.size() >= 4 && pt.amg_cg.coll == 2;
+  pt.amg_mg.on = on ? 1 : 0;
+  if (pt.amg_lev.size() > 2) {
+    AmgLevD& L2 = pt.amg_lev[2];
+    const int nd = pt.amg.nd;
+    L2.x = on ? pt.amg_mg.B + (size_t)nd * pt.amg_mg.n1 : pt.amg_x2;
+    L2.e = on ? pt.amg_mg.B + (size_t)nd * (pt.amg_mg.n1 + pt.amg_mg.n2) : pt.amg_e2;
+  }
+}
+
 int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = nullptr,
                const PosList* a0 = nullptr, const std::vector<int32_t>* row0 = nullptr) {
   const int nd = pl.nd, nb2 = nd * nd;
@@ -1220,6 +1239,15 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
                                                 h->opt_amg_collapse < 0 ? kAmgCollapseAutoLevel : std::max(1, h->opt_amg_collapse),
                                                 pt.amg_coll);
     if (!cerr.empty()) return fail(MFEA_EINVAL, cerr);
+  }
+  // levels 0 and 1 merged (amg.hpp AmgMerge): where the launches are latency-
+  // bound — level 0 under kMergeRows rows (C2: 34 k; C3's 336 k measured
+  // slower merged: its c_1 / x_2 / W rows add more bytes than two launches cost)
+  pt.amg_mplan = AmgMerge();
+  if (!rk && h->opt_amg_merge != 0 && pt.amg_coll.kc == 2 && nlev >= 4 &&
+      (h->opt_amg_merge > 0 || pl.lev[0].A.n <= kMergeRows)) {
+    const std::string merr = build_amg_merge(pl, pt.amg_coll, pt.amg_mplan);
+    if (!merr.empty()) return fail(MFEA_EINVAL, merr);
   }
   int32_t* ip = nullptr;
   double* dp = nullptr;
@@ -1388,8 +1416,32 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.w = D((size_t)nd * nf);
     pt.amg_cg.r = D((size_t)nd * nf);
     pt.amg_cg.u = F((size_t)nd * nf);
+    // the merged levels' operators, lists and vector buffer
+    pt.amg_mg = AmgMergeD{};
+    if (pt.amg_mplan.on) {
+      const AmgMerge& M = pt.amg_mplan;
+      AmgMergeD& g = pt.amg_mg;
+      g.n1 = M.n1;
+      g.n2 = M.n2;
+      g.DQ = mat(M.DQ, false, true);
+      g.U = mat(M.U, false, true);
+      g.dq_dst = I(M.dq_dst);
+      g.dq_split = M.dq_split;
+      g.dq_ext = I(M.dq_ext);
+      g.dq_ptr = I(M.dq_l.ptr);
+      g.dq_a = I(M.dq_l.a);
+      g.dq_b = I(M.dq_l.b);
+      g.u_ext = I(M.u_ext);
+      g.u_ptr = I(M.u_l.ptr);
+      g.u_a = I(M.u_l.a);
+      g.u_b = I(M.u_l.b);
+      g.B = F((size_t)nd * (M.n1 + 2 * M.n2 + 1));
+    }
   }
   HIPC(err);
+  pt.amg_x2 = nlev > 2 ? pt.amg_lev[2].x : nullptr;
+  pt.amg_e2 = nlev > 2 ? pt.amg_lev[2].e : nullptr;
+  set_merge(h, pt);
   {
     std::vector<int64_t> rows(nlev);
     for (int l = 0; l < nlev; ++l) rows[l] = pl.lev[l].A.n;
@@ -1544,7 +1596,8 @@ int upload_sweep(mfea_handle* h, Part& pt, int kind) {
 // flag; NULL: ungated)
 void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate) {
   if (pt.amg_cg.sweep) launch_sweep(h->stream, pt.amg.nd, pt.swd, pt.amg_cg, gate);
-  else launch_amg_vcycle(h->stream, pt.amg.nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, gate);
+  else launch_amg_vcycle(h->stream, pt.amg.nd, pt.amg_lev.data(), (int)pt.amg_lev.size(), pt.amg_cg, pt.amg_tail, gate,
+                         0, pt.amg_mg.on ? &pt.amg_mg : nullptr);
 }
 
 // (Re)build the hierarchy when the active set differs from the plan's.  One
@@ -1779,11 +1832,12 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   }
   if (fused) {
     launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
-    return;
+  } else {
+    for (int l = 0; l < nlev; ++l)
+      launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
+    launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
   }
-  for (int l = 0; l < nlev; ++l)
-    launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
-  launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
+  if (pt.amg_mg.on) launch_amg_merge_setup(s, nd, pt.amg_lev.data(), pt.amg_mg);
 }
 
 uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
@@ -1800,6 +1854,7 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   hipStream_t s = h->stream;
   uint64_t k = 1469598103934665603ULL;
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
+  k = fnv1a(k, &pt.amg_mg, sizeof pt.amg_mg);
   const SellOp op = sell_op(pt);
   k = fnv1a(k, &op, sizeof op);
   const void* ptrs[4] = {pt.amg_cg.row0, pt.amg_a0_ptr, pt.amg_a0_a, pt.amg_levd.ptr};
@@ -3468,6 +3523,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts)
       for (auto& L : pp->amg_lev) L.small_lanes = value;
   }
+  else if (n == "amg_merge") {
+    if (value < -1 || value > 1) return fail(MFEA_EINVAL, "amg_merge: -1 (small networks), 0 or 1");
+    h->opt_amg_merge = (int)value;
+    rebuild = true;
+  }
   else if (n == "amg_down_split") {
     h->opt_amg_down_split = value != 0;
     for (auto& pp : h->parts)
@@ -3708,6 +3768,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_restrict_lanes") *value = h->opt_amg_rlanes;
   else if (n == "amg_down_split") *value = h->opt_amg_down_split;
   else if (n == "amg_v_lanes") *value = h->opt_amg_v_lanes;
+  else if (n == "amg_merge") *value = h->opt_amg_merge;
+  else if (n == "amg_merged") *value = part0(h).amg_mg.on;  // read-only: the plan's cycle form
   else if (n == "amg_small_lanes") *value = h->opt_amg_small_lanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;

@@ -273,6 +273,40 @@ int64_t shim_coll_array(int k, const char* name, int32_t* out) {
   return (int64_t)v->size();
 }
 
+// levels 0 and 1 merged around the last collapse (amg.hpp AmgMerge)
+static AmgMerge g_merge;
+int shim_amg_merge(char* err, int errn) {
+  std::string e = build_amg_merge(g_amg, g_coll, g_merge);
+  if (!e.empty()) {
+    std::snprintf(err, errn, "%s", e.c_str());
+    return -1;
+  }
+  return g_merge.on ? 1 : 0;
+}
+int64_t shim_merge_array(const char* name, int32_t* out) {
+  const std::string n(name);
+  if (n == "n1") return g_merge.n1;
+  if (n == "n2") return g_merge.n2;
+  if (n == "dq_split") return g_merge.dq_split;
+  const std::vector<int32_t>* v = nullptr;
+  if (n == "DQ.sptr") v = &g_merge.DQ.sptr;
+  else if (n == "DQ.col") v = &g_merge.DQ.col;
+  else if (n == "dq_dst") v = &g_merge.dq_dst;
+  else if (n == "dq_ext") v = &g_merge.dq_ext;
+  else if (n == "dq.ptr") v = &g_merge.dq_l.ptr;
+  else if (n == "dq.a") v = &g_merge.dq_l.a;
+  else if (n == "dq.b") v = &g_merge.dq_l.b;
+  else if (n == "U.sptr") v = &g_merge.U.sptr;
+  else if (n == "U.col") v = &g_merge.U.col;
+  else if (n == "u_ext") v = &g_merge.u_ext;
+  else if (n == "u.ptr") v = &g_merge.u_l.ptr;
+  else if (n == "u.a") v = &g_merge.u_l.a;
+  else if (n == "u.b") v = &g_merge.u_l.b;
+  else return -1;
+  if (out && !v->empty()) std::memcpy(out, v->data(), v->size() * 4);
+  return (int64_t)v->size();
+}
+
 // one rank's share of the last distributed plan (amg_dist.cpp)
 static AmgRank g_rank;
 int shim_amg_rank(int rank, char* err, int errn) {

@@ -384,3 +384,84 @@ def test_auto_form_choice_is_collective(shim):
     tmax = tuple(max(t[k] for t in ranks) for k in range(2))
     assert [shim.shim_amg_auto_choice(*tmax) for _ in ranks] == [1, 1]
     assert shim.shim_amg_auto_choice(1e-3, 1e-3) == 1   # ties: the global hierarchy
+
+
+def test_merged_levels_equal_the_compositions(shim):
+    """Levels 0 and 1 merged around the level-2 collapse (amg.hpp AmgMerge,
+    amg_collapse.cpp build_amg_merge): the DQ and U values the plan's lists
+    give (amg.hip k_amg_mprod, here in f64) are exactly 2R̂₀ − Ã₁R̂₀, R̂₁R̂₀,
+    P̃₀ and P̃₀P̃₁ — so the 3-launch cycle applies the same preconditioner."""
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, _ = setup_case(shim, xyz, e2n, top, bot, np.ones(len(e2n)), 2)
+    amg_ref.compact_transfers(levels)
+    amg_ref.scaled_blocks(levels)
+    nlev = len(levels)
+    assert nlev >= 4
+    shim.shim_amg_collapse.restype = C.c_int
+    shim.shim_amg_collapse.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_char_p, C.c_int]
+    shim.shim_amg_merge.restype = C.c_int
+    shim.shim_amg_merge.argtypes = [C.c_char_p, C.c_int]
+    shim.shim_merge_array.restype = C.c_int64
+    shim.shim_merge_array.argtypes = [C.c_char_p, P]
+    err = C.create_string_buffer(256)
+    assert shim.shim_amg_collapse(1 << 40, 1 << 40, 2, err, 256) == 2, err.value
+    assert shim.shim_amg_merge(err, 256) == 1, err.value
+
+    def arr(name):
+        m = shim.shim_merge_array(name.encode(), None)
+        a = np.zeros(max(m, 0), np.int32)
+        if m > 0:
+            shim.shim_merge_array(name.encode(), a.ctypes.data_as(P))
+        return a
+
+    n0, n1, n2 = levels[0]["n"], levels[1]["n"], levels[2]["n"]
+    assert shim.shim_merge_array(b"n1", None) == n1 and shim.shim_merge_array(b"n2", None) == n2
+    split = shim.shim_merge_array(b"dq_split", None)
+    L0, L1 = levels[0], levels[1]
+    nd = L0["dinv"].shape[1]
+
+    def evaluate(col, ext, ptr, la, lb, X, Y, E, f, sgn):
+        out = np.zeros((len(col), nd, nd))
+        for q in np.flatnonzero(col >= 0):
+            acc = np.zeros((nd, nd))
+            for t in range(ptr[q], ptr[q + 1]):
+                acc = acc + X(q)[la[t]] @ Y[lb[t]]
+            base = f * E[ext[q]] if ext[q] >= 0 else np.zeros((nd, nd))
+            out[q] = base + sgn(q) * acc
+        return out
+
+    # DQ: c_1 rows (positions < split: Ã_1 × R̂_0, + 2 R̂_0), then x_2 rows (R̂_1 × R̂_0)
+    dcol = arr("DQ.col")
+    DQb = evaluate(dcol, arr("dq_ext"), arr("dq.ptr"), arr("dq.a"), arr("dq.b"),
+                   lambda q: L1["Atb"] if q < split else L1["Rhb"], L0["Rhb"], L0["Rhb"], 2.0,
+                   lambda q: -1.0 if q < split else 1.0)
+    dst = arr("dq_dst")
+    dq = amg_ref.to_scipy(DQb, arr("DQ.sptr"), dcol, len(dst), n0, nd).tocoo()
+    rows = dst[dq.row // nd]
+    keep_c1, keep_q = rows < n1, (rows >= n1) & (rows < n1 + n2)
+    C1 = sp.csr_matrix((dq.data[keep_c1], (rows[keep_c1] * nd + dq.row[keep_c1] % nd, dq.col[keep_c1])),
+                       shape=(n1 * nd, n0 * nd))
+    Qm = sp.csr_matrix((dq.data[keep_q], ((rows[keep_q] - n1) * nd + dq.row[keep_q] % nd, dq.col[keep_q])),
+                       shape=(n2 * nd, n0 * nd))
+    R0 = amg_ref.to_scipy(L0["Rhb"], L0["RT.sptr"], L0["RT.col"], n1, n0, nd, L0["rt_row"])
+    R1 = amg_ref.to_scipy(L1["Rhb"], L1["RT.sptr"], L1["RT.col"], n2, n1, nd, L1["rt_row"])
+    A1 = amg_ref.to_scipy(L1["Atb"], L1["A.sptr"], L1["A.col"], n1, n1, nd)
+    ref_c1 = (2.0 * R0 - A1 @ R0).toarray()
+    assert np.abs(C1.toarray() - ref_c1).max() <= 1e-12 * np.abs(ref_c1).max()
+    ref_q = (R1 @ R0).toarray()
+    assert np.abs(Qm.toarray() - ref_q).max() <= 1e-12 * np.abs(ref_q).max()
+    # U: P̃_0's row order; columns c_1 at [0, n1), e_2 at [n1 + n2, n1 + 2 n2)
+    ucol = arr("U.col")
+    Ub = evaluate(ucol, arr("u_ext"), arr("u.ptr"), arr("u.a"), arr("u.b"), lambda q: L0["PTb"], L1["PTb"],
+                  L0["PTb"], 1.0, lambda q: 1.0)
+    Ua = amg_ref.to_scipy(Ub, arr("U.sptr"), ucol, n0, n1 + 2 * n2, nd).tocoo()
+    r = L0["pt_row"][Ua.row // nd] * nd + Ua.row % nd
+    c = Ua.col // nd
+    lo, hi = c < n1, c >= n1 + n2
+    Pm = sp.csr_matrix((Ua.data[lo], (r[lo], Ua.col[lo])), shape=(n0 * nd, n1 * nd)).toarray()
+    Wm = sp.csr_matrix((Ua.data[hi], (r[hi], Ua.col[hi] - (n1 + n2) * nd)), shape=(n0 * nd, n2 * nd)).toarray()
+    assert np.abs(Pm - L0["Pt"].toarray()).max() <= 1e-12 * np.abs(Pm).max()
+    ref_w = (L0["Pt"] @ L1["Pt"]).toarray()
+    assert np.abs(Wm - ref_w).max() <= 1e-12 * np.abs(ref_w).max()
+    # indices stay inside what the device arrays hold
+    assert dst.max() <= n1 + 2 * n2 and ucol.max() < n1 + 2 * n2 and dcol.max() < n0

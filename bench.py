@@ -99,6 +99,9 @@ def amg_iteration_bytes(ai, compact=None):
       up       tb·(B+4) + 2V·n + V·n'              (P̃, c in, e out; e' in)
     collapsed below level kc (collapse_level > 0; vb blocks of V): the levels
     ≥ kc are one sweep  vapply  vb·(B+4) + 2V·n_kc  (V, x in; e out).
+    Levels 0 and 1 merged around kc = 2 (merged; dqb blocks of DQ, ub of U):
+      down     dqb·(B+4) + nb0·(B+4) + 2V·n0 + V·(n1 + n2)   (DQ, Ã_0, x_0 in; c_0, c_1, x_2 out)
+      up       ub·(B+4) + 2V·n0 + V·(n1 + n2)                (U, c_0, c_1, e_2 in; u out)
     CG: update (9·V8 + V + B + V)·n0 (u w p s x r in, p s x r out, D⁻¹, x₀ out);
         w      nb0·(Bs8+4) + (2·V8 + V)·n0         (A_0, r, u in; w out).
     """
@@ -110,6 +113,13 @@ def amg_iteration_bytes(ai, compact=None):
         compact = ai.get("cycle", 0) == 1
     kc = ai.get("collapse_level", 0) if compact else 0
     b = 0
+    if compact and kc == 2 and ai.get("merged"):
+        n0, n1, n2 = rows[0], rows[1], rows[2]
+        b += ai["merge_dq_blocks"] * (B + 4) + blocks[0] * (B + 4) + 2 * V * n0 + V * (n1 + n2)
+        b += ai["collapse_blocks"] * (B + 4) + 2 * V * n2
+        b += ai["merge_u_blocks"] * (B + 4) + 2 * V * n0 + V * (n1 + n2)
+        b += (9 * V8 + V + B + V) * n0 + blocks[0] * (Bs8 + 4) + (2 * V8 + V) * n0
+        return b
     for l in range(ai["levels"] - 1):
         n, nn = rows[l], rows[l + 1]
         Vb = V8 if l == 0 else V
@@ -527,6 +537,9 @@ def main(argv=None):
             kc = ai.get("collapse_level", 0)
             launches = 2 + (2 * kc + 1 if kc else 2 * (nl - 1))
             form = f"compact, collapsed below level {kc}" if kc else "compact"
+            if kc == 2 and ai.get("merged"):
+                launches = 5
+                form = "compact, levels 0-1 merged, collapsed below level 2"
         else:
             # levels from the first one of ≤ 2048 rows (above the coarsest) run
             # in one single-workgroup launch (the engine's default amg_tail_rows)

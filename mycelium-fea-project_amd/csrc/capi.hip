@@ -3770,6 +3770,13 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_v_lanes") *value = h->opt_amg_v_lanes;
   else if (n == "amg_merge") *value = h->opt_amg_merge;
   else if (n == "amg_merged") *value = part0(h).amg_mg.on;  // read-only: the plan's cycle form
+  else if (n == "amg_merge_dq_blocks" || n == "amg_merge_u_blocks") {  // read-only: stored blocks of DQ / U
+    const AmgMerge& M = part0(h).amg_mplan;
+    int64_t nb = 0;
+    if (M.on)
+      for (int32_t c : (n == "amg_merge_dq_blocks" ? M.DQ.col : M.U.col)) nb += c >= 0;
+    *value = nb;
+  }
   else if (n == "amg_small_lanes") *value = h->opt_amg_small_lanes;
   else if (n == "amg_op_lanes") *value = h->opt_amg_alanes;
   else if (n == "amg_tail_lds") *value = h->opt_amg_tail_lds;

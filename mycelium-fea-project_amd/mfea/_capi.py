@@ -483,7 +483,10 @@ class Engine:
                 "pair_items": items.value, "nd": nd.value, "n_dist": ndist.value,
                 "cycle": self.get_option("amg_cycle"),
                 "collapse_level": self.get_option("amg_collapse_level"),
-                "collapse_blocks": self.get_option("amg_collapse_blocks")}
+                "collapse_blocks": self.get_option("amg_collapse_blocks"),
+                "merged": self.get_option("amg_merged"),
+                "merge_dq_blocks": self.get_option("amg_merge_dq_blocks"),
+                "merge_u_blocks": self.get_option("amg_merge_u_blocks")}
 
     def amg_vcycle(self, r):
         """mfea_debug_amg_vcycle: one GAMG V-cycle u = M r (n_nodes × ND, original

@@ -72,6 +72,16 @@ def test_amg_iteration_bytes_compact_by_hand(bench):
     down1 = tb1 * (B + 4) + nb1 * (B + 4) + 2 * V * nn + V * n2
     up1 = tb1 * (B + 4) + 2 * V * nn + V * n2
     assert bench.amg_iteration_bytes(dict(ai3, collapse_level=0)) == down + up + down1 + up1 + update + w
+    # levels 0 and 1 merged around a level-2 collapse: one down sweep (DQ and
+    # Ã_0 rows), V at level 2, one up sweep (U rows)
+    n3, dqb, ub = 10, 7000, 5000
+    ai4 = {"nd": 2, "levels": 4, "rows": [n, nn, n2, n3], "blocks": [nb, nb1, 300, n3],
+           "pblocks": [1800, 600, 50, 0], "ptblocks": [tb, tb1, 80, 0], "cycle": 1, "collapse_level": 2,
+           "collapse_blocks": vb, "merged": 1, "merge_dq_blocks": dqb, "merge_u_blocks": ub}
+    mdown = dqb * (B + 4) + nb * (B + 4) + 2 * V * n + V * (nn + n2)
+    mv = vb * (B + 4) + 2 * V * n2
+    mup = ub * (B + 4) + 2 * V * n + V * (nn + n2)
+    assert bench.amg_iteration_bytes(ai4) == mdown + mv + mup + update + w
 
 
 # ---- the multi-GPU launcher (bench.py --gpus N), no GPU -----------------------

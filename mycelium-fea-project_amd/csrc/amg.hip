@@ -1370,10 +1370,16 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
   }
   // the first pass's row operands are issued behind the partials (loads
   // return in order: the scalars need only the partials) and are in flight
-  // while α, β are formed
+  // while α, β are formed — D⁻¹ for level 0's x = ω D⁻¹ r with them, and ω
+  // through scalar loads: issued per row behind the stores (vcycle_entry),
+  // they put one more round trip at the end of every row (the compiler cannot
+  // move a load of ω across the row's stores)
   const int64_t stride = (int64_t)gridDim.x * BS;
   const int64_t i0 = cg.lo + (int64_t)blockIdx.x * BS + threadIdx.x;
+  const bool x0_here = !cg.sweep && !L0.coarsest;  // (else vcycle_entry)
+  const float om0 = x0_here ? (float)amg_omega_s(L0.omega) : 0.0f;
   double u[ND], w[ND], p[ND], s[ND], x[ND], r[ND];
+  float Di[ND * ND];
   if (cg.hi > cg.lo) {
     const int64_t k = i0 < cg.hi ? i0 : cg.hi - 1;
     vload<ND>(cg.u, k, u);
@@ -1382,6 +1388,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
     vload<ND>(cg.s, k, s);
     vload<ND>(cg.x, k, x);
     vload<ND>(cg.r, k, r);
+    if (x0_here) dinv_load<ND>(L0.dinv32, k, Di);
   }
   if (norm == 1 && f0 == kInit) {
     // PETSc's preconditioned norm (KSP_NORM_PRECONDITIONED, src/fea_petsc.cpp:336-341):
@@ -1405,6 +1412,7 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
       vload<ND>(cg.s, i, s);
       vload<ND>(cg.x, i, x);
       vload<ND>(cg.r, i, r);
+      if (x0_here) dinv_load<ND>(L0.dinv32, i, Di);
     }
 #pragma unroll
     for (int a = 0; a < ND; ++a) {
@@ -1417,7 +1425,15 @@ __global__ __launch_bounds__(BS) void k_amg_cg_update(int j, AmgLevD L0, AmgCg c
     vstore<ND>(cg.s, i, s);
     vstore<ND>(cg.x, i, x);
     vstore<ND>(cg.r, i, r);
-    vcycle_entry<ND>(L0, cg, i, r);
+    if (x0_here) {  // level 0's x = ω D⁻¹ r (vcycle_entry's arithmetic)
+      float rf[ND], x0[ND];
+#pragma unroll
+      for (int a = 0; a < ND; ++a) rf[a] = (float)r[a];
+      dinv_mul<ND>(Di, om0, rf, x0);
+      vstore<ND>(L0.x, i, x0);
+    } else {
+      vcycle_entry<ND>(L0, cg, i, r);
+    }
   }
 }
 

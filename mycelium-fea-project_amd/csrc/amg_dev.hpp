@@ -394,6 +394,13 @@ constexpr double kRhoSafety = 1.45; // ω·g ≤ (4/3)·1.45 < 2
 __device__ __forceinline__ double amg_omega(const double* __restrict__ om) {
   return (4.0 / 3.0) / (om[0] > 0.0 ? om[0] : fmax(kRhoFloor, om[1] / kRhoSafety));
 }
+// ... through scalar loads (omega is written by the setup, read-only in the
+// solve's launches): no vector-load ordering, hoistable across stores
+__device__ __forceinline__ double amg_omega_s(const double* om) {
+  const auto* c = (const __attribute__((address_space(4))) double*)om;
+  const double o0 = c[0], o1 = c[1];
+  return (4.0 / 3.0) / (o0 > 0.0 ? o0 : fmax(kRhoFloor, o1 / kRhoSafety));
+}
 
 // S lanes per row (S = 2, 4) for the SELL operators with wide rows: R's rows
 // hold 7–8 blocks on average and up to 29 (A below level 0: 4–5, up to 16),

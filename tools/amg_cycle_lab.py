@@ -7,7 +7,11 @@ tests/amg_ref.py, then swaps one ingredient at a time:
   base        V(1,1), ω-damped block Jacobi, P_tent = translations (the engine)
   v22         two pre- and two post-smoothing sweeps
   cheb2       Chebyshev degree-2 smoother on D⁻¹A (PETSc GAMG's default)
+  cheb2cK     ... on levels ≥ K only (level 0 keeps V(1,1) Jacobi)
+  v22cK       two Jacobi sweeps on levels ≥ K only
+  cheb2sK / v22sK   ... on level K alone
   w / wK      W-cycle (two coarse corrections per level / on levels < K only)
+  wfK         W-cycle on levels ≥ K only
   rot         near-nullspace with the in-plane rotation: P_tent columns
               (tx, ty, θ) per aggregate (QR-orthonormalised, PyAMG fit_candidates),
               ND = 3 on every coarse level
@@ -171,14 +175,17 @@ def smooth(L, x, b, kind, sweeps):
     return x + y
 
 
-def cycle(levs, b, l, kind, sweeps, gamma, wl=99):
+def cycle(levs, b, l, kind, sweeps, gamma, wl=99, k0=0):
     L = levs[l]
     if L.coarsest:
         return np.linalg.solve(L.A.toarray(), b) if L.A.shape[0] <= 4000 else dapply(L.Dinv, b)
-    x = smooth(L, np.zeros_like(b), b, kind, sweeps)
-    for _ in range(gamma if l + 2 < len(levs) and l < wl else 1):
-        x = x + L.P @ cycle(levs, L.P.T @ (b - L.A @ x), l + 1, kind, sweeps, gamma, wl)
-    return smooth(L, x, b, kind, sweeps)
+    on = l >= k0 if k0 >= 0 else l == -k0  # k0 < 0: level −k0 alone
+    kl, sl = (kind, sweeps) if on else ("jac", 1)
+    x = smooth(L, np.zeros_like(b), b, kl, sl)
+    w_here = l < wl if wl >= 0 else l >= -wl  # wl < 0: W on levels ≥ −wl
+    for _ in range(gamma if l + 2 < len(levs) and w_here else 1):
+        x = x + L.P @ cycle(levs, L.P.T @ (b - L.A @ x), l + 1, kind, sweeps, gamma, wl, k0)
+    return smooth(L, x, b, kl, sl)
 
 
 def main():
@@ -203,16 +210,22 @@ def main():
         if rot not in hier:
             hier[rot] = build_levels(levels, Kff, 2, coords, rot)
         levs = hier[rot]
-        kind, sweeps, gamma, wl = "jac", 1, 1, 99
+        kind, sweeps, gamma, wl, k0 = "jac", 1, 1, 99, 0
         if "cheb2" in v:
             kind, sweeps = "cheb", 2
-        if v == "v22":
+        if v.startswith("v22"):
             sweeps = 2
+        if v.startswith(("cheb2c", "v22c")):
+            k0 = int(v.split("c")[-1])
+        if v.startswith(("cheb2s", "v22s")):
+            k0 = -int(v.split("s")[-1])
         if v.startswith("w"):
             gamma = 2
-            wl = int(v[1:]) if len(v) > 1 else 99
+            wl = int(v[1:]) if len(v) > 1 and v[1] != "f" else 99
+            if v.startswith("wf"):
+                wl = -int(v[2:])
         t = time.time()
-        _, it = amg_ref.pcg(Kff, b, lambda r: cycle(levs, r, 0, kind, sweeps, gamma, wl), rtol=1e-8)
+        _, it = amg_ref.pcg(Kff, b, lambda r: cycle(levs, r, 0, kind, sweeps, gamma, wl, k0), rtol=1e-8)
         print(f"{v:22s} {it:4d} its  levels {len(levs)} rows {[L.A.shape[0] for L in levs][:6]}  "
               f"({time.time() - t:.1f} s)", flush=True)
 

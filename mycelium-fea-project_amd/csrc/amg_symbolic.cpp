@@ -14,7 +14,10 @@
 //      the level-0 A / R layouts 52 % / 28 % in natural order, 97 % / 81 %
 //      with 4096-row windows.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <thread>
 
@@ -107,6 +110,18 @@ int64_t aggregate(const Csr& A, std::vector<int32_t>& agg, const std::vector<uin
 // was 4.9 s on one thread).
 constexpr int kBuildThreads = 16;
 constexpr int64_t kChunkRows = 8192;
+
+// MFEA_BUILD_TIMES=1: the symbolic phase's split on stderr (host build profile)
+struct PhaseClock {
+  bool on = std::getenv("MFEA_BUILD_TIMES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  build %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
 
 int build_threads() {
   const unsigned h = std::thread::hardware_concurrency();
@@ -439,6 +454,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       if (o < 0 || o >= world) return "internal: AMG owner out of range";
   }
   std::string err;
+  PhaseClock clk;
   // ---- stage 1, level 0: free rows, neighbours through active free-free elements
   std::vector<LevelCsr> lv(1);
   Lists a0;  // per A_0 entry: SELL slot positions of the assembled operator
@@ -528,9 +544,11 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       for (int64_t k = A.ptr[i] + 1; k < A.ptr[i + 1]; ++k)
         strong0[k] = w_entry[k] >= strength.theta * std::sqrt(d_row[i] * d_row[A.col[k]]);
   }
+  clk.lap("level-0 rows");
   for (int l = 0;; ++l) {
     LevelCsr& L = lv[l];
     const int64_t na = aggregate(L.A, L.agg, l == 0 && use_strength ? &strong0 : nullptr);
+    clk.lap(l == 0 ? "aggregate l0" : "aggregate l>0");
     if (na == 0 || l + 1 == max_levels) {
       plan.capped = na > 0;  // couplings left: the coarsest block Jacobi is then inexact
       L.agg.clear();
@@ -539,6 +557,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     L.nc = na;
     Csr An;
     if (!(err = coarsen(L, An)).empty()) return err;
+    clk.lap(l == 0 ? "coarsen l0 (P, AP, A1)" : "coarsen l>0");
     lv.emplace_back();
     lv.back().A = std::move(An);
   }
@@ -579,6 +598,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
   }
   plan.world = world;
   plan.n_dist = n_dist;
+  clk.lap("owners");
   // ---- stage 2: row labels per level (sort key: the level's A row plus, for
   // a coarse level, its R row — the two SELL matrices its rows index in the
   // V-cycle; equal keys keep their natural order, which is what keeps a
@@ -639,6 +659,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       for (int64_t i = 0; i < n; ++i) plan.lev[l].owner[perm[l][i]] = own[l][i];
     }
   }
+  clk.lap("row labels (sort_perm)");
   plan.row0.assign(nf, 0);
   for (int64_t i = 0; i < nf; ++i) plan.row0[perm[0][i]] = (int32_t)i;
   for (int l = 0; l < nlev; ++l) {
@@ -650,6 +671,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     if (!(err = layout(lv[l].A, perm[l], &perm[l], plan.lev[l].A, eA[l])).empty()) return err;
   if (!(err = to_pos(a0, eA[0], plan.lev[0].A.n_pos(), nullptr, nullptr, false, plan.a0, plan.pair_items)).empty())
     return err;
+  clk.lap("A layouts + a0 lists");
   for (int l = 0; l < nlev; ++l) {
     AmgLevel& out = plan.lev[l];
     LevelCsr& L = lv[l];
@@ -741,6 +763,7 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
     if (!(err = to_pos(L.ac, eA[l + 1], plan.lev[l + 1].A.n_pos(), &eP, &eAP, true, out.ac, plan.pair_items))
              .empty())
       return err;
+    clk.lap(l == 0 ? "level 0 P/R/AP/RT layouts+lists" : "level>0 layouts+lists");
   }
   return "";
 }

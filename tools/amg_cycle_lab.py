@@ -10,6 +10,7 @@ tests/amg_ref.py, then swaps one ingredient at a time:
   cheb2cK     ... on levels ≥ K only (level 0 keeps V(1,1) Jacobi)
   v22cK       two Jacobi sweeps on levels ≥ K only
   cheb2sK / v22sK   ... on level K alone
+  cheb2rA_B / v22rA_B   ... on levels A..B
   w / wK      W-cycle (two coarse corrections per level / on levels < K only)
   wfK         W-cycle on levels ≥ K only
   rot         near-nullspace with the in-plane rotation: P_tent columns
@@ -179,7 +180,10 @@ def cycle(levs, b, l, kind, sweeps, gamma, wl=99, k0=0):
     L = levs[l]
     if L.coarsest:
         return np.linalg.solve(L.A.toarray(), b) if L.A.shape[0] <= 4000 else dapply(L.Dinv, b)
-    on = l >= k0 if k0 >= 0 else l == -k0  # k0 < 0: level −k0 alone
+    if isinstance(k0, tuple):  # (a, b): levels a..b
+        on = k0[0] <= l <= k0[1]
+    else:
+        on = l >= k0 if k0 >= 0 else l == -k0  # k0 < 0: level −k0 alone
     kl, sl = (kind, sweeps) if on else ("jac", 1)
     x = smooth(L, np.zeros_like(b), b, kl, sl)
     w_here = l < wl if wl >= 0 else l >= -wl  # wl < 0: W on levels ≥ −wl
@@ -219,6 +223,9 @@ def main():
             k0 = int(v.split("c")[-1])
         if v.startswith(("cheb2s", "v22s")):
             k0 = -int(v.split("s")[-1])
+        if v.startswith(("cheb2r", "v22r")):  # e.g. v22r1_2: levels 1..2
+            a_, b_ = v.split("r")[-1].split("_")
+            k0 = (int(a_), int(b_))
         if v.startswith("w"):
             gamma = 2
             wl = int(v[1:]) if len(v) > 1 and v[1] != "f" else 99

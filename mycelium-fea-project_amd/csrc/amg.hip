@@ -1735,6 +1735,12 @@ static void merged_nd(hipStream_t s, const AmgLevD* lev, const AmgCg& cg, const 
   Nd.x = m.B;
   Lu.PT = m.U;
   Nu.e = m.B;
+  // DQ's wide rows at 16 lanes whatever their count, U's at one lane (C2
+  // iteration 28.1 → 26.7 µs, tools/amg_ab.py: amg_small_lanes 65536 vs 1 Mi
+  // with C3 unmerged and slower under that setting; amg_up_lanes 1 vs 2:
+  // 27.75 vs 28.2); a caller's amg_small_lanes 0 / amg_up_lanes keep theirs
+  if (Ld.small_lanes > 0) Ld.small_lanes = INT32_MAX;
+  if (Lu.ulanes <= 0) Lu.ulanes = 1;
   down_nd<ND>(s, Ld, Nd, gate);
   vapply_nd<ND>(s, lev[2], gate);
   up_te<ND, float>(s, Lu, Nu, cg.u, gate);

@@ -243,7 +243,6 @@ struct mfea_handle {
   int64_t opt_amg_tail_rows = 2048;  // GAMG: levels of at most this many rows run in one workgroup
   int opt_amg_max_levels = kAmgMaxLevels;  // GAMG: hierarchy depth cap
   int opt_amg_w_block = 0;     // GAMG: w = A u threads per block (0: by size)
-  int opt_amg_w_k = 0;         // GAMG: w = A u step width (0: by level 0's mean slice width, 1, 2)
   int opt_amg_rlanes = 0;      // GAMG: restriction lanes per coarse row (0: by width)
   int opt_amg_down_split = 0;  // GAMG compact down sweep: R̂ and Ã rows as two launches (experiment)
   int opt_amg_merge = -1;      // GAMG: levels 0 and 1 merged around a level-2 collapse (-1: small networks, 0 off, 1 on)
@@ -1127,13 +1126,15 @@ AmgStrength amg_strength(const mfea_handle* h) {
 
 // w = A u's step width: K = 2 (slices up to 2U blocks in one round trip of
 // column loads and gathers, more VGPRs) once level 0's mean slice width
-// passes U = 4 blocks
-static int amg_w_k(const mfea_handle* h, const AmgPlan& pl) {
-  if (h->opt_amg_w_k > 0) return h->opt_amg_w_k;
+// passes U = 4 blocks, or on a small network, whose launch is one chain of
+// dependent loads long and ends with its widest slices (C2 iteration 26.1 →
+// 25.4 µs; C3 66.6 vs 66.8, kept at K = 1: profiles/r5/ab_spmv_k.jsonl)
+constexpr int64_t kWideSpmvRows = 131072;
+static int amg_w_k(const AmgPlan& pl) {
   if (pl.lev.empty() || pl.lev[0].A.sptr.size() < 2) return 1;
   const auto& sp = pl.lev[0].A.sptr;
   const double mean = (double)(sp.back() - sp.front()) / (double)(sp.size() - 1);
-  return mean > 4.0 ? 2 : 1;
+  return mean > 4.0 || pl.lev[0].A.n <= kWideSpmvRows ? 2 : 1;
 }
 
 // the collapsed cycle's lowest level when chosen automatically: level 1's V
@@ -1406,7 +1407,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     pt.amg_cg.lo = rk && nlev ? rk->lo[0] : 0;
     pt.amg_cg.hi = rk && nlev ? rk->hi[0] : nf;
     pt.amg_cg.w_block = h->opt_amg_w_block;
-    pt.amg_cg.w_k = amg_w_k(h, pl);
+    pt.amg_cg.w_k = amg_w_k(pl);
     pt.amg_cg.cycle = h->opt_amg_cycle;
     pt.amg_cg.coll = pt.amg_coll.kc;
     pt.amg_cg.row0 = I(row0 ? *row0 : pl.row0);

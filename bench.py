@@ -492,6 +492,22 @@ def main(argv=None):
 
     for _ in range(a.warmup):
         one_step()
+    if mode in ("partitioned", "parts") and pc == PC_GAMG:
+        # the automatic GAMG form (amg_dist -1) tries both forms on its first
+        # two solves of an active set, building the block-Jacobi form's
+        # per-partition hierarchies on the host: keep those trials out of the
+        # timed steps whatever --warmup is (the choice is collective: every
+        # rank sees the same value)
+        for _ in range(3):
+            undecided = eng.get_option("amg_dist_chosen") < 0
+            if dist is not None:
+                import torch
+                flag = torch.tensor([1 if undecided else 0], dtype=torch.int32)
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                undecided = bool(flag.item())
+            if not undecided:
+                break
+            one_step()
     barrier_sync()
     t0 = time.perf_counter()
     stats = []

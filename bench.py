@@ -524,6 +524,14 @@ def main(argv=None):
     job_dof = n_dof * (world if mode == "replicas" else 1)
 
     force, n_active, st = stats[-1]
+    # the phase split (mfea_stats t_*_ms) from one more step with the phase
+    # events on (option phase_times; off in the timed steps: each event
+    # between two kernels idles the GPU for several µs)
+    eng.set_option("phase_times", 1)
+    ph = [one_step()[2] for _ in range(5)]
+    eng.set_option("phase_times", 0)
+    ph_ms = {f: float(np.median([getattr(x, f) for x in ph]))
+             for f in ("t_assemble_ms", "t_rhs_ms", "t_solve_ms", "t_post_ms", "t_setup_ms")}
     iters = st.iters
     # ---- roofline, live HIP events on the engine's stream, algorithmic bytes
     # per launch as in DESIGN.md §4 (partitioned: rank 0's partition, without
@@ -613,9 +621,10 @@ def main(argv=None):
         },
         "cg_iters": iters,
         "relres": st.relres,
-        "step_breakdown_ms": {"assemble": st.t_assemble_ms, "rhs": st.t_rhs_ms,
-                              "pcg": st.t_solve_ms, "post": st.t_post_ms,
-                              "amg_setup (inside pcg)": st.t_setup_ms},
+        "step_breakdown_ms": {"assemble": ph_ms["t_assemble_ms"], "rhs": ph_ms["t_rhs_ms"],
+                              "pcg": ph_ms["t_solve_ms"], "post": ph_ms["t_post_ms"],
+                              "amg_setup (inside pcg)": ph_ms["t_setup_ms"],
+                              "note": "medians of 5 untimed steps with the phase events on"},
         "roofline": {
             "kernel": kernel,
             "bound": "hbm",
@@ -652,7 +661,9 @@ def main(argv=None):
     if not a.no_jacobi and pc == PC_GAMG:
         # SURVEY §8(d)'s iteration metric: Jacobi-PCG to rtol 1e-8 on the same step
         eng.set_active(None)
+        eng.set_option("phase_times", 1)  # (its step time is the phase sum)
         fj, nj, sj = eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=PC_JACOBI), fs.MAX_STRAIN)
+        eng.set_option("phase_times", 0)
         out["jacobi_iters_1e8"] = sj.iters
         out["jacobi_step_ms"] = sj.t_assemble_ms + sj.t_rhs_ms + sj.t_solve_ms + sj.t_post_ms
     if not a.no_full_run:
@@ -679,6 +690,7 @@ def main(argv=None):
         # ICC, whole-matrix factorisations in the chain-piece multicolour
         # order (csrc/sweep.hip)
         from mfea import PC_ICC, PC_SOR
+        eng.set_option("phase_times", 1)  # (their step times are phase sums)
         for name, code in (("sor", PC_SOR), ("icc", PC_ICC)):
             eng.set_active(None)
             eng.step(dy, -dy, make_opts(rtol=a.rtol, max_it=200000, precond=code), fs.MAX_STRAIN)  # plan build

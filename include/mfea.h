@@ -86,7 +86,9 @@ typedef struct {
   double relres;     /* final ‖r‖/‖b‖ (recursive residual)                               */
   double bnorm;      /* ‖b_f‖₂                                                          */
   int64_t n_free;    /* free DOFs                                                       */
-  double t_assemble_ms, t_rhs_ms, t_solve_ms, t_post_ms; /* device time (HIP events)   */
+  double t_assemble_ms, t_rhs_ms, t_solve_ms, t_post_ms; /* device time (HIP events),
+                        recorded only with option "phase_times" 1 (0 otherwise): an
+                        event between two kernels idles the GPU for several µs      */
   double t_setup_ms; /* MFEA_PC_GAMG: numeric hierarchy setup (inside t_solve_ms)     */
   int32_t amg_levels; /* MFEA_PC_GAMG: levels of the hierarchy (0 otherwise)         */
   int32_t amg_rebuilt; /* 1 if this solve rebuilt the symbolic hierarchy (new active set) */

@@ -220,6 +220,10 @@ struct mfea_handle {
   uint64_t graph_setup_key = 0;
   hipEvent_t ev[6] = {};
   hipEvent_t ev_setup = nullptr;
+  // option "phase_times": record the phase events (mfea_stats t_*_ms).  Off by
+  // default: each event recorded between two kernels left the GPU idle for
+  // ≈ 5–10 µs (C2 step 0.771 → 0.737 ms, C3 1.665 → 1.635 without them)
+  bool opt_phase_times = false;
   bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
   bool in_step = false;        // mfea_step: the solve's end is waited for by post
   hipEvent_t poll[2] = {};
@@ -391,6 +395,12 @@ int wait_event(mfea_handle* h, hipEvent_t ev) {
     if (dt > 200e-6) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else std::this_thread::yield();
   }
+}
+
+// a phase boundary for mfea_stats (only with option phase_times)
+int phase_event(mfea_handle* h, hipEvent_t ev, hipStream_t s) {
+  if (h->opt_phase_times) HIPC(hipEventRecord(ev, s));
+  return 0;
 }
 
 int sync_stream(mfea_handle* h) {
@@ -986,6 +996,7 @@ int drive_sized(mfea_handle* h, int big, int small, int max_it, int expected, En
 
 // device times of the last solve (its events must have completed)
 void solve_times(mfea_handle* h, mfea_stats* st) {
+  if (!h->opt_phase_times) return;  // (no phase events recorded: the t_* stay 0)
   float ms = 0;
   (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
   st->t_rhs_ms = ms;
@@ -1002,8 +1013,12 @@ void solve_times(mfea_handle* h, mfea_stats* st) {
 // is not waited for here — post's wait covers it and the times are read then
 // (one host round trip less per step).
 int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
-  HIPC(hipEventRecord(h->ev[3], h->stream));
-  if (!h->in_step) RC(wait_event(h, h->ev[3]));
+  if (!h->in_step) {  // (mfea_solve: its end is waited for here)
+    HIPC(hipEventRecord(h->ev[3], h->stream));
+    RC(wait_event(h, h->ev[3]));
+  } else {
+    RC(phase_event(h, h->ev[3], h->stream));
+  }
   if (st) {
     st->iters = fin.iters;
     st->status = fin.status;
@@ -1030,7 +1045,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   const int chunk = solve_chunk_size(o);
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
-  HIPC(hipEventRecord(h->ev[1], s));
+  RC(phase_event(h, h->ev[1], s));
   launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, precond, v, pt.partials.ptr, tix(pt, 0),
                 pt.red.ptr);
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
@@ -1044,7 +1059,7 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
     launch_cg_first(s, op, o->reg, precond, v, pt.slots.ptr, pt.cg_part.ptr);
   }
   HIPC(hipGetLastError());
-  HIPC(hipEventRecord(h->ev[2], s));
+  RC(phase_event(h, h->ev[2], s));
   // option "graph" 0: launch the chunk kernels eagerly (profilers that do not
   // follow hipGraph replays; same kernels, same order)
   const bool no_graph = !h->opt_graph;
@@ -1893,14 +1908,14 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
   const int nd = pt.amg.nd;
-  HIPC(hipEventRecord(h->ev[1], s));
+  RC(phase_event(h, h->ev[1], s));
   launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
   HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
-  HIPC(hipEventRecord(h->ev[2], s));
+  RC(phase_event(h, h->ev[2], s));
   if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg));
   else enqueue_amg_setup(h, pt, o->reg);
-  HIPC(hipEventRecord(h->ev_setup, s));
+  RC(phase_event(h, h->ev_setup, s));
   h->ev_setup_used = true;
   const AmgLevD& L0 = pt.amg_lev[0];
   launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
@@ -2366,7 +2381,7 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
   const int W = nranks(h);
   const int nd = h->gamg.nd;
-  HIPC(hipEventRecord(h->ev[1], s));
+  RC(phase_event(h, h->ev[1], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 2, cg_vecs(pt), pt.partials.ptr, tix(pt, 0),
@@ -2379,9 +2394,9 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
     launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
     HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
   }
-  HIPC(hipEventRecord(h->ev[2], s));
+  RC(phase_event(h, h->ev[2], s));
   RC(enqueue_gamg_setup(h, o->reg));
-  HIPC(hipEventRecord(h->ev_setup, s));
+  RC(phase_event(h, h->ev_setup, s));
   h->ev_setup_used = true;
   // iteration 0's u and w: the V-cycle of r₀, ungated
   for (auto& pp : h->parts) {
@@ -2463,7 +2478,7 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   }
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
   const int W = nranks(h);
-  HIPC(hipEventRecord(h->ev[1], s));
+  RC(phase_event(h, h->ev[1], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     launch_cg_rhs(s, sell_op(pt), pt.code.ptr, dy_top, dy_bot, o->reg, 2, cg_vecs(pt), pt.partials.ptr,
@@ -2476,9 +2491,9 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
     launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
     HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
   }
-  HIPC(hipEventRecord(h->ev[2], s));
+  RC(phase_event(h, h->ev[2], s));
   for (auto& pp : h->parts) enqueue_amg_setup(h, *pp, o->reg);
-  HIPC(hipEventRecord(h->ev_setup, s));
+  RC(phase_event(h, h->ev_setup, s));
   h->ev_setup_used = true;
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -2561,7 +2576,7 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   const int precond = o->precond == MFEA_PC_BLOCK_JACOBI ? 1 : 0;
   const int chunk = solve_chunk_size(o);
   const int W = nranks(h);
-  HIPC(hipEventRecord(h->ev[1], s));
+  RC(phase_event(h, h->ev[1], s));
   // RHS, M⁻¹ and the global (‖b‖², ‖M⁻¹b‖²)
   for (auto& pp : h->parts) {
     Part& pt = *pp;
@@ -2587,7 +2602,7 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   }
   RC(xchg_records(h, 0, true));
   HIPC(hipGetLastError());
-  HIPC(hipEventRecord(h->ev[2], s));
+  RC(phase_event(h, h->ev[2], s));
   // each chunk (kernels + exchanges) replays as one hipGraph (option
   // "dist_graph" 0: eager launches)
   const bool dist_graph = h->opt_dist_graph;
@@ -2641,7 +2656,7 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
 int assemble_impl(mfea_handle* h, mfea_stats* st) {
   hipStream_t s = h->stream;
   h->assembled = true;
-  HIPC(hipEventRecord(h->ev[0], s));
+  RC(phase_event(h, h->ev[0], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Pattern& P = pt.P;
@@ -2649,8 +2664,8 @@ int assemble_impl(mfea_handle* h, mfea_stats* st) {
                     pt.s_elem.ptr, pt.active.ptr, h->mat, pt.G, pt.val.ptr, pt.diag.ptr);
   }
   HIPC(hipGetLastError());
-  HIPC(hipEventRecord(h->ev[1], s));
-  if (st) {
+  RC(phase_event(h, h->ev[1], s));
+  if (st && h->opt_phase_times) {
     RC(wait_event(h, h->ev[1]));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
@@ -2713,7 +2728,7 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
               mfea_stats* st) {
   hipStream_t s = h->stream;
   const bool dm = partitioned(h);
-  HIPC(hipEventRecord(h->ev[4], s));
+  RC(phase_event(h, h->ev[4], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Pattern& P = pt.P;
@@ -2753,7 +2768,7 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if (n_active) *n_active = h->n_active;
   // elements only ever fail here: a changed count means a changed set
   if (!dm && h->act_host_ok && h->n_active != h->act_count) h->act_host_ok = false;
-  if (st) {
+  if (st && h->opt_phase_times) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[4], h->ev[5]);
     st->t_post_ms = ms;
@@ -3056,7 +3071,7 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     (void)sync_stream(h);
     return rc;
   }
-  if (st) {  // every event of the step has completed (post waited)
+  if (st && h->opt_phase_times) {  // every event of the step has completed (post waited)
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
     st->t_assemble_ms = ms;
@@ -3486,6 +3501,7 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
   const std::string n(name);
   bool rebuild = false;  // options baked into the symbolic layout
   if (n == "graph") h->opt_graph = value != 0;
+  else if (n == "phase_times") h->opt_phase_times = value != 0;
   else if (n == "dist_graph") h->opt_dist_graph = value != 0;
   else if (n == "order") { h->opt_order = (int)value; rebuild = true; }
   else if (n == "lane_dof") { h->opt_lane_dof = (int)value; rebuild = true; }
@@ -3757,6 +3773,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   if (!h || !name || !value) return fail(MFEA_EINVAL, "NULL argument");
   const std::string n(name);
   if (n == "graph") *value = h->opt_graph;
+  else if (n == "phase_times") *value = h->opt_phase_times ? 1 : 0;
   else if (n == "dist_graph") *value = h->opt_dist_graph;
   else if (n == "order") *value = h->opt_order;
   else if (n == "lane_dof") *value = h->opt_lane_dof;

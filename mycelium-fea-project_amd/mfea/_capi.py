@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # mfea_set_option defaults (include/mfea_debug.h)
-DEFAULT_OPTIONS = {"graph": 1, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
+DEFAULT_OPTIONS = {"graph": 1, "phase_times": 0, "dist_graph": 1, "order": -1, "lane_dof": 0, "cg_kernel": 0,
                    "ell_block": 256, "ell_maxg": 0, "ell_compact": 1, "amg_tail_rows": 2048,
                    "amg_max_levels": 32, "amg_restrict_lanes": 0, "amg_op_lanes": 0,
                    "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,

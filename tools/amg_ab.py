@@ -43,6 +43,7 @@ def main():
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
         top, bot = synth.grips(xyz)
         eng = Engine(0)
+        eng.set_option("phase_times", 1)  # (the t_*_ms phase split)
         for kv in a.set:
             k, v = kv.split("=")
             eng.set_option(k, int(v))

@@ -31,6 +31,7 @@ def child(cfg, steps):
     xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
     top, bot = synth.grips(xyz)
     eng = Engine(0)
+    eng.set_option("phase_times", 1)  # (the t_*_ms phase split)
     eng.set_material(fs.E_mod, fs.A, fs.I)
     eng.set_mesh(xyz, e2n)
     eng.set_bc(top, bot)

@@ -12,7 +12,7 @@ for c in ("c3", "c2", "c5"):
     f = os.path.join(D, f"{T}_{c}.json")
     if os.path.exists(f) and os.path.getsize(f):
         d = json.loads(open(f).read().strip().splitlines()[-1])
-        print(c, round(d["ms_per_step"], 4), d["cg_iters"], {k: round(v, 4) for k, v in d["step_breakdown_ms"].items()},
+        print(c, round(d["ms_per_step"], 4), d["cg_iters"], {k: round(v, 4) for k, v in d["step_breakdown_ms"].items() if isinstance(v, float)},
               "spmv", round(d["roofline"]["frac"], 3), "iter_us", round(d["roofline_iteration"]["avg_iteration_us"], 2))
 f = os.path.join(D, f"{T}_trace.json")
 if os.path.exists(f):

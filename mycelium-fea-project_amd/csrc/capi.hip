@@ -1049,8 +1049,8 @@ int solve_impl(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, precond, v, pt.partials.ptr, tix(pt, 0),
                 pt.red.ptr);
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg,
-                          pt.state.ptr);
-  HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+                          pt.state.ptr,
+                          pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   const bool ell = use_ell(h, pt);
   if (ell) {
     launch_ell_init(s, ell_op(h, pt), op, precond, v, ell_vecs(pt));
@@ -1910,8 +1910,8 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const int nd = pt.amg.nd;
   RC(phase_event(h, h->ev[1], s));
   launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
-  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
-  HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                          pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   RC(phase_event(h, h->ev[2], s));
   if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg));
   else enqueue_amg_setup(h, pt, o->reg);
@@ -2391,8 +2391,8 @@ int solve_gamg_global(mfea_handle* h, double dy_top, double dy_bot, const mfea_s
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
-    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
-    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                            pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   }
   RC(phase_event(h, h->ev[2], s));
   RC(enqueue_gamg_setup(h, o->reg));
@@ -2488,8 +2488,8 @@ int solve_amg_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solv
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
-    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr);
-    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+    launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                            pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   }
   RC(phase_event(h, h->ev[2], s));
   for (auto& pp : h->parts) enqueue_amg_setup(h, *pp, o->reg);
@@ -2588,8 +2588,8 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
     Part& pt = *pp;
     launch_rank_sum(s, pt.gred, W, pt.red.ptr + 12);
     launch_cg_init_finalize(s, pt.red.ptr + 12, o->rtol, o->atol, o->norm, o->max_it, o->reg,
-                            pt.state.ptr);
-    HIPC(hipMemsetAsync(pt.cg_part.ptr, 0, 2 * 4 * kCgMaxPartials * sizeof(double), s));
+                            pt.state.ptr,
+                            pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
     launch_ell_init(s, ell_op(h, pt), sell_op(pt), precond, cg_vecs(pt), ell_vecs(pt));
     launch_ell_pack0(s, ell_op(h, pt), precond, ell_vecs(pt), pt.dv);
   }

@@ -190,8 +190,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_rhs(SellOp op, const uint8_t* __
 }
 
 // k_cg_init_finalize: stopping threshold from the reduced (‖b‖², ‖M⁻¹b‖²).
+// zero[0, nzero): the solve's partial-sum buffers, cleared here instead of by
+// a fill launch of their own (one launch boundary less per solve)
 __global__ void k_cg_init_finalize(const double* red, double rtol, double atol, int norm,
-                                   int max_it, double reg, SolveState* st) {
+                                   int max_it, double reg, SolveState* st, double* zero, int64_t nzero) {
+  for (int64_t k = threadIdx.x; k < nzero; k += blockDim.x) zero[k] = 0.0;
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const double bb = red[0], zz = red[1];
   const double ref = norm == 1 ? zz : bb;
@@ -501,9 +504,9 @@ void launch_cg_rhs(hipStream_t s, const SellOp& op, const uint8_t* code, double 
 }
 
 void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
-                             int max_it, double reg, SolveState* st) {
-  hipLaunchKernelGGL(k_cg_init_finalize, dim3(1), dim3(64), 0, s, red, rtol, atol, norm, max_it,
-                     reg, st);
+                             int max_it, double reg, SolveState* st, double* zero, int64_t nzero) {
+  hipLaunchKernelGGL(k_cg_init_finalize, dim3(1), dim3(zero ? 256 : 64), 0, s, red, rtol, atol, norm, max_it,
+                     reg, st, zero, zero ? nzero : (int64_t)0);
 }
 
 void launch_cg_first(hipStream_t s, const SellOp& op, double reg, int precond, const CgVecs& v,

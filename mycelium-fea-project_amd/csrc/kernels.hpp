@@ -151,7 +151,8 @@ void launch_cg_iter(hipStream_t s, int j, const SellOp& op, int precond, const C
 // host: mapped pinned mirror of the final SolveState (written once, when done)
 void launch_cg_advance(hipStream_t s, int chunk, Slot* slots, SolveState* st, SolveState* host, int shift = 0);
 void launch_cg_init_finalize(hipStream_t s, const double* red, double rtol, double atol, int norm,
-                             int max_it, double reg, SolveState* st);
+                             int max_it, double reg, SolveState* st,
+                             double* zero = nullptr, int64_t nzero = 0);
 int cg_block_size(int64_t rows);
 int64_t cg_grid(int64_t rows);
 

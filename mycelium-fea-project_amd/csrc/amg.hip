@@ -47,8 +47,8 @@ namespace mfea {
 // (blocks are dealt round-robin over the 8 XCDs) — a small level's chain of
 // launches then reads what the previous launch wrote from the same L2 instead
 // of another XCD's.  Speed only; −1: this block has no work.
-__device__ __forceinline__ int64_t setup_block(int x1) {
-  if (!x1) return xcd_block();
+__device__ __forceinline__ int64_t setup_block(int x1, int64_t nmain = -1) {
+  if (!x1) return nmain < 0 ? xcd_block() : xcd_block_n(nmain);  // (nmain: the launch's own blocks come first)
   return (blockIdx.x & 7) ? -1 : (int64_t)(blockIdx.x >> 3);
 }
 
@@ -568,11 +568,6 @@ __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restric
   bstore<ND>(L.CT.val32, 0, q, C);
 }
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext) {
-  const int64_t xb = setup_block(L.x1);
-  if (xb >= 0) tv_body<ND>(L, vnext, xb);
-}
-template <int ND>
 __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
   const int64_t q = blk * kBlock + threadIdx.x;
   if (q >= L.CV.npos || L.CV.col[q] < 0) return;
@@ -614,21 +609,16 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
   }
   bstore<ND>(L.CV.val32, 0, q, C);
 }
-template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L) {
-  const int64_t xb = setup_block(L.x1);
-  if (xb >= 0) vv_body<ND>(L, xb);
-}
 
 // the merged levels' operators (AmgMergeD), one output block per thread, f32
 // in list order (bitwise reproducible): DQ's c_1 rows 2 R̂_0 − Σ Ã_1·R̂_0, its
 // x_2 rows Σ R̂_1·R̂_0; U = P̃_0 (ext) + Σ P̃_0·P̃_1
+// (xb: the block of the products' own numbering — DQ's blocks, then U's)
 template <int ND>
-__global__ __launch_bounds__(kBlock) void k_amg_mprod(AmgMergeD m, const float* __restrict__ at1,
-                                                      const float* __restrict__ r0, const float* __restrict__ r1,
-                                                      const float* __restrict__ p0, const float* __restrict__ p1,
-                                                      int64_t gdq) {
-  const int64_t xb = xcd_block();
+__device__ __forceinline__ void mprod_body(const AmgMergeD& m, const float* __restrict__ at1,
+                                           const float* __restrict__ r0, const float* __restrict__ r1,
+                                           const float* __restrict__ p0, const float* __restrict__ p1,
+                                           int64_t gdq, int64_t xb) {
   const bool dq = xb < gdq;
   const AmgMatD& M = dq ? m.DQ : m.U;
   const int64_t q = (dq ? xb : xb - gdq) * kBlock + threadIdx.x;
@@ -679,6 +669,44 @@ __global__ __launch_bounds__(kBlock) void k_amg_mprod(AmgMergeD m, const float* 
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = c1 ? C[c] - S[c] : C[c] + S[c];
   bstore<ND>(M.val32, 0, q, C);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_mprod(AmgMergeD m, const float* __restrict__ at1,
+                                                      const float* __restrict__ r0, const float* __restrict__ r1,
+                                                      const float* __restrict__ p0, const float* __restrict__ p1,
+                                                      int64_t gdq) {
+  mprod_body<ND>(m, at1, r0, r1, p0, p1, gdq, xcd_block());
+}
+// Those products riding in a collapse launch (blocks from `nmain` on): their
+// inputs are complete before the collapse starts, so they need no launch of
+// their own.  All in the last one (V_kc's, the widest): C2 setup 0.211 →
+// 0.205 ms; spread over the six collapse launches each took the products'
+// own ≈ 11 µs chain — 0.226 ms
+struct MprodSlice {
+  AmgMergeD m;
+  const float *at1 = nullptr, *r0 = nullptr, *r1 = nullptr, *p0 = nullptr, *p1 = nullptr;
+  int64_t gdq = 0, b0 = 0, b1 = 0;
+};
+template <int ND>
+__device__ __forceinline__ bool mprod_side(const MprodSlice& ms, int64_t nmain) {
+  if ((int64_t)blockIdx.x < nmain) return false;
+  const int64_t xb = ms.b0 + (int64_t)blockIdx.x - nmain;
+  if (xb < ms.b1) mprod_body<ND>(ms.m, ms.at1, ms.r0, ms.r1, ms.p0, ms.p1, ms.gdq, xb);
+  return true;
+}
+// the collapse's launches (blocks [0, nmain): the level's own work)
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_tv(AmgLevD L, const float* __restrict__ vnext, MprodSlice ms,
+                                                   int64_t nmain) {
+  if (mprod_side<ND>(ms, nmain)) return;
+  const int64_t xb = setup_block(L.x1, nmain);
+  if (xb >= 0) tv_body<ND>(L, vnext, xb);
+}
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_vv(AmgLevD L, MprodSlice ms, int64_t nmain) {
+  if (mprod_side<ND>(ms, nmain)) return;
+  const int64_t xb = setup_block(L.x1, nmain);
+  if (xb >= 0) vv_body<ND>(L, xb);
 }
 
 // A_{l+1}(I, J) = Σ P[a]ᵀ·AP[b], S lanes per output block (AmgLevD::ac_lanes):
@@ -1534,16 +1562,46 @@ static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l) {
   hipLaunchKernelGGL(k_amg_rtv<ND>, xg(L, slot_grid(L.RT.npos)), dim3(kBlock), 0, s, L, lev[l + 1]);
   hipLaunchKernelGGL(k_amg_atv<ND>, xg(L, slot_grid(L.A.npos)), dim3(kBlock), 0, s, L);
 }
+// mg (merged levels 0–1, AmgMergeD): their products ride in the last of
+// these launches (MprodSlice) — the caller then skips launch_amg_merge_setup.
+// Returns whether they did.
 template <int ND>
-static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, int below = 1 << 30) {
-  if (coll <= 0) return;
-  for (int l = std::min(nlev - 2, below - 1); l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
-    const AmgLevD& L = lev[l];
-    if (!L.collapsed) return;
-    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
-    hipLaunchKernelGGL(k_amg_tv<ND>, xg(L, rows_grid(L.CT.npos)), dim3(kBlock), 0, s, L, vnext);
-    hipLaunchKernelGGL(k_amg_vv<ND>, xg(L, rows_grid(L.CV.npos)), dim3(kBlock), 0, s, L);
+static bool collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, int below = 1 << 30,
+                              const AmgMergeD* mg = nullptr) {
+  if (coll <= 0) return false;
+  const int top = std::min(nlev - 2, below - 1);
+  int nl = 0;  // launches of the collapse
+  for (int l = top; l >= coll && lev[l].collapsed; --l) nl += 2;
+  MprodSlice ms;
+  int64_t gm = 0;
+  if (mg && mg->on && nl > 0) {
+    ms.m = *mg;
+    ms.at1 = lev[1].A.at32;
+    ms.r0 = lev[0].RT.val32;
+    ms.r1 = lev[1].RT.val32;
+    ms.p0 = lev[0].PT.val32;
+    ms.p1 = lev[1].PT.val32;
+    ms.gdq = rows_grid(mg->DQ.npos).x;
+    gm = ms.gdq + rows_grid(mg->U.npos).x;
   }
+  int k = 0;
+  auto share = [&](dim3 g) {  // the next launch's slice (all in the last, V_kc's); its grid grows by it
+    ms.b0 = 0;
+    ms.b1 = k + 1 == nl ? gm : 0;
+    ++k;
+    return dim3(g.x + (unsigned)(ms.b1 - ms.b0));
+  };
+  for (int l = top; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
+    const AmgLevD& L = lev[l];
+    if (!L.collapsed) break;
+    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
+    const dim3 gt = xg(L, rows_grid(L.CT.npos)), gv = xg(L, rows_grid(L.CV.npos));
+    dim3 g = share(gt);
+    hipLaunchKernelGGL(k_amg_tv<ND>, g, dim3(kBlock), 0, s, L, vnext, ms, (int64_t)gt.x);
+    g = share(gv);
+    hipLaunchKernelGGL(k_amg_vv<ND>, g, dim3(kBlock), 0, s, L, ms, (int64_t)gv.x);
+  }
+  return gm > 0;
 }
 // the whole numeric setup of a compact-cycle hierarchy, its compact parts
 // fused into the chain's launches (k_amg_fuse_p / k_amg_fuse_ac): three
@@ -1551,11 +1609,11 @@ static void collapse_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int c
 // k_amg_a0's partner) instead of seven
 static int64_t slot_blocks(int64_t npos) { return (npos / 64 + kBlock / 64 - 1) / (kBlock / 64); }
 template <int ND>
-static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
+static bool setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, const AmgMergeD* mg) {
   auto compact = [&](int l) { return l + 1 < nlev && lev[l].compact && lev[l].PT.wmax > 0 && !lev[l].coarsest; };
   for (int l = 0; l < nlev; ++l) {
     const AmgLevD& L = lev[l];
-    if (L.A.n <= 0) return;
+    if (L.A.n <= 0) return false;
     const bool last = L.coarsest || l + 1 >= nlev;
     if (l > 0 && !L.fixed_omega)  // (fixed ω: D⁻¹ came with A_l, k_amg_ac)
       hipLaunchKernelGGL(k_amg_dinv<ND>, xg(L, rows_grid(L.A.rg.span())), dim3(kBlock), 0, s, L);
@@ -1579,23 +1637,16 @@ static void setup_fused_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll
       launch_ac<ND>(s, L, lev[l + 1].A, lev[l + 1].omega, dnext, a1, a0, true);
     }
   }
-  collapse_setup_nd<ND>(s, lev, nlev, coll);
+  return collapse_setup_nd<ND>(s, lev, nlev, coll, 1 << 30, mg);
 }
-void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
-  if (nd == 2) setup_fused_nd<2>(s, lev, nlev, coll);
-  else setup_fused_nd<3>(s, lev, nlev, coll);
+bool launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll, const AmgMergeD* mg) {
+  if (nd == 2) return setup_fused_nd<2>(s, lev, nlev, coll, mg);
+  return setup_fused_nd<3>(s, lev, nlev, coll, mg);
 }
 template <int ND>
 static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
   for (int l = 0; l + 1 < nlev; ++l) compact_level_nd<ND>(s, lev, l);
-  if (coll <= 0) return;
-  for (int l = nlev - 2; l >= coll; --l) {  // deepest first: T_l needs V_{l+1}
-    const AmgLevD& L = lev[l];
-    if (!L.collapsed) return;
-    const float* vnext = l + 2 < nlev && lev[l + 1].collapsed ? lev[l + 1].CV.val32 : nullptr;
-    hipLaunchKernelGGL(k_amg_tv<ND>, xg(L, rows_grid(L.CT.npos)), dim3(kBlock), 0, s, L, vnext);
-    hipLaunchKernelGGL(k_amg_vv<ND>, xg(L, rows_grid(L.CV.npos)), dim3(kBlock), 0, s, L);
-  }
+  collapse_setup_nd<ND>(s, lev, nlev, coll);
 }
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
   if (nd == 2) compact_setup_nd<2>(s, lev, nlev, coll);

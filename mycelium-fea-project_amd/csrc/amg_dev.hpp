@@ -163,11 +163,12 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate) {
 // contiguous row range keeps the neighbour rows a wave gathers in ITS L2
 // instead of fetching the same lines into several.  A bijection on
 // [0, gridDim.x); used for speed only, nothing depends on the placement.
-__device__ __forceinline__ int64_t xcd_block() {
-  const int64_t g = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ int64_t xcd_block_n(int64_t g) {  // over blocks [0, g) of the grid
+  const int64_t b = blockIdx.x;
   const int64_t q = g >> 3, r = g & 7, x = b & 7, i = b >> 3;
   return x * q + (x < r ? x : r) + i;
 }
+__device__ __forceinline__ int64_t xcd_block() { return xcd_block_n(gridDim.x); }
 
 // position q of a RowRange's span belongs to one of its rows (only the
 // first and last slice can hold other ranks' rows)

@@ -233,7 +233,10 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0);
 // the levels' setup (after launch_amg_a0) and the compact operators in one
 // sequence, the compact parts fused into the Galerkin chain's launches
-void launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll);
+// (mg: the merged levels' products ride in the collapse launches; returns
+// whether they did — else launch_amg_merge_setup forms them)
+bool launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll,
+                            const AmgMergeD* mg = nullptr);
 // ---- one V-cycle u = M r (the CG's r → the CG's u); gate = NULL: always,
 // else only while *gate == kRun.  tail > 0: levels [tail, nlev) run in one
 // single-workgroup launch (k_amg_tail_lds / k_amg_tail, the views passed by value).

@@ -1846,14 +1846,15 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
     launch_sweep_setup(s, nd, pt.swd, pt.amg_lev[0]);
     return;
   }
+  bool merged_done = false;
   if (fused) {
-    launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll);
+    merged_done = launch_amg_setup_fused(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll, &pt.amg_mg);
   } else {
     for (int l = 0; l < nlev; ++l)
       launch_amg_level_setup(s, nd, pt.amg_lev[l], l + 1 < nlev ? &pt.amg_lev[l + 1] : nullptr, l == 0);
     launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, compact ? pt.amg_cg.coll : 0);
   }
-  if (pt.amg_mg.on) launch_amg_merge_setup(s, nd, pt.amg_lev.data(), pt.amg_mg);
+  if (pt.amg_mg.on && !merged_done) launch_amg_merge_setup(s, nd, pt.amg_lev.data(), pt.amg_mg);
 }
 
 uint64_t fnv1a(uint64_t k, const void* p, size_t n) {

@@ -226,6 +226,10 @@ struct mfea_handle {
   bool opt_phase_times = false;
   bool ev_setup_used = false;  // the last solve recorded ev_setup (GAMG)
   bool in_step = false;        // mfea_step: the solve's end is waited for by post
+  // mfea_step's assembly also formed the GAMG solves' RHS for these grip
+  // displacements (AsmRhs); the next solve_amg uses it instead of k_amg_rhs
+  bool rhs_fused = false;
+  double rhs_dy[2] = {0.0, 0.0};
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
   bool act_all = false;  // every element is active on the device (set_active(NULL), no failure since)
@@ -1910,7 +1914,11 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const CgVecs v = cg_vecs(pt);
   const int nd = pt.amg.nd;
   RC(phase_event(h, h->ev[1], s));
-  launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
+  // (mfea_step's assembly formed it for these displacements: AsmRhs)
+  const bool rhs_done = h->rhs_fused && h->rhs_dy[0] == dy_top && h->rhs_dy[1] == dy_bot;
+  h->rhs_fused = false;
+  if (!rhs_done)
+    launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
                           pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   RC(phase_event(h, h->ev[2], s));
@@ -2654,15 +2662,32 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   return finish_solve(h, fin, st);
 }
 
-int assemble_impl(mfea_handle* h, mfea_stats* st) {
+int assemble_impl(mfea_handle* h, mfea_stats* st, const double* rhs_dy = nullptr) {
   hipStream_t s = h->stream;
   h->assembled = true;
+  h->rhs_fused = false;
   RC(phase_event(h, h->ev[0], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Pattern& P = pt.P;
+    AsmRhs q{};
+    const bool rhs = rhs_dy && h->parts.size() == 1;  // (rhs_dy: a one-partition GAMG / SOR / ICC step)
+    if (rhs) {
+      q.code = pt.code.ptr;
+      q.dy_top = rhs_dy[0];
+      q.dy_bot = rhs_dy[1];
+      q.nf = P.n_free;
+      q.r = pt.r.ptr;
+      q.x = pt.x.ptr;
+      q.partials = pt.partials.ptr;
+      q.ticket = tix(pt, 0);
+      q.red_out = pt.red.ptr;
+      h->rhs_fused = true;
+      h->rhs_dy[0] = rhs_dy[0];
+      h->rhs_dy[1] = rhs_dy[1];
+    }
     launch_assemble(s, P.n_nodes, pt.xyz_d.ptr, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr,
-                    pt.s_elem.ptr, pt.active.ptr, h->mat, pt.G, pt.val.ptr, pt.diag.ptr);
+                    pt.s_elem.ptr, pt.active.ptr, h->mat, pt.G, pt.val.ptr, pt.diag.ptr, rhs ? &q : nullptr);
   }
   HIPC(hipGetLastError());
   RC(phase_event(h, h->ev[1], s));
@@ -3061,11 +3086,17 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   RC(ensure_built(h));
   mfea_solve_opts o = opts ? *opts : default_opts();
   if (st) std::memset(st, 0, sizeof(*st));
-  RC(assemble_impl(h, nullptr));
+  // the one-partition GAMG / SOR / ICC solves take their RHS from the
+  // assembly's row pass (AsmRhs)
+  const bool fuse_rhs = !partitioned(h) && (o.precond == MFEA_PC_GAMG || o.precond == MFEA_PC_SOR ||
+                                            o.precond == MFEA_PC_ICC);
+  const double dys[2] = {dy_top, dy_bot};
+  RC(assemble_impl(h, nullptr, fuse_rhs ? dys : nullptr));
   // a solver failure stops the step loop here, as the reference does
   // (src/fea_petsc.cpp:346-354)
   h->in_step = true;
   int rc = solve_any(h, dy_top, dy_bot, &o, st);
+  h->rhs_fused = false;
   if (rc == 0) rc = post_impl(h, max_strain, total_force, n_active, st);
   h->in_step = false;
   if (rc) {

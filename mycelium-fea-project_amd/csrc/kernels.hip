@@ -63,16 +63,18 @@ __device__ __forceinline__ void bar_block(double vx, double vy, double vz, const
 // (= scipy's duplicate-summation order, src/fea_solver.py:105).  No atomics,
 // no colouring, one launch, bitwise deterministic.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __restrict__ xyz,
-                                                     const int32_t* __restrict__ slice_ptr,
-                                                     const int32_t* __restrict__ row_len,
-                                                     const int32_t* __restrict__ s_col,
-                                                     const int32_t* __restrict__ s_elem,
-                                                     const uint8_t* __restrict__ active,
-                                                     Material m, int64_t G, double* __restrict__ val,
-                                                     double* __restrict__ diag) {
-  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (row >= N) return;
+// One node row of the assembly; q (a free row of the GAMG solves): also
+// K_fk x_k into k3 — k_amg_rhs's sum of the stored −S_e terms in slot order,
+// the same bits.
+__device__ __forceinline__ void assemble_row(int64_t N, int64_t row, const double* __restrict__ xyz,
+                                             const int32_t* __restrict__ slice_ptr,
+                                             const int32_t* __restrict__ row_len,
+                                             const int32_t* __restrict__ s_col,
+                                             const int32_t* __restrict__ s_elem,
+                                             const uint8_t* __restrict__ active, const Material& m,
+                                             int64_t G, double* __restrict__ val, double* __restrict__ diag,
+                                             const AsmRhs* q, double* k3) {
+  const bool rhs = q != nullptr && row < q->nf;
   const int64_t base = (int64_t)slice_ptr[row >> 6] * 64 + (row & 63);
   const int len = row_len[row];
   const double xi = xyz[3 * row], yi = xyz[3 * row + 1], zi = xyz[3 * row + 2];
@@ -91,11 +93,12 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __
       e[u] = ok ? s_elem[idx[u]] : 0;
       j[u] = ok ? s_col[idx[u]] : (int32_t)row;
     }
-    uint8_t act[U];
+    uint8_t act[U], cd[U];
     double pj[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       act[u] = k0 + u < len ? active[e[u]] : 0;
+      cd[u] = rhs && k0 + u < len && j[u] >= q->nf ? q->code[j[u]] : 3;
 #pragma unroll
       for (int a = 0; a < 3; ++a) pj[u][a] = xyz[3 * (int64_t)j[u] + a];
     }
@@ -110,12 +113,57 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __
 #pragma unroll
         for (int c = 0; c < 6; ++c) d[c] += S[c];
       }
+      double v[6];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) val[(int64_t)c * G + idx[u]] = -S[c];
+      for (int c = 0; c < 6; ++c) v[c] = -S[c];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) val[(int64_t)c * G + idx[u]] = v[c];
+      if (cd[u] != 3) {  // a known neighbour (3: free or ghost free row, x₀ = 0)
+        const double dy = cd[u] == 2 ? q->dy_bot : q->dy_top;
+        k3[0] = fma(v[1], dy, k3[0]);
+        k3[1] = fma(v[3], dy, k3[1]);
+        k3[2] = fma(v[4], dy, k3[2]);
+      }
     }
   }
 #pragma unroll
   for (int c = 0; c < 6; ++c) diag[(int64_t)c * N + row] = d[c];
+}
+
+// RHS: the GAMG solves' RHS too (AsmRhs: k_amg_rhs's outputs from the −S_e
+// blocks in registers) — one launch fewer per step
+template <bool RHS>
+__global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __restrict__ xyz,
+                                                     const int32_t* __restrict__ slice_ptr,
+                                                     const int32_t* __restrict__ row_len,
+                                                     const int32_t* __restrict__ s_col,
+                                                     const int32_t* __restrict__ s_elem,
+                                                     const uint8_t* __restrict__ active,
+                                                     Material m, int64_t G, double* __restrict__ val,
+                                                     double* __restrict__ diag, AsmRhs q) {
+  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if constexpr (RHS) {
+    double acc[2] = {0.0, 0.0};
+    if (row < N) {
+      double k3[3] = {0.0, 0.0, 0.0};
+      assemble_row(N, row, xyz, slice_ptr, row_len, s_col, s_elem, active, m, G, val, diag, &q, k3);
+      if (row < q.nf) {
+        const double b[3] = {0.0 - k3[0], 0.0 - k3[1], 0.0 - k3[2]};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q.r[3 * row + a] = b[a];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) acc[0] = fma(b[a], b[a], acc[0]);
+      } else {
+        const uint8_t c = q.code[row];
+        const double xk[3] = {0.0, c == 3 ? 0.0 : (c == 2 ? q.dy_bot : q.dy_top), 0.0};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q.x[3 * row + a] = xk[a];
+      }
+    }
+    block_publish<2>(acc, q.partials, q.ticket, q.red_out);
+  } else {
+    if (row < N) assemble_row(N, row, xyz, slice_ptr, row_len, s_col, s_elem, active, m, G, val, diag, nullptr, nullptr);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -524,10 +572,16 @@ __global__ __launch_bounds__(kBlock) void k_spmv_csr(int j, int64_t n, const int
 
 void launch_assemble(hipStream_t s, int64_t N, const double* xyz, const int32_t* slice_ptr,
                      const int32_t* row_len, const int32_t* s_col, const int32_t* s_elem,
-                     const uint8_t* active, Material m, int64_t G, double* val, double* diag) {
+                     const uint8_t* active, Material m, int64_t G, double* val, double* diag,
+                     const AsmRhs* rhs) {
+  if (rhs) {  // (the reduction's blocks publish even when N = 0)
+    hipLaunchKernelGGL(k_assemble<true>, MFEA_GRID(grid_rows(N > 0 ? N : 1)), N, xyz, slice_ptr, row_len, s_col,
+                       s_elem, active, m, G, val, diag, *rhs);
+    return;
+  }
   if (N <= 0) return;
-  hipLaunchKernelGGL(k_assemble, MFEA_GRID(grid_rows(N)), N, xyz, slice_ptr, row_len, s_col, s_elem,
-                     active, m, G, val, diag);
+  hipLaunchKernelGGL(k_assemble<false>, MFEA_GRID(grid_rows(N)), N, xyz, slice_ptr, row_len, s_col, s_elem,
+                     active, m, G, val, diag, AsmRhs{});
 }
 
 void launch_rhs_init(hipStream_t s, int64_t N, int64_t nf, const int32_t* slice_ptr,

@@ -79,9 +79,23 @@ struct Material {
 };
 
 // ---- launchers (defined in kernels.hip) -------------------------------------
+// The GAMG solves' RHS formed in the assembly's row pass (k_amg_rhs's work:
+// b = 0 − K_fk x_k of the free rows into r, the prescribed x of the others,
+// ‖b‖² published to red) — rhs == nullptr: assembly alone
+struct AsmRhs {
+  const uint8_t* code;
+  double dy_top, dy_bot;
+  int64_t nf;
+  double* r;
+  double* x;
+  double* partials;
+  unsigned* ticket;
+  double* red_out;
+};
 void launch_assemble(hipStream_t s, int64_t N, const double* xyz, const int32_t* slice_ptr,
                      const int32_t* row_len, const int32_t* s_col, const int32_t* s_elem,
-                     const uint8_t* active, Material m, int64_t G, double* val, double* diag);
+                     const uint8_t* active, Material m, int64_t G, double* val, double* diag,
+                     const AsmRhs* rhs = nullptr);
 
 void launch_rhs_init(hipStream_t s, int64_t N, int64_t nf, const int32_t* slice_ptr,
                      const int32_t* row_len, const int32_t* s_col, const double* val,

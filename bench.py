@@ -184,6 +184,17 @@ def iteration_bytes(info, block):
     return b, "k_cg_iter (SELL: update + SpMV + reduction)"
 
 
+def new_set_steps(n_act, n_elems):
+    """Per step of a full run, 1 if it ran on an active set other than the
+    step before it.  `eng.step` reports the count AFTER its own failure
+    update, so step k runs on the set step k-1 left (step 0 on the intact
+    mesh, n_elems): step k is on a new set when n_act[k-1] != n_act[k-2]."""
+    if not n_act:
+        return []
+    ran_on = [n_elems] + list(n_act[:-1])
+    return [0] + [int(ran_on[k] != ran_on[k - 1]) for k in range(1, len(ran_on))]
+
+
 def full_run(eng, opts, fs, dmax=None):
     """The reference's whole driver loop on the bench network (src/fea_solver.py:
     216-295): N_STEPS load steps from the intact mesh, elements failing as they
@@ -209,14 +220,16 @@ def full_run(eng, opts, fs, dmax=None):
         if na == 0:
             break
     wall = _t.perf_counter() - t0
-    changed = [0] + [int(n_act[k] != n_act[k - 1]) for k in range(1, len(n_act))]  # ran on a new set
+    changed = new_set_steps(n_act, eng.n_elems)
     med = float(np.median([p for p, r in zip(per, rebuilt) if not r] or per))
     reb = [p for p, r in zip(per, rebuilt) if r]
     new_set = [p for p, c, r in zip(per, changed, rebuilt) if c and not r]
+    new_idx = [k for k, (c, r) in enumerate(zip(changed, rebuilt)) if c and not r]
     return {"steps": len(per), "wall_s": wall, "step_ms": per, "cg_iters": its, "n_active": n_act,
             "displacement_max_mm": dmax,
-            "new_active_set_steps": int(sum(changed)), "kept_hierarchy_steps": int(sum(reused)),
-            "kept_hierarchy_step_ms": new_set,
+            "new_active_set_steps": int(sum(changed)), "kept_hierarchy_steps": len(new_set),
+            "kept_hierarchy_step_ms": new_set, "kept_hierarchy_step_idx": new_idx,
+            "kept_hierarchy_worst_vs_median": (max(new_set) / med) if new_set else None,
             "rebuild_steps": int(sum(rebuilt)), "rebuild_step_ms": reb,
             "rebuild_overhead_ms": float(sum(p - med for p in reb)), "median_step_ms": med,
             "note": "all 40 load steps from the intact mesh, failures included; a step on a new active set "

@@ -25,7 +25,9 @@
 extern "C" {
 #endif
 
-#define MFEA_ABI_VERSION 7
+/* 8: MFEA_PC_SOR / MFEA_PC_ICC factorise the whole matrix (were block Jacobi
+ *    over 256-row blocks); every preconditioner honours mfea_solve_opts.norm */
+#define MFEA_ABI_VERSION 8
 
 /* error / status codes */
 #define MFEA_OK 0
@@ -47,23 +49,28 @@ extern "C" {
 #define MFEA_PC_BLOCK_JACOBI 1  /* 3×3 node-block Jacobi (exact inverse per block)   */
 #define MFEA_PC_GAMG 2          /* smoothed-aggregation AMG V-cycle, the counterpart of
                                    the reference sweep's `-pc_type gamg`
-                                   (src/fea_petsc_solverAndPC.cpp:330-391); stops on the
-                                   unpreconditioned norm.  Partitioned handles: ONE global
-                                   hierarchy whose large levels are split over the ranks
-                                   (the one-partition iteration count) or block Jacobi over
-                                   per-partition ones — per active set the faster of the
-                                   two, measured (mfea_debug.h option "amg_dist") */
+                                   (src/fea_petsc_solverAndPC.cpp:330-391).  Partitioned
+                                   handles: ONE global hierarchy whose large levels are
+                                   split over the ranks (the one-partition iteration
+                                   count) or block Jacobi over per-partition ones — per
+                                   active set the faster of the two, measured
+                                   (mfea_debug.h option "amg_dist") */
 
 #define MFEA_PC_SOR 3           /* `-pc_type sor`: SSOR (ω = 1, PETSc's default) on the
-                                   node blocks of K_ff + reg·I, block Jacobi over 256-row
-                                   blocks with multicolour sweeps inside each (PETSc's
-                                   SOR is processor-local in parallel); one partition */
+                                   node blocks of the WHOLE K_ff + reg·I, every coupling
+                                   kept, factorised in a chain-piece multicolour order
+                                   (hyphal chains of ≤ 64 rows keep their natural order;
+                                   the pieces of one colour are independent and each
+                                   piece's recurrence is a scan across a wave's lanes;
+                                   csrc/sweep.hip); one partition */
 #define MFEA_PC_ICC 4           /* `-pc_type icc` (the reference source's default PCICC,
                                    src/fea_petsc.cpp:331; also `ilu`, the same factor on
-                                   an SPD matrix): DIC(0) — incomplete block Cholesky
-                                   with A's off-diagonal blocks and a corrected diagonal —
-                                   in the same block / colour layout as MFEA_PC_SOR */
+                                   an SPD matrix): DIC(0) — incomplete block Cholesky of
+                                   the whole K_ff + reg·I with A's off-diagonal blocks and
+                                   f64 pivots D̃_i = D_i − Σ_{j<i} A_ij D̃_j⁻¹ A_ijᵀ — in
+                                   the same chain-piece multicolour order as MFEA_PC_SOR */
 
+/* Every preconditioner stops on the norm mfea_solve_opts.norm selects. */
 /* stopping norm (mfea_solve_opts.norm) */
 #define MFEA_NORM_UNPRECONDITIONED 0 /* ‖r‖₂ ≤ rtol·‖b‖₂  (SciPy cg; the metric)      */
 #define MFEA_NORM_PRECONDITIONED 1   /* ‖z‖₂ ≤ rtol·‖M⁻¹b‖₂ (PETSc KSPCG default)     */

@@ -91,7 +91,7 @@ struct Part {
   DevBuf<double> cg_part;                            // CG-CG block partials, 2 parities
   DevBuf<int32_t> slice_ptr, row_len, s_col, s_elem, e2n_d;
   DevBuf<uint8_t> active, code, elem_own;
-  DevBuf<int32_t> fail_list;  // partitioned: owned elements failed in the last post (any order)
+  DevBuf<int32_t> fail_list;  // (owned) elements failed in the last post (any order)
   DevBuf<unsigned> fail_cnt;
   DevBuf<unsigned> tickets;
   // wave-local lane operator (ell.hip); ell_ok = false → SELL kernel
@@ -129,8 +129,23 @@ struct Part {
   // a hierarchy kept over element failures (option amg_reuse): the activity
   // its floating-row mask reflects, the iterations of its first solve, and
   // whether a later solve degraded enough to rebuild
-  std::vector<uint8_t> amg_mask_key;
+  bool amg_mask_ok = false;          // amg_fmask = flt's floating set, up to flt_new
   DevBuf<uint8_t> amg_fmask;         // level-0 rows of floating pieces (amg.hpp floating_free_rows)
+  // one partition: the floating set kept current over failures (amg.hpp
+  // FloatTracker), the rows that floated since the mask's last update, the
+  // level-0 label of every free row, and the pinned / device staging of a
+  // mask update
+  FloatTracker flt;
+  std::vector<int32_t> flt_new;
+  std::vector<int32_t> row0_inv;
+  DevBuf<int32_t> fm_rows;
+  int32_t* fm_pin = nullptr;
+  size_t fm_pin_n = 0;
+  // the plan's key covers the current activity: act_sub_gen when it was
+  // built or last compared (failures only ever shrink the set, so it holds
+  // until the activity is set explicitly), and its element count
+  int64_t amg_sub_gen = -1;
+  int64_t amg_key_count = 0;
   int amg_build_iters = -1;
   bool amg_stale = false;
   bool amg_reused = false;           // the last ensure_amg kept a hierarchy built for another set
@@ -176,6 +191,9 @@ struct Part {
   XDev xd_g, xd_sg;
   DevBuf<int32_t> amg_xi;
   DevBuf<double> amg_xs, amg_xr;
+  ~Part() {
+    if (fm_pin) (void)hipHostFree(fm_pin);
+  }
 };
 
 struct mfea_handle {
@@ -302,6 +320,7 @@ struct mfea_handle {
   int64_t gamg_gen = 0;       // bumped on every upload (captured graphs hold its pointers)
   int64_t gamg_plan_gen = 0;  // bumped on every host rebuild (a new active set)
   int64_t act_gen = 1;        // bumped whenever the element activity may have changed
+  int64_t act_sub_gen = 1;    // bumped when it changed other than by failures (set_active, a rebuild)
   int64_t gamg_act_gen = 0;   // act_gen the hierarchy was built for
   DevBuf<uint8_t> gact;       // RCCL: the global activity, max-all-reduced
   DevBuf<double> gtime;       // RCCL: a host time, max-all-reduced (amg_dist -1's choice)
@@ -544,9 +563,10 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
     HIPC(up(pt.xrecv_rows.ptr, rr.data(), nr * sizeof(int32_t)));
     HIPC(pt.elem_own.alloc(E));
     HIPC(up(pt.elem_own.ptr, pl.elem_own.data(), E));
-    HIPC(pt.fail_list.alloc(std::max<int64_t>(E, 1)));
-    HIPC(pt.fail_cnt.alloc(1));
   }
+  HIPC(pt.fail_list.alloc(std::max<int64_t>(E, 1)));
+  HIPC(pt.fail_cnt.alloc(1));
+  if (!dm) pt.flt.set_graph(P.n_nodes, P.n_free, P.n_nodes - P.n_ghost, P.n_elems, P.e2n_perm.data());
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -601,6 +621,7 @@ int ensure_built(mfea_handle* h) {
     h->gpat = Pattern();
   }
   ++h->act_gen;
+  ++h->act_sub_gen;
   {  // free DOFs of the whole mesh (reported in mfea_stats)
     std::vector<uint8_t> known(h->N, 0);
     for (int64_t t : h->top) known[t] = 1;
@@ -1475,7 +1496,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     HIPC(pt.amg_fmask.alloc(std::max<int64_t>(pl.lev[0].A.n, 1)));
     HIPC(hipMemsetAsync(pt.amg_fmask.ptr, 0, pt.amg_fmask.n, s));
     pt.amg_lev[0].fmask = pt.amg_fmask.ptr;
-    pt.amg_mask_key.clear();
+    pt.amg_mask_ok = false;
   }
   // the smoothing weights (ρ̂ per level in place of the Gershgorin estimate)
   pt.amg_om_own = !rk;
@@ -1539,19 +1560,55 @@ int upload_amg_halo(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
   return 0;
 }
 
-// The floating-row mask of the active set `key` in level-0 labels (one
-// partition's own hierarchy: a partition cannot tell alone what is floating)
+// The floating-row mask of the active set `key` (= the host activity) in
+// level-0 labels, whole: the tracker's whole-graph pass (one partition's own
+// hierarchy: a partition cannot tell alone what is floating)
 int upload_fmask(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
-  std::vector<uint8_t> fl;
-  floating_free_rows(pt.P, key, fl);
+  pt.flt.init(pt.P.e2n_perm.data(), pt.P.n_elems, key.data());
+  pt.flt_new.clear();
   const std::vector<int32_t>& row0 = pt.amg.row0;
+  pt.row0_inv.assign(pt.P.n_free, -1);
   std::vector<uint8_t> m(row0.size());
-  for (size_t i = 0; i < row0.size(); ++i) m[i] = fl[row0[i]];
+  for (size_t i = 0; i < row0.size(); ++i) {
+    m[i] = pt.flt.floating[row0[i]];
+    pt.row0_inv[row0[i]] = (int32_t)i;
+  }
   if (!m.empty()) {
     HIPC(hipMemcpyAsync(pt.amg_fmask.ptr, m.data(), m.size(), hipMemcpyHostToDevice, h->stream));
     RC(sync_stream(h));
   }
-  pt.amg_mask_key = key;
+  pt.amg_mask_ok = true;
+  return 0;
+}
+
+// The rows that floated since the mask's last update (flt_new, in Pattern
+// rows) set in the device mask: a pinned list and one scatter launch on the
+// stream, no host wait (the next post waits for the step anyway, so the
+// pinned list is free again when the next failures fill it)
+int push_fmask(mfea_handle* h, Part& pt) {
+  const size_t n = pt.flt_new.size();
+  if (n == 0) return 0;
+  hipStream_t s = h->stream;
+  if (pt.fm_pin_n < n) {
+    HIPC(hipStreamSynchronize(s));
+    if (pt.fm_pin) (void)hipHostFree(pt.fm_pin);
+    pt.fm_pin = nullptr;
+    pt.fm_pin_n = 0;
+    const size_t cap = std::max<size_t>(n, 4096);
+    HIPC(hipHostMalloc(&pt.fm_pin, cap * sizeof(int32_t), hipHostMallocDefault));
+    pt.fm_pin_n = cap;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t l = pt.row0_inv[pt.flt_new[i]];
+    if (l < 0) return fail(MFEA_EINVAL, "internal: floating row outside level 0");
+    pt.fm_pin[i] = l;
+  }
+  if (pt.fm_rows.n < n) HIPC(hipStreamSynchronize(s));
+  HIPC(pt.fm_rows.alloc(std::max<size_t>(n, 4096)));
+  HIPC(hipMemcpyAsync(pt.fm_rows.ptr, pt.fm_pin, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  launch_set_flags(s, (int64_t)n, pt.fm_rows.ptr, pt.amg_fmask.ptr);
+  HIPC(hipGetLastError());
+  pt.flt_new.clear();
   return 0;
 }
 
@@ -1657,6 +1714,17 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   // no activity change since the plan / mask last matched it: nothing to do
   // (no O(E) key compares on the hot path)
   if (!dm && pt.amg_ok && !pt.amg_stale && pt.amg_seen_gen == h->act_gen) return 0;
+  // the activity moved only by failures since the plan's key was set (post
+  // kept the host activity and the floating set current from the failed
+  // ids): keep the hierarchy with no O(E) pass — the new floating rows go to
+  // the device mask as a list
+  if (!dm && pt.amg_ok && !pt.amg_stale && h->opt_amg_reuse && pt.amg_lev.size() > 1 && h->act_host_ok &&
+      pt.amg_sub_gen == h->act_sub_gen && pt.flt.valid && pt.amg_mask_ok) {
+    RC(push_fmask(h, pt));
+    pt.amg_reused = h->act_count != pt.amg_key_count;
+    pt.amg_seen_gen = h->act_gen;
+    return 0;
+  }
   std::vector<uint8_t> local;
   if (dm) {
     local.resize(pt.P.n_elems);
@@ -1671,9 +1739,10 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
     // keep the hierarchy: the numeric setup re-forms its values from the new
     // K (failed elements are zero slots); only pieces cut off from both grips
     // need care — their P_0 rows are zeroed so they stay exactly at zero
-    if (pt.amg_mask_key != key) RC(upload_fmask(h, pt, key));
+    RC(upload_fmask(h, pt, key));
     pt.amg_reused = pt.amg_key != key;
     pt.amg_seen_gen = h->act_gen;
+    pt.amg_sub_gen = h->act_sub_gen;  // key ⊆ amg_key, compared
     return 0;
   }
   if (pt.amg_ok && pt.amg_key == key) {
@@ -1708,6 +1777,8 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   pt.amg_reused = false;
   if (!dm && pt.amg_lev.size() > 1) RC(upload_fmask(h, pt, key));
   if (!dm) pt.amg_seen_gen = h->act_gen;
+  pt.amg_sub_gen = dm ? -1 : h->act_sub_gen;
+  pt.amg_key_count = (int64_t)std::count(key.begin(), key.end(), (uint8_t)1);
   ++pt.amg_gen;
   *rebuilt = true;
   return 0;
@@ -2750,6 +2821,36 @@ int apply_failures(mfea_handle* h) {
   return 0;
 }
 
+// One partition: the elements that failed in the last post (the stress
+// kernel's list) move the host activity and the floating-row tracker —
+// O(failures + what split off), no E-byte copy or whole-graph pass
+// (src/fea_solver.py:283-284: elements only ever fail).  The list's counter
+// is cleared for the next post.
+unsigned* fail_counter(Part& pt) { return reinterpret_cast<unsigned*>(pt.red.ptr + 6); }
+
+int local_failures(mfea_handle* h, Part& pt, unsigned c) {
+  if (c > (unsigned)pt.P.n_elems) return fail(MFEA_EINVAL, "internal: failed-element list overflow");
+  std::vector<int32_t> ids(c);
+  HIPC(hipMemcpy(ids.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPC(hipMemsetAsync(fail_counter(pt), 0, sizeof(unsigned), h->stream));
+  if (!h->act_host_ok || h->act_host.size() != (size_t)pt.P.n_elems) {
+    pt.flt.valid = false;
+    return 0;
+  }
+  std::sort(ids.begin(), ids.end());  // (atomic list order: the tracker's labels deterministic)
+  for (int32_t e : ids) {
+    if (e < 0 || e >= pt.P.n_elems || !h->act_host[e]) return fail(MFEA_EINVAL, "internal: bad failed element");
+    h->act_host[e] = 0;
+    pt.flt.fail(pt.P.e2n_perm.data(), h->act_host.data(), e, pt.flt_new);
+  }
+  h->act_count -= (int64_t)c;
+  if (h->act_count != h->n_active) {  // cannot happen: fall back to a download
+    h->act_host_ok = false;
+    pt.flt.valid = false;
+  }
+  return 0;
+}
+
 int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
               mfea_stats* st) {
   hipStream_t s = h->stream;
@@ -2762,10 +2863,12 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
                     pt.val.ptr, pt.diag.ptr, pt.G, pt.x.ptr, pt.partials.ptr, tix(pt, 3),
                     pt.red.ptr + 4);
     if (dm) HIPC(hipMemsetAsync(pt.fail_cnt.ptr, 0, sizeof(unsigned), s));
+    // one partition: the counter is red[6] (read back with the force and the
+    // count, no copy of its own), zero here — cleared by the host after the
+    // last failures were read (local_failures)
     launch_stress(s, P.n_elems, pt.e2n_d.ptr, pt.xyz_d.ptr, pt.x.ptr, h->mat, max_strain,
                   pt.active.ptr, pt.stress.ptr, pt.partials.ptr, tix(pt, 4), pt.red.ptr + 5,
-                  dm ? pt.elem_own.ptr : nullptr, dm ? pt.fail_list.ptr : nullptr,
-                  dm ? pt.fail_cnt.ptr : nullptr);
+                  dm ? pt.elem_own.ptr : nullptr, pt.fail_list.ptr, dm ? pt.fail_cnt.ptr : fail_counter(pt));
   }
   HIPC(hipGetLastError());
   Part& p0 = part0(h);
@@ -2774,14 +2877,18 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
     launch_rank_sum(s, p0.gred, nranks(h), p0.red.ptr + 12);
     HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 12, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   } else {
-    HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 4, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(h->ev[5], s));
   RC(wait_event(h, h->ev[5]));
   if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
   if (total_force) *total_force = h->h_red[0];
-  if ((int64_t)h->h_red[1] != h->n_active) {  // elements only ever fail here
+  unsigned nfail = 0;  // one partition: the stress kernel's failed-element count
+  if (!dm) std::memcpy(&nfail, &h->h_red[2], sizeof nfail);
+  // elements only ever fail here
+  const bool changed = (int64_t)h->h_red[1] != h->n_active || nfail > 0;
+  if (changed) {
     // every rank sees the same global count, so every rank exchanges
     if (dm && h->gkey_gen == h->act_gen) {
       RC(apply_failures(h));
@@ -2792,8 +2899,8 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
   if ((int64_t)h->h_red[1] < h->Ecount) h->act_all = false;
   h->n_active = (int64_t)h->h_red[1];
   if (n_active) *n_active = h->n_active;
-  // elements only ever fail here: a changed count means a changed set
-  if (!dm && h->act_host_ok && h->n_active != h->act_count) h->act_host_ok = false;
+  if (!dm && nfail) RC(local_failures(h, p0, nfail));
+  else if (!dm && h->act_host_ok && h->n_active != h->act_count) h->act_host_ok = false;
   if (st && h->opt_phase_times) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, h->ev[4], h->ev[5]);
@@ -3021,7 +3128,9 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   // no act_gen bump, so a partitioned handle skips its activity all-reduce
   if (!active && h->act_all) return 0;
   ++h->act_gen;
+  ++h->act_sub_gen;
   h->act_all = !active;
+  for (auto& pp : h->parts) pp->flt.valid = false;
   if (partitioned(h)) {  // the global activity is known here: no exchange needed for it
     h->gkey.assign(h->Ecount, 1);
     if (active)
@@ -3804,6 +3913,11 @@ int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t
 int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   if (!h || !name || !value) return fail(MFEA_EINVAL, "NULL argument");
   const std::string n(name);
+  // the read-only plan values need a partition to read them from
+  static const char* plan_names[] = {"amg_merged", "amg_merge_dq_blocks", "amg_merge_u_blocks", "sweep_colors",
+                                     "sweep_pieces", "amg_reused", "amg_build_iters"};
+  for (const char* pn : plan_names)
+    if (n == pn && h->parts.empty()) return fail(MFEA_ESTATE, std::string(name) + ": no partition yet");
   if (n == "graph") *value = h->opt_graph;
   else if (n == "phase_times") *value = h->opt_phase_times ? 1 : 0;
   else if (n == "dist_graph") *value = h->opt_dist_graph;

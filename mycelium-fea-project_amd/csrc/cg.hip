@@ -476,8 +476,10 @@ __global__ void k_cg_advance(int chunk, int shift, Slot* slots, SolveState* st, 
     st->status = cur.flag == kConverged ? 0 : (cur.flag == kMaxit ? -4 : -5);
     st->done = 1;
     // poison the slot the NEXT queued chunk gates on first: slots[0] for
-    // shift 0, slots[1] for shift 1 (its V-cycle 0 and w 0 test slots[1];
-    // left as kRun they would run with stale α, β and move x)
+    // shift 0, slots[1] for shift 1 (the chunk's first update tests
+    // slots[1]; left as kRun it would apply stale α, β and move x.  The
+    // V-cycle / sweep and w launches take no gate: with x, r, p, s frozen
+    // they rewrite what they wrote before, capi.hip enqueue_amg_chunk)
     slots[0].flag = kStop;
     slots[shift].flag = kStop;
     *host = *st;

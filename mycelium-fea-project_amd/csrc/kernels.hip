@@ -483,12 +483,20 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
     }
     stress[e] = sg;
     cnt[0] = (act && (!owned || owned[e])) ? 1.0 : 0.0;
-    // partitioned: an owned element failing now joins this rank's list (any
-    // order; the host sorts it) — the global activity then moves by these ids
-    // instead of an E-byte reduction (capi.hip post_impl)
-    if (fail_list && act0 && !act && owned[e]) fail_list[atomicAdd(fail_cnt, 1u)] = (int32_t)e;
+    // an (owned) element failing now joins the list (any order): the host's
+    // activity then moves by these ids instead of an E-byte copy or reduction
+    // (capi.hip post_impl / apply_failures)
+    if (fail_list && act0 && !act && (!owned || owned[e])) fail_list[atomicAdd(fail_cnt, 1u)] = (int32_t)e;
   }
   block_publish<1>(cnt, partials, ticket, red_out);
+}
+
+// out[idx[i]] = 1 for i < n (the kept GAMG hierarchy's floating-row mask:
+// rows that floated since the last upload, capi.hip push_fmask)
+__global__ __launch_bounds__(kBlock) void k_set_flags(int64_t n, const int32_t* __restrict__ idx,
+                                                      uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[idx[i]] = 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_element_stiffness(int64_t n, const double* __restrict__ p1,
@@ -647,6 +655,11 @@ void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* x
                    const uint8_t* owned, int32_t* fail_list, unsigned* fail_cnt) {
   hipLaunchKernelGGL(k_stress, MFEA_GRID(grid_rows(E > 0 ? E : 1)), E, e2n, xyz, u, m, max_strain,
                      active, stress, partials, ticket, red_out, owned, fail_list, fail_cnt);
+}
+
+void launch_set_flags(hipStream_t s, int64_t n, const int32_t* idx, uint8_t* out) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_set_flags, MFEA_GRID(grid_rows(n)), n, idx, out);
 }
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,

@@ -125,7 +125,9 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
                      const double* val, const double* diag, int64_t G, const double* u,
                      double* partials, unsigned* ticket, double* red_out);
 
-// owned (multi-partition): count only elements this partition reports; NULL = all
+// owned (multi-partition): count only elements this partition reports; NULL = all.
+// fail_list / fail_cnt: the (owned) elements that fail in this launch are
+// appended (any order; NULL = no list)
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
                    double* stress, double* partials, unsigned* ticket, double* red_out,
@@ -133,6 +135,9 @@ void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* x
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,
                               Material m, double* Ke, double* L);
+
+// out[idx[i]] = 1, i < n
+void launch_set_flags(hipStream_t s, int64_t n, const int32_t* idx, uint8_t* out);
 
 // generic scalar-CSR operator (mfea_solve_csr)
 void launch_csr_rhs_init(hipStream_t s, int64_t n, const int64_t* indptr, const int32_t* indices,

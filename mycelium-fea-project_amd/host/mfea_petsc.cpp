@@ -352,8 +352,9 @@ int main(int argc, char** argv) {
                   L.world, L.world > 1 ? "es" : "", device, stt.iters, stt.relres, o.rtol, o.atol, o.max_it,
                   o.norm == MFEA_NORM_PRECONDITIONED ? "PRECONDITIONED" : "UNPRECONDITIONED",
                   o.precond == MFEA_PC_JACOBI ? "jacobi" : o.precond == MFEA_PC_GAMG ? "gamg"
-                  : o.precond == MFEA_PC_ICC ? "icc (DIC(0), 256-row blocks, multicolour)"
-                  : o.precond == MFEA_PC_SOR ? "sor (SSOR, 256-row blocks, multicolour)" : "bjacobi (3x3 node blocks)");
+                  : o.precond == MFEA_PC_ICC ? "icc (DIC(0) of the whole matrix, chain-piece multicolour order)"
+                  : o.precond == MFEA_PC_SOR ? "sor (SSOR of the whole matrix, chain-piece multicolour order)"
+                  : "bjacobi (3x3 node blocks)");
     }
     // the whole mesh's records on rank 0 (collective; one process: a copy)
     check(mfea_gather_results(h, U.data(), E ? S.data() : nullptr, E ? A.data() : nullptr), "mfea_gather_results");

@@ -153,6 +153,26 @@ int64_t shim_floating(const uint8_t* active, uint8_t* out) {
   for (size_t i = 0; i < f.size(); ++i) n += (out[i] = f[i]);
   return n;
 }
+// FloatTracker (amg.hpp) over the last built pattern: the whole-graph pass
+// for `active`, then the elements fail_ids[0..nf) fail one after another
+// (active updated in place, as capi.hip post_impl does).  floating[n_free]:
+// the tracker's set afterwards; returns how many rows became floating
+// through the failures (each listed once in new_rows, capacity n_free)
+int64_t shim_float_track(uint8_t* active, int64_t nf, const int32_t* fail_ids, uint8_t* floating,
+                         int32_t* new_rows) {
+  FloatTracker t;
+  const int32_t* e2n = g_P.e2n_perm.data();
+  t.set_graph(g_P.n_nodes, g_P.n_free, g_P.n_nodes - g_P.n_ghost, g_P.n_elems, e2n);
+  t.init(e2n, g_P.n_elems, active);
+  std::vector<int32_t> out;
+  for (int64_t i = 0; i < nf; ++i) {
+    active[fail_ids[i]] = 0;
+    t.fail(e2n, active, fail_ids[i], out);
+  }
+  for (int64_t i = 0; i < g_P.n_free; ++i) floating[i] = t.floating[i];
+  for (size_t i = 0; i < out.size(); ++i) new_rows[i] = out[i];
+  return (int64_t)out.size();
+}
 int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   std::vector<uint8_t> a(active, active + g_P.n_elems);
   std::string e = build_amg(g_P, a, nd, g_amg, kAmgMaxLevels, nullptr, g_strength, g_layout);

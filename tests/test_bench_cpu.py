@@ -135,3 +135,17 @@ def test_bench_gpus2_without_gpu_exits_nonzero():
     assert r.returncode != 0
     assert '"metric"' not in r.stdout
     assert "partitioned solve failed" in r.stderr
+
+
+def test_new_set_steps_label_the_step_after_the_failures(bench):
+    """eng.step reports the active count after its own failure update, so the
+    step that RUNS on a new set is the one after the count moved (round-5's
+    labelling marked the failing step itself)."""
+    E = 10
+    # steps 0-2 intact; step 3 fails 2 elements, step 4 none, step 5 one, step 6 one
+    n_act = [10, 10, 10, 8, 8, 7, 6, 6]
+    assert bench.new_set_steps(n_act, E) == [0, 0, 0, 0, 1, 0, 1, 1]
+    # a failure in step 0 (b = 0: cannot happen in the reference loop) → step 1
+    assert bench.new_set_steps([9, 9], E) == [0, 1]
+    assert bench.new_set_steps([], E) == []
+    assert bench.new_set_steps([10], E) == [0]

@@ -86,8 +86,11 @@ def test_cli_sim181147_force_matches_python_golden(tmp_path, pc):
     r = run(d, "-ksp_rtol", 1e-13, "-ksp_norm_type", "unpreconditioned", *(["-pc_type", pc] if pc else []),
             "-ksp_max_it", 200000)
     assert r.returncode == 0, r.stderr
-    if pc in ("icc", None):
-        assert "PC Object: type icc" in r.stdout
+    expect = {"jacobi": "jacobi", "gamg": "gamg",
+              "icc": "icc (DIC(0) of the whole matrix, chain-piece multicolour order)",
+              "sor": "sor (SSOR of the whole matrix, chain-piece multicolour order)"}[pc or "icc"]
+    assert f"PC Object: type {expect}\n" in r.stdout
+    assert "256-row" not in r.stdout
     F = read_rt(d / "fea_results" / "force_displacement.csv").values
     Fr = read_rt(os.path.join(GOLDEN, "ref", "sim_20251117_181147", "force_displacement.csv")).values
     assert F.shape == Fr.shape

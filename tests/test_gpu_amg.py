@@ -145,6 +145,42 @@ def test_gamg_kept_hierarchy_floating_pieces_exactly_zero(engine):
         assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
 
 
+def test_gamg_failures_through_post_keep_floating_exactly_zero(engine):
+    """The reference loop with failures driven by the post kernel alone (no
+    set_active between steps, src/fea_solver.py:216-295), pulled to 3× the
+    displacement so that pieces float: the hierarchy is kept (the floating
+    set moved by the failed ids, capi.hip local_failures / push_fmask), and
+    every step's U matches the direct solve of the set it ran on and is
+    EXACTLY zero on every floating free node."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    grip = np.zeros(len(xyz), bool)
+    grip[np.concatenate([top, bot])] = True
+    seen_float = 0
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+        engine.set_active(None)
+        active = np.ones(len(e2n), bool)
+        for step in range(fo.N_STEPS):
+            dy = 3 * fo.DISPLACEMENT_MAX * step / (fo.N_STEPS - 1)
+            f, n_act, st = engine.step(dy, -dy, _opts(1e-13), fo.MAX_STRAIN)
+            assert st.status == 0, step
+            if step > 0 and n_act > 0 and step % 3 == 0:
+                fl = _floating_nodes(xyz, e2n, active, top, bot) & ~grip
+                U = engine.displacement().reshape(-1, 3)
+                K = fo.assemble_global_stiffness(xyz, e2n, active)
+                known, vals = fo.known_dof_map(top, bot, dy, -dy)
+                Uref = fo.solve_system(K, known, vals)
+                assert rel(U.ravel(), Uref) <= 1e-10, step
+                assert np.all(U[fl] == 0.0), step
+                seen_float = max(seen_float, int(fl.sum()))
+            nxt = engine.active().astype(bool)
+            assert int(nxt.sum()) == n_act and not np.any(nxt & ~active)
+            active = nxt
+            if n_act == 0:
+                break
+        assert engine.get_option("amg_reused") == 1
+    assert active.sum() < len(e2n) and seen_float > 0
+
+
 def test_gamg_hierarchy_not_kept_for_a_superset(engine):
     """A hierarchy built on a REDUCED active set holds only that set's
     elements in A_0's slot lists; elements coming back (set_active(None))

@@ -114,6 +114,40 @@ def test_partitioned_gamg_split_depths(peng, rep_rows):
     assert rel(U, sysz["U"]) <= 1e-10
 
 
+@pytest.mark.parametrize("nparts,amg_dist", [(2, 1), (3, 1), (2, 0), (4, 0)])
+def test_partitioned_gamg_preconditioned_norm(peng, engine, nparts, amg_dist):
+    """PETSc's default KSPCG test (‖M⁻¹r‖ ≤ rtol·‖M⁻¹b‖, src/fea_petsc.cpp:
+    336-341) on the partitioned GAMG forms: the stopping ratio is formed from
+    the rank-gathered ‖M⁻¹b‖ (k_amg_cg_update<DIST>).  The global hierarchy
+    (amg_dist 1) is the one-partition preconditioner, so it stops on the
+    one-partition iteration (±1) with the same ratio; block Jacobi (0) stops
+    below rtol; a tight rtol reaches the direct solve either way."""
+    from mfea import NORM_PRECONDITIONED, PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    pre = make_opts(rtol=1e-5, max_it=5000, precond=PC_GAMG, norm=NORM_PRECONDITIONED)
+    tight = make_opts(rtol=1e-14, max_it=5000, precond=PC_GAMG, norm=NORM_PRECONDITIONED)
+    with peng.options(amg_dist=amg_dist):
+        xyz, e2n, top, bot = _sim181147(peng, nparts)
+        peng.assemble()
+        st = peng.solve(dy, -dy, pre)
+        assert st.status == 0 and 0 < st.relres <= 1e-5 and st.iters > 0
+        assert peng.solve(dy, -dy, tight).status == 0
+        assert rel(peng.displacement(), sysz["U"]) <= 1e-10
+    if amg_dist == 1:
+        engine.set_parts(1)
+        engine.set_mesh(xyz, e2n)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        engine.assemble()
+        st1 = engine.solve(dy, -dy, pre)
+        assert st1.status == 0 and abs(st.iters - st1.iters) <= 1, (st.iters, st1.iters)
+        if st.iters == st1.iters:
+            # the f32 V-cycle sums split levels in another order: ‖M⁻¹r‖ moves
+            # in the 6th digit (measured 2.4e-6 relative at 2 parts)
+            assert abs(st.relres - st1.relres) <= 1e-4 * st1.relres
+
+
 @pytest.mark.parametrize("nparts,axis", [(2, -1), (3, 0), (4, 1)])
 def test_partitioned_block_jacobi_gamg_matches_direct(peng, nparts, axis):
     """Option "amg_dist" 0: block Jacobi over per-partition hierarchies inside

@@ -171,7 +171,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     from mfea import _capi
     assert declared == set(_capi.EXPORTED)
-    assert _capi.abi_version() == 7
+    assert _capi.abi_version() == 8
 
 
 def test_create_without_gpu_fails_cleanly():
@@ -215,13 +215,15 @@ def test_synthetic_generator_sizes():
 
 
 def test_petsc_writer_reproduces_cpp_golden_text(tmp_path):
-    from mfea.io_csv import write_petsc_records
+    """fea_solver.py --format petsc (csrc/records.cpp's ostream dialect) writes
+    fea_petsc.cpp's text byte for byte (src/fea_petsc.cpp:433-516)."""
+    import fea_solver as fs
     ref = os.path.join(GOLDEN, "ref", "test_I_cpp")
     st = read_rt(os.path.join(ref, "stress_record.csv")).values[:, :-1]
     ac = read_rt(os.path.join(ref, "active_elements.csv")).values[:, :-1]
     U = read_rt(os.path.join(ref, "node_displacements.csv")).values[:, :-1]
     F = read_rt(os.path.join(ref, "force_displacement.csv")).values
-    write_petsc_records(str(tmp_path), 4, 3, list(st), list(ac.astype(bool)), list(U), list(F))
+    fs.write_records(str(tmp_path), 4, 3, list(st), list(ac.astype(bool)), list(U), list(F), out_format="petsc")
     for f in ("stress_record.csv", "active_elements.csv", "node_displacements.csv",
               "force_displacement.csv"):
         assert (tmp_path / f).read_text() == open(os.path.join(ref, f)).read(), f

@@ -233,9 +233,10 @@ def full_run(eng, opts, fs, dmax=None):
             "rebuild_steps": int(sum(rebuilt)), "rebuild_step_ms": reb,
             "rebuild_overhead_ms": float(sum(p - med for p in reb)), "median_step_ms": med,
             "note": "all 40 load steps from the intact mesh, failures included; a step on a new active set "
-                    "keeps the GAMG hierarchy (floating pieces masked) unless the iteration count degraded, "
-                    "then rebuilds it (rebuild_overhead_ms = rebuild steps' time above the median step); "
-                    "no CSV IO"}
+                    "keeps the GAMG hierarchy (floating pieces masked on the device) until the time its "
+                    "solves spent on extra iterations reaches the host build's time (rent or buy), then "
+                    "rebuilds it (rebuild_overhead_ms = rebuild steps' time above the median step); "
+                    "kept_hierarchy_step_idx = the steps that ran on a new set; no CSV IO"}
 
 
 def full_run_reference(opts, fs, device):

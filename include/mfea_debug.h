@@ -29,6 +29,12 @@ int mfea_debug_set_parts(mfea_handle* h, int nparts, int axis);
  * gathers it afresh).  One partition: the device activity. */
 int mfea_debug_global_active(mfea_handle* h, uint8_t* out);
 
+/* The free nodes with no path of active elements to a grip node, as the
+ * kept GAMG hierarchy masks them (kernels.hip launch_floating: connected
+ * components on the device, for the device's current activity): out[n] = 1
+ * for such a node n (original order, n_nodes bytes).  One partition. */
+int mfea_debug_floating(mfea_handle* h, uint8_t* out);
+
 /* Tuning options of a handle (experiments and tests; the defaults are the
  * measured best; the library reads no environment variables).  Names:
  *   "graph" 0|1          single-partition CG chunks as hipGraph replays (1)
@@ -54,7 +60,9 @@ int mfea_debug_global_active(mfea_handle* h, uint8_t* out);
  *   "amg_reuse" 0|1      GAMG: keep the hierarchy over element failures, floating pieces
  *                        masked (1), or rebuild it for every new active set (0)
  *   "amg_rebuild_pct" n  GAMG: a kept hierarchy is rebuilt once a solve needs more than
- *                        n % of the iterations it took on its own set (150)
+ *                        n % of the iterations it took on its own set (800), or
+ *   "amg_rebuild_rent" n once the time its solves spent on iterations above that count
+ *                        reaches n % of the time its host build took (100; 0: off)
  *   "amg_coarse_rho_ppm" n  GAMG: ρ̂ of the levels below 0, ppm (1750000: ω = 0.76, level 0
  *                        then at its exact ρ̂ = 2); 0: the Gershgorin rule max(2, g / 1.45)
  *                        everywhere.  A solve failing with it falls back to 0 for the
@@ -68,6 +76,8 @@ int mfea_debug_global_active(mfea_handle* h, uint8_t* out);
  *   "amg_fuse_setup" 0|1 GAMG numeric setup: compact operators in the Galerkin launches (1)
  *   "amg_theta_ppm" n    GAMG strength threshold θ in ppm (PETSc -pc_gamg_threshold; 0)
  *   "sweep_piece" 1..64  SOR / ICC: rows per chain piece at most (64; sweep.hip)
+ *   "cc_tile" 512|1024|2048|4096  floating rows on the device (kernels.hip launch_floating):
+ *                        rows per LDS union-find tile (1024)
  * Read-only: "sweep_colors", "sweep_pieces" (the last SOR / ICC plan).
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);

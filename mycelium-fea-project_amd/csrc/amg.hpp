@@ -327,43 +327,6 @@ struct SweepPlan {
 };
 std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out);
 
-// Free rows [0, P.n_free) with no path of active elements to a grip row:
-// out[i] = 1.  A hierarchy kept over element failures (capi.hip ensure_amg)
-// zeroes their rows of P_0, so the preconditioner leaves them at exactly zero
-// — what the direct solve gives an unloaded floating piece.
-void floating_free_rows(const Pattern& P, const std::vector<uint8_t>& active, std::vector<uint8_t>& out);
-
-// The same floating set kept current over element FAILURES without a
-// whole-graph pass per step (capi.hip post_impl / ensure_amg).  Components of
-// the active graph carry a label and their grip-row count; a failed element
-// (a, b) starts two breadth-first searches, one from each end, advanced
-// alternately: they meet (a and b still connected: nothing changes) or the
-// smaller side runs out first — a new component, relabelled, its grips moved
-// to the new label.  A component left without grips floats.  Each failure
-// costs O(the smaller side), so a step's update is proportional to what
-// actually split off, not to E (src/fea_solver.py:268-295: elements only ever
-// fail inside the step loop; an explicit re-activation re-inits).
-// Rows: [0, n_free) free, [n_free, n_grip_end) grips, the rest (ghosts) neither.
-struct FloatTracker {
-  bool valid = false;
-  int64_t n_rows = 0, n_free = 0, n_grip_end = 0;
-  std::vector<int32_t> adj_ptr, adj_row, adj_elem;  // row → (neighbour row, element), once per pattern
-  std::vector<int32_t> comp;                        // per row: component label
-  std::vector<int64_t> grips;                       // per label: grip rows in it
-  std::vector<uint8_t> floating;                    // per free row
-  std::vector<uint32_t> stamp;                      // BFS visit marks (2 per failure)
-  uint32_t epoch = 0;
-  std::vector<int32_t> qa, qb;
-  // adjacency of the element list e2n (E×2 rows, −1: skipped) over n_rows rows
-  void set_graph(int64_t n_rows, int64_t n_free, int64_t n_grip_end, int64_t n_elems, const int32_t* e2n);
-  // the whole-graph pass (union-find) for the activity `active`
-  void init(const int32_t* e2n, int64_t n_elems, const uint8_t* active);
-  // element e has just failed (active[e] already 0, the later failures of
-  // the same step still 1): free rows that float from now on are appended
-  // to `out`
-  void fail(const int32_t* e2n, const uint8_t* active, int32_t e, std::vector<int32_t>& out);
-};
-
 // xsend_rows / xrecv_rows: Pattern rows of the plan's xsend / xrecv nodes
 std::string build_amg_halo(const Pattern& P, const std::vector<uint8_t>& active, const AmgPlan& plan,
                            const std::vector<int32_t>& xsend_rows, const std::vector<int32_t>& xrecv_rows,

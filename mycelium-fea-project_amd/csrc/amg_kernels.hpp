@@ -77,7 +77,7 @@ struct AmgLevD {
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;
   // level 0 of a hierarchy kept over element failures: rows of floating
-  // pieces (amg.hpp floating_free_rows), whose P rows are formed as zero
+  // pieces (kernels.hpp launch_floating), whose P rows are formed as zero
   const uint8_t* fmask = nullptr;
   const int32_t* agg = nullptr;
   const int32_t* pv_ptr = nullptr;

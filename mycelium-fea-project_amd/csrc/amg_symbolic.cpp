@@ -995,161 +995,4 @@ std::string build_sweep(const AmgPlan& plan, int piece_len, SweepPlan& out) {
   return "";
 }
 
-// Free rows of P with no path of active elements to a grip (known, non-ghost)
-// row: their load is zero, so the direct solve leaves them exactly at zero
-// (src/fea_solver.py:128).  Union-find over the active elements.
-void floating_free_rows(const Pattern& P, const std::vector<uint8_t>& active, std::vector<uint8_t>& out) {
-  const int64_t N = P.n_nodes;
-  std::vector<int32_t> up(N);
-  std::iota(up.begin(), up.end(), 0);
-  auto find = [&](int32_t a) {
-    while (up[a] != a) a = up[a] = up[up[a]];
-    return a;
-  };
-  const int64_t E = P.n_elems;
-  for (int64_t e = 0; e < E; ++e) {
-    if (!active[e]) continue;
-    const int32_t a = P.e2n_perm[2 * e], b = P.e2n_perm[2 * e + 1];
-    if (a < 0 || b < 0) continue;
-    const int32_t ra = find(a), rb = find(b);
-    if (ra != rb) up[std::max(ra, rb)] = std::min(ra, rb);
-  }
-  std::vector<uint8_t> anchored(N, 0);
-  for (int64_t i = P.n_free; i < N - P.n_ghost; ++i) anchored[find((int32_t)i)] = 1;
-  out.assign(P.n_free, 0);
-  for (int64_t i = 0; i < P.n_free; ++i) out[i] = anchored[find((int32_t)i)] ? 0 : 1;
-}
-
-void FloatTracker::set_graph(int64_t nr, int64_t nf, int64_t nge, int64_t E, const int32_t* e2n) {
-  n_rows = nr;
-  n_free = nf;
-  n_grip_end = nge;
-  adj_ptr.assign(nr + 1, 0);
-  for (int64_t e = 0; e < E; ++e) {
-    const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    if (a < 0 || b < 0 || a == b) continue;
-    ++adj_ptr[a + 1];
-    ++adj_ptr[b + 1];
-  }
-  for (int64_t r = 0; r < nr; ++r) adj_ptr[r + 1] += adj_ptr[r];
-  adj_row.resize(adj_ptr[nr]);
-  adj_elem.resize(adj_ptr[nr]);
-  std::vector<int32_t> fill(adj_ptr.begin(), adj_ptr.end() - 1);
-  for (int64_t e = 0; e < E; ++e) {
-    const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    if (a < 0 || b < 0 || a == b) continue;
-    adj_row[fill[a]] = b;
-    adj_elem[fill[a]++] = (int32_t)e;
-    adj_row[fill[b]] = a;
-    adj_elem[fill[b]++] = (int32_t)e;
-  }
-  stamp.assign(nr, 0);
-  epoch = 0;
-  valid = false;
-}
-
-void FloatTracker::init(const int32_t* e2n, int64_t E, const uint8_t* active) {
-  std::vector<int32_t> up(n_rows);
-  std::iota(up.begin(), up.end(), 0);
-  auto find = [&](int32_t a) {
-    while (up[a] != a) a = up[a] = up[up[a]];
-    return a;
-  };
-  for (int64_t e = 0; e < E; ++e) {
-    if (!active[e]) continue;
-    const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-    if (a < 0 || b < 0) continue;
-    const int32_t ra = find(a), rb = find(b);
-    if (ra != rb) up[std::max(ra, rb)] = std::min(ra, rb);
-  }
-  comp.resize(n_rows);
-  grips.assign(n_rows, 0);
-  for (int64_t r = 0; r < n_rows; ++r) {
-    comp[r] = find((int32_t)r);
-    if (r >= n_free && r < n_grip_end) ++grips[comp[r]];
-  }
-  floating.assign(n_free, 0);
-  for (int64_t r = 0; r < n_free; ++r) floating[r] = grips[comp[r]] ? 0 : 1;
-  valid = true;
-}
-
-void FloatTracker::fail(const int32_t* e2n, const uint8_t* active, int32_t e, std::vector<int32_t>& out) {
-  const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
-  if (!valid || a < 0 || b < 0 || a == b) return;
-  const int32_t L = comp[a];
-  if (grips[L] == 0) return;  // already floating: any piece of it floats too
-  if (epoch >= 0xFFFFFFF0u) {
-    std::fill(stamp.begin(), stamp.end(), 0u);
-    epoch = 0;
-  }
-  const uint32_t sa = ++epoch, sb = ++epoch;
-  auto grip = [&](int32_t r) -> int64_t { return r >= n_free && r < n_grip_end ? 1 : 0; };
-  qa.assign(1, a);
-  qb.assign(1, b);
-  stamp[a] = sa;
-  stamp[b] = sb;
-  int64_t ga = grip(a), gb = grip(b);
-  size_t ia = 0, ib = 0;
-  // one row of a side; true: it reached the other side's marks
-  auto expand = [&](std::vector<int32_t>& q, size_t& i, uint32_t mine, uint32_t other, int64_t& g) {
-    const int32_t r = q[i++];
-    for (int32_t k = adj_ptr[r]; k < adj_ptr[r + 1]; ++k) {
-      if (!active[adj_elem[k]]) continue;
-      const int32_t c = adj_row[k];
-      if (stamp[c] == other) return true;
-      if (stamp[c] != mine) {
-        stamp[c] = mine;
-        q.push_back(c);
-        g += grip(c);
-      }
-    }
-    return false;
-  };
-  const std::vector<int32_t>* S = nullptr;
-  int64_t gs = 0;
-  int32_t rest = -1;
-  for (;;) {
-    if (ia == qa.size()) {
-      S = &qa, gs = ga, rest = b;
-      break;
-    }
-    if (expand(qa, ia, sa, sb, ga)) return;
-    if (ib == qb.size()) {
-      S = &qb, gs = gb, rest = a;
-      break;
-    }
-    if (expand(qb, ib, sb, sa, gb)) return;
-  }
-  // *S is a whole component now: a new label with its grips
-  const int32_t nl = (int32_t)grips.size();
-  grips.push_back(gs);
-  grips[L] -= gs;
-  for (int32_t r : *S) comp[r] = nl;
-  if (gs == 0)
-    for (int32_t r : *S)
-      if (r < n_free && !floating[r]) {
-        floating[r] = 1;
-        out.push_back(r);
-      }
-  if (grips[L] == 0 && gs > 0) {  // the grips all went with S: the rest floats
-    const uint32_t sr = ++epoch;
-    qa.assign(1, rest);
-    stamp[rest] = sr;
-    for (size_t i = 0; i < qa.size(); ++i) {
-      const int32_t r = qa[i];
-      if (r < n_free && !floating[r]) {
-        floating[r] = 1;
-        out.push_back(r);
-      }
-      for (int32_t k = adj_ptr[r]; k < adj_ptr[r + 1]; ++k) {
-        const int32_t c = adj_row[k];
-        if (active[adj_elem[k]] && stamp[c] != sr) {
-          stamp[c] = sr;
-          qa.push_back(c);
-        }
-      }
-    }
-  }
-}
-
 }  // namespace mfea

@@ -33,6 +33,22 @@ namespace {
 
 thread_local std::string g_err;
 
+// MFEA_BUILD_TIMES=1 (as amg_symbolic.cpp's build split): the host side of a
+// new active set on stderr — failed-id tracking, plan build, upload, mask
+struct HostLap {
+  bool on = std::getenv("MFEA_BUILD_TIMES") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what, int64_t n = -1) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    if (n >= 0)
+      std::fprintf(stderr, "  host %-26s %8.2f ms  (%lld)\n", what, std::chrono::duration<double, std::milli>(now - t).count(), (long long)n);
+    else
+      std::fprintf(stderr, "  host %-26s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -129,24 +145,21 @@ struct Part {
   // a hierarchy kept over element failures (option amg_reuse): the activity
   // its floating-row mask reflects, the iterations of its first solve, and
   // whether a later solve degraded enough to rebuild
-  bool amg_mask_ok = false;          // amg_fmask = flt's floating set, up to flt_new
-  DevBuf<uint8_t> amg_fmask;         // level-0 rows of floating pieces (amg.hpp floating_free_rows)
-  // one partition: the floating set kept current over failures (amg.hpp
-  // FloatTracker), the rows that floated since the mask's last update, the
-  // level-0 label of every free row, and the pinned / device staging of a
-  // mask update
-  FloatTracker flt;
-  std::vector<int32_t> flt_new;
-  std::vector<int32_t> row0_inv;
-  DevBuf<int32_t> fm_rows;
-  int32_t* fm_pin = nullptr;
-  size_t fm_pin_n = 0;
+  DevBuf<uint8_t> amg_fmask;         // level-0 rows of floating pieces (kernels.hpp launch_floating)
+  const int32_t* amg_row0_inv = nullptr;  // level-0 label of every free row (carved from amg_i)
+  DevBuf<int32_t> cc_parent;         // launch_floating's scratch: component links, anchored roots
+  DevBuf<uint8_t> cc_anch;
   // the plan's key covers the current activity: act_sub_gen when it was
   // built or last compared (failures only ever shrink the set, so it holds
   // until the activity is set explicitly), and its element count
   int64_t amg_sub_gen = -1;
   int64_t amg_key_count = 0;
   int amg_build_iters = -1;
+  // the kept hierarchy's rent (option amg_rebuild_rent): the host time its
+  // build took, and the time its solves have spent since on iterations above
+  // amg_build_iters — a rebuild is bought once the rent paid reaches its price
+  double amg_build_s = 0.0;
+  double amg_excess_s = 0.0;
   bool amg_stale = false;
   bool amg_reused = false;           // the last ensure_amg kept a hierarchy built for another set
   int64_t amg_seen_gen = -1;         // act_gen at which the plan / mask last matched the activity
@@ -191,9 +204,6 @@ struct Part {
   XDev xd_g, xd_sg;
   DevBuf<int32_t> amg_xi;
   DevBuf<double> amg_xs, amg_xr;
-  ~Part() {
-    if (fm_pin) (void)hipHostFree(fm_pin);
-  }
 };
 
 struct mfea_handle {
@@ -299,7 +309,14 @@ struct mfea_handle {
   // until a solve needs more than amg_rebuild_pct % of the iterations of the
   // hierarchy's first solve (+2), then rebuild; 0 rebuild on every new active set
   int opt_amg_reuse = 1;
-  int opt_amg_rebuild_pct = 150;
+  int opt_cc_tile = 1024;  // floating rows on the device: rows per LDS tile (512, 1024, 2048, 4096; C3 73 µs at 512-1024, C5 0.6 ms at 1024-2048)
+  int opt_amg_rebuild_pct = 800;
+  // ... or once the time its solves spent on iterations above that count
+  // reaches this % of the time the last build took (0: off).  Rent-or-buy:
+  // a C5 rebuild costs 2.4 s of host work — ≈ 80 steps — so a kept hierarchy
+  // that needs 40-100 % more iterations is kept; at most twice the cost of
+  // the best choice in hindsight (measured)
+  int opt_amg_rebuild_rent = 100;
   int opt_amg_dist = -1;          // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block
                                   // Jacobi over per-partition hierarchies, -1 whichever solves faster (measured)
   int64_t opt_amg_rep_rows = 32768;  // distributed V-cycle: levels of at most this many rows are replicated
@@ -566,7 +583,6 @@ int upload_part(mfea_handle* h, Part& pt, bool dm) {
   }
   HIPC(pt.fail_list.alloc(std::max<int64_t>(E, 1)));
   HIPC(pt.fail_cnt.alloc(1));
-  if (!dm) pt.flt.set_graph(P.n_nodes, P.n_free, P.n_nodes - P.n_ghost, P.n_elems, P.e2n_perm.data());
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
@@ -1290,6 +1306,12 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     const std::string merr = build_amg_merge(pl, pt.amg_coll, pt.amg_mplan);
     if (!merr.empty()) return fail(MFEA_EINVAL, merr);
   }
+  // the level-0 label of every free row (the floating mask's scatter, launch_floating)
+  std::vector<int32_t> row0_inv;
+  if (!rk && nlev > 1) {
+    row0_inv.assign(pl.row0.size(), -1);
+    for (size_t i = 0; i < pl.row0.size(); ++i) row0_inv[pl.row0[i]] = (int32_t)i;
+  }
   int32_t* ip = nullptr;
   double* dp = nullptr;
   float* fp = nullptr;
@@ -1442,6 +1464,7 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     }
     pt.amg_a0_ptr = I(a0 ? a0->ptr : pl.a0.ptr);
     pt.amg_a0_a = I(a0 ? a0->a : pl.a0.a);
+    pt.amg_row0_inv = !rk && nlev > 1 ? I(row0_inv) : nullptr;
     const int64_t nf = nlev ? pl.lev[0].A.n : 0;
     pt.amg_cg.n = nf;
     pt.amg_cg.lo = rk && nlev ? rk->lo[0] : 0;
@@ -1496,7 +1519,6 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
     HIPC(pt.amg_fmask.alloc(std::max<int64_t>(pl.lev[0].A.n, 1)));
     HIPC(hipMemsetAsync(pt.amg_fmask.ptr, 0, pt.amg_fmask.n, s));
     pt.amg_lev[0].fmask = pt.amg_fmask.ptr;
-    pt.amg_mask_ok = false;
   }
   // the smoothing weights (ρ̂ per level in place of the Gershgorin estimate)
   pt.amg_om_own = !rk;
@@ -1560,55 +1582,19 @@ int upload_amg_halo(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
   return 0;
 }
 
-// The floating-row mask of the active set `key` (= the host activity) in
-// level-0 labels, whole: the tracker's whole-graph pass (one partition's own
-// hierarchy: a partition cannot tell alone what is floating)
-int upload_fmask(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
-  pt.flt.init(pt.P.e2n_perm.data(), pt.P.n_elems, key.data());
-  pt.flt_new.clear();
-  const std::vector<int32_t>& row0 = pt.amg.row0;
-  pt.row0_inv.assign(pt.P.n_free, -1);
-  std::vector<uint8_t> m(row0.size());
-  for (size_t i = 0; i < row0.size(); ++i) {
-    m[i] = pt.flt.floating[row0[i]];
-    pt.row0_inv[row0[i]] = (int32_t)i;
-  }
-  if (!m.empty()) {
-    HIPC(hipMemcpyAsync(pt.amg_fmask.ptr, m.data(), m.size(), hipMemcpyHostToDevice, h->stream));
-    RC(sync_stream(h));
-  }
-  pt.amg_mask_ok = true;
-  return 0;
-}
-
-// The rows that floated since the mask's last update (flt_new, in Pattern
-// rows) set in the device mask: a pinned list and one scatter launch on the
-// stream, no host wait (the next post waits for the step anyway, so the
-// pinned list is free again when the next failures fill it)
-int push_fmask(mfea_handle* h, Part& pt) {
-  const size_t n = pt.flt_new.size();
-  if (n == 0) return 0;
-  hipStream_t s = h->stream;
-  if (pt.fm_pin_n < n) {
-    HIPC(hipStreamSynchronize(s));
-    if (pt.fm_pin) (void)hipHostFree(pt.fm_pin);
-    pt.fm_pin = nullptr;
-    pt.fm_pin_n = 0;
-    const size_t cap = std::max<size_t>(n, 4096);
-    HIPC(hipHostMalloc(&pt.fm_pin, cap * sizeof(int32_t), hipHostMallocDefault));
-    pt.fm_pin_n = cap;
-  }
-  for (size_t i = 0; i < n; ++i) {
-    const int32_t l = pt.row0_inv[pt.flt_new[i]];
-    if (l < 0) return fail(MFEA_EINVAL, "internal: floating row outside level 0");
-    pt.fm_pin[i] = l;
-  }
-  if (pt.fm_rows.n < n) HIPC(hipStreamSynchronize(s));
-  HIPC(pt.fm_rows.alloc(std::max<size_t>(n, 4096)));
-  HIPC(hipMemcpyAsync(pt.fm_rows.ptr, pt.fm_pin, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  launch_set_flags(s, (int64_t)n, pt.fm_rows.ptr, pt.amg_fmask.ptr);
+// The floating-row mask of the device's current activity in level-0 labels
+// (one partition's own hierarchy: a partition cannot tell alone what is
+// floating): connected components on the device (kernels.hpp
+// launch_floating), four launches on the stream, no host pass or wait
+int enqueue_fmask(mfea_handle* h, Part& pt) {
+  const Pattern& P = pt.P;
+  if (P.n_free == 0 || !pt.amg_row0_inv) return 0;
+  HIPC(pt.cc_parent.alloc(std::max<int64_t>(P.n_nodes, 1)));
+  HIPC(pt.cc_anch.alloc(std::max<int64_t>(P.n_nodes, 1)));
+  launch_floating(h->stream, P.n_nodes, P.n_free, P.n_nodes - P.n_ghost, pt.slice_ptr.ptr, pt.row_len.ptr,
+                  pt.s_col.ptr, pt.s_elem.ptr, pt.active.ptr, pt.cc_parent.ptr, pt.cc_anch.ptr, pt.amg_row0_inv,
+                  pt.amg_fmask.ptr, h->opt_cc_tile);
   HIPC(hipGetLastError());
-  pt.flt_new.clear();
   return 0;
 }
 
@@ -1715,12 +1701,11 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   // (no O(E) key compares on the hot path)
   if (!dm && pt.amg_ok && !pt.amg_stale && pt.amg_seen_gen == h->act_gen) return 0;
   // the activity moved only by failures since the plan's key was set (post
-  // kept the host activity and the floating set current from the failed
-  // ids): keep the hierarchy with no O(E) pass — the new floating rows go to
-  // the device mask as a list
+  // kept the host activity current from the failed ids): keep the hierarchy
+  // with no host O(E) pass — the floating mask is recomputed on the device
   if (!dm && pt.amg_ok && !pt.amg_stale && h->opt_amg_reuse && pt.amg_lev.size() > 1 && h->act_host_ok &&
-      pt.amg_sub_gen == h->act_sub_gen && pt.flt.valid && pt.amg_mask_ok) {
-    RC(push_fmask(h, pt));
+      pt.amg_sub_gen == h->act_sub_gen) {
+    RC(enqueue_fmask(h, pt));
     pt.amg_reused = h->act_count != pt.amg_key_count;
     pt.amg_seen_gen = h->act_gen;
     return 0;
@@ -1739,7 +1724,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
     // keep the hierarchy: the numeric setup re-forms its values from the new
     // K (failed elements are zero slots); only pieces cut off from both grips
     // need care — their P_0 rows are zeroed so they stay exactly at zero
-    RC(upload_fmask(h, pt, key));
+    RC(enqueue_fmask(h, pt));
     pt.amg_reused = pt.amg_key != key;
     pt.amg_seen_gen = h->act_gen;
     pt.amg_sub_gen = h->act_sub_gen;  // key ⊆ amg_key, compared
@@ -1756,6 +1741,8 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
     return 0;
   }
   pt.amg_ok = false;
+  HostLap clk;
+  const auto build_t0 = std::chrono::steady_clock::now();
   AmgLayout lay;
   lay.spatial = h->opt_amg_spatial;
   lay.by_a = h->opt_amg_cycle == 1;
@@ -1764,18 +1751,23 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
                               amg_strength(h), lay);
   if (err.empty() && sweep) err = build_sweep_bounded(pt.amg, h->opt_sweep_piece, pt.sweep);
   if (!err.empty()) return fail(MFEA_EINVAL, "AMG setup: " + err);
+  clk.lap("plan build");
   destroy_graph(h);
   pt.amg_kind = kind;
   RC(upload_amg(h, pt, pt.amg));
   RC(upload_sweep(h, pt, kind));
   if (dm) RC(upload_amg_halo(h, pt, key));
+  clk.lap("plan upload");
   pt.dev_plan = 0;
   pt.amg_key = key;
   pt.amg_ok = true;
   pt.amg_stale = false;
   pt.amg_build_iters = -1;
+  pt.amg_excess_s = 0.0;
+  pt.amg_build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - build_t0).count();
   pt.amg_reused = false;
-  if (!dm && pt.amg_lev.size() > 1) RC(upload_fmask(h, pt, key));
+  if (!dm && pt.amg_lev.size() > 1) RC(enqueue_fmask(h, pt));
+  clk.lap("floating mask");
   if (!dm) pt.amg_seen_gen = h->act_gen;
   pt.amg_sub_gen = dm ? -1 : h->act_sub_gen;
   pt.amg_key_count = (int64_t)std::count(key.begin(), key.end(), (uint8_t)1);
@@ -1979,7 +1971,9 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   Part& pt = part0(h);
   hipStream_t s = h->stream;
   bool rebuilt = false;
+  HostLap clk;
   RC(ensure_amg(h, pt, &rebuilt, o->precond));
+  clk.lap("ensure_amg");
   const int chunk = o->chunk > 0 ? solve_chunk_size(o) : 2;
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
@@ -2011,6 +2005,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const int expected = std::max(0, std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16) - 1);
   SolveState fin;
   int rc;
+  const auto drive_t0 = std::chrono::steady_clock::now();
   // x to row order behind every planned batch (see drive_planned)
   auto finish = [&]() -> int {
     launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
@@ -2079,6 +2074,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                      &fin, finish, exact_rem);
   }
   if (rc) return rc;
+  clk.lap("solve (setup + iterations)", fin.iters);
   if (fin.status != 0 && pt.amg_reused) {
     // a hierarchy kept from another active set failed: rebuild for this one
     // before anything else is blamed (the ω retry below would otherwise run
@@ -2093,9 +2089,17 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   if (fin.status == 0) pt.amg_last_iters = fin.iters;
   if (fin.status == 0 && !pt.amg_reused) {
     pt.amg_build_iters = fin.iters;  // the hierarchy on the set it was built for
-  } else if (pt.amg_reused && pt.amg_build_iters >= 0 &&
-             fin.iters > (int64_t)pt.amg_build_iters * h->opt_amg_rebuild_pct / 100 + 2) {
-    pt.amg_stale = true;  // degraded: the next solve rebuilds for its active set
+  } else if (pt.amg_reused && pt.amg_build_iters >= 0) {
+    // rent or buy: the iterations above the hierarchy's own count cost this
+    // solve's time per iteration; once that rent adds up to the last build's
+    // time, or one solve needs far more (amg_rebuild_pct), rebuild
+    const double t_it = std::chrono::duration<double>(std::chrono::steady_clock::now() - drive_t0).count() /
+                        std::max<int64_t>(1, fin.iters + 1);
+    if (fin.iters > pt.amg_build_iters) pt.amg_excess_s += (fin.iters - pt.amg_build_iters) * t_it;
+    const bool rent_due = h->opt_amg_rebuild_rent > 0 &&
+                          pt.amg_excess_s >= pt.amg_build_s * h->opt_amg_rebuild_rent / 100.0;
+    if (rent_due || fin.iters > (int64_t)pt.amg_build_iters * h->opt_amg_rebuild_pct / 100 + 2)
+      pt.amg_stale = true;  // degraded: the next solve rebuilds for its active set
   }
   rc = finish_solve(h, fin, st);
   if (st) {
@@ -2822,32 +2826,25 @@ int apply_failures(mfea_handle* h) {
 }
 
 // One partition: the elements that failed in the last post (the stress
-// kernel's list) move the host activity and the floating-row tracker —
-// O(failures + what split off), no E-byte copy or whole-graph pass
-// (src/fea_solver.py:283-284: elements only ever fail).  The list's counter
-// is cleared for the next post.
+// kernel's list) move the host activity — O(failures), no E-byte copy or
+// O(E) pass (src/fea_solver.py:283-284: elements only ever fail).  The
+// list's counter is cleared for the next post.
 unsigned* fail_counter(Part& pt) { return reinterpret_cast<unsigned*>(pt.red.ptr + 6); }
 
 int local_failures(mfea_handle* h, Part& pt, unsigned c) {
+  HostLap clk;
   if (c > (unsigned)pt.P.n_elems) return fail(MFEA_EINVAL, "internal: failed-element list overflow");
   std::vector<int32_t> ids(c);
   HIPC(hipMemcpy(ids.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
   HIPC(hipMemsetAsync(fail_counter(pt), 0, sizeof(unsigned), h->stream));
-  if (!h->act_host_ok || h->act_host.size() != (size_t)pt.P.n_elems) {
-    pt.flt.valid = false;
-    return 0;
-  }
-  std::sort(ids.begin(), ids.end());  // (atomic list order: the tracker's labels deterministic)
+  if (!h->act_host_ok || h->act_host.size() != (size_t)pt.P.n_elems) return 0;
   for (int32_t e : ids) {
     if (e < 0 || e >= pt.P.n_elems || !h->act_host[e]) return fail(MFEA_EINVAL, "internal: bad failed element");
     h->act_host[e] = 0;
-    pt.flt.fail(pt.P.e2n_perm.data(), h->act_host.data(), e, pt.flt_new);
   }
   h->act_count -= (int64_t)c;
-  if (h->act_count != h->n_active) {  // cannot happen: fall back to a download
-    h->act_host_ok = false;
-    pt.flt.valid = false;
-  }
+  clk.lap("failed ids", (int64_t)c);
+  if (h->act_count != h->n_active) h->act_host_ok = false;  // cannot happen: fall back to a download
   return 0;
 }
 
@@ -3130,7 +3127,6 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
   ++h->act_gen;
   ++h->act_sub_gen;
   h->act_all = !active;
-  for (auto& pp : h->parts) pp->flt.valid = false;
   if (partitioned(h)) {  // the global activity is known here: no exchange needed for it
     h->gkey.assign(h->Ecount, 1);
     if (active)
@@ -3768,6 +3764,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     if (value < 100 || value > 100000) return fail(MFEA_EINVAL, "amg_rebuild_pct: 100 .. 100000");
     h->opt_amg_rebuild_pct = (int)value;
   }
+  else if (n == "amg_rebuild_rent") {
+    if (value < 0 || value > 100000) return fail(MFEA_EINVAL, "amg_rebuild_rent: 0 .. 100000");
+    h->opt_amg_rebuild_rent = (int)value;
+  }
   else if (n == "amg_dist") {
     if (value < -1 || value > 1)
       return fail(MFEA_EINVAL, "amg_dist: 0 (block Jacobi over partitions), 1 (global hierarchy), -1 (faster)");
@@ -3778,6 +3778,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     if (value < 0) return fail(MFEA_EINVAL, "amg_rep_rows: >= 0");
     h->opt_amg_rep_rows = value;
     h->gamg_ok = false;
+  }
+  else if (n == "cc_tile") {
+    if (value != 512 && value != 1024 && value != 2048 && value != 4096)
+      return fail(MFEA_EINVAL, "cc_tile: 512, 1024, 2048 or 4096");
+    h->opt_cc_tile = (int)value;
   }
   else if (n == "part_slack_pct") {
     if (value < 0 || value > 45) return fail(MFEA_EINVAL, "part_slack_pct: 0..45");
@@ -3973,10 +3978,12 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_dist") *value = h->opt_amg_dist;
   else if (n == "amg_reuse") *value = h->opt_amg_reuse;
   else if (n == "amg_rebuild_pct") *value = h->opt_amg_rebuild_pct;
+  else if (n == "amg_rebuild_rent") *value = h->opt_amg_rebuild_rent;
   else if (n == "amg_reused") *value = part0(h).amg_reused ? 1 : 0;  // read-only: the last solve kept a hierarchy built for another set
   else if (n == "amg_build_iters") *value = part0(h).amg_build_iters;  // read-only
   else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
+  else if (n == "cc_tile") *value = h->opt_cc_tile;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);
   return 0;
@@ -3990,6 +3997,30 @@ int mfea_debug_global_active(mfea_handle* h, uint8_t* out) {
   if (partitioned(h)) RC(global_active(h, key));
   else RC(gather_active(h, key));
   std::copy(key.begin(), key.end(), out);
+  return 0;
+}
+
+int mfea_debug_floating(mfea_handle* h, uint8_t* out) {
+  if (!h || !out) return fail(MFEA_EINVAL, "bad argument");
+  RC(set_device(h));
+  RC(ensure_built(h));
+  if (partitioned(h)) return fail(MFEA_ESTATE, "mfea_debug_floating: one partition");
+  Part& pt = part0(h);
+  const Pattern& P = pt.P;
+  std::memset(out, 0, (size_t)h->N);
+  if (P.n_free == 0) return 0;
+  DevBuf<uint8_t> mask;
+  HIPC(mask.alloc(P.n_free));
+  HIPC(pt.cc_parent.alloc(std::max<int64_t>(P.n_nodes, 1)));
+  HIPC(pt.cc_anch.alloc(std::max<int64_t>(P.n_nodes, 1)));
+  launch_floating(h->stream, P.n_nodes, P.n_free, P.n_nodes - P.n_ghost, pt.slice_ptr.ptr, pt.row_len.ptr,
+                  pt.s_col.ptr, pt.s_elem.ptr, pt.active.ptr, pt.cc_parent.ptr, pt.cc_anch.ptr, nullptr, mask.ptr,
+                  h->opt_cc_tile);
+  HIPC(hipGetLastError());
+  std::vector<uint8_t> m(P.n_free);
+  HIPC(hipMemcpyAsync(m.data(), mask.ptr, P.n_free, hipMemcpyDeviceToHost, h->stream));
+  RC(sync_stream(h));
+  for (int64_t r = 0; r < P.n_free; ++r) out[P.perm[r]] = m[r];
   return 0;
 }
 

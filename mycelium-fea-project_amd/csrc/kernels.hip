@@ -491,12 +491,153 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
   block_publish<1>(cnt, partials, ticket, red_out);
 }
 
-// out[idx[i]] = 1 for i < n (the kept GAMG hierarchy's floating-row mask:
-// rows that floated since the last upload, capi.hip push_fmask)
-__global__ __launch_bounds__(kBlock) void k_set_flags(int64_t n, const int32_t* __restrict__ idx,
-                                                      uint8_t* __restrict__ out) {
+// ---------------------------------------------------------------------------
+// Floating free rows on the device: connected components of the active
+// element graph, then per component whether a grip row is in it.  A free
+// row of a component without a grip is floating: zero load, so the direct
+// solve leaves it at exactly zero (src/fea_solver.py:128) and the kept GAMG
+// hierarchy masks its P_0 row (capi.hip enqueue_fmask).  Replaces a host
+// union-find over every element per new active set.
+//
+// The rows are in depth-first order of the free-node graph (symbolic.hpp):
+// hyphal chains are runs of consecutive rows, so nearly every coupling joins
+// two rows of the same 4096-row tile.  Pass 1 (one workgroup per tile) runs
+// union-find over the tile's own couplings in LDS and links every row to its
+// tile-local root; pass 2 hooks the few couplings between tiles into those
+// roots with CAS in HBM; pass 3 flattens.  Roots only ever link under smaller
+// rows, so every component ends at its smallest row whatever order the
+// hooks ran in: the result is deterministic.
+// ---------------------------------------------------------------------------
+constexpr int kSlice = 64;  // SELL-64 rows per slice (symbolic.hpp)
+
+__device__ __forceinline__ int32_t cc_load(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the root of v, halving the path behind it (a parent only ever moves to a
+// smaller row of the same component, so a racing shortcut stays valid)
+__device__ __forceinline__ int32_t cc_root(int32_t* parent, int32_t v) {
+  int32_t cur = cc_load(parent + v);
+  if (cur != v) {
+    int32_t prev = v, next;
+    while (cur > (next = cc_load(parent + cur))) {
+      __hip_atomic_store(parent + prev, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+
+__device__ __forceinline__ int32_t lds_root(volatile int32_t* lp, int32_t v) {
+  int32_t cur = lp[v], next;
+  if (cur != v) {
+    int32_t prev = v;
+    while (cur > (next = lp[cur])) {
+      lp[prev] = next;
+      prev = cur;
+      cur = next;
+    }
+  }
+  return cur;
+}
+
+// pass 1: union-find over the couplings inside one tile of rows, in LDS;
+// parent[row] = its tile-local root (a global row), anchored[row] = 0
+template <int kCcTile>
+__global__ __launch_bounds__(kBlock) void k_cc_local(int64_t n, const int32_t* __restrict__ slice_ptr,
+                                                     const int32_t* __restrict__ row_len,
+                                                     const int32_t* __restrict__ s_col,
+                                                     const int32_t* __restrict__ s_elem,
+                                                     const uint8_t* __restrict__ active, int32_t* __restrict__ parent,
+                                                     uint8_t* __restrict__ anchored) {
+  __shared__ int32_t lp[kCcTile];
+  const int64_t base = (int64_t)blockIdx.x * kCcTile;
+  const int rows = (int)min<int64_t>(kCcTile, n - base);
+  for (int i = threadIdx.x; i < rows; i += kBlock) lp[i] = i;
+  __syncthreads();
+  for (int i = threadIdx.x; i < rows; i += kBlock) {
+    const int64_t r = base + i;
+    const int len = row_len[r];
+    const int64_t p0 = (int64_t)slice_ptr[r >> 6] * kSlice + (r & 63);
+    for (int k = 0; k < len; ++k) {
+      const int64_t pos = p0 + (int64_t)k * kSlice;
+      const int32_t c = s_col[pos];
+      const int64_t j = (int64_t)c - base;
+      if (c < 0 || j <= i || j >= rows || !active[s_elem[pos]]) continue;
+      int32_t a = lds_root(lp, i), b = lds_root(lp, (int32_t)j);
+      while (a != b) {  // hook the larger root under the smaller
+        if (a > b) {
+          const int32_t t = a;
+          a = b;
+          b = t;
+        }
+        const int32_t old = atomicCAS(&lp[b], b, a);
+        if (old == b) break;
+        b = lds_root(lp, old);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < rows; i += kBlock) {
+    int32_t c = lp[i], next;
+    while (c > (next = lp[c])) c = next;
+    parent[base + i] = (int32_t)(base + c);
+    anchored[base + i] = 0;
+  }
+}
+
+// pass 2: the couplings between tiles hook tile roots together (CAS in HBM)
+__global__ __launch_bounds__(kBlock) void k_cc_cross(int64_t n, const int32_t* __restrict__ slice_ptr,
+                                                     const int32_t* __restrict__ row_len,
+                                                     const int32_t* __restrict__ s_col,
+                                                     const int32_t* __restrict__ s_elem,
+                                                     const uint8_t* __restrict__ active, int32_t* parent,
+                                                     int tile_rows) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= n) return;
+  const int len = row_len[r];
+  const int64_t p0 = (int64_t)slice_ptr[r >> 6] * kSlice + (r & 63);
+  const int64_t tile = r / tile_rows;
+  for (int k = 0; k < len; ++k) {
+    const int64_t pos = p0 + (int64_t)k * kSlice;
+    const int32_t c = s_col[pos];
+    if (c <= r || c / tile_rows == tile || !active[s_elem[pos]]) continue;
+    int32_t a = cc_root(parent, (int32_t)r), b = cc_root(parent, c);
+    while (a != b) {
+      if (a > b) {
+        const int32_t t = a;
+        a = b;
+        b = t;
+      }
+      const int32_t old = atomicCAS(parent + b, b, a);
+      if (old == b) break;
+      b = cc_root(parent, old);
+    }
+  }
+}
+
+// pass 3: every row's parent to its root (the walk writes nothing but the
+// row's own link, so a concurrent walk reads either link — both lead to the
+// root); grip rows [g0, g1) mark their root anchored
+__global__ __launch_bounds__(kBlock) void k_cc_flatten(int64_t n, int32_t* parent, int64_t g0, int64_t g1,
+                                                       uint8_t* __restrict__ anchored) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) out[idx[i]] = 1;
+  if (i >= n) return;
+  const int32_t old = cc_load(parent + i);
+  int32_t r = old, next;
+  while (r > (next = cc_load(parent + r))) r = next;
+  if (r != old) __hip_atomic_store(parent + i, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (i >= g0 && i < g1) anchored[r] = 1;
+}
+
+// mask[label[i]] = 1 iff free row i's component holds no grip row
+__global__ __launch_bounds__(kBlock) void k_cc_mask(int64_t nf, const int32_t* __restrict__ parent,
+                                                    const uint8_t* __restrict__ anchored,
+                                                    const int32_t* __restrict__ label, uint8_t* __restrict__ mask) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nf) return;
+  mask[label ? label[i] : i] = anchored[parent[i]] ? 0 : 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_element_stiffness(int64_t n, const double* __restrict__ p1,
@@ -657,9 +798,19 @@ void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* x
                      active, stress, partials, ticket, red_out, owned, fail_list, fail_cnt);
 }
 
-void launch_set_flags(hipStream_t s, int64_t n, const int32_t* idx, uint8_t* out) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_set_flags, MFEA_GRID(grid_rows(n)), n, idx, out);
+void launch_floating(hipStream_t s, int64_t n_rows, int64_t n_free, int64_t grip_end, const int32_t* slice_ptr,
+                     const int32_t* row_len, const int32_t* s_col, const int32_t* s_elem, const uint8_t* active,
+                     int32_t* parent, uint8_t* anchored, const int32_t* label, uint8_t* mask, int tile_rows) {
+  if (n_free <= 0) return;
+  tile_rows = tile_rows == 512 || tile_rows == 1024 || tile_rows == 4096 ? tile_rows : 2048;
+  const int64_t tiles = (n_rows + tile_rows - 1) / tile_rows;
+  auto local = tile_rows == 512 ? k_cc_local<512> : tile_rows == 1024 ? k_cc_local<1024>
+               : tile_rows == 4096 ? k_cc_local<4096> : k_cc_local<2048>;
+  hipLaunchKernelGGL(local, MFEA_GRID(tiles), n_rows, slice_ptr, row_len, s_col, s_elem, active, parent, anchored);
+  hipLaunchKernelGGL(k_cc_cross, MFEA_GRID(grid_rows(n_rows)), n_rows, slice_ptr, row_len, s_col, s_elem, active,
+                     parent, tile_rows);
+  hipLaunchKernelGGL(k_cc_flatten, MFEA_GRID(grid_rows(n_rows)), n_rows, parent, n_free, grip_end, anchored);
+  hipLaunchKernelGGL(k_cc_mask, MFEA_GRID(grid_rows(n_free)), n_free, parent, anchored, label, mask);
 }
 
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,

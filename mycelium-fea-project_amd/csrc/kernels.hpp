@@ -136,8 +136,15 @@ void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* x
 void launch_element_stiffness(hipStream_t s, int64_t n, const double* p1, const double* p2,
                               Material m, double* Ke, double* L);
 
-// out[idx[i]] = 1, i < n
-void launch_set_flags(hipStream_t s, int64_t n, const int32_t* idx, uint8_t* out);
+// floating free rows of the active element graph given as the SELL-64
+// operator pattern (rows [0, n_free) free, [n_free, grip_end) grips; slot
+// (row, k): neighbour s_col, element s_elem): mask[label[i]] = 1 for a free
+// row i whose component holds no grip row (label NULL: i).  parent /
+// anchored: n_rows scratch each.  Four launches, no host wait.
+void launch_floating(hipStream_t s, int64_t n_rows, int64_t n_free, int64_t grip_end, const int32_t* slice_ptr,
+                     const int32_t* row_len, const int32_t* s_col, const int32_t* s_elem, const uint8_t* active,
+                     int32_t* parent, uint8_t* anchored, const int32_t* label, uint8_t* mask,
+                     int tile_rows = 2048);
 
 // generic scalar-CSR operator (mfea_solve_csr)
 void launch_csr_rhs_init(hipStream_t s, int64_t n, const int64_t* indptr, const int32_t* indices,

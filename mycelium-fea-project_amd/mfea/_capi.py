@@ -19,8 +19,8 @@ DEFAULT_OPTIONS = {"graph": 1, "phase_times": 0, "dist_graph": 1, "order": -1, "
                    "amg_tail_lds": 1, "dist_timeout_ms": 60000, "part_slack_pct": 35, "amg_dist": -1,
                    "amg_rep_rows": 32768, "amg_cycle": 1, "amg_fuse_setup": 1,
                    "amg_up_lanes": 0, "amg_spatial": -1, "amg_collapse": -1, "amg_collapse_mb": 32,
-                   "amg_collapse_pairs": 8000000, "amg_theta_ppm": 0, "amg_reuse": 1, "amg_rebuild_pct": 150,
-                   "amg_coarse_rho_ppm": 1750000, "sweep_piece": 64}
+                   "amg_collapse_pairs": 8000000, "amg_theta_ppm": 0, "amg_reuse": 1, "amg_rebuild_pct": 800, "amg_rebuild_rent": 100,
+                   "amg_coarse_rho_ppm": 1750000, "sweep_piece": 64, "cc_tile": 1024}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))
@@ -125,6 +125,7 @@ _sig = {
     "mfea_debug_trace_iteration": (C.c_int, [_P, C.c_int, _P, C.c_int64, C.POINTER(C.c_int64)]),
     "mfea_debug_set_parts": (C.c_int, [_P, C.c_int, C.c_int]),
     "mfea_debug_global_active": (C.c_int, [_P, C.c_void_p]),
+    "mfea_debug_floating": (C.c_int, [_P, C.c_void_p]),
     "mfea_set_option": (C.c_int, [_P, C.c_char_p, C.c_int64]),
     "mfea_get_option": (C.c_int, [_P, C.c_char_p, C.POINTER(C.c_int64)]),
     "mfea_debug_amg_vcycle": (C.c_int, [_P, _P, _P]),
@@ -321,6 +322,13 @@ class Engine:
         (mfea_debug_global_active)."""
         out = np.zeros(self.n_elems, np.uint8)
         _check(_lib.mfea_debug_global_active(self._h, out.ctypes.data_as(C.c_void_p)))
+        return out.astype(bool)
+
+    def floating(self) -> np.ndarray:
+        """Free nodes cut off from both grips by the current activity, from the
+        device's connected components (mfea_debug_floating)."""
+        out = np.zeros(self.n_nodes, np.uint8)
+        _check(_lib.mfea_debug_floating(self._h, out.ctypes.data_as(C.c_void_p)))
         return out.astype(bool)
 
     def set_parts(self, nparts: int, axis: int = -1):

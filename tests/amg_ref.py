@@ -112,13 +112,17 @@ def _binv(D):
     return out
 
 
-def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho=RHO_COARSE):
+def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho=RHO_COARSE, dmask=None):
     """The per-solve numeric setup of amg.hip on the plan: fills A (blocks),
     dinv, omega, P, AP for every level.  val/diag: the assembled SELL values.
     fmask: per level-0 row, 1 = a floating row whose P_0 row is formed as zero
     (a hierarchy kept over element failures, amg.hip pvals_body).
     coarse_rho: ρ̂ of the levels below 0 (0: the Gershgorin rule, as level 0
-    and the engine after a failed solve)."""
+    and the engine after a failed solve).
+    dmask: per level-0 row, 1 = a row dropped from the tentative prolongator
+    (P_tent(i, ·) = 0: no identity block, and its A_ki terms left out of its
+    neighbours' P sums) — floating rows and the split-off pieces of kept
+    aggregates (amg.hip pvals_body)."""
     L0 = levels[0]
     n0 = L0["n"]
     row, k = pos_rows(L0["A.sptr"], n0)
@@ -157,11 +161,16 @@ def numeric_setup(levels, val, diag, G, N, nd, reg=1e-12, fmask=None, coarse_rho
         if L["coarsest"]:
             break
         prow, _ = pos_rows(L["P.sptr"], n)
-        S = seg_sum(Ab[L["pv.a"]], L["pv.ptr"])
+        items = Ab[L["pv.a"]]
+        if l == 0 and dmask is not None:
+            items = items * (dmask[L["A.col"][L["pv.a"]]] == 0)[:, None, None]
+        S = seg_sum(items, L["pv.ptr"])
         okp = (L["P.col"] >= 0) & (prow >= 0)
         Pb = np.zeros_like(S)
         Pb[okp] = -L["omega"] * np.einsum("pab,pbc->pac", Dinv[prow[okp]], S[okp])
         ident = okp & (L["P.col"] == np.where(prow >= 0, L["agg"][np.maximum(prow, 0)], -9))
+        if l == 0 and dmask is not None:
+            ident &= dmask[np.maximum(prow, 0)] == 0
         Pb[ident] += np.eye(nd)
         if l == 0 and fmask is not None:
             Pb[okp & (fmask[np.maximum(prow, 0)] != 0)] = 0.0

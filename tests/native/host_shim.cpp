@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <numeric>
 #include <vector>
 
 #include "amg.hpp"
@@ -13,6 +14,33 @@
 #include "symbolic.hpp"
 
 using namespace mfea;
+
+// Free rows of P with no path of active elements to a grip (known, non-ghost)
+// row: their load is zero, so the direct solve leaves them exactly at zero
+// (src/fea_solver.py:128).  Union-find over the active elements.
+static void floating_free_rows(const Pattern& P, const std::vector<uint8_t>& active, std::vector<uint8_t>& out) {
+  const int64_t N = P.n_nodes;
+  std::vector<int32_t> up(N);
+  std::iota(up.begin(), up.end(), 0);
+  auto find = [&](int32_t a) {
+    while (up[a] != a) a = up[a] = up[up[a]];
+    return a;
+  };
+  const int64_t E = P.n_elems;
+  for (int64_t e = 0; e < E; ++e) {
+    if (!active[e]) continue;
+    const int32_t a = P.e2n_perm[2 * e], b = P.e2n_perm[2 * e + 1];
+    if (a < 0 || b < 0) continue;
+    const int32_t ra = find(a), rb = find(b);
+    if (ra != rb) up[std::max(ra, rb)] = std::min(ra, rb);
+  }
+  std::vector<uint8_t> anchored(N, 0);
+  for (int64_t i = P.n_free; i < N - P.n_ghost; ++i) anchored[find((int32_t)i)] = 1;
+  out.assign(P.n_free, 0);
+  for (int64_t i = 0; i < P.n_free; ++i) out[i] = anchored[find((int32_t)i)] ? 0 : 1;
+}
+
+
 
 static Pattern g_P;
 
@@ -144,34 +172,16 @@ void shim_amg_strength(double theta, double kb_kax) {
   g_strength.theta = theta;
   g_strength.kb_kax = kb_kax;
 }
-// floating_free_rows (amg.hpp) of the last built pattern: out[n_free] in
-// pattern row order; returns the number of floating rows
+// Free rows of the last built pattern with no path of active elements to a
+// grip row (union-find; the host restatement of kernels.hip's device
+// components, launch_floating): out[n_free] in pattern row order; returns
+// the number of floating rows
 int64_t shim_floating(const uint8_t* active, uint8_t* out) {
   std::vector<uint8_t> a(active, active + g_P.n_elems), f;
   floating_free_rows(g_P, a, f);
   int64_t n = 0;
   for (size_t i = 0; i < f.size(); ++i) n += (out[i] = f[i]);
   return n;
-}
-// FloatTracker (amg.hpp) over the last built pattern: the whole-graph pass
-// for `active`, then the elements fail_ids[0..nf) fail one after another
-// (active updated in place, as capi.hip post_impl does).  floating[n_free]:
-// the tracker's set afterwards; returns how many rows became floating
-// through the failures (each listed once in new_rows, capacity n_free)
-int64_t shim_float_track(uint8_t* active, int64_t nf, const int32_t* fail_ids, uint8_t* floating,
-                         int32_t* new_rows) {
-  FloatTracker t;
-  const int32_t* e2n = g_P.e2n_perm.data();
-  t.set_graph(g_P.n_nodes, g_P.n_free, g_P.n_nodes - g_P.n_ghost, g_P.n_elems, e2n);
-  t.init(e2n, g_P.n_elems, active);
-  std::vector<int32_t> out;
-  for (int64_t i = 0; i < nf; ++i) {
-    active[fail_ids[i]] = 0;
-    t.fail(e2n, active, fail_ids[i], out);
-  }
-  for (int64_t i = 0; i < g_P.n_free; ++i) floating[i] = t.floating[i];
-  for (size_t i = 0; i < out.size(); ++i) new_rows[i] = out[i];
-  return (int64_t)out.size();
 }
 int shim_amg(const uint8_t* active, int nd, char* err, int errn) {
   std::vector<uint8_t> a(active, active + g_P.n_elems);

@@ -116,7 +116,7 @@ def test_gamg_kept_hierarchy_floating_pieces_exactly_zero(engine):
     the reverse change back to the intact set."""
     xyz, e2n, top, bot = _sim181147(engine)
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
-    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000, amg_rebuild_rent=0):
         engine.set_active(None)
         engine.assemble()
         st0 = engine.solve(dy, -dy, _opts(1e-13))
@@ -145,6 +145,43 @@ def test_gamg_kept_hierarchy_floating_pieces_exactly_zero(engine):
         assert rel(engine.displacement(), fo.solve_system(K, known, vals)) <= 1e-10
 
 
+@pytest.mark.parametrize("frac", [0.0, 0.01, 0.06, 0.3, 0.7, 1.0])
+def test_device_floating_rows_match_scipy_components(engine, frac):
+    """The floating mask's connected components on the device (kernels.hip
+    launch_floating: CAS root hooking, deterministic roots) against SciPy's
+    csgraph on the same activity: the free nodes with no active path to a
+    grip, exactly; run twice, bitwise the same."""
+    xyz, e2n, top, bot = _sim181147(engine)
+    grip = np.zeros(len(xyz), bool)
+    grip[np.concatenate([top, bot])] = True
+    rng = np.random.default_rng(int(frac * 1000) + 3)
+    active = rng.random(len(e2n)) >= frac
+    engine.set_active(active)
+    fl = engine.floating()
+    ref = _floating_nodes(xyz, e2n, active, top, bot) & ~grip
+    assert np.array_equal(fl, ref), (int(fl.sum()), int(ref.sum()))
+    assert np.array_equal(engine.floating(), fl)
+    engine.set_active(None)
+
+
+def test_device_floating_rows_tiled_network(engine):
+    """The same on the 1×5-tile C2 network (110 k DOF) with 20 % of the
+    elements out: many components, hooks racing across the whole grid."""
+    from mfea import synth
+    xyz, e2n = synth.tiled_mesh(1, 5)
+    top, bot = synth.grips(xyz)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc(top, bot)
+    grip = np.zeros(len(xyz), bool)
+    grip[np.concatenate([top, bot])] = True
+    active = np.random.default_rng(5).random(len(e2n)) >= 0.2
+    engine.set_active(active)
+    ref = _floating_nodes(xyz, e2n, active, top, bot) & ~grip
+    assert ref.sum() > 100
+    assert np.array_equal(engine.floating(), ref)
+    engine.set_active(None)
+
+
 def test_gamg_failures_through_post_keep_floating_exactly_zero(engine):
     """The reference loop with failures driven by the post kernel alone (no
     set_active between steps, src/fea_solver.py:216-295), pulled to 3× the
@@ -156,7 +193,7 @@ def test_gamg_failures_through_post_keep_floating_exactly_zero(engine):
     grip = np.zeros(len(xyz), bool)
     grip[np.concatenate([top, bot])] = True
     seen_float = 0
-    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000, amg_rebuild_rent=0):
         engine.set_active(None)
         active = np.ones(len(e2n), bool)
         for step in range(fo.N_STEPS):
@@ -191,7 +228,7 @@ def test_gamg_hierarchy_not_kept_for_a_superset(engine):
     known, vals = fo.known_dof_map(top, bot, dy, -dy)
     rng = np.random.default_rng(11)
     active = rng.random(len(e2n)) > 0.03
-    with engine.options(amg_reuse=1, amg_rebuild_pct=100000):
+    with engine.options(amg_reuse=1, amg_rebuild_pct=100000, amg_rebuild_rent=0):
         engine.set_active(active)
         engine.assemble()
         assert engine.solve(dy, -dy, _opts(1e-13)).status == 0

@@ -53,6 +53,12 @@ def _mesh(engine, name):
 
 @pytest.mark.parametrize("mesh", ["sim181147", "C2_1x5", "C5_2x2", "sim135507_3d"])
 def test_sweeps_match_direct(engine, mesh):
+    """The 1e-10 bar at rtol 1e-13 on PETSc's preconditioned norm (its KSPCG
+    default for these PCs) and at 1e-14 on the unpreconditioned residual —
+    one decade past SURVEY §8(d)'s parity rtol of 1e-13, which GAMG and
+    Jacobi meet: at an unpreconditioned 1e-13 the one-level sweeps leave their
+    residual in the smooth modes, and SOR lands at 2.2e-10 on C2
+    (profiles/r5/attain_C2.log).  The exception is stated in DESIGN.md §2."""
     from mfea import NORM_PRECONDITIONED, NORM_UNPRECONDITIONED, PC_ICC, PC_JACOBI, PC_SOR
     xyz, e2n, top, bot = _mesh(engine, mesh)
     dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)

@@ -435,7 +435,8 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& T = L.PT;
   int64_t q, i;
   int k;
-  if (!slot_wave(T, 0, T.npos / 64, q, i, k, blk) || i >= T.n || T.col[q] < 0) return;
+  if (!slot_wave(T, T.rg.p0 / 64, T.rg.p1 / 64, q, i, k, blk) || i >= T.n || T.col[q] < 0 || !pos_mine(T.rg, q))
+    return;
   const int32_t qp = L.pt_p[q];
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
   dinv_load<ND>(L.dinv32, L.pt_row[i], Di);
@@ -467,7 +468,7 @@ __device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int
   const AmgMatD& T = L.RT;
   int64_t q, J;
   int k;
-  if (!slot_wave(T, 0, T.npos / 64, q, J, k, blk) || J >= T.n) return;
+  if (!slot_wave(T, T.rg.p0 / 64, T.rg.p1 / 64, q, J, k, blk) || J >= T.n || !pos_mine(T.rg, q)) return;
   const int32_t i = T.col[q];
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
@@ -498,7 +499,8 @@ __device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& A = L.A;
   int64_t q, i;
   int k;
-  if (!slot_wave(A, 0, A.npos / 64, q, i, k, blk) || i >= A.n || A.col[q] < 0) return;
+  if (!slot_wave(A, A.rg.p0 / 64, A.rg.p1 / 64, q, i, k, blk) || i >= A.n || A.col[q] < 0 || !pos_mine(A.rg, q))
+    return;
   double Di[ND * ND], m[ND * ND], o[ND * ND];
   dinv_load<ND>(L.dinv32, i, Di);
   bload<ND>(A.val32, 0, q, m);
@@ -1002,11 +1004,13 @@ template <int ND, int S, int KF = 2>
 __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64_t gc, const int32_t* gate) {
   const bool run = gate_open(gate);
   const int64_t xb = xcd_block();
+  // (rows [rg.lo, rg.hi) of each row set: a distributed level's own rows,
+  // swept from the slice boundary below lo; one partition: all of them)
   if (xb < gc) {
     const AmgMatD& R = L.RT;
     const int64_t t = xb * kBlock + threadIdx.x;
-    const int64_t n = R.n;
-    const int64_t I = t / S;
+    const int64_t n = R.rg.hi;
+    const int64_t I = R.rg.lo64() + t / S;
     const int sub = (int)(t % S);
     if (I - (threadIdx.x & 63) / S >= n) return;
     const int64_t Ic = I < n ? I : n - 1;
@@ -1018,10 +1022,10 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
     for (int a = 0; a < ND; ++a) xc[a] = 0.0f;
     if constexpr (S == 1) sell_mac<ND, false, 3>(R.col, R.val32, R.npos, base, w, L.x, xc);
     else sell_mac_sub<ND, S, false>(R.col, R.val32, base, w, sub, L.x, xc);
-    if (I < n && sub == 0 && run) vstore<ND>(N.x, L.rt_row[I], xc);
+    if (I < n && I >= R.rg.lo && sub == 0 && run) vstore<ND>(N.x, L.rt_row[I], xc);
   } else {
-    const int64_t i = (xb - gc) * kBlock + threadIdx.x;
-    const int64_t n = L.A.n;
+    const int64_t i = L.A.rg.lo64() + (xb - gc) * kBlock + threadIdx.x;
+    const int64_t n = L.A.rg.hi;
     if (i - (threadIdx.x & 63) >= n) return;
     const int64_t ii = i < n ? i : n - 1;
     int64_t base;
@@ -1032,7 +1036,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_down(AmgLevD L, AmgLevD N, int64
 #pragma unroll
     for (int a = 0; a < ND; ++a) y[a] = x[a] + x[a];
     sell_mac<ND, true, KF>(L.A.col, L.A.at32, L.A.npos, base, w, L.x, y);
-    if (i < n && run) vstore<ND>(L.t, i, y);
+    if (i < n && i >= L.A.rg.lo && run) vstore<ND>(L.t, i, y);
   }
 }
 
@@ -1044,8 +1048,8 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
   const bool run = gate_open(gate);
   const AmgMatD& T = L.PT;
   const int64_t t = xcd_block() * kBlock + threadIdx.x;
-  const int64_t n = T.n;
-  const int64_t a = t / S;
+  const int64_t n = T.rg.hi;  // rows [rg.lo, rg.hi): a distributed level's own P̃ rows
+  const int64_t a = T.rg.lo64() + t / S;
   const int sub = (int)(t % S);
   if (a - (threadIdx.x & 63) / S >= n) return;
   const int64_t aa = a < n ? a : n - 1;
@@ -1062,7 +1066,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_up(AmgLevD L, AmgLevD N, TE* __r
   const float* src = N.coarsest ? N.x : N.e;
   if constexpr (S == 1) sell_mac<ND, false, 3>(T.col, T.val32, T.npos, base, w, src, y);
   else sell_mac_sub<ND, S, false>(T.col, T.val32, base, w, sub, src, y);
-  if (a < n && sub == 0 && run) vstore<ND>(e, i, y);
+  if (a < n && a >= T.rg.lo && sub == 0 && run) vstore<ND>(e, i, y);
 }
 
 // The collapsed cycle below level kc: e_kc = V x_kc in one sweep (V's rows
@@ -1555,12 +1559,19 @@ void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLe
 }
 
 template <int ND>
-static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l) {
+static void compact_level_nd(hipStream_t s, const AmgLevD* lev, int l, int parts = kCompactAll) {
   const AmgLevD& L = lev[l];
   if (!L.compact || L.PT.wmax <= 0) return;
-  hipLaunchKernelGGL(k_amg_ptv<ND>, xg(L, slot_grid(L.PT.npos)), dim3(kBlock), 0, s, L);
-  hipLaunchKernelGGL(k_amg_rtv<ND>, xg(L, slot_grid(L.RT.npos)), dim3(kBlock), 0, s, L, lev[l + 1]);
-  hipLaunchKernelGGL(k_amg_atv<ND>, xg(L, slot_grid(L.A.npos)), dim3(kBlock), 0, s, L);
+  if (parts & kCompactPT)
+    hipLaunchKernelGGL(k_amg_ptv<ND>, xg(L, slot_grid(L.PT.rg.npos())), dim3(kBlock), 0, s, L);
+  if (parts & kCompactRT)
+    hipLaunchKernelGGL(k_amg_rtv<ND>, xg(L, slot_grid(L.RT.rg.npos())), dim3(kBlock), 0, s, L, lev[l + 1]);
+  if (parts & kCompactAT)
+    hipLaunchKernelGGL(k_amg_atv<ND>, xg(L, slot_grid(L.A.rg.npos())), dim3(kBlock), 0, s, L);
+}
+void launch_amg_compact_level(hipStream_t s, int nd, const AmgLevD* lev, int l, int parts) {
+  if (nd == 2) compact_level_nd<2>(s, lev, l, parts);
+  else compact_level_nd<3>(s, lev, l, parts);
 }
 // mg (merged levels 0–1, AmgMergeD): their products ride in the last of
 // these launches (MprodSlice) — the caller then skips launch_amg_merge_setup.
@@ -1644,13 +1655,13 @@ bool launch_amg_setup_fused(hipStream_t s, int nd, const AmgLevD* lev, int nlev,
   return setup_fused_nd<3>(s, lev, nlev, coll, mg);
 }
 template <int ND>
-static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll) {
-  for (int l = 0; l + 1 < nlev; ++l) compact_level_nd<ND>(s, lev, l);
+static void compact_setup_nd(hipStream_t s, const AmgLevD* lev, int nlev, int coll, int l0) {
+  for (int l = l0; l + 1 < nlev; ++l) compact_level_nd<ND>(s, lev, l);
   collapse_setup_nd<ND>(s, lev, nlev, coll);
 }
-void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll) {
-  if (nd == 2) compact_setup_nd<2>(s, lev, nlev, coll);
-  else compact_setup_nd<3>(s, lev, nlev, coll);
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll, int l0) {
+  if (nd == 2) compact_setup_nd<2>(s, lev, nlev, coll, l0);
+  else compact_setup_nd<3>(s, lev, nlev, coll, l0);
 }
 
 // lanes per row: the restriction by R's mean slice width, the f32 operators
@@ -1735,7 +1746,7 @@ int amg_up_lanes(const AmgLevD& L) { return lanes_for(L.PT, L.ulanes, 8.0, 16.0)
 template <int ND>
 static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int32_t* gate) {
   const int S = amg_down_lanes(L);
-  const int64_t gr = rows_grid(S * L.RT.n).x, ga = rows_grid(L.A.n).x;
+  const int64_t gr = rows_grid(S * L.RT.rg.span()).x, ga = rows_grid(L.A.rg.span()).x;
   auto go = [&](int64_t gc, int64_t blocks) {
     const dim3 g((unsigned)blocks);
     if (S == 16) hipLaunchKernelGGL((k_amg_down<ND, 16>), g, dim3(kBlock), 0, s, L, N, gc, gate);
@@ -1754,7 +1765,7 @@ static void down_nd(hipStream_t s, const AmgLevD& L, const AmgLevD& N, const int
 template <int ND, class TE>
 static void up_te(hipStream_t s, const AmgLevD& L, const AmgLevD& N, TE* e, const int32_t* gate) {
   const int S = amg_up_lanes(L);
-  const dim3 g(rows_grid(S * L.PT.n));
+  const dim3 g(rows_grid(S * L.PT.rg.span()));
   if (S == 4) hipLaunchKernelGGL((k_amg_up<ND, 4, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else if (S == 2) hipLaunchKernelGGL((k_amg_up<ND, 2, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
   else hipLaunchKernelGGL((k_amg_up<ND, 1, TE>), g, dim3(kBlock), 0, s, L, N, e, gate);
@@ -1859,6 +1870,14 @@ static int clamp_tail(int tail, int nlev) {
   if (tail >= nlev - 1) return 0;  // nothing below the coarsest to fuse
   if (tail > 0 && nlev - tail > kTailMaxLev) return nlev - kTailMaxLev;  // the kernel argument holds 4 levels
   return tail;
+}
+void launch_amg_down(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD& N) {
+  if (nd == 2) down_nd<2>(s, L, N, nullptr);
+  else down_nd<3>(s, L, N, nullptr);
+}
+void launch_amg_up(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD& N, float* e) {
+  if (nd == 2) up_te<2, float>(s, L, N, e, nullptr);
+  else up_te<3, float>(s, L, N, e, nullptr);
 }
 void launch_amg_vcycle(hipStream_t s, int nd, const AmgLevD* lev, int nlev, const AmgCg& cg,
                        int tail, const int32_t* gate, int l0, const AmgMergeD* mg) {

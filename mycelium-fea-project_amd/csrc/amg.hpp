@@ -109,6 +109,7 @@ struct AmgLevel {
   SellPat RT;                  // nc × n, rows by RT length inside windows (rt_row)
   std::vector<int32_t> rt_row; // RT row → the level-(l+1) row
   std::vector<int32_t> rt_pt;  // RT position → PT position (value = PT[rt_pt]ᵀ)
+  std::vector<int64_t> rt_own; // distributed (level l+1 ≤ n_dist): RT rows owner-major, per-rank bounds
 };
 
 struct AmgPlan {
@@ -224,6 +225,14 @@ struct AmgRank {
   // rows read, A·P positions of the rows its A_{l+1} rows read
   std::vector<XPlan> sp, sap;
   XPlan sg;  // A positions of level n_dist: all-gather
+  // the compact cycle on a plan split at level 0 only (n_dist = 1, levels ≥ 1
+  // replicated): this rank's R̂_0 rows [rtlo, rthi); level-0
+  // rows its Ã_0 and R̂_0 rows read (the down sweep's x_0 halo); for the
+  // setup of R̂_0 = s' D_1⁻¹ P̃_0ᵀ D_0 / ω, the P̃_0 positions and the
+  // level-0 diagonal-block positions (A_0 slot 0) its R̂_0 rows read
+  bool compact = false;
+  int64_t rtlo = 0, rthi = 0;
+  XPlan xc, spt, sd;
 };
 // rank r's share of a distributed plan (plan.n_dist ≥ 1)
 std::string build_amg_rank(const AmgPlan& plan, int rank, AmgRank& out);

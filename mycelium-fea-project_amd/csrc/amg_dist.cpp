@@ -161,6 +161,48 @@ std::string build_amg_rank(const AmgPlan& plan, int rank, AmgRank& out) {
     }
     out.sg = make_plan(sg, rank);
   }
+  // the compact cycle: only level 0 split, its R̂_0 rows owner-major
+  const AmgLevel& L0 = plan.lev[0];
+  if (nd == 1 && nlev >= 2 && !L0.coarsest && L0.PT.n == L0.A.n && L0.RT.n == plan.lev[1].A.n &&
+      (int64_t)L0.rt_own.size() == world + 1 && (int64_t)L0.ap_own.size() == world + 1) {
+    out.compact = true;
+    out.rtlo = L0.rt_own[rank];
+    out.rthi = L0.rt_own[rank + 1];
+    std::vector<int32_t> rt_owner(L0.RT.n, 0), pt_owner(L0.PT.n, 0);
+    for (int q = 0; q < world; ++q) {
+      for (int64_t I = L0.rt_own[q]; I < L0.rt_own[q + 1]; ++I) rt_owner[I] = q;
+      for (int64_t a = L0.ap_own[q]; a < L0.ap_own[q + 1]; ++a) pt_owner[a] = q;
+    }
+    // x_0 halo of the down sweep: the columns of its Ã_0 (A_0's pattern) and R̂_0 rows
+    Need nx(world);
+    need_rows(L0.A, L0.owner, L0.owner, nx);
+    need_rows(L0.RT, rt_owner, L0.owner, nx);
+    out.xc = make_plan(nx, rank);
+    // P̃_0 positions and level-0 diagonal blocks read by each rank's R̂_0 rows
+    std::vector<int32_t> pt_srow(L0.PT.sptr.empty() ? 0 : L0.PT.sptr.back(), 0);
+    for (size_t sl = 0; sl + 1 < L0.PT.sptr.size(); ++sl)
+      for (int32_t t = L0.PT.sptr[sl]; t < L0.PT.sptr[sl + 1]; ++t) pt_srow[t] = (int32_t)sl;
+    Need npt(world), ndg(world);
+    for (int64_t I = 0; I < L0.RT.n; ++I) {
+      const int32_t q = rt_owner[I];
+      for (int k = 0; k < L0.RT.rlen[I]; ++k) {
+        const int64_t qq = L0.RT.pos(I, k);
+        const int32_t i = L0.RT.col[qq];
+        if (i < 0) continue;
+        const int32_t pp = L0.rt_pt[qq];
+        const int64_t a = 64 * (int64_t)pt_srow[pp >> 6] + (pp & 63);
+        if (pt_owner[a] != q) npt.by_rank[q].emplace_back(pp, pt_owner[a]);
+        if (L0.owner[i] != q) ndg.by_rank[q].emplace_back((int32_t)L0.A.pos(i, 0), L0.owner[i]);
+      }
+    }
+    for (auto* n : {&npt, &ndg})
+      for (auto& v : n->by_rank) {
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+      }
+    out.spt = make_plan(npt, rank);
+    out.sd = make_plan(ndg, rank);
+  }
   return "";
 }
 

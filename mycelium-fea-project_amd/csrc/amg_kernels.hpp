@@ -227,10 +227,18 @@ void launch_amg_a0(hipStream_t s, int nd, const AmgLevD& L0, const SellOp& sop, 
 constexpr int kSetupDinv = 1, kSetupP = 2, kSetupAP = 4, kSetupAC = 8, kSetupAll = 15;  // (kSetupAP: + P̃, R̃)
 void launch_amg_level_setup(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD* next, bool level0,
                             int stage = kSetupAll);
-// the compact cycle's operators of every level (after every level's setup:
-// R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã; then, deepest first, the
-// collapsed operators T, V of levels ≥ kc (coll > 0)
-void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0);
+// the compact cycle's operators of every level from l0 (after every level's
+// setup: R̂ needs the next level's D⁻¹ and ω): P̃, R̂, Ã; then, deepest first,
+// the collapsed operators T, V of levels ≥ kc (coll > 0)
+void launch_amg_compact_setup(hipStream_t s, int nd, const AmgLevD* lev, int nlev, int coll = 0, int l0 = 0);
+// ... of one level, on its row ranges (the distributed setup exchanges P̃ and
+// diagonal blocks between forming P̃ and R̂)
+constexpr int kCompactPT = 1, kCompactRT = 2, kCompactAT = 4, kCompactAll = 7;
+void launch_amg_compact_level(hipStream_t s, int nd, const AmgLevD* lev, int l, int parts);
+// one compact sweep of level L on its row ranges: down (x_{l+1} = R̂ x_l into
+// N.x, c_l = 2x_l − Ã x_l into L.t) and up (e = c_l + P̃ e_{l+1})
+void launch_amg_down(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD& N);
+void launch_amg_up(hipStream_t s, int nd, const AmgLevD& L, const AmgLevD& N, float* e);
 // the levels' setup (after launch_amg_a0) and the compact operators in one
 // sequence, the compact parts fused into the Galerkin chain's launches
 // (mg: the merged levels' products ride in the collapse launches; returns

@@ -742,7 +742,11 @@ std::string build_amg(const Pattern& P, const std::vector<uint8_t>& active, int 
       {
         std::vector<int64_t> key(L.nc);
         for (int64_t J = 0; J < L.nc; ++J) key[J] = RT.ptr[J + 1] - RT.ptr[J];
-        prt = sort_perm(key, nullptr, world, nullptr, spatial ? &bases[l + 1] : nullptr);
+        // distributed: owner-major by the coarse row's owner, so a rank's R̂
+        // rows are one range (the compact cycle on a split level)
+        const bool om1 = dist && l + 1 <= n_dist && l + 1 < (int)own.size();
+        prt = sort_perm(key, om1 ? &own[l + 1] : nullptr, world, om1 ? &out.rt_own : nullptr,
+                        spatial ? &bases[l + 1] : nullptr);
       }
       if (!(err = layout(RT, prt, &perm[l], out.RT, eRT)).empty()) return err;
       out.rt_row.assign(L.nc, 0);

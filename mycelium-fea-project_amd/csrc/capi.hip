@@ -202,6 +202,7 @@ struct Part {
   };
   std::vector<XDev> xd_a, xd_r, xd_p, xd_sp, xd_sap;
   XDev xd_g, xd_sg;
+  XDev xd_c, xd_spt, xd_sd;  // the compact cycle split at level 0 (AmgRank::compact)
   DevBuf<int32_t> amg_xi;
   DevBuf<double> amg_xs, amg_xr;
 };
@@ -320,6 +321,11 @@ struct mfea_handle {
   int opt_amg_dist = -1;          // partitioned GAMG: 1 the global hierarchy (distributed V-cycle), 0 block
                                   // Jacobi over per-partition hierarchies, -1 whichever solves faster (measured)
   int64_t opt_amg_rep_rows = 32768;  // distributed V-cycle: levels of at most this many rows are replicated
+  // distributed V-cycle: 1 the compact cycle with level 0 split and every
+  // level below replicated (x_0 halo, x_1 all-gather, u halo: three exchange
+  // points per iteration), 0 the four-step cycle over the levels of more than
+  // amg_rep_rows rows (four exchange points per split level)
+  int opt_amg_dist_cycle = 1;
   // distributed GAMG (partitioned handles, option "amg_dist" 1): the whole
   // mesh's pattern and node owners (built with the partitions), and ONE
   // global hierarchy for the current global element activity
@@ -1291,10 +1297,11 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
   hipStream_t s = h->stream;
   size_t ni = 0, ndd = 0, nff = 0;
   pt.amg_coll = AmgCollapse();
-  if (!rk && h->opt_amg_cycle == 1 && h->opt_amg_collapse != 0) {
+  // (a distributed plan: collapsed among its replicated levels only)
+  if ((!rk || rk->compact) && h->opt_amg_cycle == 1 && h->opt_amg_collapse != 0) {
+    const int min_level = h->opt_amg_collapse < 0 ? kAmgCollapseAutoLevel : std::max(1, h->opt_amg_collapse);
     const std::string cerr = build_amg_collapse(pl, h->opt_amg_collapse_mb << 20, h->opt_amg_collapse_pairs,
-                                                h->opt_amg_collapse < 0 ? kAmgCollapseAutoLevel : std::max(1, h->opt_amg_collapse),
-                                                pt.amg_coll);
+                                                rk ? std::max(min_level, rk->n_dist) : min_level, pt.amg_coll);
     if (!cerr.empty()) return fail(MFEA_EINVAL, cerr);
   }
   // levels 0 and 1 merged (amg.hpp AmgMerge): where the launches are latency-
@@ -1430,17 +1437,21 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
           const double mean = L.ac.ptr.empty() ? 0.0 : (double)L.ac.ptr.back() / (double)np;
           d.ac_lanes = mean > 24.0 ? 8 : mean > 12.0 ? 4 : mean > 6.0 ? 2 : 1;
         }
-        // the compact cycle's P̃ / R̃ (one partition's hierarchy only: the
-        // distributed V-cycle exchanges per four-step step)
-        if (!rk && L.PT.n == n) {
+        // the compact cycle's P̃ / R̃: one partition's hierarchy, or a
+        // distributed one split at level 0 only (rk->compact: level 0 on this
+        // rank's P̃ / R̂ / Ã rows, the replicated levels whole; the four-step
+        // distributed cycle exchanges per step instead)
+        const bool cmp = !rk || (rk->compact && (l == 0 || l >= rk->n_dist));
+        if (cmp && L.PT.n == n) {
+          const bool own = rk && l < rk->n_dist;
           d.PT = mat(L.PT, false, true);
           d.A.at32 = F((size_t)nb2 * d.A.npos);
-          d.PT.rg = row_range(L.PT, 0, n);
+          d.PT.rg = own ? row_range(L.PT, rk->aplo[l], rk->aphi[l]) : row_range(L.PT, 0, n);
           d.pt_row = I(L.pt_row);
           d.pt_ap = I(L.pt_ap);
           d.pt_p = I(L.pt_p);
           d.RT = mat(L.RT, false, true);
-          d.RT.rg = row_range(L.RT, 0, L.RT.n);
+          d.RT.rg = own ? row_range(L.RT, rk->rtlo, rk->rthi) : row_range(L.RT, 0, L.RT.n);
           d.rt_pt = I(L.rt_pt);
           d.rt_row = I(L.rt_row);
           d.compact = h->opt_amg_cycle;
@@ -1488,7 +1499,9 @@ int upload_amg(mfea_handle* h, Part& pt, const AmgPlan& pl, const AmgRank* rk = 
       g.n1 = M.n1;
       g.n2 = M.n2;
       g.DQ = mat(M.DQ, false, true);
+      g.DQ.rg = row_range(M.DQ, 0, M.DQ.n);
       g.U = mat(M.U, false, true);
+      g.U.rg = row_range(M.U, 0, M.U.n);
       g.dq_dst = I(M.dq_dst);
       g.dq_split = M.dq_split;
       g.dq_ext = I(M.dq_ext);
@@ -2164,6 +2177,9 @@ int upload_xplans(mfea_handle* h, Part& pt) {
   for (const auto& x : rk.sp) size(x, 8 * nd * nd);
   for (const auto& x : rk.sap) size(x, 8 * nd * nd);
   size(rk.sg, 8 * nd * nd);
+  size(rk.xc, 4 * nd);
+  size(rk.spt, 4 * nd * nd);
+  size(rk.sd, 4 * nd * nd);
   HIPC(pt.amg_xi.alloc(items));
   HIPC(pt.amg_xs.alloc(stage / 8 + 1));
   HIPC(pt.amg_xr.alloc(stage / 8 + 1));
@@ -2192,10 +2208,16 @@ int upload_xplans(mfea_handle* h, Part& pt) {
   for (const auto& x : rk.sp) pt.xd_sp.push_back(put(x));
   for (const auto& x : rk.sap) pt.xd_sap.push_back(put(x));
   pt.xd_sg = put(rk.sg);
+  pt.xd_c = put(rk.xc);
+  pt.xd_spt = put(rk.spt);
+  pt.xd_sd = put(rk.sd);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(s));
   return 0;
 }
+
+// the distributed V-cycle in its compact form (option amg_dist_cycle)
+bool dist_compact(const mfea_handle* h) { return h->opt_amg_dist_cycle == 1 && h->opt_amg_cycle == 1; }
 
 // (Re)build the global hierarchy (host) when the element activity may have
 // changed (act_gen) and actually did.
@@ -2214,7 +2236,8 @@ int ensure_gamg_plan(mfea_handle* h, bool* rebuilt) {
     h->gamg_ok = false;
     AmgDistSpec spec;
     spec.world = nranks(h);
-    spec.rep_rows = h->opt_amg_rep_rows;
+    const bool compact = dist_compact(h);
+    spec.rep_rows = compact ? INT64_MAX : h->opt_amg_rep_rows;
     spec.owner.resize(h->gpat.n_free);
     for (int64_t i = 0; i < h->gpat.n_free; ++i) spec.owner[i] = h->gowner[h->gpat.perm[i]];
     std::string err = build_amg(h->gpat, key, lane_dofs(h), h->gamg, h->opt_amg_max_levels, &spec,
@@ -2223,6 +2246,7 @@ int ensure_gamg_plan(mfea_handle* h, bool* rebuilt) {
     for (auto& pp : h->parts) {
       Part& pt = *pp;
       err = build_amg_rank(h->gamg, pt.rank, pt.amg_rank);
+      if (!compact) pt.amg_rank.compact = false;  // (a four-step plan split at level 0 only)
       if (err.empty())
         err = build_amg_level0(h->gamg, h->gpat, pt.amg_rank, pt.P, pt.plan.node_g, pt.plan.elem_g, key, pt.g_a0,
                                pt.g_row0);
@@ -2372,6 +2396,24 @@ int enqueue_gamg_setup(mfea_handle* h, double reg) {
             [ns](Part& p) -> void* { return p.amg_lev[ns].A.val32; }, nb2, 4));
     }
   }
+  if (part0(h).amg_rank.compact && nlev > 1) {
+    // the compact operators: level 0's Ã_0 and P̃_0 on this rank's rows; the
+    // P̃_0 blocks and level-0 diagonal blocks other ranks' R̂_0 rows read; its
+    // own R̂_0 rows; the replicated levels whole, then their collapse
+    for (auto& pp : h->parts)
+      launch_amg_compact_level(s, nd, pp->amg_lev.data(), 0, kCompactPT | kCompactAT);
+    HIPC(hipGetLastError());
+    RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_spt; },
+          [](Part& p) -> void* { return p.amg_lev[0].PT.val32; }, nb2, 4));
+    RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_sd; },
+          [](Part& p) -> void* { return p.amg_lev[0].A.val32; }, nb2, 4));
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_amg_compact_level(s, nd, pt.amg_lev.data(), 0, kCompactRT);
+      launch_amg_compact_setup(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg.coll, 1);
+    }
+    HIPC(hipGetLastError());
+  }
   return 0;
 }
 
@@ -2382,6 +2424,25 @@ int enqueue_gamg_vcycle(mfea_handle* h, int j) {
   const AmgPlan& pl = h->gamg;
   const int nd = pl.nd, nlev = (int)pl.lev.size(), ns = pl.n_dist;
   if (nlev <= 1) return 0;  // the update's vcycle_entry solved the only level
+  if (part0(h).amg_rank.compact) {
+    // split at level 0 only: x_0 halo → down_0 (this rank's R̂_0 rows into
+    // x_1, its Ã_0 rows into c_0) → x_1 all-gather → the replicated compact
+    // cycle from level 1 (collapsed as on one partition) → up_0 on this
+    // rank's P̃_0 rows into u.  Three exchange points with the u halo.
+    RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_c; }, [](Part& p) -> void* { return p.amg_lev[0].x; },
+          nd, 4));
+    for (auto& pp : h->parts) launch_amg_down(s, nd, pp->amg_lev[0], pp->amg_lev[1]);
+    HIPC(hipGetLastError());
+    RC(gx(h, [](Part& p) -> const Part::XDev& { return p.xd_g; }, [](Part& p) -> void* { return p.amg_lev[1].x; },
+          nd, 4));
+    for (auto& pp : h->parts) {
+      Part& pt = *pp;
+      launch_amg_vcycle(s, nd, pt.amg_lev.data(), nlev, pt.amg_cg, 0, nullptr, 1);
+      launch_amg_up(s, nd, pt.amg_lev[0], pt.amg_lev[1], pt.amg_cg.u);
+    }
+    HIPC(hipGetLastError());
+    return 0;
+  }
   const int top = std::min(ns, nlev - 1);  // split levels with a level below
   (void)j;  // no gate (enqueue_amg_chunk): past the stop every launch rewrites the same values
   auto gate = [](Part&) -> const int32_t* { return nullptr; };
@@ -3779,6 +3840,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_rep_rows = value;
     h->gamg_ok = false;
   }
+  else if (n == "amg_dist_cycle") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_dist_cycle: 0 (four-step) or 1 (compact)");
+    h->opt_amg_dist_cycle = (int)value;
+    h->gamg_ok = false;
+  }
   else if (n == "cc_tile") {
     if (value != 512 && value != 1024 && value != 2048 && value != 4096)
       return fail(MFEA_EINVAL, "cc_tile: 512, 1024, 2048 or 4096");
@@ -3984,6 +4050,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "cc_tile") *value = h->opt_cc_tile;
+  else if (n == "amg_dist_cycle") *value = h->opt_amg_dist_cycle;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);
   return 0;

@@ -360,6 +360,11 @@ int64_t shim_rank_array(const char* name, int l, int64_t* out) {
   else if (n == "aphi") v = &g_rank.aphi;
   else if (n == "rlo") v = &g_rank.rlo;
   else if (n == "rhi") v = &g_rank.rhi;
+  std::vector<int64_t> one;
+  if (n == "rtlo" || n == "rthi" || n == "compact") {
+    one.push_back(n == "rtlo" ? g_rank.rtlo : n == "rthi" ? g_rank.rthi : (int64_t)g_rank.compact);
+    v = &one;
+  }
   if (v) {
     if (out) std::memcpy(out, v->data(), v->size() * 8);
     return (int64_t)v->size();
@@ -375,6 +380,9 @@ int64_t shim_rank_array(const char* name, int l, int64_t* out) {
   else if (pn == "sap") x = &g_rank.sap.at(l);
   else if (pn == "xg") x = &g_rank.xg;
   else if (pn == "sg") x = &g_rank.sg;
+  else if (pn == "xc") x = &g_rank.xc;
+  else if (pn == "spt") x = &g_rank.spt;
+  else if (pn == "sd") x = &g_rank.sd;
   else return -1;
   std::vector<int64_t> t;
   if (fn == "peers") t.assign(x->peers.begin(), x->peers.end());

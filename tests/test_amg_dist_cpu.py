@@ -20,6 +20,7 @@ import ctypes as C
 
 import numpy as np
 import pytest
+import scipy.sparse as sp
 
 import amg_ref
 import fea_oracle as fo
@@ -113,8 +114,10 @@ def _rank(shim, r, nlev, n_dist):
     fields = ("peers", "soff", "scnt", "roff", "rcnt", "sidx", "ridx")
     for kind in ("xa", "xr", "xp", "sp", "sap"):
         rk[kind] = [{f: arr(f"{kind}.{f}", l) for f in fields} for l in range(n_dist)]
-    for kind in ("xg", "sg"):
+    for kind in ("xg", "sg", "xc", "spt", "sd"):
         rk[kind] = {f: arr(f"{kind}.{f}") for f in fields}
+    for k in ("rtlo", "rthi", "compact"):
+        rk[k] = int(arr(k)[0])
     return rk
 
 
@@ -295,3 +298,88 @@ def test_rank_level0_from_partition_pattern(shim, world):
     mine = got[valid]
     assert not np.isnan(mine).any()
     assert np.allclose(mine, ref, rtol=1e-14, atol=1e-14 * np.abs(ref).max())
+
+
+def _compact_dist_vcycle(levels, ranks, rvec, nd):
+    """The compact schedule of capi.hip enqueue_gamg_vcycle (AmgRank::compact:
+    level 0 split, every level below replicated), rank by rank with NaN
+    wherever a rank holds no value: x_0 on its rows, the xc halo, down_0 (its
+    Ã_0 rows → c_0, its R̂_0 rows → x_1), the x_1 all-gather (xg), the
+    replicated cycle from level 1, up_0 on its P̃_0 rows."""
+    W = len(ranks)
+    L0, N = levels[0], levels[1]
+    blk = lambda M: sp.block_diag(list(M), format="csr")  # noqa: E731
+    s_n = 1.0 if N["coarsest"] else N["omega"]
+    Rhat = (s_n * blk(N["dinv"]) @ L0["Rt"] @ blk(np.linalg.inv(L0["dinv"])) / L0["omega"]).tocsr()
+    At = (L0["omega"] * blk(L0["dinv"]) @ L0["A"]).tocsr()
+    r2 = rvec.reshape(-1, nd)
+    x0 = [np.full(r2.shape, np.nan) for _ in range(W)]
+    x1 = [np.full((N["n"], nd), np.nan) for _ in range(W)]
+    c0 = [np.full(r2.shape, np.nan) for _ in range(W)]
+    for r, rk in enumerate(ranks):
+        rs = slice(int(rk["lo"][0]), int(rk["hi"][0]))
+        x0[r][rs] = L0["omega"] * np.einsum("iab,ib->ia", L0["dinv"][rs], r2[rs])
+    _xchg(ranks, [rk["xc"] for rk in ranks], x0)
+
+    def rows_of(M, idx, v):  # rows idx (node rows) of M times v; NaN if a read value is missing
+        d = (idx[:, None] * nd + np.arange(nd)).ravel()
+        sub = M[d]
+        vv = v.reshape(-1)
+        cols = np.unique(sub.indices)
+        assert not np.isnan(vv[cols]).any(), "a read value neither owned nor received"
+        return (sub @ np.nan_to_num(vv)).reshape(-1, nd)
+
+    for r, rk in enumerate(ranks):
+        own = np.arange(int(rk["lo"][0]), int(rk["hi"][0]))
+        c0[r][own] = 2.0 * x0[r][own] - rows_of(At, own, x0[r])
+        rows1 = L0["rt_row"][int(rk["rtlo"]):int(rk["rthi"])]
+        x1[r][rows1] = rows_of(Rhat, rows1, x0[r])
+    _xchg(ranks, [rk["xg"] for rk in ranks], x1)
+    u = np.full(r2.shape, np.nan)
+    for r, rk in enumerate(ranks):
+        assert not np.isnan(x1[r]).any()
+        e1 = amg_ref.vcycle_scaled(levels, (1, x1[r].reshape(-1))).reshape(-1, nd)
+        rows0 = L0["pt_row"][int(rk["aplo"][0]):int(rk["aphi"][0])]
+        u[rows0] = c0[r][rows0] + rows_of(L0["Pt"], rows0, e1)
+    return u.reshape(-1)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_compact_distributed_vcycle_equals_global(shim, world):
+    """The compact distributed cycle (level 0 split over the ranks, every level
+    below replicated: capi.hip enqueue_gamg_vcycle's AmgRank::compact branch)
+    gives the one-partition compact cycle's output on every rank's rows,
+    every value it reads owned or received through xc / xg; its R̂_0 rows
+    cover level 1 once; its setup reads only owned or received P̃_0 blocks
+    (spt) and level-0 diagonal blocks (sd)."""
+    xyz, e2n, top, bot = _golden22k()
+    levels, Kff, b, n_dist, ranks = _case(shim, xyz, e2n, top, bot, world, 1 << 40)
+    assert n_dist == 1 and all(rk["compact"] for rk in ranks)
+    amg_ref.compact_transfers(levels)
+    L0, N = levels[0], levels[1]
+    spans = sorted((rk["rtlo"], rk["rthi"]) for rk in ranks)
+    assert spans[0][0] == 0 and spans[-1][1] == N["n"]
+    assert all(a[1] == b_[0] for a, b_ in zip(spans, spans[1:]))
+    for rk_i, rk in enumerate(ranks):  # R̂_0 rows of rank r produce level-1 rows r owns
+        rows1 = L0["rt_row"][rk["rtlo"]:rk["rthi"]]
+        assert np.all(N["owner"][rows1] == rk_i)
+    rng = np.random.default_rng(world)
+    r = rng.standard_normal(b.size)
+    ud = _compact_dist_vcycle(levels, ranks, r, 2)
+    ug = amg_ref.vcycle_scaled(levels, r)
+    assert not np.isnan(ud).any()
+    assert np.allclose(ud, ug, rtol=1e-12, atol=1e-12 * np.abs(ug).max())
+    # the R̂_0 setup: P̃_0 positions and diagonal blocks read, owned or received
+    ptrow, _ = amg_ref.pos_rows(L0["PT.sptr"], L0["n"])
+    rtrow, _ = amg_ref.pos_rows(L0["RT.sptr"], N["n"])
+    arow, ak = amg_ref.pos_rows(L0["A.sptr"], L0["n"])
+    for rk in ranks:
+        pt_ok = (ptrow >= rk["aplo"][0]) & (ptrow < rk["aphi"][0])
+        pt_ok[rk["spt"]["ridx"]] = True
+        d_ok = (arow >= rk["lo"][0]) & (arow < rk["hi"][0]) & (ak == 0)
+        d_ok[rk["sd"]["ridx"]] = True
+        mine = np.flatnonzero((rtrow >= rk["rtlo"]) & (rtrow < rk["rthi"]) & (L0["RT.col"] >= 0))
+        assert pt_ok[L0["rt_pt"][mine]].all()
+        cols = L0["RT.col"][mine]
+        dpos = np.array([np.flatnonzero((arow == c) & (ak == 0))[0] for c in np.unique(cols)])
+        assert d_ok[dpos].all()

@@ -100,7 +100,7 @@ def test_partitioned_gamg_split_depths(peng, rep_rows):
     from mfea import PC_GAMG, make_opts
     sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
     dy = float(sysz["dy"])
-    with peng.options(amg_rep_rows=rep_rows, amg_dist=1):
+    with peng.options(amg_rep_rows=rep_rows, amg_dist=1, amg_dist_cycle=0):
         _sim181147(peng, 3)
         peng.assemble()
         st = peng.solve(dy, -dy, make_opts(rtol=1e-13, max_it=2000, precond=PC_GAMG))
@@ -112,6 +112,53 @@ def test_partitioned_gamg_split_depths(peng, rep_rows):
     if rep_rows == 1 << 30:
         assert info["n_dist"] == 1
     assert rel(U, sysz["U"]) <= 1e-10
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_partitioned_compact_cycle_matches_four_step_and_one_partition(peng, engine, nparts):
+    """The distributed V-cycle in its compact form (option amg_dist_cycle 1:
+    level 0 split, the levels below replicated and collapsed as on one
+    partition; capi.hip enqueue_gamg_vcycle) against the four-step form and
+    the one-partition hierarchy: U to 1e-10 of the direct solve and within
+    1e-12·‖U‖ of the four-step form at rtol 1e-14, the one-partition
+    iteration count at 1e-8 (±1), and one cycle's output equal to the
+    one-partition compact cycle's up to f32 rounding."""
+    from mfea import PC_GAMG, make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    dy = float(sysz["dy"])
+    out = {}
+    for cyc in (1, 0):
+        with peng.options(amg_dist=1, amg_dist_cycle=cyc):
+            xyz, e2n, top, bot = _sim181147(peng, nparts)
+            peng.assemble()
+            st = peng.solve(dy, -dy, make_opts(rtol=1e-14, max_it=2000, precond=PC_GAMG))
+            assert st.status == 0, cyc
+            U = peng.displacement()
+            st8 = peng.solve(dy, -dy, make_opts(rtol=1e-8, max_it=2000, precond=PC_GAMG))
+            info = peng.amg_info()
+            # a random residual on the loaded rows (zero on the grips and on
+            # the pieces cut off from them, as every CG residual is there:
+            # their near-singular coarse blocks would amplify anything else)
+            import scipy.sparse as sps
+            from scipy.sparse.csgraph import connected_components
+            rng = np.random.default_rng(4)
+            r = rng.standard_normal((len(xyz), 2))
+            g = sps.coo_matrix((np.ones(len(e2n)), (e2n[:, 0], e2n[:, 1])), shape=(len(xyz),) * 2)
+            _, lab = connected_components(g, directed=False)
+            anchored = np.zeros(lab.max() + 1, bool)
+            anchored[lab[np.concatenate([top, bot])]] = True
+            known = ~anchored[lab]
+            known[np.concatenate([top, bot])] = True
+            r[known] = 0
+            u = peng.amg_vcycle(r)
+        out[cyc] = (U, st8.iters, info, u)
+        assert rel(U, sysz["U"]) <= 1e-10, cyc
+    assert out[1][2]["n_dist"] == 1
+    assert np.linalg.norm(out[1][0] - out[0][0]) <= 1e-12 * np.linalg.norm(out[0][0]) * 100
+    it1, _ = _its_one_partition(engine, xyz, e2n, top, bot, dy)
+    assert abs(out[1][1] - it1) <= 1, (out[1][1], it1)
+    u1 = engine.amg_vcycle(r)
+    assert rel(out[1][3], u1) <= 1e-5
 
 
 @pytest.mark.parametrize("nparts,amg_dist", [(2, 1), (3, 1), (2, 0), (4, 0)])

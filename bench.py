@@ -74,6 +74,11 @@ def parse(argv=None):
                     help="1 GPU: run the partitioned solve with this many partitions on it")
     ap.add_argument("--no-full-run", action="store_true",
                     help="skip the 40-step run (all load steps, with failures) after the timed steps")
+    ap.add_argument("--amg-dist", type=int, default=1, choices=[-1, 0, 1],
+                    help="N > 1 GAMG form: 1 the global hierarchy's distributed V-cycle (default: holds the "
+                         "one-partition iteration count on any network), 0 block Jacobi over per-partition "
+                         "hierarchies (as fast only where the cuts follow weak couplings, e.g. the tiled "
+                         "network's seams), -1 the engine's automatic choice")
     ap.add_argument("--no-jacobi", action="store_true",
                     help="skip the Jacobi-PCG leg (SURVEY §8d's iteration metric) after the timed steps")
     return ap.parse_args(argv)
@@ -441,6 +446,12 @@ def main(argv=None):
             eng.set_partition_axis(-1)  # the min-cut px × py grid (partition.hpp)
         elif mode == "parts":
             eng.set_parts(a.parts, -1)
+        if mode in ("partitioned", "parts"):
+            # the global hierarchy's compact distributed cycle by default: block
+            # Jacobi over partitions matches it here only because the tiled
+            # network's cuts follow its weak tile seams (190-310 iterations
+            # instead of 16 on the grown reference network)
+            eng.set_option("amg_dist", a.amg_dist)
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=a.config.startswith("C5"))
         top, bot = synth.grips(xyz)
         eng.set_material(fs.E_mod, fs.A, fs.I)
@@ -665,9 +676,12 @@ def main(argv=None):
                       "setup_pair_items": ai["pair_items"], "split_levels": ai["n_dist"]}
     if mode in ("partitioned", "parts") and pc == PC_GAMG:
         ch = eng.get_option("amg_dist_chosen")
+        how = ("option amg_dist -1: the faster of the two, measured in warmup" if a.amg_dist < 0
+               else f"--amg-dist {a.amg_dist}")
         out["config"]["amg_partitions"] = {
-            0: "block Jacobi over per-partition hierarchies", 1: "distributed V-cycle of one global hierarchy",
-            -1: "undecided"}[ch] + " (option amg_dist -1: the faster of the two, measured in warmup)"
+            0: "block Jacobi over per-partition hierarchies",
+            1: "distributed V-cycle of one global hierarchy (compact: level 0 split, levels below replicated)",
+            -1: "undecided"}[ch] + f" ({how})"
     if note:
         out["note"] = note
 

@@ -56,7 +56,11 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *   "amg_dist" -1|0|1    partitioned GAMG: block Jacobi over per-partition hierarchies (0),
  *                        the distributed V-cycle of one global hierarchy (1), or per
  *                        active set whichever of the two solved faster (-1)
- *   "amg_rep_rows" n     distributed V-cycle: levels of at most n rows replicated (32768)
+ *   "amg_rep_rows" n     distributed V-cycle (four-step form): levels of at most n rows replicated (32768)
+ *   "amg_dist_cycle" 0|1 distributed V-cycle: the compact form, level 0 split and every level
+ *                        below replicated (1), or the four-step form over the split levels (0)
+ *   "dist_sums" 0|1      GAMG over RCCL: the CG's per-rank sums as one all-reduce of a
+ *                        zero-padded [world][4] buffer (1) or send / receive pairs (0)
  *   "amg_reuse" 0|1      GAMG: keep the hierarchy over element failures, floating pieces
  *                        masked (1), or rebuild it for every new active set (0)
  *   "amg_rebuild_pct" n  GAMG: a kept hierarchy is rebuilt once a solve needs more than
@@ -84,7 +88,8 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 
 /* The current value of an option of mfea_set_option (as it would be passed
  * back: part_slack_pct in percent, dist_timeout_ms in ms), or of the
- * read-only "amg_dist_chosen": the form option "amg_dist" -1 picked for the
+ * read-only "amg_dist_chosen": the partitioned GAMG form in use — the one
+ * option "amg_dist" names, or with "amg_dist" -1 the one picked for the
  * current active set (0 block Jacobi, 1 global hierarchy, -1 not yet). */
 int mfea_get_option(mfea_handle* h, const char* name, int64_t* value);
 

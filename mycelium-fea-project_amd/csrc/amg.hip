@@ -1362,14 +1362,23 @@ __global__ __launch_bounds__(BS) void k_amg_cg_w(int j, AmgLevD L0, AmgCg cg, Sl
 // order, as wave_partials does) → its row of gall[q] and gsend.  Every rank
 // then adds the gathered rows in rank order (k_amg_cg_update<DIST>): the same
 // bits everywhere, so α, β and the stopping test agree across ranks.
+// zero_w > 0 (the rows travel as ONE all-reduce sum, capi.hip xchg_sums):
+// the other ranks' rows [0, zero_w) of gall are zeroed, so the sum of the
+// ranks' buffers is every rank's row exactly (x + 0 + … + 0 = x)
 template <int PU>
-__global__ __launch_bounds__(64) void k_amg_gsum(const double* __restrict__ p, double* row, double* gsend) {
+__global__ __launch_bounds__(64) void k_amg_gsum(const double* __restrict__ p, double* all, int rank, int zero_w,
+                                                 double* gsend) {
   double S[4];
   wave_partials<PU>(p, S);
-  if (threadIdx.x == 0) {
+  const int lane = threadIdx.x;
+  if (lane < zero_w && lane != rank) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) all[4 * lane + c] = 0.0;
+  }
+  if (lane == 0) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      row[c] = S[c];
+      all[4 * rank + c] = S[c];
       gsend[c] = S[c];
     }
   }
@@ -1961,12 +1970,13 @@ void launch_amg_cg_w(hipStream_t s, int nd, int j, bool first, const AmgLevD& L0
 }
 
 void launch_amg_gsum(hipStream_t s, const AmgCg& cg, const double* part_q, const AmgDist& d, int q) {
-  double* row = d.gall[q] + 4 * d.rank;
+  double* all = d.gall[q];
+  const int r = d.rank, zw = d.zero_w;
   switch (pu_of_grid(amg_w_grid(cg))) {  // the w kernel's grid = its partial count
-    case 1: hipLaunchKernelGGL(k_amg_gsum<1>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
-    case 2: hipLaunchKernelGGL(k_amg_gsum<2>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
-    case 4: hipLaunchKernelGGL(k_amg_gsum<4>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
-    default: hipLaunchKernelGGL(k_amg_gsum<8>, dim3(1), dim3(64), 0, s, part_q, row, d.gsend); break;
+    case 1: hipLaunchKernelGGL(k_amg_gsum<1>, dim3(1), dim3(64), 0, s, part_q, all, r, zw, d.gsend); break;
+    case 2: hipLaunchKernelGGL(k_amg_gsum<2>, dim3(1), dim3(64), 0, s, part_q, all, r, zw, d.gsend); break;
+    case 4: hipLaunchKernelGGL(k_amg_gsum<4>, dim3(1), dim3(64), 0, s, part_q, all, r, zw, d.gsend); break;
+    default: hipLaunchKernelGGL(k_amg_gsum<8>, dim3(1), dim3(64), 0, s, part_q, all, r, zw, d.gsend); break;
   }
 }
 
@@ -2026,6 +2036,38 @@ __global__ __launch_bounds__(kBlock) void k_xunpack(const T* __restrict__ buf, c
   if (k >= n * width) return;
   const int64_t it = k / width, c = k - it * width;
   dst[(int64_t)idx[it] * width + c] = buf[k];
+}
+// partitions on one device: every (sender, receiver) transfer of an
+// exchange in ONE launch, item to item (no staging buffers): pair p moves
+// src_p[sidx_p[k]] → dst_p[ridx_p[k]], k < cnt_p, width scalars each
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_xcopy(XPairs pr, int width) {
+  const int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int p = 0;
+  while (p + 1 < pr.n && k >= pr.off[p + 1] * width) ++p;  // (≤ 64 pairs, uniform prefix)
+  if (p >= pr.n || k >= pr.off[p + 1] * width) return;
+  const int64_t kk = k - pr.off[p] * width, it = kk / width, c = kk - it * width;
+  const T* __restrict__ src = (const T*)pr.src[p];
+  T* __restrict__ dst = (T*)pr.dst[p];
+  dst[(int64_t)pr.ridx[p][it] * width + c] = src[(int64_t)pr.sidx[p][it] * width + c];
+}
+void launch_xcopy(hipStream_t s, const XPairs& pr, int width, int bytes) {
+  if (pr.n <= 0 || pr.off[pr.n] <= 0) return;
+  const dim3 g = rows_grid(pr.off[pr.n] * width);
+  if (bytes == 8) hipLaunchKernelGGL(k_xcopy<double>, g, dim3(kBlock), 0, s, pr, width);
+  else hipLaunchKernelGGL(k_xcopy<float>, g, dim3(kBlock), 0, s, pr, width);
+}
+// partitions on one device: every partition's 4 CG sums (gsend) into row
+// `rank` of every other partition's gathered sums, one launch
+__global__ __launch_bounds__(kBlock) void k_gall_copy(GallCopy g) {
+  const int t = threadIdx.x, n = g.n;
+  for (int idx = t; idx < n * n * 4; idx += kBlock) {
+    const int a = idx / (4 * n), b = (idx / 4) % n, c = idx & 3;
+    if (a != b) g.gall[b][4 * g.rank[a] + c] = g.gsend[a][c];
+  }
+}
+void launch_gall_copy(hipStream_t s, const GallCopy& g) {
+  if (g.n > 1) hipLaunchKernelGGL(k_gall_copy, dim3(1), dim3(kBlock), 0, s, g);
 }
 void launch_xpack(hipStream_t s, const void* src, const int32_t* idx, int64_t n, int width, int bytes, void* buf) {
   if (n <= 0) return;

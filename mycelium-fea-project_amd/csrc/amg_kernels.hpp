@@ -203,6 +203,7 @@ void launch_sweep(hipStream_t s, int nd, const SweepD& sw, const AmgCg& cg, cons
 // per-rank partial sums, its ghost couplings and the u halo buffers.
 struct AmgDist {
   int rank = 0;
+  int zero_w = 0;  // > 0: the sums travel as one all-reduce over [zero_w][4] (the other rows zeroed)
   double* gall[2] = {nullptr, nullptr};  // [64][4] per-rank partial sums by parity
   double* gsend = nullptr;               // [4] this rank's, sent to every rank
   const int32_t* gptr = nullptr;         // per level-0 row: ghost couplings
@@ -259,6 +260,26 @@ void launch_amg_vstep(hipStream_t s, int nd, const AmgLevD* lev, int l, const Am
 // ---- exchanges of the distributed V-cycle and setup (amg.hpp XPlan): items
 // of `width` scalars, gathered into / scattered from a contiguous buffer
 void launch_xpack(hipStream_t s, const void* src, const int32_t* idx, int64_t n, int width, int bytes, void* buf);
+// partitions on one device: an exchange's transfers between partitions in one
+// launch, straight from the sender's array to the receiver's (off: prefix of
+// the pairs' item counts)
+constexpr int kMaxXPairs = 48;
+struct XPairs {
+  int n = 0;
+  int64_t off[kMaxXPairs + 1] = {};
+  const void* src[kMaxXPairs] = {};
+  void* dst[kMaxXPairs] = {};
+  const int32_t* sidx[kMaxXPairs] = {};
+  const int32_t* ridx[kMaxXPairs] = {};
+};
+void launch_xcopy(hipStream_t s, const XPairs& pr, int width, int bytes);
+struct GallCopy {
+  int n = 0;
+  const double* gsend[64] = {};
+  double* gall[64] = {};
+  int rank[64] = {};
+};
+void launch_gall_copy(hipStream_t s, const GallCopy& g);
 void launch_xunpack(hipStream_t s, const void* buf, const int32_t* idx, int64_t n, int width, int bytes, void* dst);
 // the first smoothing step x = s·D⁻¹ b (s = ω, 1 on the coarsest level) of
 // the listed rows of level N (the rows the replicated level's all-gather brought)

@@ -326,6 +326,11 @@ struct mfea_handle {
   // points per iteration), 0 the four-step cycle over the levels of more than
   // amg_rep_rows rows (four exchange points per split level)
   int opt_amg_dist_cycle = 1;
+  // GAMG over RCCL: the CG's per-rank partial sums as ONE ncclAllReduce of
+  // [world][4] doubles, every rank's buffer zero but its own row (1; the sum
+  // is then each row exactly, summed by every rank in rank order as before),
+  // or as world − 1 send / receive pairs per rank (0)
+  int opt_dist_sums = 1;
   // distributed GAMG (partitioned handles, option "amg_dist" 1): the whole
   // mesh's pattern and node owners (built with the partitions), and ONE
   // global hierarchy for the current global element activity
@@ -1582,6 +1587,7 @@ int upload_amg_halo(mfea_handle* h, Part& pt, const std::vector<uint8_t>& key) {
   d.gall[0] = pt.dv.gall[0];
   d.gall[1] = pt.dv.gall[1];
   d.gsend = pt.dv.gsend;
+  d.zero_w = h->world > 1 && h->opt_dist_sums == 1 ? h->world : 0;
   d.send_rows = ib;
   d.n_send = (int64_t)a;
   d.gptr = ib + a;
@@ -1842,6 +1848,11 @@ int xchg_u(mfea_handle* h) {
 // every rank's 4 partial sums (gsend) → row `rank` of every rank's gall[q]
 int xchg_sums(mfea_handle* h, int q) {
   hipStream_t s = h->stream;
+  if (h->world > 1 && h->opt_dist_sums == 1) {  // one all-reduce: every row but the own zeroed (k_amg_gsum)
+    Part& pt = part0(h);
+    NCCLC(ncclAllReduce(pt.dv.gall[q], pt.dv.gall[q], (size_t)4 * h->world, ncclFloat64, ncclSum, h->comm, s));
+    return 0;
+  }
   if (h->world > 1) {
     Part& pt = part0(h);
     NCCLC(ncclGroupStart());
@@ -1849,11 +1860,16 @@ int xchg_sums(mfea_handle* h, int q) {
     NCCLC(ncclGroupEnd());
     return 0;
   }
-  for (auto& a : h->parts)
-    for (auto& b : h->parts)
-      if (b != a)
-        HIPC(hipMemcpyAsync(b->dv.gall[q] + 4 * a->rank, a->dv.gsend, 4 * sizeof(double),
-                            hipMemcpyDeviceToDevice, s));
+  GallCopy g;  // partitions on one device: one launch for every pair
+  for (auto& a : h->parts) {
+    if (g.n == 64) return fail(MFEA_EINVAL, "internal: more than 64 partitions");
+    g.gsend[g.n] = a->dv.gsend;
+    g.gall[g.n] = a->dv.gall[q];
+    g.rank[g.n] = a->rank;
+    ++g.n;
+  }
+  launch_gall_copy(s, g);
+  HIPC(hipGetLastError());
   return 0;
 }
 
@@ -2279,6 +2295,7 @@ int ensure_gamg(mfea_handle* h, bool* rebuilt) {
     d.gall[0] = pt.dv.gall[0];
     d.gall[1] = pt.dv.gall[1];
     d.gsend = pt.dv.gsend;
+    d.zero_w = h->world > 1 && h->opt_dist_sums == 1 ? h->world : 0;
     pt.dev_plan = 1;
   }
   if (up) ++h->gamg_gen;
@@ -2292,6 +2309,36 @@ int ensure_gamg(mfea_handle* h, bool* rebuilt) {
 template <class GetPlan, class GetVec>
 int gx(mfea_handle* h, GetPlan plan, GetVec vec, int width, int bytes) {
   hipStream_t s = h->stream;
+  if (h->world <= 1) {  // partitions on one device: every transfer in one launch, array to array
+    XPairs pr;
+    for (auto& a : h->parts) {
+      const Part::XDev& da = plan(*a);
+      const XPlan& xa = *da.x;
+      for (size_t i = 0; i < xa.peers.size(); ++i) {
+        if (!xa.scnt[i]) continue;
+        Part& b = *h->parts[xa.peers[i]];
+        const Part::XDev& db = plan(b);
+        const XPlan& xb = *db.x;
+        const auto it = std::lower_bound(xb.peers.begin(), xb.peers.end(), a->rank);
+        const size_t jb = (size_t)(it - xb.peers.begin());
+        if (it == xb.peers.end() || *it != a->rank || xb.rcnt[jb] != xa.scnt[i])
+          return fail(MFEA_EINVAL, "internal: asymmetric GAMG exchange plan");
+        if (pr.n == kMaxXPairs) {
+          launch_xcopy(s, pr, width, bytes);
+          pr = XPairs();
+        }
+        pr.src[pr.n] = vec(*a);
+        pr.dst[pr.n] = vec(b);
+        pr.sidx[pr.n] = da.s + xa.soff[i];
+        pr.ridx[pr.n] = db.r + xb.roff[jb];
+        pr.off[pr.n + 1] = pr.off[pr.n] + xa.scnt[i];
+        ++pr.n;
+      }
+    }
+    launch_xcopy(s, pr, width, bytes);
+    HIPC(hipGetLastError());
+    return 0;
+  }
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Part::XDev& d = plan(pt);
@@ -3845,6 +3892,12 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->opt_amg_dist_cycle = (int)value;
     h->gamg_ok = false;
   }
+  else if (n == "dist_sums") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "dist_sums: 1 (all-reduce) or 0 (send / receive pairs)");
+    h->opt_dist_sums = (int)value;
+    for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
+    destroy_graph(h);  // captured chunks hold the old exchange
+  }
   else if (n == "cc_tile") {
     if (value != 512 && value != 1024 && value != 2048 && value != 4096)
       return fail(MFEA_EINVAL, "cc_tile: 512, 1024, 2048 or 4096");
@@ -4047,10 +4100,12 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_rebuild_rent") *value = h->opt_amg_rebuild_rent;
   else if (n == "amg_reused") *value = part0(h).amg_reused ? 1 : 0;  // read-only: the last solve kept a hierarchy built for another set
   else if (n == "amg_build_iters") *value = part0(h).amg_build_iters;  // read-only
-  else if (n == "amg_dist_chosen") *value = h->amg_auto.choice;  // read-only: -1 undecided
+  else if (n == "amg_dist_chosen")  // read-only: the form in use (-1: the automatic choice still undecided)
+    *value = h->opt_amg_dist >= 0 ? h->opt_amg_dist : h->amg_auto.choice;
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "cc_tile") *value = h->opt_cc_tile;
   else if (n == "amg_dist_cycle") *value = h->opt_amg_dist_cycle;
+  else if (n == "dist_sums") *value = h->opt_dist_sums;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);
   else return fail(MFEA_EINVAL, "unknown option " + n);
   return 0;

@@ -357,3 +357,48 @@ def test_dropin_record_gather_world2():
         p.join(120)
         assert p.exitcode == 0
     assert all(q.get(timeout=10) for _ in range(WORLD))
+
+
+def _sums_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    rng = np.random.default_rng(100 + rank)
+    mine = rng.standard_normal(4) * 10.0 ** rng.integers(-20, 20, 4)
+    # capi.hip xchg_sums (dist_sums 1): every rank's [world][4] buffer zero but
+    # its own row (k_amg_gsum zero_w), one all-reduce sum
+    buf = torch.zeros(world, 4, dtype=torch.float64)
+    buf[rank] = torch.from_numpy(mine)
+    dist.all_reduce(buf)
+    # ... equals the all-gather of the rows (the p2p form, dist_sums 0) bit for bit
+    rows = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(rows, torch.from_numpy(mine))
+    ok = bool(torch.equal(buf, torch.stack(rows)))
+    # and every rank then sums the rows in rank order to the same bits
+    s = np.zeros(4)
+    for r in range(world):
+        s = s + buf[r].numpy()
+    allsum = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(allsum, torch.from_numpy(s))
+    ok = ok and all(torch.equal(a, allsum[0]) for a in allsum)
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cg_sums_allreduce_equals_rank_gather(world):
+    """The GAMG CG's per-rank partial sums as one all-reduce of a zero-padded
+    [world][4] buffer (capi.hip xchg_sums, option dist_sums 1) carry exactly
+    the rows the send / receive pairs carried (x + 0 + … + 0 = x), so every
+    rank forms bitwise the same α, β and stopping test as before."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sums_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get() for _ in range(world))
+    assert all(res[r] for r in range(world)), res

@@ -149,6 +149,11 @@ struct Part {
   const int32_t* amg_row0_inv = nullptr;  // level-0 label of every free row (carved from amg_i)
   DevBuf<int32_t> cc_parent;         // launch_floating's scratch: component links, anchored roots
   DevBuf<uint8_t> cc_anch;
+  // element colouring for the element-centric assembly (option asm_kernel 1),
+  // built at first use: ec_state 0 not built, 1 usable, -1 not colourable
+  ElemColour ec;
+  int ec_state = 0;
+  DevBuf<int32_t> ec_entry, ec_pos;
   // the plan's key covers the current activity: act_sub_gen when it was
   // built or last compared (failures only ever shrink the set, so it holds
   // until the activity is set explicitly), and its element count
@@ -310,6 +315,9 @@ struct mfea_handle {
   // until a solve needs more than amg_rebuild_pct % of the iterations of the
   // hierarchy's first solve (+2), then rebuild; 0 rebuild on every new active set
   int opt_amg_reuse = 1;
+  // assembly: 0 row gather (one launch, fused GAMG RHS), 1 element colours
+  // (a launch per colour), 2 element pass + row pass (two launches)
+  int opt_asm_kernel = 0;
   int opt_cc_tile = 1024;  // floating rows on the device: rows per LDS tile (512, 1024, 2048, 4096; C3 73 µs at 512-1024, C5 0.6 ms at 1024-2048)
   int opt_amg_rebuild_pct = 800;
   // ... or once the time its solves spent on iterations above that count
@@ -2845,6 +2853,28 @@ int solve_dist(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_op
   return finish_solve(h, fin, st);
 }
 
+// the element colouring of pt's pattern on the device (symbolic.hpp
+// build_elem_colour), once per pattern; false: not colourable (more than 64
+// colours, or an element with one row slot) — the row gather runs instead
+bool ensure_colour(mfea_handle* h, Part& pt) {
+  if (pt.ec_state) return pt.ec_state > 0;
+  pt.ec_state = -1;
+  if (!build_elem_colour(pt.P, pt.ec).empty()) return false;
+  if (pt.ec.entry.empty() && pt.P.n_elems) return false;
+  if (pt.ec_entry.alloc(std::max<size_t>(pt.ec.entry.size(), 1)) != hipSuccess ||
+      pt.ec_pos.alloc(std::max<size_t>(pt.ec.pos.size(), 1)) != hipSuccess)
+    return false;
+  if (!pt.ec.entry.empty() &&
+      hipMemcpyAsync(pt.ec_entry.ptr, pt.ec.entry.data(), pt.ec.entry.size() * sizeof(int32_t),
+                     hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return false;
+  if (!pt.ec.pos.empty() && hipMemcpyAsync(pt.ec_pos.ptr, pt.ec.pos.data(), pt.ec.pos.size() * sizeof(int32_t),
+                                           hipMemcpyHostToDevice, h->stream) != hipSuccess)
+    return false;
+  pt.ec_state = 1;
+  return true;
+}
+
 int assemble_impl(mfea_handle* h, mfea_stats* st, const double* rhs_dy = nullptr) {
   hipStream_t s = h->stream;
   h->assembled = true;
@@ -2853,6 +2883,16 @@ int assemble_impl(mfea_handle* h, mfea_stats* st, const double* rhs_dy = nullptr
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Pattern& P = pt.P;
+    if (h->opt_asm_kernel == 1 && ensure_colour(h, pt)) {
+      launch_assemble_colour(s, pt.ec.colors, pt.ec.cstart.data(), pt.ec_entry.ptr, pt.e2n_d.ptr, pt.ec_pos.ptr,
+                             pt.xyz_d.ptr, pt.active.ptr, h->mat, pt.G, P.n_nodes, pt.val.ptr, pt.diag.ptr);
+      continue;  // (RHS: its own kernel in the solve, rhs_fused stays false)
+    }
+    if (h->opt_asm_kernel == 2 && ensure_colour(h, pt)) {
+      launch_assemble_elems(s, P.n_elems, P.n_nodes, pt.e2n_d.ptr, pt.ec_pos.ptr, pt.xyz_d.ptr, pt.active.ptr,
+                            h->mat, pt.slice_ptr.ptr, pt.row_len.ptr, pt.G, pt.val.ptr, pt.diag.ptr);
+      continue;
+    }
     AsmRhs q{};
     const bool rhs = rhs_dy && h->parts.size() == 1;  // (rhs_dy: a one-partition GAMG / SOR / ICC step)
     if (rhs) {
@@ -3898,6 +3938,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "asm_kernel") {
+    if (value < 0 || value > 2)
+      return fail(MFEA_EINVAL, "asm_kernel: 0 (row gather), 1 (element colours), 2 (element pass + row pass)");
+    h->opt_asm_kernel = (int)value;
+  }
   else if (n == "cc_tile") {
     if (value != 512 && value != 1024 && value != 2048 && value != 4096)
       return fail(MFEA_EINVAL, "cc_tile: 512, 1024, 2048 or 4096");
@@ -4104,6 +4149,11 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
     *value = h->opt_amg_dist >= 0 ? h->opt_amg_dist : h->amg_auto.choice;
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "cc_tile") *value = h->opt_cc_tile;
+  else if (n == "asm_kernel") *value = h->opt_asm_kernel;
+  else if (n == "asm_colours") {
+    *value = 0;
+    for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);
+  }
   else if (n == "amg_dist_cycle") *value = h->opt_amg_dist_cycle;
   else if (n == "dist_sums") *value = h->opt_dist_sums;
   else if (n == "part_slack_pct") *value = (int64_t)std::llround(h->opt_part_slack * 100.0);

@@ -130,6 +130,97 @@ __device__ __forceinline__ void assemble_row(int64_t N, int64_t row, const doubl
   for (int c = 0; c < 6; ++c) diag[(int64_t)c * N + row] = d[c];
 }
 
+// ---------------------------------------------------------------------------
+// Assembly, element-centric (option "asm_kernel" 1; north_star's "one
+// wavefront per element batch … colour-partitioned writes"): one lane per
+// element of a 64-element batch of ONE colour (symbolic.hpp ElemColour).
+// S_e — the bar's BᵀDB, which for this element is k_ax nnᵀ + k_b (I − nnᵀ):
+// six values — is formed ONCE per element in registers (the row gather forms
+// it twice, once per endpoint row), −S_e goes to the element's slot in each
+// endpoint row, and +S_e is added to both rows' diagonal blocks: no two
+// elements of a colour share a node, so the colour's launch adds without
+// atomics, and the colours run in order — deterministic.  Same S bits as the
+// row gather (bar_block is endpoint-symmetric); the diagonal sums run in
+// colour order instead of slot order (within a few ulps).  diag is zeroed
+// before the first colour.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_assemble_colour(int64_t e0, int64_t e1, const int32_t* __restrict__ entry,
+                                                            const int32_t* __restrict__ e2n,
+                                                            const int32_t* __restrict__ epos,
+                                                            const double* __restrict__ xyz,
+                                                            const uint8_t* __restrict__ active, Material m,
+                                                            int64_t G, int64_t N, double* __restrict__ val,
+                                                            double* __restrict__ diag) {
+  const int64_t k = e0 + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= e1) return;
+  const int32_t e = entry[k];
+  if (e < 0) return;
+  const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
+  const int32_t pa = epos[2 * e], pb = epos[2 * e + 1];
+  double S[6] = {0, 0, 0, 0, 0, 0};
+  if (active[e])
+    bar_block(xyz[3 * (int64_t)b] - xyz[3 * (int64_t)a], xyz[3 * (int64_t)b + 1] - xyz[3 * (int64_t)a + 1],
+              xyz[3 * (int64_t)b + 2] - xyz[3 * (int64_t)a + 2], m, S, nullptr);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    val[(int64_t)c * G + pa] = -S[c];
+    val[(int64_t)c * G + pb] = -S[c];
+  }
+  double da[6], db[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    da[c] = diag[(int64_t)c * N + a];
+    db[c] = diag[(int64_t)c * N + b];
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    diag[(int64_t)c * N + a] = da[c] + S[c];
+    diag[(int64_t)c * N + b] = db[c] + S[c];
+  }
+}
+
+// Assembly, element pass + row pass (option "asm_kernel" 2): one lane per
+// element forms S_e once and writes −S_e to its two slots (no two elements
+// share a slot: no conflicts, no colours, one launch); then one lane per row
+// sums −val over its slots in slot order into the diagonal block — the row
+// gather's own order, so K is bit for bit the row gather's.
+__global__ __launch_bounds__(kBlock) void k_assemble_elems(int64_t E, const int32_t* __restrict__ e2n,
+                                                           const int32_t* __restrict__ epos,
+                                                           const double* __restrict__ xyz,
+                                                           const uint8_t* __restrict__ active, Material m,
+                                                           int64_t G, double* __restrict__ val) {
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (e >= E) return;
+  const int32_t pa = epos[2 * e], pb = epos[2 * e + 1];
+  if (pa < 0) return;
+  const int32_t a = e2n[2 * e], b = e2n[2 * e + 1];
+  double S[6] = {0, 0, 0, 0, 0, 0};
+  if (active[e])
+    bar_block(xyz[3 * (int64_t)b] - xyz[3 * (int64_t)a], xyz[3 * (int64_t)b + 1] - xyz[3 * (int64_t)a + 1],
+              xyz[3 * (int64_t)b + 2] - xyz[3 * (int64_t)a + 2], m, S, nullptr);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    val[(int64_t)c * G + pa] = -S[c];
+    val[(int64_t)c * G + pb] = -S[c];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_diag_rows(int64_t N, const int32_t* __restrict__ slice_ptr,
+                                                      const int32_t* __restrict__ row_len, int64_t G,
+                                                      const double* __restrict__ val, double* __restrict__ diag) {
+  const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (row >= N) return;
+  const int64_t base = (int64_t)slice_ptr[row >> 6] * 64 + (row & 63);
+  const int len = row_len[row];
+  double d[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < len; ++k) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) d[c] += -val[(int64_t)c * G + base + (int64_t)k * 64];
+  }
+#pragma unroll
+  for (int c = 0; c < 6; ++c) diag[(int64_t)c * N + row] = d[c];
+}
+
 // RHS: the GAMG solves' RHS too (AsmRhs: k_amg_rhs's outputs from the −S_e
 // blocks in registers) — one launch fewer per step
 template <bool RHS>
@@ -731,6 +822,25 @@ void launch_assemble(hipStream_t s, int64_t N, const double* xyz, const int32_t*
   if (N <= 0) return;
   hipLaunchKernelGGL(k_assemble<false>, MFEA_GRID(grid_rows(N)), N, xyz, slice_ptr, row_len, s_col, s_elem,
                      active, m, G, val, diag, AsmRhs{});
+}
+
+void launch_assemble_colour(hipStream_t s, int colors, const int32_t* cstart, const int32_t* entry,
+                            const int32_t* e2n, const int32_t* epos, const double* xyz, const uint8_t* active,
+                            Material m, int64_t G, int64_t N, double* val, double* diag) {
+  if (N > 0) (void)hipMemsetAsync(diag, 0, (size_t)6 * N * sizeof(double), s);
+  for (int c = 0; c < colors; ++c) {
+    const int64_t e0 = cstart[c], e1 = cstart[c + 1];
+    if (e1 > e0)
+      hipLaunchKernelGGL(k_assemble_colour, MFEA_GRID(grid_rows(e1 - e0)), e0, e1, entry, e2n, epos, xyz, active, m,
+                         G, N, val, diag);
+  }
+}
+
+void launch_assemble_elems(hipStream_t s, int64_t E, int64_t N, const int32_t* e2n, const int32_t* epos,
+                           const double* xyz, const uint8_t* active, Material m, const int32_t* slice_ptr,
+                           const int32_t* row_len, int64_t G, double* val, double* diag) {
+  if (E > 0) hipLaunchKernelGGL(k_assemble_elems, MFEA_GRID(grid_rows(E)), E, e2n, epos, xyz, active, m, G, val);
+  if (N > 0) hipLaunchKernelGGL(k_diag_rows, MFEA_GRID(grid_rows(N)), N, slice_ptr, row_len, G, val, diag);
 }
 
 void launch_rhs_init(hipStream_t s, int64_t N, int64_t nf, const int32_t* slice_ptr,

@@ -97,6 +97,18 @@ void launch_assemble(hipStream_t s, int64_t N, const double* xyz, const int32_t*
                      const uint8_t* active, Material m, int64_t G, double* val, double* diag,
                      const AsmRhs* rhs = nullptr);
 
+// element-centric assembly over an element colouring (symbolic.hpp
+// ElemColour; cstart on the host): diag zeroed, then one launch per colour
+void launch_assemble_colour(hipStream_t s, int colors, const int32_t* cstart, const int32_t* entry,
+                            const int32_t* e2n, const int32_t* epos, const double* xyz, const uint8_t* active,
+                            Material m, int64_t G, int64_t N, double* val, double* diag);
+
+// element pass (−S_e to both slots, one launch) + row pass (diagonal blocks
+// in slot order: K bit for bit the row gather's)
+void launch_assemble_elems(hipStream_t s, int64_t E, int64_t N, const int32_t* e2n, const int32_t* epos,
+                           const double* xyz, const uint8_t* active, Material m, const int32_t* slice_ptr,
+                           const int32_t* row_len, int64_t G, double* val, double* diag);
+
 void launch_rhs_init(hipStream_t s, int64_t N, int64_t nf, const int32_t* slice_ptr,
                      const int32_t* row_len, const int32_t* s_col, const double* val,
                      const double* diag, int64_t G, const uint8_t* code, double dy_top,

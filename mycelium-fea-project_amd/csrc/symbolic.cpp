@@ -399,4 +399,53 @@ void export_csr(const Pattern& P, const std::vector<uint8_t>& active,
   }
 }
 
+std::string build_elem_colour(const Pattern& P, ElemColour& out) {
+  out = ElemColour();
+  const int64_t E = P.n_elems, N = P.n_nodes;
+  out.pos.assign(2 * E, -1);
+  for (int64_t r = 0; r < N; ++r) {
+    const int64_t base = (int64_t)P.slice_ptr[r >> 6] * kSlice + (r & 63);
+    for (int k = 0; k < P.row_len[r]; ++k) {
+      const int64_t q = base + (int64_t)k * kSlice;
+      const int32_t e = P.s_elem[q];
+      if (e < 0) continue;
+      const int side = P.e2n_perm[2 * e] == r ? 0 : 1;
+      out.pos[2 * e + side] = (int32_t)q;
+    }
+  }
+  for (int64_t e = 0; e < E; ++e)
+    if ((out.pos[2 * e] >= 0) != (out.pos[2 * e + 1] >= 0)) return "element colouring: an element with one row slot";
+  // elements with both slots, by their first row
+  std::vector<std::pair<int64_t, int32_t>> order;
+  order.reserve(E);
+  for (int64_t e = 0; e < E; ++e)
+    if (out.pos[2 * e] >= 0 && out.pos[2 * e + 1] >= 0)
+      order.emplace_back(std::min(P.e2n_perm[2 * e], P.e2n_perm[2 * e + 1]), (int32_t)e);
+  std::sort(order.begin(), order.end());
+  std::vector<uint64_t> used(N, 0);
+  std::vector<int8_t> col(E, -1);
+  int colors = 0;
+  for (const auto& re : order) {
+    const int32_t e = re.second, a = P.e2n_perm[2 * e], b = P.e2n_perm[2 * e + 1];
+    const uint64_t busy = used[a] | used[b];
+    if (~busy == 0) return "element colouring: more than 64 colours";
+    const int c = __builtin_ctzll(~busy);
+    col[e] = (int8_t)c;
+    used[a] |= 1ull << c;
+    used[b] |= 1ull << c;
+    colors = std::max(colors, c + 1);
+  }
+  out.colors = colors;
+  std::vector<std::vector<int32_t>> by(colors);
+  for (const auto& re : order) by[col[re.second]].push_back(re.second);  // (first-row order kept)
+  out.cstart.assign(colors + 1, 0);
+  for (int c = 0; c < colors; ++c) {
+    const int64_t n = (int64_t)by[c].size(), padded = (n + kSlice - 1) / kSlice * kSlice;
+    out.cstart[c + 1] = out.cstart[c] + (int32_t)padded;
+    out.entry.insert(out.entry.end(), by[c].begin(), by[c].end());
+    out.entry.insert(out.entry.end(), (size_t)(padded - n), -1);
+  }
+  return "";
+}
+
 }  // namespace mfea

@@ -43,6 +43,25 @@ struct Pattern {
   bool planar = false;             // every z == 0
 };
 
+// Element colouring for the element-centric assembly (kernels.hip
+// k_assemble_colour, option "asm_kernel" 1; BASELINE north_star's "one
+// wavefront per element batch … colour-partitioned writes"): no two elements
+// of one colour share a node, so a colour's element batches add their S_e
+// into the two endpoint rows' diagonal blocks without atomics or conflicts.
+// Greedy over the elements by their first row (the lowest colour free at both
+// endpoints, ≤ 64 colours); within a colour the elements run by that row, so
+// a batch's slot writes land in neighbouring rows.  entry: per colour a run of
+// element ids padded to whole 64-element batches (−1), cstart[c] its start;
+// pos[2e], pos[2e+1]: the element's SELL positions in its two rows (−1 for
+// skipped / self-loop elements, which the assembly leaves out).
+struct ElemColour {
+  int colors = 0;
+  std::vector<int32_t> cstart;  // colors + 1, in entries
+  std::vector<int32_t> entry;   // element id or −1
+  std::vector<int32_t> pos;     // E × 2
+};
+std::string build_elem_colour(const Pattern& P, ElemColour& out);
+
 // sort_window: 0/1 = original node order, kOrderDFS = depth-first order of the
 // free-node graph (default; chains contiguous), >1 = degree sort inside
 // windows of that many rows.

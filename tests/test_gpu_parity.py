@@ -154,6 +154,79 @@ def test_assembly_with_inactive_elements(engine):
 
 
 # ---------------------------------------------------------------------------
+# element-centric colour assembly (option asm_kernel 1, kernels.hip
+# k_assemble_colour): off-diagonal blocks bit for bit the row gather's (the
+# same S_e bits), diagonal blocks summed in colour order within the
+# sequential-sum bound of the reference's csr_matrix, as the row gather's are
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mesh", ["test_X", "sim_20251117_175809", "sim_20251115_135507"])
+def test_colour_assembly_matches_row_gather(engine, mesh):
+    nodes, elems = load_mesh(mesh)
+    xyz, e2n = nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values
+    active = np.random.default_rng(5).random(len(e2n)) > 0.2
+    Kref = fo.assemble_global_stiffness(xyz, e2n, active)
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc([], [])
+    engine.set_active(active)
+    engine.assemble()
+    ip0, ix0, dv0 = engine.export_csr()
+    engine.set_option("asm_kernel", 1)
+    engine.assemble()
+    ip, ix, dv = engine.export_csr()
+    assert 0 < engine.get_option("asm_colours") <= 64
+    assert np.array_equal(ip, ip0) and np.array_equal(ix, ix0)
+    rows = np.repeat(np.arange(len(ip) - 1), np.diff(ip))
+    off = rows // 3 != ix // 3
+    assert np.array_equal(dv[off], dv0[off])
+    check_assembly(dv, Kref, xyz, e2n, active)
+    engine.assemble()  # deterministic: colours in order, no atomics
+    assert np.array_equal(engine.export_csr()[2], dv)
+    engine.set_option("asm_kernel", 2)  # element pass + row pass: the row gather's bits
+    engine.assemble()
+    assert np.array_equal(engine.export_csr()[2], dv0)
+
+
+@pytest.mark.parametrize("precond", [0, 2])
+def test_colour_assembly_solve_matches_direct(engine, precond):
+    from mfea import make_opts
+    sysz = np.load(os.path.join(GOLDEN, "sys_sim_20251117_181147_step20.npz"))
+    _sim181147(engine)
+    engine.set_option("asm_kernel", 1)
+    engine.assemble()
+    st = engine.solve(float(sysz["dy"]), -float(sysz["dy"]),
+                      make_opts(rtol=1e-13, max_it=200000, precond=precond))
+    assert st.status == 0
+    assert rel(engine.displacement(), sysz["U"]) <= 1e-10
+
+
+def test_colour_assembly_steps_match_row_gather(engine):
+    """A loading run with failures: the same failed sets and reactions as the
+    row gather (GAMG, whose RHS then runs as its own kernel)."""
+    from mfea import make_opts
+    nodes, elems = load_mesh("sim_20251117_175809")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    out = []
+    for kern in (0, 1, 2):
+        engine.set_option("asm_kernel", kern)
+        engine.set_mesh(xyz, elems[["n1", "n2"]].values)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        f, n = [], []
+        for k in range(1, 25):
+            d = 0.004 * k
+            fk, nk, st = engine.step(d, -d, make_opts(rtol=1e-12, precond=2), 0.018)
+            assert st.status == 0
+            f.append(fk)
+            n.append(nk)
+        out.append((np.array(f), np.array(n)))
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.all(np.abs(out[0][0] - out[1][0]) <= 1e-8 * np.max(np.abs(out[0][0])))
+    assert np.array_equal(out[0][1], out[2][1])
+    assert np.all(np.abs(out[0][0] - out[2][0]) <= 1e-8 * np.max(np.abs(out[0][0])))
+
+
+# ---------------------------------------------------------------------------
 # solve (src/fea_solver.py:112-135): ≤ 1e-10 relative L2 vs the direct solve
 # ---------------------------------------------------------------------------
 def _sim181147(engine):

@@ -82,7 +82,10 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *   "sweep_piece" 1..64  SOR / ICC: rows per chain piece at most (64; sweep.hip)
  *   "cc_tile" 512|1024|2048|4096  floating rows on the device (kernels.hip launch_floating):
  *                        rows per LDS union-find tile (1024)
- * Read-only: "sweep_colors", "sweep_pieces" (the last SOR / ICC plan).
+ *   "asm_kernel" 0|1|2   assembly: row gather, GAMG RHS fused (0); element colours, one
+ *                        launch per colour (1); element pass + row pass (2) — DESIGN.md §0
+ * Read-only: "sweep_colors", "sweep_pieces" (the last SOR / ICC plan), "asm_colours"
+ * (the element colouring's colours once asm_kernel 1 or 2 has run; 0 before).
  * Options that change the symbolic layout rebuild it at the next call. */
 int mfea_set_option(mfea_handle* h, const char* name, int64_t value);
 

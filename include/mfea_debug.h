@@ -82,6 +82,9 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *   "sweep_piece" 1..64  SOR / ICC: rows per chain piece at most (64; sweep.hip)
  *   "cc_tile" 512|1024|2048|4096  floating rows on the device (kernels.hip launch_floating):
  *                        rows per LDS union-find tile (1024)
+ *   "spec_post" 0|1      mfea_step, one partition, GAMG / SOR / ICC: the post kernels enqueued
+ *                        behind the solve's planned batch, one host wait for both (1); a
+ *                        batch that was not the last has its post's failures undone
  *   "asm_kernel" 0|1|2   assembly: row gather, GAMG RHS fused (0); element colours, one
  *                        launch per colour (1); element pass + row pass (2) — DESIGN.md §0
  * Read-only: "sweep_colors", "sweep_pieces" (the last SOR / ICC plan), "asm_colours"

@@ -264,6 +264,15 @@ struct mfea_handle {
   // displacements (AsmRhs); the next solve_amg uses it instead of k_amg_rhs
   bool rhs_fused = false;
   double rhs_dy[2] = {0.0, 0.0};
+  // mfea_step, one partition (option "spec_post"): the post kernels and
+  // their read-back are enqueued behind the solve's planned batch, before the
+  // host waits for it, so the one wait covers both — one host round trip per
+  // step instead of two.  spec_on: this step may; spec_launched: enqueued
+  // behind the last batch (undone by k_unfail when the solve goes on)
+  int opt_spec_post = 1;
+  bool spec_on = false;
+  bool spec_launched = false;
+  double spec_strain = 0.0;
   hipEvent_t poll[2] = {};
   int64_t n_active = 0;
   bool act_all = false;  // every element is active on the device (set_active(NULL), no failure since)
@@ -1076,7 +1085,7 @@ int finish_solve(mfea_handle* h, const SolveState& fin, mfea_stats* st) {
   if (!h->in_step) {  // (mfea_solve: its end is waited for here)
     HIPC(hipEventRecord(h->ev[3], h->stream));
     RC(wait_event(h, h->ev[3]));
-  } else {
+  } else if (!h->spec_launched) {  // (a speculative post recorded it before itself)
     RC(phase_event(h, h->ev[3], h->stream));
   }
   if (st) {
@@ -2003,6 +2012,9 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   return 0;
 }
 
+int spec_post(mfea_handle* h);
+int spec_undo(mfea_handle* h);
+
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
   Part& pt = part0(h);
@@ -2047,7 +2059,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   auto finish = [&]() -> int {
     launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
     HIPC(hipGetLastError());
-    return 0;
+    return spec_post(h);  // (mfea_step: the post behind the batch, one wait for both)
   };
   if (no_graph) {
     rc = drive_planned(h, chunk, o->max_it, expected,
@@ -2111,6 +2123,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                      &fin, finish, exact_rem);
   }
   if (rc) return rc;
+  if (fin.status != 0) RC(spec_undo(h));
   clk.lap("solve (setup + iterations)", fin.iters);
   if (fin.status != 0 && pt.amg_reused) {
     // a hierarchy kept from another active set failed: rebuild for this one
@@ -2996,8 +3009,9 @@ int local_failures(mfea_handle* h, Part& pt, unsigned c) {
   return 0;
 }
 
-int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
-              mfea_stats* st) {
+// the post kernels (reaction, stress / failures) and the read-back of their
+// sums into h_red, ev[5] behind them
+int enqueue_post(mfea_handle* h, double max_strain) {
   hipStream_t s = h->stream;
   const bool dm = partitioned(h);
   RC(phase_event(h, h->ev[4], s));
@@ -3025,6 +3039,37 @@ int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n
     HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 4, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   }
   HIPC(hipEventRecord(h->ev[5], s));
+  return 0;
+}
+
+// Speculative post (mfea_handle::spec_on), enqueued by the solve's batch end:
+// the solve's end event, then the post — after first undoing the failures a
+// post enqueued behind an earlier batch marked (that solve went on)
+int spec_post(mfea_handle* h) {
+  if (!h->spec_on) return 0;
+  Part& pt = part0(h);
+  if (h->spec_launched) launch_unfail(h->stream, pt.fail_list.ptr, fail_counter(pt), pt.active.ptr);
+  RC(phase_event(h, h->ev[3], h->stream));
+  RC(enqueue_post(h, h->spec_strain));
+  h->spec_launched = true;
+  return 0;
+}
+// the solve did not end with that batch's state: undo its post's failures
+int spec_undo(mfea_handle* h) {
+  if (!h->spec_launched) return 0;
+  Part& pt = part0(h);
+  launch_unfail(h->stream, pt.fail_list.ptr, fail_counter(pt), pt.active.ptr);
+  HIPC(hipGetLastError());
+  h->spec_launched = false;
+  return 0;
+}
+
+int post_impl(mfea_handle* h, double max_strain, double* total_force, int64_t* n_active,
+              mfea_stats* st) {
+  const bool dm = partitioned(h);
+  if (!h->spec_launched) RC(enqueue_post(h, max_strain));
+  h->spec_launched = false;
+  Part& p0 = part0(h);
   RC(wait_event(h, h->ev[5]));
   if (!dm && p0.P.n_top == 0) h->h_red[0] = 0.0;
   if (!dm && p0.P.n_elems == 0) h->h_red[1] = 0.0;
@@ -3348,8 +3393,13 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   // a solver failure stops the step loop here, as the reference does
   // (src/fea_petsc.cpp:346-354)
   h->in_step = true;
+  h->spec_on = fuse_rhs && h->opt_spec_post;
+  h->spec_strain = max_strain;
+  h->spec_launched = false;
   int rc = solve_any(h, dy_top, dy_bot, &o, st);
+  h->spec_on = false;
   h->rhs_fused = false;
+  if (rc) (void)spec_undo(h);
   if (rc == 0) rc = post_impl(h, max_strain, total_force, n_active, st);
   h->in_step = false;
   if (rc) {
@@ -3938,6 +3988,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "spec_post") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "spec_post: 0 or 1");
+    h->opt_spec_post = (int)value;
+  }
   else if (n == "asm_kernel") {
     if (value < 0 || value > 2)
       return fail(MFEA_EINVAL, "asm_kernel: 0 (row gather), 1 (element colours), 2 (element pass + row pass)");
@@ -4150,6 +4204,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "amg_rep_rows") *value = h->opt_amg_rep_rows;
   else if (n == "cc_tile") *value = h->opt_cc_tile;
   else if (n == "asm_kernel") *value = h->opt_asm_kernel;
+  else if (n == "spec_post") *value = h->opt_spec_post;
   else if (n == "asm_colours") {
     *value = 0;
     for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);

@@ -582,6 +582,17 @@ __global__ __launch_bounds__(kBlock) void k_stress(int64_t E, const int32_t* __r
   block_publish<1>(cnt, partials, ticket, red_out);
 }
 
+// Undo a post's failures (capi.hip spec_undo): the elements k_stress listed
+// are active again and the list's counter is zero — a post enqueued behind a
+// CG batch that turned out not to be the last one leaves no trace
+__global__ __launch_bounds__(kBlock) void k_unfail(const int32_t* __restrict__ fail_list, unsigned* cnt,
+                                                   uint8_t* __restrict__ active) {
+  const unsigned c = *cnt;
+  for (unsigned k = threadIdx.x; k < c; k += kBlock) active[fail_list[k]] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) *cnt = 0u;
+}
+
 // ---------------------------------------------------------------------------
 // Floating free rows on the device: connected components of the active
 // element graph, then per component whether a grip row is in it.  A free
@@ -906,6 +917,10 @@ void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* x
                    const uint8_t* owned, int32_t* fail_list, unsigned* fail_cnt) {
   hipLaunchKernelGGL(k_stress, MFEA_GRID(grid_rows(E > 0 ? E : 1)), E, e2n, xyz, u, m, max_strain,
                      active, stress, partials, ticket, red_out, owned, fail_list, fail_cnt);
+}
+
+void launch_unfail(hipStream_t s, const int32_t* fail_list, unsigned* cnt, uint8_t* active) {
+  hipLaunchKernelGGL(k_unfail, dim3(1), dim3(kBlock), 0, s, fail_list, cnt, active);
 }
 
 void launch_floating(hipStream_t s, int64_t n_rows, int64_t n_free, int64_t grip_end, const int32_t* slice_ptr,

@@ -140,6 +140,8 @@ void launch_reaction(hipStream_t s, int64_t row0, int64_t nrows, int64_t N,
 // owned (multi-partition): count only elements this partition reports; NULL = all.
 // fail_list / fail_cnt: the (owned) elements that fail in this launch are
 // appended (any order; NULL = no list)
+// k_stress's failures undone: listed elements active again, counter zero
+void launch_unfail(hipStream_t s, const int32_t* fail_list, unsigned* cnt, uint8_t* active);
 void launch_stress(hipStream_t s, int64_t E, const int32_t* e2n, const double* xyz,
                    const double* u, Material m, double max_strain, uint8_t* active,
                    double* stress, double* partials, unsigned* ticket, double* red_out,

@@ -226,6 +226,34 @@ def test_colour_assembly_steps_match_row_gather(engine):
     assert np.all(np.abs(out[0][0] - out[2][0]) <= 1e-8 * np.max(np.abs(out[0][0])))
 
 
+def test_speculative_post_matches_waited_post(engine):
+    """Option spec_post: the post behind the solve's planned batch.  A run
+    whose tolerance alternates (the planned batch now too short — its post's
+    failures undone, the solve goes on — now too long) gives the same forces,
+    activity and stresses, bit for bit, as the post after the solve's wait."""
+    from mfea import make_opts
+    nodes, elems = load_mesh("sim_20251117_175809")
+    xyz = nodes[["x", "y", "z"]].values
+    top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
+    runs = []
+    for spec in (0, 1):
+        engine.set_option("spec_post", spec)
+        engine.set_mesh(xyz, elems[["n1", "n2"]].values)
+        engine.set_bc(top, bot)
+        engine.set_active(None)
+        rec = []
+        for k in range(1, 25):
+            d = 0.004 * k
+            f, n, st = engine.step(d, -d, make_opts(rtol=1e-5 if k % 3 else 1e-12, precond=2), 0.018)
+            assert st.status == 0
+            rec.append((f, n, st.iters, engine.stress().copy(), engine.active().copy()))
+        runs.append(rec)
+    assert sum(r[1] < runs[0][0][1] for r in runs[0]) > 0  # elements failed
+    for a, b in zip(*runs):
+        assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
+        assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+
+
 # ---------------------------------------------------------------------------
 # solve (src/fea_solver.py:112-135): ≤ 1e-10 relative L2 vs the direct solve
 # ---------------------------------------------------------------------------

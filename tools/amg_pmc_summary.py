@@ -24,14 +24,20 @@ def load(d, pattern):
 
 
 def iterations(disp, reps):
-    """disp: list of (dispatch_id, name, grid, value) sorted by id → last reps iterations"""
+    """disp: list of (dispatch_id, name, grid, value) sorted by id → the last
+    reps iterations: GAMG kernels only, cut at every k_amg_cg_update, keeping
+    the segments of the most common launch sequence (the profiled graph
+    replays; a solve's first or last iteration, or a floating-row pass after
+    the reps, has another)"""
+    disp = [r for r in disp if "k_amg_" in r[1]]
     starts = [k for k, r in enumerate(disp) if "k_amg_cg_update" in r[1]]
-    starts = starts[-reps:]
-    its = []
-    for a, s in enumerate(starts):
-        e = starts[a + 1] if a + 1 < len(starts) else len(disp)
-        its.append(disp[s:e])
-    return its
+    segs = [disp[s:(starts[a + 1] if a + 1 < len(starts) else len(disp))] for a, s in enumerate(starts)]
+    sig = lambda seg: tuple((r[1], r[2]) for r in seg)
+    counts = defaultdict(int)
+    for seg in segs:
+        counts[sig(seg)] += 1
+    best = max(counts, key=counts.get) if counts else ()
+    return [seg for seg in segs if sig(seg) == best][-reps:]
 
 
 def short(n):

@@ -82,6 +82,10 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *   "sweep_piece" 1..64  SOR / ICC: rows per chain piece at most (64; sweep.hip)
  *   "cc_tile" 512|1024|2048|4096  floating rows on the device (kernels.hip launch_floating):
  *                        rows per LDS union-find tile (1024)
+ *   "setup_entry" 0|1    GAMG / SOR / ICC (one partition, option graph 1): the solve's entry
+ *                        launches — level-0 b, the first preconditioner application, w = A u,
+ *                        update 0 — captured in the numeric setup's graph (1; off while
+ *                        phase_times records the setup's end)
  *   "spec_post" 0|1      mfea_step, one partition, GAMG / SOR / ICC: the post kernels enqueued
  *                        behind the solve's planned batch, one host wait for both (1); a
  *                        batch that was not the last has its post's failures undone

@@ -270,6 +270,9 @@ struct mfea_handle {
   // step instead of two.  spec_on: this step may; spec_launched: enqueued
   // behind the last batch (undone by k_unfail when the solve goes on)
   int opt_spec_post = 1;
+  // the solve's entry launches (cg_init, first V-cycle, w, update 0) in the
+  // captured setup graph (option "setup_entry")
+  int opt_setup_entry = 1;
   bool spec_on = false;
   bool spec_launched = false;
   double spec_strain = 0.0;
@@ -1980,7 +1983,23 @@ uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
 // eager launches cost the host ≈ 5–8 µs each (kernel arguments of 1.5–3 KB),
 // more than the GPU spends on the deep levels' kernels; recaptured whenever
 // anything the launches read changes (the key hashes all of it)
-int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
+void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate);
+
+// The solve's entry behind the setup: level-0 b from the CG's r, the first
+// preconditioner application, w = A u, update 0 (solve_amg)
+void enqueue_amg_entry(mfea_handle* h, Part& pt) {
+  hipStream_t s = h->stream;
+  const int nd = pt.amg.nd;
+  const AmgLevD& L0 = pt.amg_lev[0];
+  launch_amg_cg_init(s, nd, L0, pt.amg_cg, cg_vecs(pt).r[0]);
+  launch_precond(h, pt, nullptr);
+  launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
+  launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
+}
+
+// entry: the solve's entry launches captured behind the setup (no phase
+// event between them): one graph, no graph → eager launch boundary
+int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = false) {
   hipStream_t s = h->stream;
   uint64_t k = 1469598103934665603ULL;
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
@@ -1993,6 +2012,13 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
   k = fnv1a(k, &pt.swd, sizeof pt.swd);
   k = fnv1a(k, ints, sizeof ints);
   k = fnv1a(k, &reg, sizeof reg);
+  if (entry) {
+    const CgVecs v = cg_vecs(pt);
+    const void* eptrs[4] = {v.r[0], pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr};
+    k = fnv1a(k, eptrs, sizeof eptrs);
+    k = fnv1a(k, &pt.amg_cg, sizeof pt.amg_cg);
+    k = fnv1a(k, &pt.amg_kind, sizeof pt.amg_kind);
+  }
   if (!h->graph_setup || h->graph_setup_key != k) {
     if (h->graph_setup) {
       HIPC(hipStreamSynchronize(s));  // no replay of the old graph in flight
@@ -2002,6 +2028,7 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg) {
     hipGraph_t g;
     HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue_amg_setup(h, pt, reg);
+    if (entry) enqueue_amg_entry(h, pt);
     HIPC(hipStreamEndCapture(s, &g));
     const hipError_t e = hipGraphInstantiate(&h->graph_setup, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
@@ -2036,15 +2063,15 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
                           pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   RC(phase_event(h, h->ev[2], s));
-  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg));
+  // (phase times: the setup's end is an event between the setup and the entry)
+  const bool entry = h->opt_graph && h->opt_setup_entry && !h->opt_phase_times;
+  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg, entry));
   else enqueue_amg_setup(h, pt, o->reg);
-  RC(phase_event(h, h->ev_setup, s));
-  h->ev_setup_used = true;
-  const AmgLevD& L0 = pt.amg_lev[0];
-  launch_amg_cg_init(s, nd, L0, pt.amg_cg, v.r[0]);
-  launch_precond(h, pt, nullptr);
-  launch_amg_cg_w(s, nd, 0, true, L0, pt.amg_cg, pt.slots.ptr, pt.cg_part.ptr);
-  launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
+  if (!entry) {
+    RC(phase_event(h, h->ev_setup, s));
+    h->ev_setup_used = true;
+    enqueue_amg_entry(h, pt);
+  }
   HIPC(hipGetLastError());
   const int tag = -1000 - (int)(pt.amg_gen % 1000000);
   const bool no_graph = !h->opt_graph;
@@ -3988,6 +4015,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "setup_entry") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "setup_entry: 0 or 1");
+    h->opt_setup_entry = (int)value;
+  }
   else if (n == "spec_post") {
     if (value != 0 && value != 1) return fail(MFEA_EINVAL, "spec_post: 0 or 1");
     h->opt_spec_post = (int)value;
@@ -4205,6 +4236,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "cc_tile") *value = h->opt_cc_tile;
   else if (n == "asm_kernel") *value = h->opt_asm_kernel;
   else if (n == "spec_post") *value = h->opt_spec_post;
+  else if (n == "setup_entry") *value = h->opt_setup_entry;
   else if (n == "asm_colours") {
     *value = 0;
     for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--values", nargs="+", type=int, default=[0, 2, 4])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--phase", type=int, default=1,
+                    help="0: no phase events (the bench's steps; wall time only, dev_ms 0)")
     ap.add_argument("--set", nargs="*", default=[], help="name=value options held fixed for every run")
     ap.add_argument("--chunk", type=int, nargs="*", default=[0],
                     help="solve chunk sizes to sweep as well (0: the engine's default)")
@@ -43,7 +45,7 @@ def main():
         xyz, e2n = synth.tiled_mesh(nx, ny, chords=cfg.startswith("C5"))
         top, bot = synth.grips(xyz)
         eng = Engine(0)
-        eng.set_option("phase_times", 1)  # (the t_*_ms phase split)
+        eng.set_option("phase_times", a.phase)  # (the t_*_ms phase split)
         for kv in a.set:
             k, v = kv.split("=")
             eng.set_option(k, int(v))

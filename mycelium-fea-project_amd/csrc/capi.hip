@@ -274,6 +274,7 @@ struct mfea_handle {
   // captured setup graph (option "setup_entry")
   int opt_setup_entry = 1;
   bool spec_on = false;
+  bool spec_used = false;  // one speculative post per step: behind the planned batch only
   bool spec_launched = false;
   double spec_strain = 0.0;
   hipEvent_t poll[2] = {};
@@ -405,6 +406,20 @@ int nranks(const mfea_handle* h) { return h->world > 1 ? h->world : (int)h->part
 
 // ticket set k (one per reducing kernel kind; see device_util.hpp layout)
 unsigned* tix(Part& pt, int k) { return pt.tickets.ptr + (size_t)k * kTicketStride; }
+// Host-facing copies and fills on the handle's stream, waited for.  The
+// stream is non-blocking: a null-stream hipMemcpy / hipMemset is not ordered
+// with it, so a fill of the activity could still be landing while the next
+// assembly read it (an intermittent breakdown after set_active(NULL), a
+// K assembled from a mix of the old and the new activity).
+hipError_t hmemcpy(mfea_handle* h, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+  const hipError_t e = hipMemcpyAsync(dst, src, n, k, h->stream);
+  return e == hipSuccess ? hipStreamSynchronize(h->stream) : e;
+}
+hipError_t hmemset(mfea_handle* h, void* dst, int v, size_t n) {
+  const hipError_t e = hipMemsetAsync(dst, v, n, h->stream);
+  return e == hipSuccess ? hipStreamSynchronize(h->stream) : e;
+}
+
 double* cg_part_buf(Part& pt, int par) { return pt.cg_part.ptr + (size_t)par * 4 * kCgMaxPartials; }
 
 void destroy_graph(mfea_handle* h) {
@@ -1570,7 +1585,7 @@ int current_active(mfea_handle* h, Part& pt) {
   if (h->act_host_ok && h->act_host.size() == (size_t)pt.P.n_elems) return 0;
   h->act_host.resize(pt.P.n_elems);
   if (pt.P.n_elems)
-    HIPC(hipMemcpy(h->act_host.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
+    HIPC(hmemcpy(h, h->act_host.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
   h->act_count = (int64_t)std::count(h->act_host.begin(), h->act_host.end(), (uint8_t)1);
   h->act_host_ok = true;
   return 0;
@@ -1752,7 +1767,7 @@ int ensure_amg(mfea_handle* h, Part& pt, bool* rebuilt, int kind = MFEA_PC_GAMG)
   std::vector<uint8_t> local;
   if (dm) {
     local.resize(pt.P.n_elems);
-    if (pt.P.n_elems) HIPC(hipMemcpy(local.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
+    if (pt.P.n_elems) HIPC(hmemcpy(h, local.data(), pt.active.ptr, pt.P.n_elems, hipMemcpyDeviceToHost));
   } else {
     RC(current_active(h, pt));
   }
@@ -2208,7 +2223,7 @@ int global_active(mfea_handle* h, std::vector<uint8_t>& key) {
     Part& pt = *pp;
     const int64_t E = pt.P.n_elems;
     std::vector<uint8_t> a(E);
-    if (E) HIPC(hipMemcpy(a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    if (E) HIPC(hmemcpy(h, a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
     for (int64_t le = 0; le < E; ++le)
       if (pt.plan.elem_own[le]) key[pt.plan.elem_g[le]] = a[le];
   }
@@ -2973,10 +2988,10 @@ int apply_failures(mfea_handle* h) {
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     unsigned c = 0;
-    HIPC(hipMemcpy(&c, pt.fail_cnt.ptr, sizeof c, hipMemcpyDeviceToHost));
+    HIPC(hmemcpy(h, &c, pt.fail_cnt.ptr, sizeof c, hipMemcpyDeviceToHost));
     if (c > (unsigned)pt.P.n_elems) return fail(MFEA_EINVAL, "internal: failed-element list overflow");
     std::vector<int32_t> l(c);
-    if (c) HIPC(hipMemcpy(l.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (c) HIPC(hmemcpy(h, l.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
     for (int32_t le : l) ids.push_back((int32_t)pt.plan.elem_g[le]);
   }
   if (h->world > 1) {
@@ -3023,7 +3038,7 @@ int local_failures(mfea_handle* h, Part& pt, unsigned c) {
   HostLap clk;
   if (c > (unsigned)pt.P.n_elems) return fail(MFEA_EINVAL, "internal: failed-element list overflow");
   std::vector<int32_t> ids(c);
-  HIPC(hipMemcpy(ids.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPC(hmemcpy(h, ids.data(), pt.fail_list.ptr, c * sizeof(int32_t), hipMemcpyDeviceToHost));
   HIPC(hipMemsetAsync(fail_counter(pt), 0, sizeof(unsigned), h->stream));
   if (!h->act_host_ok || h->act_host.size() != (size_t)pt.P.n_elems) return 0;
   for (int32_t e : ids) {
@@ -3069,13 +3084,16 @@ int enqueue_post(mfea_handle* h, double max_strain) {
   return 0;
 }
 
-// Speculative post (mfea_handle::spec_on), enqueued by the solve's batch end:
-// the solve's end event, then the post — after first undoing the failures a
-// post enqueued behind an earlier batch marked (that solve went on)
+// Speculative post (mfea_handle::spec_on), enqueued behind the solve's
+// planned batch: the solve's end event, then the post.  At any later batch
+// end the solve went on: that post's failures are undone and post runs after
+// the solve's wait as usual
 int spec_post(mfea_handle* h) {
   if (!h->spec_on) return 0;
-  Part& pt = part0(h);
-  if (h->spec_launched) launch_unfail(h->stream, pt.fail_list.ptr, fail_counter(pt), pt.active.ptr);
+  // a later batch end (the planned batch was not the last: SOR / ICC chunks,
+  // a first solve): undo, and let post run after the solve as usual
+  if (h->spec_used) return spec_undo(h);
+  h->spec_used = true;
   RC(phase_event(h, h->ev[3], h->stream));
   RC(enqueue_post(h, h->spec_strain));
   h->spec_launched = true;
@@ -3209,7 +3227,7 @@ int gather_active(mfea_handle* h, std::vector<uint8_t>& out) {
     Part& pt = *pp;
     const int64_t E = pt.P.n_elems;
     std::vector<uint8_t> a(E);
-    if (E) HIPC(hipMemcpy(a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    if (E) HIPC(hmemcpy(h, a.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
     if (!partitioned(h)) {
       out = a;
       return 0;
@@ -3362,10 +3380,10 @@ int mfea_set_active(mfea_handle* h, const uint8_t* active) {
       std::vector<uint8_t> a(E);
       for (int64_t le = 0; le < E; ++le)
         a[le] = active[partitioned(h) ? pt.plan.elem_g[le] : le] ? 1 : 0;
-      HIPC(hipMemcpy(pt.active.ptr, a.data(), E, hipMemcpyHostToDevice));
+      HIPC(hmemcpy(h, pt.active.ptr, a.data(), E, hipMemcpyHostToDevice));
       if (!partitioned(h)) h->act_host = std::move(a);
     } else {
-      HIPC(hipMemset(pt.active.ptr, 1, E));
+      HIPC(hmemset(h, pt.active.ptr, 1, E));
       if (!partitioned(h)) h->act_host.assign(E, 1);
     }
   }
@@ -3423,6 +3441,7 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   h->spec_on = fuse_rhs && h->opt_spec_post;
   h->spec_strain = max_strain;
   h->spec_launched = false;
+  h->spec_used = false;
   int rc = solve_any(h, dy_top, dy_bot, &o, st);
   h->spec_on = false;
   h->rhs_fused = false;
@@ -3452,7 +3471,7 @@ int mfea_get_displacement(mfea_handle* h, double* U) {
     const Pattern& P = pt.P;
     const int64_t N = P.n_nodes;
     std::vector<double> xp(3 * N);
-    if (N) HIPC(hipMemcpy(xp.data(), pt.x.ptr, 3 * N * sizeof(double), hipMemcpyDeviceToHost));
+    if (N) HIPC(hmemcpy(h, xp.data(), pt.x.ptr, 3 * N * sizeof(double), hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < N; ++i) {
       const int64_t ln = P.perm[i];
       if (dm && pt.plan.ghost[ln]) continue;
@@ -3472,11 +3491,11 @@ int mfea_get_stress(mfea_handle* h, double* stress) {
     const int64_t E = pt.P.n_elems;
     if (!E) continue;
     if (!partitioned(h)) {
-      HIPC(hipMemcpy(stress, pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, stress, pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
       continue;
     }
     std::vector<double> sl(E);
-    HIPC(hipMemcpy(sl.data(), pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
+    HIPC(hmemcpy(h, sl.data(), pt.stress.ptr, E * sizeof(double), hipMemcpyDeviceToHost));
     for (int64_t le = 0; le < E; ++le)
       if (pt.plan.elem_own[le]) stress[pt.plan.elem_g[le]] = sl[le];
   }
@@ -3492,11 +3511,11 @@ int mfea_get_active(mfea_handle* h, uint8_t* active) {
     const int64_t E = pt.P.n_elems;
     if (!E) continue;
     if (!partitioned(h)) {
-      HIPC(hipMemcpy(active, pt.active.ptr, E, hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, active, pt.active.ptr, E, hipMemcpyDeviceToHost));
       continue;
     }
     std::vector<uint8_t> al(E);
-    HIPC(hipMemcpy(al.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+    HIPC(hmemcpy(h, al.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
     for (int64_t le = 0; le < E; ++le)
       if (pt.plan.elem_own[le]) active[pt.plan.elem_g[le]] = al[le];
   }
@@ -3538,9 +3557,9 @@ int mfea_export_csr(mfea_handle* h, int64_t* nnz, int64_t* indptr, int32_t* indi
   const int64_t N = P.n_nodes, E = P.n_elems;
   std::vector<double> diag6(6 * N), val6(6 * pt.G);
   std::vector<uint8_t> act(E);
-  if (N) HIPC(hipMemcpy(diag6.data(), pt.diag.ptr, 6 * N * sizeof(double), hipMemcpyDeviceToHost));
-  if (pt.G) HIPC(hipMemcpy(val6.data(), pt.val.ptr, 6 * pt.G * sizeof(double), hipMemcpyDeviceToHost));
-  if (E) HIPC(hipMemcpy(act.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
+  if (N) HIPC(hmemcpy(h, diag6.data(), pt.diag.ptr, 6 * N * sizeof(double), hipMemcpyDeviceToHost));
+  if (pt.G) HIPC(hmemcpy(h, val6.data(), pt.val.ptr, 6 * pt.G * sizeof(double), hipMemcpyDeviceToHost));
+  if (E) HIPC(hmemcpy(h, act.data(), pt.active.ptr, E, hipMemcpyDeviceToHost));
   std::vector<int64_t> ip;
   std::vector<int32_t> ix;
   std::vector<double> dv;
@@ -3975,7 +3994,7 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
       for (auto& L : pp->amg_lev)
         if (L.PT.n > 0) L.compact = (int)value;
       if (!pp->amg_lev.empty() && pp->amg_levd.n >= pp->amg_lev.size())
-        HIPC(hipMemcpy(pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
+        HIPC(hmemcpy(h, pp->amg_levd.ptr, pp->amg_lev.data(), pp->amg_lev.size() * sizeof(AmgLevD),
                        hipMemcpyHostToDevice));
     }
   }
@@ -4076,7 +4095,7 @@ int mfea_debug_amg_vcycle(mfea_handle* h, const double* r, double* u) {
       const int64_t g = dm ? pt.plan.node_g[P.perm[i]] : P.perm[i];
       for (int a = 0; a < nd; ++a) b[3 * i + a] = r[nd * g + a];
     }
-    HIPC(hipMemcpy(pt.q.ptr, b.data(), b.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPC(hmemcpy(h, pt.q.ptr, b.data(), b.size() * sizeof(double), hipMemcpyHostToDevice));
     launch_amg_cg_init(s, nd, pt.amg_lev[0], pt.amg_cg, pt.q.ptr);
   }
   if (dm) {
@@ -4094,8 +4113,8 @@ int mfea_debug_amg_vcycle(mfea_handle* h, const double* r, double* u) {
     std::vector<float> uf((size_t)nd * cg.n);
     std::vector<int32_t> row0(cg.n);
     if (cg.n) {
-      HIPC(hipMemcpy(uf.data(), cg.u, uf.size() * sizeof(float), hipMemcpyDeviceToHost));
-      HIPC(hipMemcpy(row0.data(), cg.row0, row0.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, uf.data(), cg.u, uf.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, row0.data(), cg.row0, row0.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
     }
     for (int64_t i = cg.lo; i < cg.hi; ++i) {
       const int64_t lr = row0[i];
@@ -4129,30 +4148,30 @@ int mfea_debug_amg_vector(mfea_handle* h, int l, int which, double* out, int64_t
     std::vector<double> v((size_t)w * L.A.n, 0.0);
     if (which == 4) {  // D⁻¹ blocks
       std::vector<float> f(v.size());
-      HIPC(hipMemcpy(f.data(), d.dinv32, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, f.data(), d.dinv32, f.size() * sizeof(float), hipMemcpyDeviceToHost));
       for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
     } else if (which == 5) {  // the Gershgorin bound g, every row
       double om[2];
-      HIPC(hipMemcpy(om, d.omega, sizeof(om), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, om, d.omega, sizeof(om), hipMemcpyDeviceToHost));
       std::fill(v.begin(), v.end(), om[1]);
     } else if (which == 6) {  // diagonal blocks of A (slot 0 of every row)
       std::vector<float> a((size_t)nd * nd * d.A.npos);
-      HIPC(hipMemcpy(a.data(), d.A.val32, a.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, a.data(), d.A.val32, a.size() * sizeof(float), hipMemcpyDeviceToHost));
       for (int64_t i = 0; i < L.A.n; ++i)
         for (int c = 0; c < nd * nd; ++c) v[(size_t)nd * nd * i + c] = a[(size_t)nd * nd * L.A.pos(i, 0) + c];
     } else if (l == 0 && (which == 0 || which == 3)) {
       if (which == 0) {
-        HIPC(hipMemcpy(v.data(), pt.amg_cg.r, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+        HIPC(hmemcpy(h, v.data(), pt.amg_cg.r, v.size() * sizeof(double), hipMemcpyDeviceToHost));
       } else {
         std::vector<float> f(v.size());
-        HIPC(hipMemcpy(f.data(), pt.amg_cg.u, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+        HIPC(hmemcpy(h, f.data(), pt.amg_cg.u, f.size() * sizeof(float), hipMemcpyDeviceToHost));
         for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
       }
     } else {
       const float* src = which == 0 ? d.b : which == 1 ? d.x : which == 2 ? d.t : d.e;
       if (!src) return fail(MFEA_EINVAL, "no such vector on this level");
       std::vector<float> f(v.size());
-      HIPC(hipMemcpy(f.data(), src, f.size() * sizeof(float), hipMemcpyDeviceToHost));
+      HIPC(hmemcpy(h, f.data(), src, f.size() * sizeof(float), hipMemcpyDeviceToHost));
       for (size_t k = 0; k < f.size(); ++k) v[k] = f[k];
     }
     const bool split = dm && l < pl.n_dist;
@@ -4392,7 +4411,7 @@ int mfea_gather_results(mfea_handle* h, double* U, double* stress, uint8_t* acti
         pk.push_back(Al[e] ? 1.0 : 0.0);
       }
     HIPC(buf.alloc(pk.size() + 1));
-    HIPC(hipMemcpy(buf.ptr, pk.data(), pk.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPC(hmemcpy(h, buf.ptr, pk.data(), pk.size() * sizeof(double), hipMemcpyHostToDevice));
     NCCLC(ncclGroupStart());
     if (!pk.empty()) NCCLC(ncclSend(buf.ptr, pk.size(), ncclFloat64, 0, h->comm, s));
     NCCLC(ncclGroupEnd());
@@ -4405,7 +4424,7 @@ int mfea_gather_results(mfea_handle* h, double* U, double* stress, uint8_t* acti
   NCCLC(ncclGroupEnd());
   RC(sync_stream(h));
   std::vector<double> all(off[W]);
-  if (off[W]) HIPC(hipMemcpy(all.data(), buf.ptr, off[W] * sizeof(double), hipMemcpyDeviceToHost));
+  if (off[W]) HIPC(hmemcpy(h, all.data(), buf.ptr, off[W] * sizeof(double), hipMemcpyDeviceToHost));
   std::vector<int64_t> at(off.begin(), off.end() - 1);
   for (int64_t n = 0; n < N; ++n) {
     const int p = node_rank(n);

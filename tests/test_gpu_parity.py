@@ -226,6 +226,29 @@ def test_colour_assembly_steps_match_row_gather(engine):
     assert np.all(np.abs(out[0][0] - out[2][0]) <= 1e-8 * np.max(np.abs(out[0][0])))
 
 
+def test_set_active_is_ordered_with_the_next_assembly(engine):
+    """The activity's upload runs on the handle's (non-blocking) stream: a
+    null-stream fill could still be landing while the next assembly read it —
+    a K from a mix of two activities, once in ≈ 100 sequences (capi.hip
+    hmemcpy / hmemset).  The same K every time, the reference's bits."""
+    nodes, elems = load_mesh("sim_20251117_181147")
+    xyz, e2n = nodes[["x", "y", "z"]].values, elems[["n1", "n2"]].values
+    engine.set_mesh(xyz, e2n)
+    engine.set_bc([], [])
+    reduced = np.random.default_rng(11).random(len(e2n)) > 0.03
+    ref = None
+    for _ in range(40):
+        engine.set_active(reduced)
+        engine.assemble()
+        engine.set_active(None)
+        engine.assemble()
+        dv = engine.export_csr()[2]
+        ref = dv if ref is None else ref
+        assert np.array_equal(dv, ref)
+    K = fo.assemble_global_stiffness(xyz, e2n, np.ones(len(e2n), bool))
+    check_assembly(ref, K, xyz, e2n, np.ones(len(e2n), bool))
+
+
 def test_speculative_post_matches_waited_post(engine):
     """Option spec_post: the post behind the solve's planned batch.  A run
     whose tolerance alternates (the planned batch now too short — its post's

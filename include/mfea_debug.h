@@ -86,6 +86,13 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *                        launches — level-0 b, the first preconditioner application, w = A u,
  *                        update 0 — captured in the numeric setup's graph (1; off while
  *                        phase_times records the setup's end)
+ *   "step_graph" 0|1     mfea_step, one partition, GAMG / SOR / ICC, graphs on, no phase
+ *                        events, asm_kernel 0: the assembly with the fused RHS and the CG
+ *                        start at the head of the setup graph (0: measured slower — the
+ *                        eager assembly overlaps the host's plan checks)
+ *   "batch_graph" 0|1    mfea_step, one partition, GAMG / SOR / ICC, graphs on, no phase
+ *                        events: the solve's planned batch, its finish and the post as ONE
+ *                        captured graph of the batch's exact length (1)
  *   "spec_post" 0|1      mfea_step, one partition, GAMG / SOR / ICC: the post kernels enqueued
  *                        behind the solve's planned batch, one host wait for both (1); a
  *                        batch that was not the last has its post's failures undone

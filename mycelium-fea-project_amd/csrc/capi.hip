@@ -248,6 +248,12 @@ struct mfea_handle {
   static constexpr int kRemGraphs = 64;
   hipGraphExec_t graph_rem[kRemGraphs] = {};
   int graph_rem_ell = -1;
+  // mfea_step (option "batch_graph"): the planned batch as ONE graph of its
+  // exact length with the finish and the post kernels behind it, one graph
+  // per length, keyed by the plan and the failure strain
+  hipGraphExec_t graph_batch[kRemGraphs] = {};
+  int graph_batch_ell = -1;
+  double graph_batch_strain = 0.0;
   // GAMG: the numeric setup's launches (≈ 30) as one graph, keyed by a hash
   // of every argument they take (the level views, the level-0 operator, reg)
   hipGraphExec_t graph_setup = nullptr;
@@ -273,6 +279,18 @@ struct mfea_handle {
   // the solve's entry launches (cg_init, first V-cycle, w, update 0) in the
   // captured setup graph (option "setup_entry")
   int opt_setup_entry = 1;
+  // mfea_step, one partition, GAMG / SOR / ICC, graphs on, no phase events:
+  // the planned batch, the finish and the post as one captured graph
+  int opt_batch_graph = 1;
+  // mfea_step likewise: the assembly with the fused RHS and the CG start
+  // captured at the head of the setup graph, the grip displacements read from
+  // pinned h_red[14..15] by a copy node (option "step_graph").  Off: measured
+  // 13 µs slower per step at C2 and C3 (profiles/r6/ab_step_graph_wall.log) —
+  // an eager assembly runs while the host checks the plan and the setup
+  // graph's key; deferred, the GPU waits for that host work
+  int opt_step_graph = 0;
+  bool asm_pending = false;  // mfea_step deferred its assembly to solve_amg
+  DevBuf<double> d_dy;
   bool spec_on = false;
   bool spec_used = false;  // one speculative post per step: behind the planned batch only
   bool spec_launched = false;
@@ -433,6 +451,11 @@ void destroy_graph(mfea_handle* h) {
     g = nullptr;
   }
   h->graph_rem_ell = -1;
+  for (auto& g : h->graph_batch) {
+    if (g) (void)hipGraphExecDestroy(g);
+    g = nullptr;
+  }
+  h->graph_batch_ell = -1;
   h->graph = nullptr;
   h->graph_chunk = 0;
   h->graph_precond = -1;
@@ -1065,6 +1088,39 @@ int drive_sized(mfea_handle* h, int big, int small, int max_it, int expected, En
   RC(after());
   HIPC(hipEventRecord(h->poll[0], s));
   RC(wait_event(h, h->poll[0]));
+  while (!hs[0].done && done_its < (int64_t)max_it + 3 * small) {
+    RC(enqueue(small));
+    RC(after());
+    HIPC(hipEventRecord(h->poll[0], s));
+    RC(wait_event(h, h->poll[0]));
+    done_its += small;
+  }
+  RC(sync_stream(h));
+  *out = h->h_state[0];
+  if (!out->done) {
+    out->status = MFEA_EMAXIT;
+    out->iters = max_it;
+  }
+  return 0;
+}
+
+// mfea_step's planned batch as one graph (solve_amg, option batch_graph):
+// the batch's iterations, the finish and the post; the post counts as the
+// step's speculative post (mfea_handle::spec_used), so when the solve goes on
+// in small chunks their first batch end undoes its failures (spec_post)
+template <class Launch, class Enqueue, class After>
+int drive_batch(mfea_handle* h, int small, int max_it, int need, Launch&& launch, Enqueue&& enqueue,
+                SolveState* out, After&& after) {
+  hipStream_t s = h->stream;
+  volatile SolveState* hs = h->h_state;
+  hs[0].done = 0;
+  RC(launch());
+  h->spec_used = true;
+  h->spec_launched = true;
+  HIPC(hipEventRecord(h->ev[5], s));  // the post's read-back: the end of the batch
+  HIPC(hipEventRecord(h->poll[0], s));
+  RC(wait_event(h, h->poll[0]));
+  int64_t done_its = need;
   while (!hs[0].done && done_its < (int64_t)max_it + 3 * small) {
     RC(enqueue(small));
     RC(after());
@@ -1994,10 +2050,6 @@ uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
   return k;
 }
 
-// The numeric setup replayed as one captured graph (single partition): the
-// eager launches cost the host ≈ 5–8 µs each (kernel arguments of 1.5–3 KB),
-// more than the GPU spends on the deep levels' kernels; recaptured whenever
-// anything the launches read changes (the key hashes all of it)
 void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate);
 
 // The solve's entry behind the setup: level-0 b from the CG's r, the first
@@ -2012,9 +2064,37 @@ void enqueue_amg_entry(mfea_handle* h, Part& pt) {
   launch_amg_cg_update(s, nd, 0, L0, pt.amg_cg, pt.slots.ptr, pt.state.ptr, pt.cg_part.ptr);  // update 0
 }
 
-// entry: the solve's entry launches captured behind the setup (no phase
-// event between them): one graph, no graph → eager launch boundary
-int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = false) {
+// mfea_step's deferred assembly (option step_graph) at the head of the setup
+// graph: the grip displacements from pinned h_red[14..15] (a copy node, read
+// at replay), the row gather with the fused RHS reading them from d_dy, the
+// CG start — k_assemble<true> / k_cg_init_finalize exactly as eager
+void enqueue_step_head(mfea_handle* h, Part& pt, const mfea_solve_opts* o) {
+  hipStream_t s = h->stream;
+  const Pattern& P = pt.P;
+  (void)hipMemcpyAsync(h->d_dy.ptr, h->h_red + 14, 2 * sizeof(double), hipMemcpyHostToDevice, s);
+  AsmRhs q{};
+  q.code = pt.code.ptr;
+  q.dyp = h->d_dy.ptr;
+  q.nf = P.n_free;
+  q.r = pt.r.ptr;
+  q.x = pt.x.ptr;
+  q.partials = pt.partials.ptr;
+  q.ticket = tix(pt, 0);
+  q.red_out = pt.red.ptr;
+  launch_assemble(s, P.n_nodes, pt.xyz_d.ptr, pt.slice_ptr.ptr, pt.row_len.ptr, pt.s_col.ptr, pt.s_elem.ptr,
+                  pt.active.ptr, h->mat, pt.G, pt.val.ptr, pt.diag.ptr, &q);
+  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                          pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
+}
+
+// The numeric setup replayed as one captured graph (single partition): the
+// eager launches cost the host ≈ 5–8 µs each (kernel arguments of 1.5–3 KB),
+// more than the GPU spends on the deep levels' kernels; recaptured whenever
+// anything the launches read changes (the key hashes all of it).  entry: the
+// solve's entry launches captured behind the setup (no phase event between
+// them); head (non-null): mfea_step's assembly and CG start before it
+int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = false,
+                           const mfea_solve_opts* head = nullptr) {
   hipStream_t s = h->stream;
   uint64_t k = 1469598103934665603ULL;
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
@@ -2034,6 +2114,17 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
     k = fnv1a(k, &pt.amg_cg, sizeof pt.amg_cg);
     k = fnv1a(k, &pt.amg_kind, sizeof pt.amg_kind);
   }
+  if (head) {
+    const void* hptrs[10] = {pt.xyz_d.ptr, pt.s_elem.ptr, pt.active.ptr, pt.code.ptr, pt.r.ptr,
+                             pt.x.ptr, pt.partials.ptr, pt.red.ptr, h->d_dy.ptr, h->h_red};
+    k = fnv1a(k, hptrs, sizeof hptrs);
+    const double hd[3] = {head->rtol, head->atol, head->reg};
+    const int hi[2] = {head->norm, head->max_it};
+    k = fnv1a(k, hd, sizeof hd);
+    k = fnv1a(k, hi, sizeof hi);
+    k = fnv1a(k, &h->mat, sizeof h->mat);
+    k = fnv1a(k, &pt.tickets.ptr, sizeof pt.tickets.ptr);
+  }
   if (!h->graph_setup || h->graph_setup_key != k) {
     if (h->graph_setup) {
       HIPC(hipStreamSynchronize(s));  // no replay of the old graph in flight
@@ -2042,6 +2133,7 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
     }
     hipGraph_t g;
     HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    if (head) enqueue_step_head(h, pt, head);
     enqueue_amg_setup(h, pt, reg);
     if (entry) enqueue_amg_entry(h, pt);
     HIPC(hipStreamEndCapture(s, &g));
@@ -2056,6 +2148,8 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
 
 int spec_post(mfea_handle* h);
 int spec_undo(mfea_handle* h);
+int assemble_impl(mfea_handle* h, mfea_stats* st, const double* rhs_dy);
+int enqueue_post_work(mfea_handle* h, double max_strain);
 
 int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opts* o,
               mfea_stats* st) {
@@ -2069,18 +2163,27 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const SellOp op = sell_op(pt);
   const CgVecs v = cg_vecs(pt);
   const int nd = pt.amg.nd;
+  // mfea_step's deferred assembly: at the head of the setup graph, or now
+  const bool head = h->asm_pending && h->opt_graph && !h->opt_phase_times;
+  if (h->asm_pending) {
+    h->asm_pending = false;
+    if (head) HIPC(h->d_dy.alloc(2));
+    else RC(assemble_impl(h, nullptr, h->h_red + 14));
+  }
   RC(phase_event(h, h->ev[1], s));
-  // (mfea_step's assembly formed it for these displacements: AsmRhs)
-  const bool rhs_done = h->rhs_fused && h->rhs_dy[0] == dy_top && h->rhs_dy[1] == dy_bot;
-  h->rhs_fused = false;
-  if (!rhs_done)
-    launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
-  launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
-                          pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
+  if (!head) {
+    // (mfea_step's assembly formed it for these displacements: AsmRhs)
+    const bool rhs_done = h->rhs_fused && h->rhs_dy[0] == dy_top && h->rhs_dy[1] == dy_bot;
+    h->rhs_fused = false;
+    if (!rhs_done)
+      launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
+    launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                            pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
+  }
   RC(phase_event(h, h->ev[2], s));
   // (phase times: the setup's end is an event between the setup and the entry)
   const bool entry = h->opt_graph && h->opt_setup_entry && !h->opt_phase_times;
-  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg, entry));
+  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg, entry, head ? o : nullptr));
   else enqueue_amg_setup(h, pt, o->reg);
   if (!entry) {
     RC(phase_event(h, h->ev_setup, s));
@@ -2156,13 +2259,53 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
       }
       h->graph_rem_ell = tag;
     }
-    if (exact_rem && h->graph_rem[rem] == nullptr) RC(capture(&h->graph_rem[rem], rem));
-    rc = drive_sized(h, big, chunk, o->max_it, expected,
-                     [&](int n) -> int {
-                       HIPC(hipGraphLaunch(n == chunk ? h->graph : n == big ? h->graph_big : h->graph_rem[n], s));
-                       return 0;
-                     },
-                     &fin, finish, exact_rem);
+    // mfea_step: the planned batch, the finish and the post as ONE graph of
+    // the batch's exact length (option batch_graph; C2 / C3: two graph
+    // launches and four eager ones fewer per step)
+    const bool batch = h->spec_on && !h->spec_used && h->opt_batch_graph && !h->opt_phase_times &&
+                       o->chunk <= 0 && need < mfea_handle::kRemGraphs;
+    if (batch) {
+      if (h->graph_batch_ell != tag || h->graph_batch_strain != h->spec_strain) {
+        for (auto& g : h->graph_batch) {
+          if (g) (void)hipGraphExecDestroy(g);
+          g = nullptr;
+        }
+        h->graph_batch_ell = tag;
+        h->graph_batch_strain = h->spec_strain;
+      }
+      if (h->graph_batch[need] == nullptr) {
+        hipGraph_t g;
+        HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        enqueue_amg_chunk(h, pt, need);
+        launch_amg_finish(s, nd, pt.amg_cg, pt.x.ptr);
+        const int prc = enqueue_post_work(h, h->spec_strain);
+        const hipError_t ec = hipStreamEndCapture(s, &g);
+        RC(prc);
+        HIPC(ec);
+        hipError_t e = hipGraphInstantiate(&h->graph_batch[need], g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIPC(e);
+      }
+      rc = drive_batch(h, chunk, o->max_it, need,
+                       [&]() -> int {
+                         HIPC(hipGraphLaunch(h->graph_batch[need], s));
+                         return 0;
+                       },
+                       [&](int n) -> int {
+                         HIPC(hipGraphLaunch(h->graph, s));
+                         (void)n;
+                         return 0;
+                       },
+                       &fin, finish);
+    } else {
+      if (exact_rem && h->graph_rem[rem] == nullptr) RC(capture(&h->graph_rem[rem], rem));
+      rc = drive_sized(h, big, chunk, o->max_it, expected,
+                       [&](int n) -> int {
+                         HIPC(hipGraphLaunch(n == chunk ? h->graph : n == big ? h->graph_big : h->graph_rem[n], s));
+                         return 0;
+                       },
+                       &fin, finish, exact_rem);
+    }
   }
   if (rc) return rc;
   if (fin.status != 0) RC(spec_undo(h));
@@ -3053,10 +3196,18 @@ int local_failures(mfea_handle* h, Part& pt, unsigned c) {
 
 // the post kernels (reaction, stress / failures) and the read-back of their
 // sums into h_red, ev[5] behind them
+int enqueue_post_work(mfea_handle* h, double max_strain);
 int enqueue_post(mfea_handle* h, double max_strain) {
+  RC(phase_event(h, h->ev[4], h->stream));
+  RC(enqueue_post_work(h, max_strain));
+  HIPC(hipEventRecord(h->ev[5], h->stream));
+  return 0;
+}
+// the post's kernels and the read-back of their sums into the pinned h_red
+// (capturable: the batch graph holds them)
+int enqueue_post_work(mfea_handle* h, double max_strain) {
   hipStream_t s = h->stream;
   const bool dm = partitioned(h);
-  RC(phase_event(h, h->ev[4], s));
   for (auto& pp : h->parts) {
     Part& pt = *pp;
     const Pattern& P = pt.P;
@@ -3080,7 +3231,6 @@ int enqueue_post(mfea_handle* h, double max_strain) {
   } else {
     HIPC(hipMemcpyAsync(h->h_red, p0.red.ptr + 4, 3 * sizeof(double), hipMemcpyDeviceToHost, s));
   }
-  HIPC(hipEventRecord(h->ev[5], s));
   return 0;
 }
 
@@ -3434,7 +3584,18 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   const bool fuse_rhs = !partitioned(h) && (o.precond == MFEA_PC_GAMG || o.precond == MFEA_PC_SOR ||
                                             o.precond == MFEA_PC_ICC);
   const double dys[2] = {dy_top, dy_bot};
-  RC(assemble_impl(h, nullptr, fuse_rhs ? dys : nullptr));
+  // one partition, GAMG / SOR / ICC, graphs on, no phase events, the row
+  // gather: the assembly rides at the head of the solve's setup graph
+  const bool defer = fuse_rhs && h->opt_step_graph && h->opt_graph && !h->opt_phase_times && h->opt_asm_kernel == 0;
+  if (defer) {
+    h->h_red[14] = dy_top;
+    h->h_red[15] = dy_bot;
+    h->asm_pending = true;
+    h->assembled = true;
+    h->rhs_fused = false;
+  } else {
+    RC(assemble_impl(h, nullptr, fuse_rhs ? dys : nullptr));
+  }
   // a solver failure stops the step loop here, as the reference does
   // (src/fea_petsc.cpp:346-354)
   h->in_step = true;
@@ -3445,6 +3606,11 @@ int mfea_step(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   int rc = solve_any(h, dy_top, dy_bot, &o, st);
   h->spec_on = false;
   h->rhs_fused = false;
+  if (h->asm_pending) {  // (the solve ended before its assembly: never on success)
+    h->asm_pending = false;
+    if (rc == 0) rc = assemble_impl(h, nullptr);
+    else h->assembled = false;
+  }
   if (rc) (void)spec_undo(h);
   if (rc == 0) rc = post_impl(h, max_strain, total_force, n_active, st);
   h->in_step = false;
@@ -4034,6 +4200,14 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "step_graph") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "step_graph: 0 or 1");
+    h->opt_step_graph = (int)value;
+  }
+  else if (n == "batch_graph") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "batch_graph: 0 or 1");
+    h->opt_batch_graph = (int)value;
+  }
   else if (n == "setup_entry") {
     if (value != 0 && value != 1) return fail(MFEA_EINVAL, "setup_entry: 0 or 1");
     h->opt_setup_entry = (int)value;
@@ -4256,6 +4430,8 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "asm_kernel") *value = h->opt_asm_kernel;
   else if (n == "spec_post") *value = h->opt_spec_post;
   else if (n == "setup_entry") *value = h->opt_setup_entry;
+  else if (n == "batch_graph") *value = h->opt_batch_graph;
+  else if (n == "step_graph") *value = h->opt_step_graph;
   else if (n == "asm_colours") {
     *value = 0;
     for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);

@@ -234,6 +234,10 @@ __global__ __launch_bounds__(kBlock) void k_assemble(int64_t N, const double* __
                                                      double* __restrict__ diag, AsmRhs q) {
   const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if constexpr (RHS) {
+    if (q.dyp) {
+      q.dy_top = q.dyp[0];
+      q.dy_bot = q.dyp[1];
+    }
     double acc[2] = {0.0, 0.0};
     if (row < N) {
       double k3[3] = {0.0, 0.0, 0.0};

@@ -85,6 +85,7 @@ struct Material {
 struct AsmRhs {
   const uint8_t* code;
   double dy_top, dy_bot;
+  const double* dyp;  // non-null: (dy_top, dy_bot) from device memory (a captured step graph)
   int64_t nf;
   double* r;
   double* x;

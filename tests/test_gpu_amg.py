@@ -579,3 +579,25 @@ def test_coarse_overrelaxation_fallback(engine):
         assert engine.get_option("amg_safe_omega") == 1
         assert rel(engine.displacement(), sysz["U"]) <= 1e-10
     assert engine.get_option("amg_safe_omega") == 0  # a new weight, a new chance
+
+
+@pytest.mark.parametrize("precond", ["gamg", "icc"])
+def test_setup_entry_in_the_graph_is_bitwise_the_eager_entry(engine, precond):
+    """Option setup_entry: the solve's entry launches (level-0 b, the first
+    preconditioner application, w, update 0) replayed inside the setup's
+    graph give the eager launches' iterates bit for bit, step after step."""
+    from mfea import PC_GAMG, PC_ICC, make_opts
+    _sim181147(engine)
+    pc = PC_GAMG if precond == "gamg" else PC_ICC
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    runs = []
+    for entry in (0, 1):
+        engine.set_option("setup_entry", entry)
+        engine.set_active(None)
+        out = []
+        for k in (1, 2, 3):
+            f, n, st = engine.step(k * dy, -k * dy, make_opts(rtol=1e-10, max_it=20000, precond=pc), 0.018)
+            out.append((f, st.iters, engine.displacement().copy()))
+        runs.append(out)
+    for a, b in zip(*runs):
+        assert a[0] == b[0] and a[1] == b[1] and np.array_equal(a[2], b[2])

@@ -250,7 +250,8 @@ def test_set_active_is_ordered_with_the_next_assembly(engine):
 
 
 def test_speculative_post_matches_waited_post(engine):
-    """Option spec_post: the post behind the solve's planned batch.  A run
+    """Options spec_post / batch_graph: the post behind the solve's planned
+    batch (eager, or captured with the batch in one graph).  A run
     whose tolerance alternates (the planned batch now too short — its post's
     failures undone, the solve goes on — now too long) gives the same forces,
     activity and stresses, bit for bit, as the post after the solve's wait."""
@@ -259,8 +260,11 @@ def test_speculative_post_matches_waited_post(engine):
     xyz = nodes[["x", "y", "z"]].values
     top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
     runs = []
-    for spec in (0, 1):
+    # batch: the batch + post as one graph; head: the assembly in the setup graph
+    for spec, batch, head in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)):
         engine.set_option("spec_post", spec)
+        engine.set_option("batch_graph", batch)
+        engine.set_option("step_graph", head)
         engine.set_mesh(xyz, elems[["n1", "n2"]].values)
         engine.set_bc(top, bot)
         engine.set_active(None)
@@ -272,9 +276,10 @@ def test_speculative_post_matches_waited_post(engine):
             rec.append((f, n, st.iters, engine.stress().copy(), engine.active().copy()))
         runs.append(rec)
     assert sum(r[1] < runs[0][0][1] for r in runs[0]) > 0  # elements failed
-    for a, b in zip(*runs):
-        assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
-        assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
+            assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4])
 
 
 # ---------------------------------------------------------------------------

@@ -42,9 +42,9 @@ struct HostLap {
     if (!on) return;
     const auto now = std::chrono::steady_clock::now();
     if (n >= 0)
-      std::fprintf(stderr, "  host %-26s %8.2f ms  (%lld)\n", what, std::chrono::duration<double, std::milli>(now - t).count(), (long long)n);
+      std::fprintf(stderr, "  host %-26s %8.3f ms  (%lld)\n", what, std::chrono::duration<double, std::milli>(now - t).count(), (long long)n);
     else
-      std::fprintf(stderr, "  host %-26s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+      std::fprintf(stderr, "  host %-26s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
     t = now;
   }
 };
@@ -289,6 +289,7 @@ struct mfea_handle {
   // an eager assembly runs while the host checks the plan and the setup
   // graph's key; deferred, the GPU waits for that host work
   int opt_step_graph = 0;
+  int opt_graph_start = 1;  // the CG start (k_cg_init_finalize) at the setup graph's head
   bool asm_pending = false;  // mfea_step deferred its assembly to solve_amg
   DevBuf<double> d_dy;
   bool spec_on = false;
@@ -2044,9 +2045,18 @@ void enqueue_amg_setup(mfea_handle* h, Part& pt, double reg) {
   if (pt.amg_mg.on && !merged_done) launch_amg_merge_setup(s, nd, pt.amg_lev.data(), pt.amg_mg);
 }
 
+// FNV-1a over 8-byte words (then the tail bytes): the setup graph's key is
+// hashed on every solve while the GPU runs the assembly, over ≈ 10 KB of level
+// views — byte by byte that host work outlasted C2's assembly
 uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
   const unsigned char* b = static_cast<const unsigned char*>(p);
-  for (size_t i = 0; i < n; ++i) k = (k ^ b[i]) * 1099511628211ULL;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, b + i, 8);
+    k = (k ^ w) * 1099511628211ULL;
+  }
+  for (; i < n; ++i) k = (k ^ b[i]) * 1099511628211ULL;
   return k;
 }
 
@@ -2094,7 +2104,7 @@ void enqueue_step_head(mfea_handle* h, Part& pt, const mfea_solve_opts* o) {
 // solve's entry launches captured behind the setup (no phase event between
 // them); head (non-null): mfea_step's assembly and CG start before it
 int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = false,
-                           const mfea_solve_opts* head = nullptr) {
+                           const mfea_solve_opts* head = nullptr, const mfea_solve_opts* start = nullptr) {
   hipStream_t s = h->stream;
   uint64_t k = 1469598103934665603ULL;
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
@@ -2113,6 +2123,14 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
     k = fnv1a(k, eptrs, sizeof eptrs);
     k = fnv1a(k, &pt.amg_cg, sizeof pt.amg_cg);
     k = fnv1a(k, &pt.amg_kind, sizeof pt.amg_kind);
+  }
+  if (start) {  // the CG start (k_cg_init_finalize) at the graph's head
+    const double sd[3] = {start->rtol, start->atol, start->reg};
+    const int si[2] = {start->norm, start->max_it};
+    const void* sp[3] = {pt.red.ptr, pt.state.ptr, pt.cg_part.ptr};
+    k = fnv1a(k ^ 0x5a5a, sd, sizeof sd);
+    k = fnv1a(k, si, sizeof si);
+    k = fnv1a(k, sp, sizeof sp);
   }
   if (head) {
     const void* hptrs[10] = {pt.xyz_d.ptr, pt.s_elem.ptr, pt.active.ptr, pt.code.ptr, pt.r.ptr,
@@ -2134,6 +2152,9 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
     hipGraph_t g;
     HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     if (head) enqueue_step_head(h, pt, head);
+    if (start)
+      launch_cg_init_finalize(s, pt.red.ptr, start->rtol, start->atol, start->norm, start->max_it, start->reg,
+                              pt.state.ptr, pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
     enqueue_amg_setup(h, pt, reg);
     if (entry) enqueue_amg_entry(h, pt);
     HIPC(hipStreamEndCapture(s, &g));
@@ -2171,20 +2192,25 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     else RC(assemble_impl(h, nullptr, h->h_red + 14));
   }
   RC(phase_event(h, h->ev[1], s));
+  // the CG start inside the setup graph when no phase event separates them
+  const bool start_in_graph = h->opt_graph && h->opt_graph_start && !h->opt_phase_times && !head;
   if (!head) {
     // (mfea_step's assembly formed it for these displacements: AsmRhs)
     const bool rhs_done = h->rhs_fused && h->rhs_dy[0] == dy_top && h->rhs_dy[1] == dy_bot;
     h->rhs_fused = false;
     if (!rhs_done)
       launch_cg_rhs(s, op, pt.code.ptr, dy_top, dy_bot, o->reg, 2, v, pt.partials.ptr, tix(pt, 0), pt.red.ptr);
-    launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
-                            pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
+    if (!start_in_graph)
+      launch_cg_init_finalize(s, pt.red.ptr, o->rtol, o->atol, o->norm, o->max_it, o->reg, pt.state.ptr,
+                              pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
   }
   RC(phase_event(h, h->ev[2], s));
   // (phase times: the setup's end is an event between the setup and the entry)
   const bool entry = h->opt_graph && h->opt_setup_entry && !h->opt_phase_times;
-  if (h->opt_graph) RC(launch_amg_setup_graph(h, pt, o->reg, entry, head ? o : nullptr));
+  if (h->opt_graph)
+    RC(launch_amg_setup_graph(h, pt, o->reg, entry, head ? o : nullptr, start_in_graph ? o : nullptr));
   else enqueue_amg_setup(h, pt, o->reg);
+  clk.lap("to the setup graph");
   if (!entry) {
     RC(phase_event(h, h->ev_setup, s));
     h->ev_setup_used = true;
@@ -4200,6 +4226,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "graph_start") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "graph_start: 0 or 1");
+    h->opt_graph_start = (int)value;
+  }
   else if (n == "step_graph") {
     if (value != 0 && value != 1) return fail(MFEA_EINVAL, "step_graph: 0 or 1");
     h->opt_step_graph = (int)value;
@@ -4432,6 +4462,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "setup_entry") *value = h->opt_setup_entry;
   else if (n == "batch_graph") *value = h->opt_batch_graph;
   else if (n == "step_graph") *value = h->opt_step_graph;
+  else if (n == "graph_start") *value = h->opt_graph_start;
   else if (n == "asm_colours") {
     *value = 0;
     for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);

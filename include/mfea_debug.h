@@ -86,6 +86,8 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *                        launches — level-0 b, the first preconditioner application, w = A u,
  *                        update 0 — captured in the numeric setup's graph (1; off while
  *                        phase_times records the setup's end)
+ *   "combo_graph" 0|1    with batch_graph: the batch, finish and post behind the numeric
+ *                        setup in the setup's graph — one graph launch per step (1)
  *   "graph_start" 0|1    GAMG / SOR / ICC, graphs on, no phase events: the CG start
  *                        (k_cg_init_finalize) at the head of the setup graph (1)
  *   "step_graph" 0|1     mfea_step, one partition, GAMG / SOR / ICC, graphs on, no phase

@@ -252,6 +252,10 @@ struct mfea_handle {
   // exact length with the finish and the post kernels behind it, one graph
   // per length, keyed by the plan and the failure strain
   hipGraphExec_t graph_batch[kRemGraphs] = {};
+  // ... and (option "combo_graph") behind the numeric setup in the setup's
+  // graph: one graph launch per step, one cached graph per batch length
+  hipGraphExec_t graph_combo[kRemGraphs] = {};
+  uint64_t graph_combo_key[kRemGraphs] = {};
   int graph_batch_ell = -1;
   double graph_batch_strain = 0.0;
   // GAMG: the numeric setup's launches (≈ 30) as one graph, keyed by a hash
@@ -289,7 +293,8 @@ struct mfea_handle {
   // an eager assembly runs while the host checks the plan and the setup
   // graph's key; deferred, the GPU waits for that host work
   int opt_step_graph = 0;
-  int opt_graph_start = 1;  // the CG start (k_cg_init_finalize) at the setup graph's head
+  int opt_graph_start = 1;
+  int opt_combo_graph = 0;  // the CG start (k_cg_init_finalize) at the setup graph's head
   bool asm_pending = false;  // mfea_step deferred its assembly to solve_amg
   DevBuf<double> d_dy;
   bool spec_on = false;
@@ -457,6 +462,8 @@ void destroy_graph(mfea_handle* h) {
     g = nullptr;
   }
   h->graph_batch_ell = -1;
+  // (not the combined graphs: one may be in flight when the solve recaptures
+  // its chunk graphs; their keys replace them, mfea_destroy frees them)
   h->graph = nullptr;
   h->graph_chunk = 0;
   h->graph_precond = -1;
@@ -1111,10 +1118,10 @@ int drive_sized(mfea_handle* h, int big, int small, int max_it, int expected, En
 // in small chunks their first batch end undoes its failures (spec_post)
 template <class Launch, class Enqueue, class After>
 int drive_batch(mfea_handle* h, int small, int max_it, int need, Launch&& launch, Enqueue&& enqueue,
-                SolveState* out, After&& after) {
+                SolveState* out, After&& after, bool launched = false) {
   hipStream_t s = h->stream;
   volatile SolveState* hs = h->h_state;
-  hs[0].done = 0;
+  if (!launched) hs[0].done = 0;
   RC(launch());
   h->spec_used = true;
   h->spec_launched = true;
@@ -2061,6 +2068,7 @@ uint64_t fnv1a(uint64_t k, const void* p, size_t n) {
 }
 
 void launch_precond(mfea_handle* h, Part& pt, const int32_t* gate);
+int enqueue_post_work(mfea_handle* h, double max_strain);
 
 // The solve's entry behind the setup: level-0 b from the CG's r, the first
 // preconditioner application, w = A u, update 0 (solve_amg)
@@ -2104,7 +2112,8 @@ void enqueue_step_head(mfea_handle* h, Part& pt, const mfea_solve_opts* o) {
 // solve's entry launches captured behind the setup (no phase event between
 // them); head (non-null): mfea_step's assembly and CG start before it
 int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = false,
-                           const mfea_solve_opts* head = nullptr, const mfea_solve_opts* start = nullptr) {
+                           const mfea_solve_opts* head = nullptr, const mfea_solve_opts* start = nullptr,
+                           int tail = 0, int tag = 0) {
   hipStream_t s = h->stream;
   uint64_t k = 1469598103934665603ULL;
   k = fnv1a(k, pt.amg_lev.data(), pt.amg_lev.size() * sizeof(AmgLevD));
@@ -2142,6 +2151,41 @@ int launch_amg_setup_graph(mfea_handle* h, Part& pt, double reg, bool entry = fa
     k = fnv1a(k, hi, sizeof hi);
     k = fnv1a(k, &h->mat, sizeof h->mat);
     k = fnv1a(k, &pt.tickets.ptr, sizeof pt.tickets.ptr);
+  }
+  if (tail > 0) {
+    // the step's whole GPU work but the assembly: setup, entry, the planned
+    // batch of `tail` iterations, the finish, the post (mfea_step, batch_graph)
+    k = fnv1a(k ^ 0xc0b0, &tail, sizeof tail);
+    k = fnv1a(k, &tag, sizeof tag);
+    k = fnv1a(k, &h->spec_strain, sizeof h->spec_strain);
+    hipGraphExec_t& gc = h->graph_combo[tail];
+    if (!gc || h->graph_combo_key[tail] != k) {
+      if (gc) {
+        HIPC(hipStreamSynchronize(s));
+        (void)hipGraphExecDestroy(gc);
+        gc = nullptr;
+      }
+      hipGraph_t g;
+      HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      if (head) enqueue_step_head(h, pt, head);
+      if (start)
+        launch_cg_init_finalize(s, pt.red.ptr, start->rtol, start->atol, start->norm, start->max_it, start->reg,
+                                pt.state.ptr, pt.cg_part.ptr, 2 * 4 * kCgMaxPartials);
+      enqueue_amg_setup(h, pt, reg);
+      enqueue_amg_entry(h, pt);
+      enqueue_amg_chunk(h, pt, tail);
+      launch_amg_finish(s, pt.amg.nd, pt.amg_cg, pt.x.ptr);
+      const int prc = enqueue_post_work(h, h->spec_strain);
+      const hipError_t ec = hipStreamEndCapture(s, &g);
+      RC(prc);
+      HIPC(ec);
+      const hipError_t e = hipGraphInstantiate(&gc, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPC(e);
+      h->graph_combo_key[tail] = k;
+    }
+    HIPC(hipGraphLaunch(gc, s));
+    return 0;
   }
   if (!h->graph_setup || h->graph_setup_key != k) {
     if (h->graph_setup) {
@@ -2207,8 +2251,24 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
   RC(phase_event(h, h->ev[2], s));
   // (phase times: the setup's end is an event between the setup and the entry)
   const bool entry = h->opt_graph && h->opt_setup_entry && !h->opt_phase_times;
+  const int tag = -1000 - (int)(pt.amg_gen % 1000000);
+  // the converging update is iteration `iters`; update 0 ran in the entry, so
+  // `expected` more updates = expected / chunk chunks (drive_planned adds one
+  // for the update it assumes the chunk starts with: pass expected − 1)
+  const int expected = std::max(0, std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16) - 1);
+  const int need = std::max(1, expected + 1);
+  // mfea_step: the planned batch, the finish and the post as ONE graph of the
+  // batch's exact length (option batch_graph), behind the setup in the same
+  // graph (option combo_graph)
+  const bool batch = h->spec_on && !h->spec_used && h->opt_batch_graph && !h->opt_phase_times &&
+                     o->chunk <= 0 && need < mfea_handle::kRemGraphs && h->opt_graph;
+  const bool combo = batch && entry && h->opt_combo_graph;
+  // (combo: the graph reaches the batch's end and publishes the state; the
+  // host's copy of the flag is cleared before it can)
+  if (combo) h->h_state[0].done = 0;
   if (h->opt_graph)
-    RC(launch_amg_setup_graph(h, pt, o->reg, entry, head ? o : nullptr, start_in_graph ? o : nullptr));
+    RC(launch_amg_setup_graph(h, pt, o->reg, entry, head ? o : nullptr, start_in_graph ? o : nullptr,
+                              combo ? need : 0, tag));
   else enqueue_amg_setup(h, pt, o->reg);
   clk.lap("to the setup graph");
   if (!entry) {
@@ -2217,12 +2277,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     enqueue_amg_entry(h, pt);
   }
   HIPC(hipGetLastError());
-  const int tag = -1000 - (int)(pt.amg_gen % 1000000);
   const bool no_graph = !h->opt_graph;
-  // the converging update is iteration `iters`; update 0 ran above, so
-  // `expected` more updates = expected / chunk chunks (drive_planned adds one
-  // for the update it assumes the chunk starts with: pass expected − 1)
-  const int expected = std::max(0, std::min(o->max_it, pt.amg_last_iters > 0 ? pt.amg_last_iters : 16) - 1);
   SolveState fin;
   int rc;
   const auto drive_t0 = std::chrono::steady_clock::now();
@@ -2275,7 +2330,6 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
     // depends on the chunk's parity): an odd iteration count no longer runs
     // one gated iteration — which costs as much as a live one — nor two
     // extra chunk boundaries (C3 at 15 iterations: 8 + 7 instead of 8 + 4×2)
-    const int need = std::max(1, expected + 1);
     const int rem = big > chunk ? need - (need / big) * big : 0;
     const bool exact_rem = rem > 0 && rem != chunk && rem < mfea_handle::kRemGraphs;
     if (h->graph_rem_ell != tag) {  // another plan: the cached lengths hold its pointers
@@ -2285,11 +2339,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
       }
       h->graph_rem_ell = tag;
     }
-    // mfea_step: the planned batch, the finish and the post as ONE graph of
-    // the batch's exact length (option batch_graph; C2 / C3: two graph
-    // launches and four eager ones fewer per step)
-    const bool batch = h->spec_on && !h->spec_used && h->opt_batch_graph && !h->opt_phase_times &&
-                       o->chunk <= 0 && need < mfea_handle::kRemGraphs;
+    // (batch_graph: C2 / C3 two graph launches and four eager ones fewer per step)
     if (batch) {
       if (h->graph_batch_ell != tag || h->graph_batch_strain != h->spec_strain) {
         for (auto& g : h->graph_batch) {
@@ -2299,7 +2349,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
         h->graph_batch_ell = tag;
         h->graph_batch_strain = h->spec_strain;
       }
-      if (h->graph_batch[need] == nullptr) {
+      if (!combo && h->graph_batch[need] == nullptr) {
         hipGraph_t g;
         HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         enqueue_amg_chunk(h, pt, need);
@@ -2314,7 +2364,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
       }
       rc = drive_batch(h, chunk, o->max_it, need,
                        [&]() -> int {
-                         HIPC(hipGraphLaunch(h->graph_batch[need], s));
+                         if (!combo) HIPC(hipGraphLaunch(h->graph_batch[need], s));  // (combo: launched with the setup)
                          return 0;
                        },
                        [&](int n) -> int {
@@ -2322,7 +2372,7 @@ int solve_amg(mfea_handle* h, double dy_top, double dy_bot, const mfea_solve_opt
                          (void)n;
                          return 0;
                        },
-                       &fin, finish);
+                       &fin, finish, combo);
     } else {
       if (exact_rem && h->graph_rem[rem] == nullptr) RC(capture(&h->graph_rem[rem], rem));
       rc = drive_sized(h, big, chunk, o->max_it, expected,
@@ -3459,6 +3509,8 @@ int mfea_destroy(mfea_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   destroy_graph(h);
   if (h->graph_setup) (void)hipGraphExecDestroy(h->graph_setup);
+  for (auto& g : h->graph_combo)
+    if (g) (void)hipGraphExecDestroy(g);
   h->parts.clear();
   if (h->comm) (void)ncclCommDestroy(h->comm);
   for (auto& ev : h->ev)
@@ -4226,6 +4278,10 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     for (auto& pp : h->parts) pp->amg_dist.zero_w = value && h->world > 1 ? h->world : 0;
     destroy_graph(h);  // captured chunks hold the old exchange
   }
+  else if (n == "combo_graph") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "combo_graph: 0 or 1");
+    h->opt_combo_graph = (int)value;
+  }
   else if (n == "graph_start") {
     if (value != 0 && value != 1) return fail(MFEA_EINVAL, "graph_start: 0 or 1");
     h->opt_graph_start = (int)value;
@@ -4463,6 +4519,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "batch_graph") *value = h->opt_batch_graph;
   else if (n == "step_graph") *value = h->opt_step_graph;
   else if (n == "graph_start") *value = h->opt_graph_start;
+  else if (n == "combo_graph") *value = h->opt_combo_graph;
   else if (n == "asm_colours") {
     *value = 0;
     for (auto& pp : h->parts) *value = std::max<int64_t>(*value, pp->ec_state > 0 ? pp->ec.colors : 0);

@@ -261,10 +261,12 @@ def test_speculative_post_matches_waited_post(engine):
     top, bot = fo.grip_nodes(xyz, nodes["node_id"].values, 1.5)
     runs = []
     # batch: the batch + post as one graph; head: the assembly in the setup graph
-    for spec, batch, head in ((0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 1, 1)):
+    # combo: the batch and the post behind the setup in one graph
+    for spec, batch, head, combo in ((0, 0, 0, 0), (1, 0, 0, 0), (1, 1, 0, 0), (1, 1, 0, 1), (1, 1, 1, 1)):
         engine.set_option("spec_post", spec)
         engine.set_option("batch_graph", batch)
         engine.set_option("step_graph", head)
+        engine.set_option("combo_graph", combo)
         engine.set_mesh(xyz, elems[["n1", "n2"]].values)
         engine.set_bc(top, bot)
         engine.set_active(None)

@@ -293,8 +293,9 @@ struct mfea_handle {
   // an eager assembly runs while the host checks the plan and the setup
   // graph's key; deferred, the GPU waits for that host work
   int opt_step_graph = 0;
-  int opt_graph_start = 1;
-  int opt_combo_graph = 0;  // the CG start (k_cg_init_finalize) at the setup graph's head
+  int opt_graph_start = 1;  // the CG start (k_cg_init_finalize) at the setup graph's head
+  // with batch_graph: the batch, finish and post behind the setup in one graph
+  int opt_combo_graph = 0;
   bool asm_pending = false;  // mfea_step deferred its assembly to solve_amg
   DevBuf<double> d_dy;
   bool spec_on = false;

@@ -295,7 +295,7 @@ struct mfea_handle {
   int opt_step_graph = 0;
   int opt_graph_start = 1;  // the CG start (k_cg_init_finalize) at the setup graph's head
   // with batch_graph: the batch, finish and post behind the setup in one graph
-  int opt_combo_graph = 0;
+  int opt_combo_graph = 1;
   bool asm_pending = false;  // mfea_step deferred its assembly to solve_amg
   DevBuf<double> d_dy;
   bool spec_on = false;

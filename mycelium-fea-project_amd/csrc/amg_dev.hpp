@@ -229,18 +229,22 @@ __device__ __forceinline__ void sell_step(const int32_t* __restrict__ col, const
                                           int64_t base, int k, int ws, int sub, XP x, C* y) {
   int32_t c[U];
   int64_t q[U];
+  C m[U][ND * ND], xc[U][ND];
+  // the slots' values need only the position: issued with the columns, so
+  // the gathers' wait (vmcnt counts in order) leaves them in flight and the
+  // dependent round trip carries the gathers alone
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     q[u] = k + u < ws ? base + (int64_t)((k + u) * S + sub) * 64 : base;
     c[u] = k + u < ws ? col[q[u]] : -1;
   }
-  C m[U][ND * ND], xc[U][ND];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if constexpr (SYM) bload_sym<ND>(val, 0, q[u], m[u]);
     else bload<ND>(val, 0, q[u], m[u]);
-    vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u) vload<ND>(x, c[u] >= 0 ? c[u] : 0, xc[u]);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
 #pragma unroll

@@ -343,8 +343,10 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   int k;
   if (!slot_wave(P, P.rg.p0 / 64, P.rg.p1 / 64, q, i, k, blk)) return;
   if (i < P.rg.lo || i >= P.rg.hi) return;
+  // the list bounds and D⁻¹ need no column: issued with it (one round trip
+  // fewer ahead of the list's gathers)
   const int32_t J = P.col[q];
-  if (J < 0) return;
+  const int t0 = L.pv_ptr[q], t1 = L.pv_ptr[q + 1];
   double S[ND * ND], pm[ND * ND], Di[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) {
@@ -352,7 +354,8 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
     pm[c] = 0.0;
     Di[c] = L.dinv32[i * (ND * ND) + c];
   }
-  list_sum<ND>(L.pv_ptr[q], L.pv_ptr[q + 1], L.pv_a, L.A.val32, L.A.npos, S);
+  if (J < 0) return;
+  list_sum<ND>(t0, t1, L.pv_a, L.A.val32, L.A.npos, S);
   mm_acc<ND>(Di, S, pm);
   const double om = amg_omega(L.omega);
 #pragma unroll
@@ -394,17 +397,26 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
     bstore<ND>(L.R.val32, L.R.npos, qr, t);
   }
   const int64_t q = L.AP.rg.p0 + k;
-  if (q >= L.AP.rg.p1 || L.AP.col[q] < 0 || !pos_mine(L.AP.rg, q)) return;
+  if (q >= L.AP.rg.p1) return;
+  // the column (padding test), the list bounds and P̃'s operand indices in
+  // one round trip
+  const int32_t jc = L.AP.col[q];
+  const int t0 = L.ap_ptr[q], t1 = L.ap_ptr[q + 1];
+  int32_t qp = -1;
+  int64_t r = 0;
+  if constexpr (PTV) {
+    qp = L.pt_p[q];
+    r = 64 * (int64_t)L.PT.srow[q >> 6] + (q & 63);  // the A·P / P̃ row
+  }
+  if (jc < 0 || !pos_mine(L.AP.rg, q)) return;
   double C[ND * ND], Di[ND * ND], pm[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = pm[c] = 0.0;
   if constexpr (PTV) {
-    const int64_t r = 64 * (int64_t)L.PT.srow[q >> 6] + (q & 63);  // the A·P / P̃ row
     dinv_load<ND>(L.dinv32, L.pt_row[r], Di);
-    const int32_t qp = L.pt_p[q];
     if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
   }
-  pair_sum<ND, false>(L.ap_ptr[q], L.ap_ptr[q + 1], L.ap_a, L.ap_b, L.A.val32, L.A.npos, L.P.val32, L.P.npos, C);
+  pair_sum<ND, false>(t0, t1, L.ap_a, L.ap_b, L.A.val32, L.A.npos, L.P.val32, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
   if constexpr (PTV) {
     // from the stored (f32) A·P block, as k_amg_ptv forms it: the same bits
@@ -435,12 +447,13 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& T = L.PT;
   int64_t q, i;
   int k;
-  if (!slot_wave(T, T.rg.p0 / 64, T.rg.p1 / 64, q, i, k, blk) || i >= T.n || T.col[q] < 0 || !pos_mine(T.rg, q))
-    return;
-  const int32_t qp = L.pt_p[q];
+  if (!slot_wave(T, T.rg.p0 / 64, T.rg.p1 / 64, q, i, k, blk) || i >= T.n) return;
+  const int32_t jc = T.col[q];  // (with the operands' indices: one round trip)
+  const int32_t qp = L.pt_p[q], qa = L.pt_ap[q], ir = L.pt_row[i];
+  if (jc < 0 || !pos_mine(T.rg, q)) return;
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
-  dinv_load<ND>(L.dinv32, L.pt_row[i], Di);
-  bload<ND>(L.apval, 0, L.pt_ap[q], ap);
+  dinv_load<ND>(L.dinv32, ir, Di);
+  bload<ND>(L.apval, 0, qa, ap);
   if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
   else {
 #pragma unroll
@@ -470,10 +483,11 @@ __device__ __forceinline__ void rtv_body(const AmgLevD& L, const AmgLevD& N, int
   int k;
   if (!slot_wave(T, T.rg.p0 / 64, T.rg.p1 / 64, q, J, k, blk) || J >= T.n || !pos_mine(T.rg, q)) return;
   const int32_t i = T.col[q];
+  const int32_t qt = L.rt_pt[q], jr = L.rt_row[J];  // (with the column: one round trip)
   if (i < 0) return;
   double p[ND * ND], Dn[ND * ND], D[ND * ND], t[ND * ND], u[ND * ND], o[ND * ND];
-  bload<ND>(L.PT.val32, 0, L.rt_pt[q], p);
-  dinv_load<ND>(N.dinv32, L.rt_row[J], Dn);
+  bload<ND>(L.PT.val32, 0, qt, p);
+  dinv_load<ND>(N.dinv32, jr, Dn);
   bload<ND>(L.A.val32, 0, (int64_t)L.A.sptr[i >> 6] * 64 + (i & 63), D);
   const double sc = (N.coarsest ? 1.0 : amg_omega(N.omega)) / amg_omega(L.omega);
 #pragma unroll
@@ -499,11 +513,12 @@ __device__ __forceinline__ void atv_body(const AmgLevD& L, int64_t blk) {
   const AmgMatD& A = L.A;
   int64_t q, i;
   int k;
-  if (!slot_wave(A, A.rg.p0 / 64, A.rg.p1 / 64, q, i, k, blk) || i >= A.n || A.col[q] < 0 || !pos_mine(A.rg, q))
-    return;
+  if (!slot_wave(A, A.rg.p0 / 64, A.rg.p1 / 64, q, i, k, blk) || i >= A.n) return;
   double Di[ND * ND], m[ND * ND], o[ND * ND];
+  const int32_t jc = A.col[q];  // (the operands need no column: one round trip)
   dinv_load<ND>(L.dinv32, i, Di);
   bload<ND>(A.val32, 0, q, m);
+  if (jc < 0 || !pos_mine(A.rg, q)) return;
   const double om = amg_omega(L.omega);
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) o[c] = 0.0;
@@ -536,11 +551,13 @@ __device__ __forceinline__ void fmm_acc(const float* A, const float* B, float* C
 template <int ND>
 __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restrict__ vnext, int64_t blk) {
   const int64_t q = blk * kBlock + threadIdx.x;
-  if (q >= L.CT.npos || L.CT.col[q] < 0) return;
+  if (q >= L.CT.npos) return;
+  const int32_t jc = L.CT.col[q];
+  const int t0 = L.ct_ptr[q], t1 = L.ct_ptr[q + 1];  // (with the column: one round trip)
+  if (jc < 0) return;
   float C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
-  const int t0 = L.ct_ptr[q], t1 = L.ct_ptr[q + 1];
   constexpr int U = 4;  // items in flight (list order kept: the same sums)
   for (int t = t0; t < t1; t += U) {
     int32_t a[U], b[U];
@@ -572,9 +589,14 @@ __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restric
 template <int ND>
 __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
   const int64_t q = blk * kBlock + threadIdx.x;
-  if (q >= L.CV.npos || L.CV.col[q] < 0) return;
-  float C[ND * ND];
+  if (q >= L.CV.npos) return;
+  // the column, the list bounds and the extra term's index in one round trip
+  const int32_t jc = L.CV.col[q];
+  const int t0 = L.cv_ptr[q], t1 = L.cv_ptr[q + 1];
   const int32_t ea = L.cv_ext[q];
+  const int32_t dg = L.cv_diag[q];
+  if (jc < 0) return;
+  float C[ND * ND];
   if (ea >= 0) {
     bload<ND>(L.A.at32, 0, ea, C);
 #pragma unroll
@@ -583,11 +605,10 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
   }
-  if (L.cv_diag[q]) {
+  if (dg) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) C[a * ND + a] += 2.0f;
   }
-  const int t0 = L.cv_ptr[q], t1 = L.cv_ptr[q + 1];
   constexpr int U = 4;  // items in flight (list order kept: the same sums)
   for (int t = t0; t < t1; t += U) {
     int32_t a[U], b[U];
@@ -624,18 +645,21 @@ __device__ __forceinline__ void mprod_body(const AmgMergeD& m, const float* __re
   const bool dq = xb < gdq;
   const AmgMatD& M = dq ? m.DQ : m.U;
   const int64_t q = (dq ? xb : xb - gdq) * kBlock + threadIdx.x;
-  if (q >= M.npos || M.col[q] < 0) return;
+  if (q >= M.npos) return;
   const bool c1 = dq && q < m.dq_split;
   const int32_t* ext = dq ? m.dq_ext : m.u_ext;
   const int32_t* lp = dq ? m.dq_ptr : m.u_ptr;
   const int32_t* la = dq ? m.dq_a : m.u_a;
   const int32_t* lb = dq ? m.dq_b : m.u_b;
+  const int32_t jc = M.col[q];
+  const int t0 = lp[q], t1 = lp[q + 1];  // (with the column: one round trip)
+  const int32_t e = ext[q];
+  if (jc < 0) return;
   const float* X = dq ? (c1 ? at1 : r1) : p0;
   const float* Y = dq ? r0 : p1;
   float S[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) S[c] = 0.0f;
-  const int t0 = lp[q], t1 = lp[q + 1];
   constexpr int U = 4;
   for (int t = t0; t < t1; t += U) {
     int32_t a[U], b[U];
@@ -658,7 +682,6 @@ __device__ __forceinline__ void mprod_body(const AmgMergeD& m, const float* __re
     }
   }
   float C[ND * ND];
-  const int32_t e = ext[q];
   if (e >= 0) {
     bload<ND>(dq ? r0 : p0, 0, e, C);
     const float f = dq ? 2.0f : 1.0f;
@@ -725,11 +748,13 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
   const int64_t q = L.ac_rg.p0 + t / S;
   const int sub = (int)(t % S);
   // (the S lanes of a block share q: they leave together)
-  if (q >= L.ac_rg.p1 || Ac.col[q] < 0 || !pos_mine(L.ac_rg, q)) return;
+  if (q >= L.ac_rg.p1) return;
+  const int32_t jc = Ac.col[q];
+  const int t0 = L.ac_ptr[q], t1 = L.ac_ptr[q + 1];  // (with the column: one round trip)
+  if (jc < 0 || !pos_mine(L.ac_rg, q)) return;
   double C[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = 0.0;
-  const int t0 = L.ac_ptr[q], t1 = L.ac_ptr[q + 1];
   constexpr int U = 4;
   for (int k = t0 + sub; k < t1; k += U * S) {  // U of this lane's pairs in flight
     int32_t ia[U], ib[U];

@@ -2093,6 +2093,8 @@ void enqueue_step_head(mfea_handle* h, Part& pt, const mfea_solve_opts* o) {
   (void)hipMemcpyAsync(h->d_dy.ptr, h->h_red + 14, 2 * sizeof(double), hipMemcpyHostToDevice, s);
   AsmRhs q{};
   q.code = pt.code.ptr;
+  q.top_end = P.n_free + P.n_top;
+  q.bot_end = P.n_nodes - P.n_ghost;
   q.dyp = h->d_dy.ptr;
   q.nf = P.n_free;
   q.r = pt.r.ptr;
@@ -3172,6 +3174,8 @@ int assemble_impl(mfea_handle* h, mfea_stats* st, const double* rhs_dy = nullptr
     const bool rhs = rhs_dy && h->parts.size() == 1;  // (rhs_dy: a one-partition GAMG / SOR / ICC step)
     if (rhs) {
       q.code = pt.code.ptr;
+      q.top_end = P.n_free + P.n_top;
+      q.bot_end = P.n_nodes - P.n_ghost;
       q.dy_top = rhs_dy[0];
       q.dy_bot = rhs_dy[1];
       q.nf = P.n_free;

@@ -84,21 +84,32 @@ __device__ __forceinline__ void assemble_row(int64_t N, int64_t row, const doubl
   // batch instead of two per slot; the sums stay in slot order
   constexpr int U = 4;
   for (int k0 = 0; k0 < len; k0 += U) {
+    // every load unconditional (a slot past the row's end re-reads its
+    // batch's first slot, k0 < len), the masks applied after: a guarded or
+    // selected load made hipcc branch per slot and wait vmcnt(0) in each
+    // branch — the batch's gathers had run one slot at a time
     int64_t idx[U];
     int32_t e[U], j[U];
+    bool ok[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = k0 + u < len;
-      idx[u] = base + (int64_t)(ok ? k0 + u : k0) * 64;
-      e[u] = ok ? s_elem[idx[u]] : 0;
-      j[u] = ok ? s_col[idx[u]] : (int32_t)row;
+      ok[u] = k0 + u < len;
+      idx[u] = base + (int64_t)(ok[u] ? k0 + u : k0) * 64;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      e[u] = s_elem[idx[u]];
+      j[u] = s_col[idx[u]];
     }
     uint8_t act[U], cd[U];
     double pj[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      act[u] = k0 + u < len ? active[e[u]] : 0;
-      cd[u] = rhs && k0 + u < len && j[u] >= q->nf ? q->code[j[u]] : 3;
+      const uint8_t av = active[e[u]];
+      act[u] = ok[u] ? av : 0;
+      // the neighbour's class from its row position (no load: a select on a
+      // loaded code made codegen branch around the load and wait in it)
+      cd[u] = rhs && ok[u] && j[u] >= q->nf ? (j[u] < q->top_end ? 1 : j[u] < q->bot_end ? 2 : 3) : 3;
 #pragma unroll
       for (int a = 0; a < 3; ++a) pj[u][a] = xyz[3 * (int64_t)j[u] + a];
     }

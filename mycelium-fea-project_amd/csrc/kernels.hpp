@@ -86,6 +86,9 @@ struct AsmRhs {
   const uint8_t* code;
   double dy_top, dy_bot;
   const double* dyp;  // non-null: (dy_top, dy_bot) from device memory (a captured step graph)
+  // row classes by position (symbolic.hpp Pattern): top grip rows
+  // [nf, top_end), bottom rows [top_end, bot_end), ghost rows after
+  int64_t top_end, bot_end;
   int64_t nf;
   double* r;
   double* x;

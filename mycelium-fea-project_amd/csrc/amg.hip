@@ -414,7 +414,10 @@ __device__ __forceinline__ void ap_body(const AmgLevD& L, int64_t blk) {
   for (int c = 0; c < ND * ND; ++c) C[c] = pm[c] = 0.0;
   if constexpr (PTV) {
     dinv_load<ND>(L.dinv32, L.pt_row[r], Di);
-    if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
+    // (unconditional load, masked: a guarded one made codegen branch and wait)
+    bload<ND>(L.P.val32, 0, qp >= 0 ? qp : 0, pm);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) pm[c] = keep_or_zero(pm[c], qp >= 0);
   }
   pair_sum<ND, false>(t0, t1, L.ap_a, L.ap_b, L.A.val32, L.A.npos, L.P.val32, L.P.npos, C);
   bstore<ND>(L.apval, L.AP.npos, q, C);
@@ -454,11 +457,9 @@ __device__ __forceinline__ void ptv_body(const AmgLevD& L, int64_t blk) {
   double Di[ND * ND], ap[ND * ND], pm[ND * ND], m[ND * ND];
   dinv_load<ND>(L.dinv32, ir, Di);
   bload<ND>(L.apval, 0, qa, ap);
-  if (qp >= 0) bload<ND>(L.P.val32, 0, qp, pm);
-  else {
+  bload<ND>(L.P.val32, 0, qp >= 0 ? qp : 0, pm);  // (unconditional, masked)
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
-  }
+  for (int c = 0; c < ND * ND; ++c) pm[c] = keep_or_zero(pm[c], qp >= 0);
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
   mm_acc<ND>(Di, ap, m);
@@ -597,14 +598,9 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
   const int32_t dg = L.cv_diag[q];
   if (jc < 0) return;
   float C[ND * ND];
-  if (ea >= 0) {
-    bload<ND>(L.A.at32, 0, ea, C);
+  bload<ND>(L.A.at32, 0, ea >= 0 ? ea : 0, C);  // (unconditional, masked)
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] = -C[c];
-  } else {
-#pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
-  }
+  for (int c = 0; c < ND * ND; ++c) C[c] = keep_or_zero(-C[c], ea >= 0);
   if (dg) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) C[a * ND + a] += 2.0f;
@@ -682,14 +678,11 @@ __device__ __forceinline__ void mprod_body(const AmgMergeD& m, const float* __re
     }
   }
   float C[ND * ND];
-  if (e >= 0) {
-    bload<ND>(dq ? r0 : p0, 0, e, C);
+  bload<ND>(dq ? r0 : p0, 0, e >= 0 ? e : 0, C);  // (unconditional, masked)
+  {
     const float f = dq ? 2.0f : 1.0f;
 #pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] *= f;
-  } else {
-#pragma unroll
-    for (int c = 0; c < ND * ND; ++c) C[c] = 0.0f;
+    for (int c = 0; c < ND * ND; ++c) C[c] = keep_or_zero(C[c] * f, e >= 0);
   }
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) C[c] = c1 ? C[c] - S[c] : C[c] + S[c];

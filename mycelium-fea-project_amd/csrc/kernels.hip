@@ -542,10 +542,25 @@ __global__ __launch_bounds__(kBlock) void k_reaction(int64_t row0, int64_t nrows
     const int len = row_len[row];
     double fy = diag[N + row] * u[3 * row] + diag[3 * N + row] * u[3 * row + 1] +
                 diag[4 * N + row] * u[3 * row + 2];
-    for (int k = 0; k < len; ++k) {
-      const int64_t idx = base + (int64_t)k * 64;
-      const int64_t c = s_col[idx];
-      fy += val[G + idx] * u[3 * c] + val[3 * G + idx] * u[3 * c + 1] + val[4 * G + idx] * u[3 * c + 2];
+    // slots in batches of four, each batch's columns and values issued before
+    // its gathers (one latency chain per batch, not per slot); the padding
+    // lanes of a batch re-read slot k0 and add nothing.  Terms in slot order.
+    constexpr int U = 4;
+    for (int k0 = 0; k0 < len; k0 += U) {
+      int64_t idx[U], c[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        idx[q] = base + (int64_t)(k0 + q < len ? k0 + q : k0) * 64;
+        c[q] = s_col[idx[q]];
+      }
+      double t[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        t[q] = val[G + idx[q]] * u[3 * c[q]] + val[3 * G + idx[q]] * u[3 * c[q] + 1] +
+               val[4 * G + idx[q]] * u[3 * c[q] + 2];
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        if (k0 + q < len) fy += t[q];
     }
     f[0] = fy;
   }

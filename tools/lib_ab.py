@@ -37,18 +37,20 @@ def child(cfg, steps):
     eng.set_bc(top, bot)
     eng.set_active(None)
     eng.step(dy, -dy, opts, fs.MAX_STRAIN)
-    dev, wall = [], []
+    dev, wall, post = [], [], []
     for _ in range(steps):
         eng.set_active(None)
         t = time.perf_counter()
-        _, _, st = eng.step(dy, -dy, opts, fs.MAX_STRAIN)
+        f, _, st = eng.step(dy, -dy, opts, fs.MAX_STRAIN)
         wall.append(1e3 * (time.perf_counter() - t))
         dev.append(st.t_assemble_ms + st.t_rhs_ms + st.t_solve_ms + st.t_post_ms)
+        post.append(st.t_post_ms)
     it_us = 1e3 * eng.profile_iteration(PC_GAMG, reps=30)
     spmv_us = 1e3 * eng.profile_spmv(reps=100)
     U = eng.displacement()
     print(json.dumps({"iters": st.iters, "relres": st.relres, "setup_ms": st.t_setup_ms,
                       "dev_ms_med": float(np.median(dev)), "wall_ms_med": float(np.median(wall)),
+                      "post_ms_med": float(np.median(post)), "force": float(f),
                       "iter_us": round(it_us, 2), "spmv_us": round(spmv_us, 2),
                       "U_md5": hashlib.md5(np.ascontiguousarray(U).tobytes()).hexdigest()[:12]}))
     eng.close()

@@ -121,6 +121,56 @@ __global__ __launch_bounds__(kBlock) void k_amg_dinv(AmgLevD L) {
   }
 }
 
+// Level 0's off-diagonal blocks of a row, slots k0 … k0+U−1 (A_ij = Σ of the
+// listed SELL slots' K_ij, list order), each handed to blk(q, m): the lists'
+// bounds, their first entries and those entries' values are each issued for
+// the U slots together — three dependent round trips per batch, where a slot
+// by slot walk took two per slot.  A list's further entries (two nodes joined
+// by more than one element) are walked after.  Padding and slots past the row
+// (empty lists) load what slot k0 / list entry 0 hold and are skipped.
+template <int ND, int U, class Blk>
+__device__ __forceinline__ void a0_slots(const SellOp& sop, const int32_t* __restrict__ ptr,
+                                         const int32_t* __restrict__ lst, int64_t base, int k0, int w,
+                                         Blk&& blk) {
+  int32_t t0[U], t1[U], g[U];
+  int64_t q[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    q[u] = base + (int64_t)(k0 + u < w ? k0 + u : k0) * 64;
+    t0[u] = ptr[q[u]];
+    t1[u] = ptr[q[u] + 1];
+  }
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    ok[u] = k0 + u < w && t0[u] < t1[u];
+    g[u] = lst[ok[u] ? t0[u] : 0];
+  }
+  double v6[U][6];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v6[u][c] = sop.val[(int64_t)c * sop.G + g[u]];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    double m[ND * ND], e[ND * ND];
+    sym_to<ND>(v6[u], e);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) m[c] = 0.0 + e[c];
+    for (int t = t0[u] + 1; t < t1[u]; ++t) {
+      double w6[6];
+      const int64_t gs = lst[t];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) w6[c] = sop.val[(int64_t)c * sop.G + gs];
+      sym_to<ND>(w6, e);
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+    }
+    blk(q[u], m);
+  }
+}
+
 // Level 0 in one row-wise pass (one launch where a0 and a level-0 D⁻¹ were two):
 // per row i, the diagonal K_ii + reg·I from the assembled diagonal, its exact
 // inverse, every off-diagonal block (Σ of the listed SELL slots' K_ij = −S_e,
@@ -171,34 +221,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
           for (int b = 0; b < ND; ++b) rs[a] += fabs(pm[a * ND + b]);
         }
       }
-      constexpr int U = 4;  // slots whose lists are in flight together
-      for (int k0 = 1; k0 < w; k0 += U) {
-        int32_t t0[U], t1[U];
-        int64_t q[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          q[u] = base + (int64_t)(k0 + u < w ? k0 + u : k0) * 64;
-          t0[u] = k0 + u < w ? ptr[q[u]] : 0;
-          t1[u] = k0 + u < w ? ptr[q[u] + 1] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (t0[u] == t1[u]) continue;  // padding (or past the row)
-          double m[ND * ND];
-#pragma unroll
-          for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
-          for (int t = t0[u]; t < t1[u]; ++t) {
-            double v6[6], e[ND * ND];
-            const int64_t gs = lst[t];
-#pragma unroll
-            for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
-            sym_to<ND>(v6, e);
-#pragma unroll
-            for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
-          }
-          bstore<ND>(A.val32, A.npos, q[u], m);
-          bstore_sym<ND>(A.sym, A.npos, q[u], m);
-          if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q[u], m);
+      for (int k0 = 1; k0 < w; k0 += 4)
+        a0_slots<ND, 4>(sop, ptr, lst, base, k0, w, [&](int64_t q, const double* m) {
+          bstore<ND>(A.val32, A.npos, q, m);
+          bstore_sym<ND>(A.sym, A.npos, q, m);
+          if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q, m);
           double pm[ND * ND];
 #pragma unroll
           for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
@@ -207,8 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
           for (int a = 0; a < ND; ++a)
 #pragma unroll
             for (int b = 0; b < ND; ++b) rs[a] += fabs(pm[a * ND + b]);
-        }
-      }
+        });
 #pragma unroll
       for (int a = 0; a < ND; ++a) g = fmax(g, rs[a]);
     }
@@ -273,37 +299,13 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0full(AmgLevD L, SellOp sop, co
     bstore<ND>(A.at32, 0, q, o);
   };
   if (A.at32) at_store(base, D);
-  constexpr int U = 4;
-  for (int k0 = 1; k0 < w; k0 += U) {
-    int32_t t0[U], t1[U];
-    int64_t q[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = base + (int64_t)(k0 + u < w ? k0 + u : k0) * 64;
-      t0[u] = k0 + u < w ? ptr[q[u]] : 0;
-      t1[u] = k0 + u < w ? ptr[q[u] + 1] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t0[u] == t1[u]) continue;  // padding (or past the row)
-      double m[ND * ND];
-#pragma unroll
-      for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
-      for (int t = t0[u]; t < t1[u]; ++t) {
-        double v6[6], e[ND * ND];
-        const int64_t gs = lst[t];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
-        sym_to<ND>(v6, e);
-#pragma unroll
-        for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
-      }
-      bstore<ND>(A.val32, A.npos, q[u], m);
-      bstore_sym<ND>(A.sym, A.npos, q[u], m);
-      if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q[u], m);
-      if (A.at32) at_store(q[u], m);
-    }
-  }
+  for (int k0 = 1; k0 < w; k0 += 4)
+    a0_slots<ND, 4>(sop, ptr, lst, base, k0, w, [&](int64_t q, const double* m) {
+      bstore<ND>(A.val32, A.npos, q, m);
+      bstore_sym<ND>(A.sym, A.npos, q, m);
+      if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q, m);
+      if (A.at32) at_store(q, m);
+    });
   const AmgMatD& P = L.P;
   if (L.coarsest || P.wmax <= 0 || i < P.rg.lo || i >= P.rg.hi) return;
   int64_t pb;

@@ -345,10 +345,13 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   int k;
   if (!slot_wave(P, P.rg.p0 / 64, P.rg.p1 / 64, q, i, k, blk)) return;
   if (i < P.rg.lo || i >= P.rg.hi) return;
-  // the list bounds and D⁻¹ need no column: issued with it (one round trip
-  // fewer ahead of the list's gathers)
+  // the list bounds, D⁻¹ and the row's aggregate / floating flag need no
+  // column: issued with it (one round trip fewer ahead of the list's gathers,
+  // none after them)
   const int32_t J = P.col[q];
   const int t0 = L.pv_ptr[q], t1 = L.pv_ptr[q + 1];
+  const int32_t ai = L.agg[i];
+  const bool floating = L.fmask && L.fmask[i];
   double S[ND * ND], pm[ND * ND], Di[ND * ND];
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) {
@@ -362,11 +365,11 @@ __device__ __forceinline__ void pvals_body(const AmgLevD& L, int64_t blk) {
   const double om = amg_omega(L.omega);
 #pragma unroll
   for (int c = 0; c < ND * ND; ++c) pm[c] = -om * pm[c];
-  if (J == L.agg[i]) {
+  if (J == ai) {
 #pragma unroll
     for (int a = 0; a < ND; ++a) pm[a * ND + a] += 1.0;
   }
-  if (L.fmask && L.fmask[i]) {  // a floating row: no coarse correction reaches it
+  if (floating) {  // a floating row: no coarse correction reaches it
 #pragma unroll
     for (int c = 0; c < ND * ND; ++c) pm[c] = 0.0;
   }
@@ -576,15 +579,18 @@ __device__ __forceinline__ void tv_body(const AmgLevD& L, const float* __restric
       bload<ND>(L.RT.val32, 0, b[u], r[u]);
       bload<ND>(vnext ? vnext : L.RT.val32, 0, a[u] >= 0 ? a[u] : 0, v[u]);  // (no V below: a < 0, a dummy read)
     }
+    // unconditional sums (guarded ones let codegen sink each item's loads into
+    // its branch: one item's round trips after another): past the list r = 0,
+    // and a < 0 (R̂'s block alone) multiplies by the identity — exact, the
+    // same sums
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
-      if (a[u] < 0) {
 #pragma unroll
-        for (int c = 0; c < ND * ND; ++c) C[c] += r[u][c];
-      } else {
-        fmm_acc<ND>(v[u], r[u], C);
+      for (int c = 0; c < ND * ND; ++c) {
+        r[u][c] = keep_or_zero(r[u][c], t + u < t1);
+        v[u][c] = keep_or_zero(v[u][c], a[u] >= 0) + (a[u] < 0 && c % (ND + 1) == 0 ? 1.0f : 0.0f);
       }
+      fmm_acc<ND>(v[u], r[u], C);
     }
   }
   bstore<ND>(L.CT.val32, 0, q, C);
@@ -623,8 +629,9 @@ __device__ __forceinline__ void vv_body(const AmgLevD& L, int64_t blk) {
       bload<ND>(L.CT.val32, 0, b[u], tb[u]);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
+    for (int u = 0; u < U; ++u) {  // (past the list: exact zeros, as tv_body)
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) p[u][c] = keep_or_zero(p[u][c], t + u < t1);
       fmm_acc<ND>(p[u], tb[u], C);
     }
   }
@@ -674,8 +681,9 @@ __device__ __forceinline__ void mprod_body(const AmgMergeD& m, const float* __re
       bload<ND>(Y, 0, b[u], y[u]);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
+    for (int u = 0; u < U; ++u) {  // (past the list: exact zeros, as tv_body)
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) x[u][c] = keep_or_zero(x[u][c], t + u < t1);
       fmm_acc<ND>(x[u], y[u], S);
     }
   }
@@ -766,8 +774,11 @@ __device__ __forceinline__ void ac_body(const AmgLevD& L, const AmgMatD& Ac, int
       bload<ND>(L.apval, 0, ib[u], y[u]);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (k + u * S < t1) mtm_acc<ND>(x[u], y[u], C);
+    for (int u = 0; u < U; ++u) {  // (past the list: exact zeros, as pair_sum_u)
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) x[u][c] = keep_or_zero(x[u][c], k + u * S < t1);
+      mtm_acc<ND>(x[u], y[u], C);
+    }
   }
   if constexpr (S > 1) {
 #pragma unroll

@@ -365,9 +365,13 @@ __device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __rest
       bload<ND>(X, 0, ia[u], x[u]);
       bload<ND>(Y, 0, ib[u], y[u]);
     }
+    // the pairs past the list (they re-read pair t0) add exact zeros: a
+    // guarded sum let codegen sink each pair's loads into its branch — one
+    // pair's index and block round trips after another instead of U at once
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) x[u][c] = keep_or_zero(x[u][c], t + u < t1);
       if (TX) mtm_acc<ND>(x[u], y[u], C);
       else mm_acc<ND>(x[u], y[u], C);
     }
@@ -392,11 +396,9 @@ __device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __rest
 #pragma unroll
     for (int u = 0; u < U; ++u) bload<ND>(X, 0, ia[u], x[u]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (t + u >= t1) break;
+    for (int u = 0; u < U; ++u)  // (past the list: exact zeros, as pair_sum_u)
 #pragma unroll
-      for (int c = 0; c < ND * ND; ++c) S[c] += x[u][c];
-    }
+      for (int c = 0; c < ND * ND; ++c) S[c] += keep_or_zero(x[u][c], t + u < t1);
   }
 }
 template <int ND, class TX_>

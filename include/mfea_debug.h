@@ -86,6 +86,9 @@ int mfea_debug_floating(mfea_handle* h, uint8_t* out);
  *                        launches — level-0 b, the first preconditioner application, w = A u,
  *                        update 0 — captured in the numeric setup's graph (1; off while
  *                        phase_times records the setup's end)
+ *   "amg_a0_slot" 0|1    GAMG at a fixed level-0 ω without the fused P_0 / Ã_0 pass: level
+ *                        0's blocks and D⁻¹ one thread per SELL position (1) instead of
+ *                        one per row (0); the same bits
  *   "combo_graph" 0|1    with batch_graph: the batch, finish and post behind the numeric
  *                        setup in the setup's graph — one graph launch per step (1)
  *   "graph_start" 0|1    GAMG / SOR / ICC, graphs on, no phase events: the CG start

@@ -251,6 +251,62 @@ __global__ __launch_bounds__(kBlock) void k_amg_a0dinv(AmgLevD L, SellOp sop, co
   }
 }
 
+// Level 0 at a fixed ω without the P / Ã part (k_amg_a0full): no Gershgorin
+// bound to gather per row, so one thread per SELL position (slot_wave) — a
+// row's blocks are formed side by side, three dependent round trips (list
+// bounds, list entry, values) for every block where k_amg_a0dinv's row
+// thread walked its slots four at a time.  Slot 0 (the diagonal, wave-
+// uniform) also writes the row's D⁻¹.  The blocks and D⁻¹ are k_amg_a0dinv's
+// bit for bit.
+template <int ND>
+__global__ __launch_bounds__(kBlock) void k_amg_a0slot(AmgLevD L, SellOp sop, const int32_t* __restrict__ row0,
+                                                       const int32_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ lst, double reg) {
+  const AmgMatD& A = L.A;
+  int64_t q, i;
+  int k;
+  if (!slot_wave(A, A.rg.p0 / 64, A.rg.p1 / 64, q, i, k, xcd_block()) || i >= A.n) return;
+  if (i < A.rg.lo || i >= A.rg.hi) return;
+  if (k == 0) {
+    double s6[6], D[ND * ND], Di[ND * ND];
+    const int64_t r = row0[i];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s6[c] = sop.diag[(int64_t)c * sop.N + r];
+    s6[0] += reg;
+    s6[3] += reg;
+    s6[5] += reg;
+    sym_to<ND>(s6, D);
+    bstore<ND>(A.val32, A.npos, q, D);
+    bstore_sym<ND>(A.sym, A.npos, q, D);
+    if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q, D);
+    binv<ND>(D, Di);
+    if (L.dinv) {
+#pragma unroll
+      for (int c = 0; c < ND * ND; ++c) L.dinv[i * (ND * ND) + c] = Di[c];
+    }
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) L.dinv32[i * (ND * ND) + c] = (float)Di[c];
+    return;
+  }
+  const int t0 = ptr[q], t1 = ptr[q + 1];
+  if (t0 == t1) return;  // padding
+  double m[ND * ND];
+#pragma unroll
+  for (int c = 0; c < ND * ND; ++c) m[c] = 0.0;
+  for (int t = t0; t < t1; ++t) {
+    double v6[6], e[ND * ND];
+    const int64_t gs = lst[t];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v6[c] = sop.val[(int64_t)c * sop.G + gs];
+    sym_to<ND>(v6, e);
+#pragma unroll
+    for (int c = 0; c < ND * ND; ++c) m[c] += e[c];
+  }
+  bstore<ND>(A.val32, A.npos, q, m);
+  bstore_sym<ND>(A.sym, A.npos, q, m);
+  if (!L.compact) bstore_sym<ND>(A.sym32, A.npos, q, m);
+}
+
 // Level 0 at a fixed ω (AmgLevD::fixed_omega: ρ̂_0 = 2, the exact level-0
 // bound): k_amg_a0dinv's row pass without the Gershgorin bound, plus — from
 // the same row's blocks — the compact cycle's Ã_0 = ω D⁻¹ A_0 and the row's
@@ -1563,6 +1619,12 @@ static void a0_nd(hipStream_t s, const AmgLevD& L0, const SellOp& sop, const int
   if (L0.A.n <= 0) return;
   if (full) {  // fixed ω: Ã_0 and P_0 too, no bound (the fused setup skips level 0's P/Ã launch)
     hipLaunchKernelGGL(k_amg_a0full<ND>, rows_grid(L0.A.rg.span()), dim3(kBlock), 0, s, L0, sop, row0, p, a, reg);
+    return;
+  }
+  if (L0.fixed_omega && L0.a0slot) {  // no bound to form: one thread per position
+    const int64_t blocks = (L0.A.rg.npos() / 64 + kBlock / 64 - 1) / (kBlock / 64);
+    hipLaunchKernelGGL(k_amg_a0slot<ND>, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s, L0, sop,
+                       row0, p, a, reg);
     return;
   }
   // level 0's bound, max'ed by the blocks (not at a fixed ω: nothing reads it)

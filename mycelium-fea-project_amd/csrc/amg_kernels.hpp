@@ -73,6 +73,7 @@ struct AmgLevD {
   int ulanes = 0;    // compact up sweep: lanes per P̃ row (0: by P̃'s mean width)
   int x1 = 0;        // the numeric setup's launches over this level run on one XCD (amg.hip setup_block)
   int fixed_omega = 0;  // ω from omega[0] (no Gershgorin bound): the fused setup forms D⁻¹ with A (k_amg_ac)
+  int a0slot = 0;       // level 0 (fixed ω, not a0full): one thread per position (k_amg_a0slot)
   int a0full = 0;       // level 0 (fixed ω): A_0, D⁻¹, Ã_0 and P_0 in one row pass (k_amg_a0full)
   // transfer to level l+1 (not on the coarsest level)
   AmgMatD P;

@@ -340,6 +340,7 @@ struct mfea_handle {
   // Gershgorin-safe value.  A solve that fails with it falls back to the safe
   // value for the handle's lifetime (amg_safe_omega, omega_fallback).
   int64_t opt_amg_coarse_rho_ppm = 1750000;
+  int opt_amg_a0_slot = 1;  // level 0's blocks one thread per position (k_amg_a0slot) at a fixed ω
   bool amg_safe_omega = false;
   int64_t opt_amg_x1_rows = 2048;  // GAMG setup: levels of at most this many rows run on one XCD (0: never;
                                    // C3: levels 4-5 gain 1-2 µs per launch, level 3 at 8192 lost as much)
@@ -1333,6 +1334,7 @@ int apply_coarse_omega(mfea_handle* h, Part& pt) {
     AmgLevD& d = pt.amg_lev[l];
     d.fixed_omega = pt.amg_om_own && l > 0 && rho > 0.0 ? 1 : 0;
     d.a0full = 0;
+    d.a0slot = l == 0 ? h->opt_amg_a0_slot : 0;
     HIPC(hipMemsetAsync(d.omega, 0, sizeof(double), s));
     if (l > 0 && rho > 0.0) HIPC(hipMemcpyAsync(d.omega, &rho, sizeof(double), hipMemcpyHostToDevice, s));
   }
@@ -4221,6 +4223,11 @@ int mfea_set_option(mfea_handle* h, const char* name, int64_t value) {
     h->amg_safe_omega = false;
     rebuild = true;
   }
+  else if (n == "amg_a0_slot") {
+    if (value != 0 && value != 1) return fail(MFEA_EINVAL, "amg_a0_slot: 0 or 1");
+    h->opt_amg_a0_slot = (int)value;
+    rebuild = true;
+  }
   else if (n == "sweep_piece") {
     if (value < 1 || value > 64) return fail(MFEA_EINVAL, "sweep_piece: 1..64");
     h->opt_sweep_piece = (int)value;
@@ -4490,6 +4497,7 @@ int mfea_get_option(mfea_handle* h, const char* name, int64_t* value) {
   else if (n == "sweep_pieces") *value = part0(h).sweep.n_pieces;  // read-only
   else if (n == "amg_up_lanes") *value = h->opt_amg_up_lanes;
   else if (n == "amg_coarse_rho_ppm") *value = h->opt_amg_coarse_rho_ppm;
+  else if (n == "amg_a0_slot") *value = h->opt_amg_a0_slot;
   else if (n == "amg_safe_omega") *value = h->amg_safe_omega ? 1 : 0;  // read-only
   else if (n == "amg_spatial") *value = h->opt_amg_spatial;
   else if (n == "amg_collapse") *value = h->opt_amg_collapse;

@@ -23,7 +23,7 @@ DEFAULT_OPTIONS = {"graph": 1, "phase_times": 0, "dist_graph": 1, "order": -1, "
                    "amg_coarse_rho_ppm": 1750000, "sweep_piece": 64, "cc_tile": 1024,
                    "asm_kernel": 0, "spec_post": 1, "setup_entry": 1,
                    "batch_graph": 1, "step_graph": 0,
-                   "graph_start": 1, "combo_graph": 1}
+                   "graph_start": 1, "combo_graph": 1, "amg_a0_slot": 1}
 CG_KERNEL = {"auto": 0, "lanes": 1, "sell": 2}
 
 LIB_PATH = os.environ.get("MFEA_LIB", os.path.join(os.path.dirname(_HERE), "libmfea.so"))

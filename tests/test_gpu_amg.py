@@ -581,6 +581,34 @@ def test_coarse_overrelaxation_fallback(engine):
     assert engine.get_option("amg_safe_omega") == 0  # a new weight, a new chance
 
 
+def test_level0_blocks_per_position_are_bitwise_the_row_pass(engine):
+    """Option amg_a0_slot: level 0's blocks and D⁻¹ formed one thread per SELL
+    position (k_amg_a0slot) give the row pass's (k_amg_a0dinv) solves bit for
+    bit — on the reference network and on a C2-shaped tiled one."""
+    from mfea import PC_GAMG, make_opts, synth
+    dy = fo.DISPLACEMENT_MAX * 20 / (fo.N_STEPS - 1)
+    xyz, e2n = synth.tiled_mesh(1, 5)
+    top, bot = synth.grips(xyz)
+    for mesh in ("ref", "tiled"):
+        runs = []
+        for slot in (0, 1):
+            with engine.options(amg_a0_slot=slot):
+                if mesh == "ref":
+                    _sim181147(engine)
+                else:
+                    engine.set_mesh(xyz, e2n)
+                    engine.set_bc(top, bot)
+                    engine.set_active(None)
+                out = []
+                for k in (1, 2):
+                    f, n, st = engine.step(k * dy, -k * dy, make_opts(rtol=1e-10, max_it=20000, precond=PC_GAMG), 0.018)
+                    assert st.status == 0
+                    out.append((f, st.iters, engine.displacement().copy()))
+                runs.append(out)
+        for a, b in zip(*runs):
+            assert a[0] == b[0] and a[1] == b[1] and np.array_equal(a[2], b[2]), mesh
+
+
 @pytest.mark.parametrize("precond", ["gamg", "icc"])
 def test_setup_entry_in_the_graph_is_bitwise_the_eager_entry(engine, precond):
     """Option setup_entry: the solve's entry launches (level-0 b, the first

@@ -345,8 +345,7 @@ __device__ __forceinline__ void dinv_apply(const TD* __restrict__ dinv, int64_t 
 
 // C += Σ_t X[a_t]·Y[b_t] (TX: X[a_t]ᵀ·Y[b_t]) over one index list, in list
 // order, U pairs' loads in flight per step (every pair is two dependent hops:
-// index, then blocks).  Lists longer than 4 take steps of 8 (the Galerkin
-// product's lists run ≈ 2–30 pairs).
+// index, then blocks); pair_sum takes steps of 4.
 template <int ND, bool TX, int U, class TX_, class TY_>
 __device__ __forceinline__ void pair_sum_u(int t0, int t1, const int32_t* __restrict__ la,
                                            const int32_t* __restrict__ lb, const TX_* __restrict__ X,
@@ -381,8 +380,11 @@ template <int ND, bool TX, class TX_, class TY_>
 __device__ __forceinline__ void pair_sum(int t0, int t1, const int32_t* __restrict__ la,
                                          const int32_t* __restrict__ lb, const TX_* __restrict__ X,
                                          int64_t /*nx*/, const TY_* __restrict__ Y, int64_t /*ny*/, double* C) {
-  if (t1 - t0 > 4) pair_sum_u<ND, TX, 8>(t0, t1, la, lb, X, Y, C);
-  else pair_sum_u<ND, TX, 4>(t0, t1, la, lb, X, Y, C);
+  // four pairs a step whatever the length: the eight-pair path for lists
+  // over four (its VGPRs set the kernel's occupancy: A·P 92 → 74) measured
+  // slower now that every step's loads are in flight together (C3 setup
+  // −13 µs, C5 −160 µs, profiles/r6/ab_pair_sum_u4.log)
+  pair_sum_u<ND, TX, 4>(t0, t1, la, lb, X, Y, C);
 }
 // S += Σ_t X[a_t] over one index list, in list order
 template <int ND, int U, class TX_>
@@ -404,8 +406,7 @@ __device__ __forceinline__ void list_sum_u(int t0, int t1, const int32_t* __rest
 template <int ND, class TX_>
 __device__ __forceinline__ void list_sum(int t0, int t1, const int32_t* __restrict__ la,
                                          const TX_* __restrict__ X, int64_t /*nx*/, double* S) {
-  if (t1 - t0 > 4) list_sum_u<ND, 8>(t0, t1, la, X, S);
-  else list_sum_u<ND, 4>(t0, t1, la, X, S);
+  list_sum_u<ND, 4>(t0, t1, la, X, S);  // (steps of 4, as pair_sum: profiles/r6/ab_list_sum_u4.log)
 }
 
 constexpr double kRhoFloor = 2.0;   // the exact level-0 bound (see the header)
